@@ -1,0 +1,176 @@
+// Python bindings for the IDunno-MI355X HIP kernels.
+//
+// Every entry point validates the operand shapes/dtypes/devices it is handed
+// before it launches anything (a malformed launch on a shared MI355X box can
+// fault the whole node), then launches on PyTorch's *current* HIP stream so
+// the ops compose with torch.cuda.graph capture (hipGraph) and side streams.
+#include <ATen/hip/HIPContext.h>
+#include <torch/extension.h>
+
+#include "kernels.h"
+
+using namespace idunno;
+
+static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_DT(t, dt) TORCH_CHECK((t).scalar_type() == (dt), #t " has wrong dtype")
+
+// y = act(conv(x, w) + bias (+ res))
+//   x   : [B, H, W, C] fp16 NHWC (C == 4 for the small-C stem path, else C % 64 == 0)
+//   w   : [Cout, Kpad] fp16, K ordered (kh, kw, c) [big] or (kh, kw8, c4) [small]
+//   bias: [Cout] fp32
+//   res : optional [B, Ho, Wo, Cout] fp16
+torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
+                          c10::optional<torch::Tensor> res, int64_t KH, int64_t KW, int64_t stride,
+                          int64_t pad, bool relu, bool out_f32, int64_t tile) {
+  CHECK_DEV(x);
+  CHECK_DEV(w);
+  CHECK_DEV(bias);
+  CHECK_CONTIG(x);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(bias);
+  CHECK_DT(x, torch::kHalf);
+  CHECK_DT(w, torch::kHalf);
+  CHECK_DT(bias, torch::kFloat);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 2 && bias.dim() == 1, "bad ranks");
+  TORCH_CHECK(KH >= 1 && KW >= 1 && stride >= 1 && pad >= 0, "bad conv geometry");
+  const int B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Cout = w.size(0), Kpad = w.size(1);
+  TORCH_CHECK(bias.size(0) == Cout, "bias/Cout mismatch");
+  TORCH_CHECK(Cout % 4 == 0, "Cout must be a multiple of 4");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty output");
+  const bool small = (C == 4);
+  ConvArgs a{};
+  if (small) {
+    const int nsub = (KW + 7) / 8;
+    TORCH_CHECK(Kpad == KH * nsub * 32, "small-C weight must be [Cout, KH*ceil(KW/8)*32]");
+    a.nsub = nsub;
+    a.nK = KH * nsub;
+    a.cblk = 1;
+  } else {
+    TORCH_CHECK(C % 64 == 0, "C must be 4 or a multiple of 64, got ", C);
+    TORCH_CHECK(Kpad == KH * KW * C, "weight must be [Cout, KH*KW*C]");
+    a.cblk = C / 64;
+    a.nK = KH * KW * a.cblk;
+    a.nsub = 1;
+  }
+  const long M = (long)B * Ho * Wo;
+  TORCH_CHECK(M < (1L << 31) && (long)B * H * W * C < (1L << 31), "tensor too large for int32 indexing");
+  torch::Tensor y = torch::empty({B, Ho, Wo, Cout}, x.options().dtype(out_f32 ? torch::kFloat : torch::kHalf));
+  const half_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    auto& r = *res;
+    CHECK_DEV(r);
+    CHECK_CONTIG(r);
+    CHECK_DT(r, torch::kHalf);
+    TORCH_CHECK(r.dim() == 4 && r.size(0) == B && r.size(1) == Ho && r.size(2) == Wo && r.size(3) == Cout,
+                "residual shape mismatch");
+    TORCH_CHECK(!out_f32 || !small, "unsupported combination");
+    rp = reinterpret_cast<const half_t*>(r.data_ptr());
+  }
+  a.x = reinterpret_cast<const half_t*>(x.data_ptr());
+  a.w = reinterpret_cast<const half_t*>(w.data_ptr());
+  a.bias = bias.data_ptr<float>();
+  a.res = rp;
+  a.y = y.data_ptr();
+  a.B = B; a.H = H; a.W = W; a.C = C;
+  a.Ho = Ho; a.Wo = Wo; a.Cout = Cout; a.ldy = Cout;
+  a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
+  a.M = (int)M;
+  a.Kpad = Kpad;
+  a.relu = relu ? 1 : 0;
+  if (M == 0) return y;
+  const int t = tile >= 0 ? (int)tile : conv_pick_tile(a.M, Cout);
+  TORCH_CHECK(t >= 0 && t <= 3, "tile id out of range");
+  conv_igemm_launch(a, small, out_f32, t, cur_stream());
+  return y;
+}
+
+torch::Tensor preprocess(torch::Tensor img) {
+  CHECK_DEV(img);
+  CHECK_CONTIG(img);
+  CHECK_DT(img, torch::kUInt8);
+  TORCH_CHECK(img.dim() == 4 && img.size(3) == 3, "img must be [B, H, W, 3] uint8");
+  auto out = torch::empty({img.size(0), img.size(1), img.size(2), 4}, img.options().dtype(torch::kHalf));
+  const long npix = img.size(0) * img.size(1) * img.size(2);
+  if (npix) preprocess_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), npix, cur_stream());
+  return out;
+}
+
+torch::Tensor resize_crop(torch::Tensor img, int64_t resize, int64_t crop) {
+  CHECK_DEV(img);
+  CHECK_CONTIG(img);
+  CHECK_DT(img, torch::kUInt8);
+  TORCH_CHECK(img.dim() == 4 && img.size(3) == 3, "img must be [B, H, W, 3] uint8");
+  const int B = img.size(0), Hi = img.size(1), Wi = img.size(2);
+  int Hr, Wr;
+  if (Hi <= Wi) {
+    Hr = resize;
+    Wr = (int)((long)resize * Wi / Hi);
+  } else {
+    Wr = resize;
+    Hr = (int)((long)resize * Hi / Wi);
+  }
+  TORCH_CHECK(Hr >= crop && Wr >= crop, "crop larger than resized image");
+  auto out = torch::empty({B, crop, crop, 4}, img.options().dtype(torch::kHalf));
+  if (B) resize_crop_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), B, Hi, Wi, Hr, Wr,
+                            crop, cur_stream());
+  return out;
+}
+
+torch::Tensor maxpool2d_nhwc(torch::Tensor x, int64_t k, int64_t s, int64_t pad) {
+  CHECK_DEV(x);
+  CHECK_CONTIG(x);
+  CHECK_DT(x, torch::kHalf);
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "x must be [B,H,W,C] with C % 8 == 0");
+  TORCH_CHECK(k >= 1 && s >= 1 && pad >= 0 && 2 * pad <= k, "bad pool geometry");
+  const int B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Ho = (H + 2 * pad - k) / s + 1, Wo = (W + 2 * pad - k) / s + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty output");
+  auto y = torch::empty({B, Ho, Wo, C}, x.options());
+  if (B) maxpool_launch(reinterpret_cast<const half_t*>(x.data_ptr()), reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, C,
+                        Ho, Wo, k, s, pad, cur_stream());
+  return y;
+}
+
+torch::Tensor global_avgpool_nhwc(torch::Tensor x) {
+  CHECK_DEV(x);
+  CHECK_CONTIG(x);
+  CHECK_DT(x, torch::kHalf);
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "x must be [B,H,W,C] with C % 8 == 0");
+  const int B = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  auto y = torch::empty({B, C}, x.options());
+  if (B) avgpool_launch(reinterpret_cast<const half_t*>(x.data_ptr()), reinterpret_cast<half_t*>(y.data_ptr()), B, HW, C,
+                        cur_stream());
+  return y;
+}
+
+std::vector<torch::Tensor> softmax_top1(torch::Tensor logits) {
+  CHECK_DEV(logits);
+  CHECK_DT(logits, torch::kFloat);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [rows, N] with unit column stride");
+  const int rows = logits.size(0), N = logits.size(1), ld = logits.stride(0);
+  auto cls = torch::empty({rows}, logits.options().dtype(torch::kInt));
+  auto prob = torch::empty({rows}, logits.options());
+  if (rows) softmax_top1_launch(logits.data_ptr<float>(), ld, N, rows, cls.data_ptr<int>(), prob.data_ptr<float>(),
+                                cur_stream());
+  return {cls, prob};
+}
+
+int64_t pick_tile(int64_t M, int64_t Cout) { return conv_pick_tile((int)M, (int)Cout); }
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "IDunno-MI355X native HIP kernels (gfx950)";
+  m.def("conv2d_nhwc", &conv2d_nhwc, "implicit-GEMM MFMA conv + bias (+res) (+relu)", py::arg("x"), py::arg("w"),
+        py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
+        py::arg("relu"), py::arg("out_f32") = false, py::arg("tile") = -1);
+  m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 NHWC4");
+  m.def("resize_crop", &resize_crop, "bilinear resize + centre crop + normalise");
+  m.def("maxpool2d_nhwc", &maxpool2d_nhwc, "NHWC max pool");
+  m.def("global_avgpool_nhwc", &global_avgpool_nhwc, "NHWC global average pool");
+  m.def("softmax_top1", &softmax_top1, "fused row softmax + argmax");
+  m.def("pick_tile", &pick_tile, "tile id the conv heuristic picks for (M, Cout)");
+}

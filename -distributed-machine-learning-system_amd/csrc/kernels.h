@@ -1,0 +1,38 @@
+// Host-visible launch entry points of the HIP kernels (one definition of the
+// argument structs shared by the kernel TUs and the Python bindings).
+#pragma once
+#include "common.h"
+
+namespace idunno {
+
+struct ConvArgs {
+  const half_t* x;     // NHWC [B][H][W][C]
+  const half_t* w;     // [Cout][Kpad]
+  const float* bias;   // [Cout]
+  const half_t* res;   // NHWC [B][Ho][Wo][Cout] or nullptr
+  void* y;             // NHWC [B][Ho][Wo][ldy]  (fp16 or fp32)
+  int B, H, W, C;
+  int Ho, Wo, Cout, ldy;
+  int KH, KW, stride, pad;
+  int M;        // B*Ho*Wo
+  int nK;       // number of K stages
+  int cblk;     // BIG: C / BK
+  int nsub;     // SMALL: stages per kh row
+  int Kpad;     // row length of w
+  int relu;
+  int tiles_n;  // ceil(Cout / BN)
+  int tiles_m;  // ceil(M / BM)
+};
+
+void conv_igemm_launch(ConvArgs a, bool small, bool out_f32, int tile, hipStream_t st);
+int conv_pick_tile(int M, int Cout);
+void preprocess_launch(const uint8_t* img, half_t* out, long npix, hipStream_t st);
+void resize_crop_launch(const uint8_t* img, half_t* out, int B, int Hi, int Wi, int Hr, int Wr,
+                        int crop, hipStream_t st);
+void maxpool_launch(const half_t* x, half_t* y, int B, int H, int W, int C, int Ho, int Wo, int k,
+                    int s, int pad, hipStream_t st);
+void avgpool_launch(const half_t* x, half_t* y, int B, int HW, int C, hipStream_t st);
+void softmax_top1_launch(const float* logits, int ld, int N, int rows, int* cls, float* prob,
+                         hipStream_t st);
+
+}  // namespace idunno

@@ -1,0 +1,194 @@
+// Memory-bound companions of the implicit-GEMM conv:
+//   * preprocess      uint8 HWC images -> normalised fp16 NHWC (C padded to 4)
+//                     (replaces ToTensor + Normalize, reference alexnet_resnet.py:57-62)
+//   * resize_crop     bilinear resize (shorter side -> `resize`) + centre crop,
+//                     fused with the normalisation (reference :57-59, Resize(256)
+//                     + CenterCrop(224)) for real, non-224 inputs
+//   * maxpool2d       NHWC 3x3 (any k/stride/pad), 8 channels per lane
+//   * global_avgpool  NHWC [B][HW][C] -> [B][C]
+//   * softmax_top1    row softmax + argmax fused, one wave per row
+//                     (replaces softmax + topk(1), reference :80-84)
+// All loads/stores are 8-16 bytes per lane (cdna_hip_programming Guideline 13).
+#include "../kernels.h"
+
+namespace idunno {
+
+// ImageNet statistics (reference alexnet_resnet.py:61)
+__constant__ float kMean[3] = {0.485f, 0.456f, 0.406f};
+__constant__ float kInvStd[3] = {1.0f / 0.229f, 1.0f / 0.224f, 1.0f / 0.225f};
+
+// One thread per pixel: 3 bytes in, 8 bytes (4 halfs) out.
+__global__ void preprocess_kernel(const uint8_t* __restrict__ img, half_t* __restrict__ out,
+                                  long npix) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+  const uint8_t* s = img + p * 3;
+  half4v o;
+  o[0] = (half_t)(((float)s[0] * (1.f / 255.f) - kMean[0]) * kInvStd[0]);
+  o[1] = (half_t)(((float)s[1] * (1.f / 255.f) - kMean[1]) * kInvStd[1]);
+  o[2] = (half_t)(((float)s[2] * (1.f / 255.f) - kMean[2]) * kInvStd[2]);
+  o[3] = (half_t)0.f;
+  *reinterpret_cast<half4v*>(out + p * 4) = o;
+}
+
+void preprocess_launch(const uint8_t* img, half_t* out, long npix, hipStream_t st) {
+  const int bs = 256;
+  const long grid = (npix + bs - 1) / bs;
+  hipLaunchKernelGGL(preprocess_kernel, dim3((unsigned)grid), dim3(bs), 0, st, img, out, npix);
+}
+
+// Bilinear resize of an (Hi x Wi) uint8 HWC image so that its shorter side is
+// `rs`, then a centre crop of `crop` x `crop`, then normalisation.  Matches
+// torchvision's Resize (bilinear, half-pixel centres, no antialias) + CenterCrop.
+__global__ void resize_crop_kernel(const uint8_t* __restrict__ img, half_t* __restrict__ out,
+                                   int B, int Hi, int Wi, int Hr, int Wr, int crop) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long npix = (long)B * crop * crop;
+  if (p >= npix) return;
+  const int b = (int)(p / (crop * crop));
+  const int r = (int)(p - (long)b * crop * crop);
+  const int oy = r / crop, ox = r - oy * crop;
+  const int top = (Hr - crop + 1) / 2, left = (Wr - crop + 1) / 2;  // round((H-c)/2)
+  const int y = oy + top, x = ox + left;
+  const float sy = (float)Hi / (float)Hr, sx = (float)Wi / (float)Wr;
+  float fy = ((float)y + 0.5f) * sy - 0.5f, fx = ((float)x + 0.5f) * sx - 0.5f;
+  fy = fmaxf(fy, 0.f);
+  fx = fmaxf(fx, 0.f);
+  int y0 = (int)fy, x0 = (int)fx;
+  y0 = min(y0, Hi - 1);
+  x0 = min(x0, Wi - 1);
+  const int y1 = min(y0 + 1, Hi - 1), x1 = min(x0 + 1, Wi - 1);
+  const float wy = fy - (float)y0, wx = fx - (float)x0;
+  const uint8_t* base = img + (size_t)b * Hi * Wi * 3;
+  half4v o;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float v00 = base[((size_t)y0 * Wi + x0) * 3 + c], v01 = base[((size_t)y0 * Wi + x1) * 3 + c];
+    const float v10 = base[((size_t)y1 * Wi + x0) * 3 + c], v11 = base[((size_t)y1 * Wi + x1) * 3 + c];
+    const float v = (v00 * (1.f - wx) + v01 * wx) * (1.f - wy) + (v10 * (1.f - wx) + v11 * wx) * wy;
+    o[c] = (half_t)((v * (1.f / 255.f) - kMean[c]) * kInvStd[c]);
+  }
+  o[3] = (half_t)0.f;
+  *reinterpret_cast<half4v*>(out + p * 4) = o;
+}
+
+void resize_crop_launch(const uint8_t* img, half_t* out, int B, int Hi, int Wi, int Hr, int Wr,
+                        int crop, hipStream_t st) {
+  const long npix = (long)B * crop * crop;
+  const int bs = 256;
+  hipLaunchKernelGGL(resize_crop_kernel, dim3((unsigned)((npix + bs - 1) / bs)), dim3(bs), 0, st,
+                     img, out, B, Hi, Wi, Hr, Wr, crop);
+}
+
+// NHWC max-pool; C % 8 == 0.  One thread = 8 channels of one output pixel.
+__global__ void maxpool_kernel(const half_t* __restrict__ x, half_t* __restrict__ y, int B, int H,
+                               int W, int C, int Ho, int Wo, int k, int s, int pad) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cv = C / 8;
+  const long total = (long)B * Ho * Wo * cv;
+  if (t >= total) return;
+  const int c8 = (int)(t % cv);
+  long pix = t / cv;
+  const int ow = (int)(pix % Wo);
+  pix /= Wo;
+  const int oh = (int)(pix % Ho);
+  const int b = (int)(pix / Ho);
+  half8v m;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m[i] = (half_t)(-65504.f);
+  const int ih0 = oh * s - pad, iw0 = ow * s - pad;
+  for (int dy = 0; dy < k; ++dy) {
+    const int ih = ih0 + dy;
+    if ((unsigned)ih >= (unsigned)H) continue;
+    for (int dx = 0; dx < k; ++dx) {
+      const int iw = iw0 + dx;
+      if ((unsigned)iw >= (unsigned)W) continue;
+      const half8v v = *reinterpret_cast<const half8v*>(x + (((size_t)b * H + ih) * W + iw) * C + c8 * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) m[i] = v[i] > m[i] ? v[i] : m[i];
+    }
+  }
+  *reinterpret_cast<half8v*>(y + (size_t)t * 8) = m;
+}
+
+void maxpool_launch(const half_t* x, half_t* y, int B, int H, int W, int C, int Ho, int Wo, int k,
+                    int s, int pad, hipStream_t st) {
+  const long total = (long)B * Ho * Wo * (C / 8);
+  const int bs = 256;
+  hipLaunchKernelGGL(maxpool_kernel, dim3((unsigned)((total + bs - 1) / bs)), dim3(bs), 0, st, x, y,
+                     B, H, W, C, Ho, Wo, k, s, pad);
+}
+
+// NHWC global average pool -> [B][C] fp16.  One thread = 8 channels of one image.
+__global__ void avgpool_kernel(const half_t* __restrict__ x, half_t* __restrict__ y, int B, int HW,
+                               int C) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cv = C / 8;
+  if (t >= (long)B * cv) return;
+  const int b = (int)(t / cv), c8 = (int)(t % cv);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const half_t* p = x + (size_t)b * HW * C + c8 * 8;
+  for (int i = 0; i < HW; ++i) {
+    const half8v v = *reinterpret_cast<const half8v*>(p + (size_t)i * C);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+  }
+  const float inv = 1.f / (float)HW;
+  half8v o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (half_t)(acc[j] * inv);
+  *reinterpret_cast<half8v*>(y + (size_t)b * C + c8 * 8) = o;
+}
+
+void avgpool_launch(const half_t* x, half_t* y, int B, int HW, int C, hipStream_t st) {
+  const long total = (long)B * (C / 8);
+  const int bs = 256;
+  hipLaunchKernelGGL(avgpool_kernel, dim3((unsigned)((total + bs - 1) / bs)), dim3(bs), 0, st, x, y,
+                     B, HW, C);
+}
+
+// Row softmax + top-1: one 64-lane wave per row of fp32 logits.
+// prob(top1) = 1 / sum_j exp(x_j - x_max).  Ties resolve to the lowest index
+// (torch.topk semantics on CPU).
+__global__ void softmax_top1_kernel(const float* __restrict__ logits, int ld, int N, int rows,
+                                    int* __restrict__ cls, float* __restrict__ prob) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= rows) return;
+  const float* r = logits + (size_t)wave * ld;
+  float best = -INFINITY;
+  int bidx = 0x7fffffff;
+  for (int j = lane; j < N; j += 64) {
+    const float v = r[j];
+    if (v > best) {
+      best = v;
+      bidx = j;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bidx, o, 64);
+    if (ov > best || (ov == best && oi < bidx)) {
+      best = ov;
+      bidx = oi;
+    }
+  }
+  float s = 0.f;
+  for (int j = lane; j < N; j += 64) s += __expf(r[j] - best);
+  s = wave_sum(s);
+  if (lane == 0) {
+    cls[wave] = bidx;
+    prob[wave] = 1.f / s;
+  }
+}
+
+void softmax_top1_launch(const float* logits, int ld, int N, int rows, int* cls, float* prob,
+                         hipStream_t st) {
+  const int bs = 256;  // 4 rows per block
+  const int grid = (rows + 3) / 4;
+  hipLaunchKernelGGL(softmax_top1_kernel, dim3(grid), dim3(bs), 0, st, logits, ld, N, rows, cls,
+                     prob);
+}
+
+}  // namespace idunno

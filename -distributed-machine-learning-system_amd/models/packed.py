@@ -1,0 +1,350 @@
+"""Inference programs: reference modules -> BN-folded, MFMA-packed op lists.
+
+``compile_model(module)`` turns an eval-mode ResNet / AlexNet into a flat list
+of ops whose weights are laid out for the gfx950 implicit-GEMM kernel:
+
+  * BatchNorm folded into the preceding conv: w' = w * g/sqrt(v+eps),
+    b' = beta - mean * g/sqrt(v+eps)  ("BN folded into conv
+    weights/bias at load time")
+  * conv weights [Cout, Cin, KH, KW] -> [Cout, KH, KW, Cin] fp16 (K contiguous)
+  * RGB stems (Cin = 3) -> [Cout, KH, ceil(KW/8)*8, 4] (one K-stage per kh row)
+  * AlexNet fc6 columns permuted from NCHW-flatten to NHWC-flatten order
+  * dropout elided (identity in eval), AdaptiveAvgPool(6,6) elided at 224 input
+
+The same program runs on two executors: ``HipRunner`` (the real path, HIP
+kernels, fp16 activations / fp32 accumulation) and ``emulate`` (fp32 torch
+re-execution of the *packed* weights — used on CPU to test folding/packing
+without a GPU).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import reference as ref
+
+
+@dataclass
+class Conv:
+    w: torch.Tensor          # packed [Cout, Kpad] fp16
+    b: torch.Tensor          # [Cout] fp32
+    cin: int
+    cout: int
+    kh: int
+    kw: int
+    stride: int
+    pad: int
+    relu: bool
+    small: bool = False      # RGB stem packing
+
+    def to(self, device):
+        return Conv(self.w.to(device), self.b.to(device), self.cin, self.cout, self.kh, self.kw,
+                    self.stride, self.pad, self.relu, self.small)
+
+    @property
+    def flops_per_out_pixel(self) -> int:
+        return 2 * self.cin * self.kh * self.kw * self.cout
+
+
+@dataclass
+class Block:
+    """Residual block: convs in order; the last conv fuses +identity and ReLU."""
+    convs: list
+    down: Conv | None = None
+
+    def to(self, device):
+        return Block([c.to(device) for c in self.convs], self.down.to(device) if self.down else None)
+
+
+@dataclass
+class Program:
+    name: str
+    kind: str                 # "resnet" | "alexnet"
+    stem: Conv | None = None  # resnet
+    blocks: list = field(default_factory=list)
+    features: list = field(default_factory=list)  # alexnet: ("conv", Conv) | ("pool", (k, s, p))
+    fcs: list = field(default_factory=list)       # list[Conv] as 1x1 convs (last -> fp32 logits)
+    num_classes: int = 1000
+
+    def to(self, device):
+        p = Program(self.name, self.kind, self.stem.to(device) if self.stem else None,
+                    [b.to(device) for b in self.blocks],
+                    [(k, v.to(device) if k == "conv" else v) for k, v in self.features],
+                    [f.to(device) for f in self.fcs], self.num_classes)
+        return p
+
+    def param_bytes(self) -> int:
+        tot = 0
+        for c in self.all_convs():
+            tot += c.w.numel() * c.w.element_size() + c.b.numel() * 4
+        return tot
+
+    def all_convs(self):
+        if self.stem is not None:
+            yield self.stem
+        for b in self.blocks:
+            yield from b.convs
+            if b.down is not None:
+                yield b.down
+        for k, v in self.features:
+            if k == "conv":
+                yield v
+        yield from self.fcs
+
+
+# ---------------------------------------------------------------------------
+# packing
+# ---------------------------------------------------------------------------
+
+def fold_bn(w: torch.Tensor, b: torch.Tensor | None, bn: nn.BatchNorm2d | None):
+    """Fold an eval-mode BatchNorm into the preceding conv's (w, b), in fp64."""
+    w = w.detach().double()
+    b = torch.zeros(w.shape[0], dtype=torch.float64) if b is None else b.detach().double()
+    if bn is None:
+        return w.float(), b.float()
+    scale = bn.weight.detach().double() / torch.sqrt(bn.running_var.detach().double() + bn.eps)
+    w = w * scale.view(-1, 1, 1, 1)
+    b = (b - bn.running_mean.detach().double()) * scale + bn.bias.detach().double()
+    return w.float(), b.float()
+
+
+def pack_conv_weight(w: torch.Tensor) -> tuple[torch.Tensor, bool]:
+    """[Cout, Cin, KH, KW] fp32 -> packed fp16 [Cout, Kpad], small flag."""
+    cout, cin, kh, kw = w.shape
+    if cin <= 4:
+        nsub = (kw + 7) // 8
+        p = torch.zeros(cout, kh, nsub * 8, 4, dtype=torch.float32)
+        p[:, :, :kw, :cin] = w.permute(0, 2, 3, 1)
+        return p.reshape(cout, kh * nsub * 32).half().contiguous(), True
+    if cin % 64 != 0:
+        raise ValueError(f"Cin={cin} unsupported (need 3/4 or a multiple of 64)")
+    return w.permute(0, 2, 3, 1).reshape(cout, kh * kw * cin).half().contiguous(), False
+
+
+def unpack_conv_weight(c: Conv) -> torch.Tensor:
+    """Inverse of pack_conv_weight -> fp32 [Cout, Cin, KH, KW]."""
+    w = c.w.float()
+    if c.small:
+        nsub = (c.kw + 7) // 8
+        return w.view(c.cout, c.kh, nsub * 8, 4)[:, :, :c.kw, :c.cin].permute(0, 3, 1, 2).contiguous()
+    return w.view(c.cout, c.kh, c.kw, c.cin).permute(0, 3, 1, 2).contiguous()
+
+
+def make_conv(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, relu: bool) -> Conv:
+    w, b = fold_bn(conv.weight, conv.bias, bn)
+    pw, small = pack_conv_weight(w)
+    return Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, conv.kernel_size[0],
+                conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small)
+
+
+def make_fc(lin: nn.Linear, relu: bool, perm: torch.Tensor | None = None) -> Conv:
+    w = lin.weight.detach().float()
+    if perm is not None:
+        w = w[:, perm]
+    k = w.shape[1]
+    if k % 64 != 0:
+        raise ValueError(f"FC in_features={k} must be a multiple of 64")
+    return Conv(w.half().contiguous(), lin.bias.detach().float().contiguous(), k, w.shape[0], 1, 1, 1,
+                0, relu, False)
+
+
+def compile_model(m: nn.Module, name: str) -> Program:
+    m = m.eval()
+    if isinstance(m, ref.ResNet):
+        p = Program(name, "resnet", stem=make_conv(m.conv1, m.bn1, True))
+        for li in range(1, 5):
+            for blk in getattr(m, f"layer{li}"):
+                down = make_conv(blk.downsample[0], blk.downsample[1], False) if blk.downsample else None
+                if isinstance(blk, ref.BasicBlock):
+                    convs = [make_conv(blk.conv1, blk.bn1, True), make_conv(blk.conv2, blk.bn2, True)]
+                else:
+                    convs = [make_conv(blk.conv1, blk.bn1, True), make_conv(blk.conv2, blk.bn2, True),
+                             make_conv(blk.conv3, blk.bn3, True)]
+                p.blocks.append(Block(convs, down))
+        p.fcs = [make_fc(m.fc, False)]
+        p.num_classes = m.fc.out_features
+        return p
+    if isinstance(m, ref.AlexNet):
+        p = Program(name, "alexnet")
+        mods = list(m.features)
+        i = 0
+        while i < len(mods):
+            mod = mods[i]
+            if isinstance(mod, nn.Conv2d):
+                relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
+                p.features.append(("conv", make_conv(mod, None, relu)))
+                i += 2 if relu else 1
+                continue
+            if isinstance(mod, nn.MaxPool2d):
+                p.features.append(("pool", (mod.kernel_size, mod.stride, mod.padding)))
+            i += 1
+        # NCHW flatten (c, h, w) -> our NHWC flatten (h, w, c)
+        c, hw = 256, 36
+        perm = torch.arange(c * hw).view(c, hw).t().reshape(-1)
+        lins = [mm for mm in m.classifier if isinstance(mm, nn.Linear)]
+        p.fcs = [make_fc(lins[0], True, perm), make_fc(lins[1], True), make_fc(lins[2], False)]
+        p.num_classes = lins[2].out_features
+        return p
+    raise TypeError(f"cannot compile {type(m).__name__}")
+
+
+def build_program(name: str, seed: int = 0, randomize_bn: bool = False) -> Program:
+    name = ref.canonical(name)
+    return compile_model(ref.build(name, seed=seed, randomize_bn=randomize_bn), name)
+
+
+# ---------------------------------------------------------------------------
+# fp32 torch emulation of a packed program (CPU-testable)
+# ---------------------------------------------------------------------------
+
+def _emu_conv(c: Conv, x: torch.Tensor, res: torch.Tensor | None = None) -> torch.Tensor:
+    y = F.conv2d(x, unpack_conv_weight(c).to(x.device), c.b.to(x.device), c.stride, c.pad)
+    if res is not None:
+        y = y + res
+    return F.relu(y) if c.relu else y
+
+
+@torch.no_grad()
+def emulate(p: Program, img_u8: torch.Tensor) -> torch.Tensor:
+    """fp32 logits of the packed program on NCHW torch ops."""
+    x = ref.preprocess_u8(img_u8)
+    if p.kind == "resnet":
+        x = F.max_pool2d(_emu_conv(p.stem, x), 3, 2, 1)
+        for blk in p.blocks:
+            idt = x if blk.down is None else _emu_conv(blk.down, x)
+            y = x
+            for c in blk.convs[:-1]:
+                y = _emu_conv(c, y)
+            x = _emu_conv(blk.convs[-1], y, idt)
+        x = x.mean(dim=(2, 3))
+    else:
+        for k, v in p.features:
+            x = _emu_conv(v, x) if k == "conv" else F.max_pool2d(x, *v)
+        x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+    for fc in p.fcs:
+        x = F.linear(x, fc.w.float().to(x.device), fc.b.to(x.device))
+        if fc.relu:
+            x = F.relu(x)
+    return x
+
+
+# ---------------------------------------------------------------------------
+# HIP runner
+# ---------------------------------------------------------------------------
+
+class HipRunner:
+    """Runs a packed Program through the gfx950 kernels.
+
+    ``forward(img_u8)`` takes uint8 [B,224,224,3] on the GPU and returns
+    (class int32 [B], prob fp32 [B]).  ``capture(batch)`` records the whole
+    forward into a hipGraph (torch.cuda.CUDAGraph == hipGraph on ROCm) with a
+    static input buffer, removing per-kernel launch overhead.
+    """
+
+    def __init__(self, program: Program, device=None):
+        from .. import ops
+
+        ops.load()
+        self.ops = ops
+        self.device = torch.device(device or "cuda")
+        self.p = program.to(self.device)
+        self._graphs: dict[int, tuple] = {}
+
+    # -- eager forward ------------------------------------------------------
+    def logits(self, img_u8: torch.Tensor) -> torch.Tensor:
+        o = self.ops
+        p = self.p
+        if img_u8.shape[1:3] == (224, 224):
+            x = o.preprocess(img_u8)
+        else:
+            x = o.resize_crop(img_u8, 256, 224)
+        if p.kind == "resnet":
+            s = p.stem
+            x = o.conv2d(x, s.w, s.b, s.kh, s.kw, s.stride, s.pad, s.relu)
+            x = o.maxpool2d(x, 3, 2, 1)
+            for blk in p.blocks:
+                idt = x
+                if blk.down is not None:
+                    d = blk.down
+                    idt = o.conv2d(x, d.w, d.b, d.kh, d.kw, d.stride, d.pad, False)
+                y = x
+                for c in blk.convs[:-1]:
+                    y = o.conv2d(y, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu)
+                c = blk.convs[-1]
+                x = o.conv2d(y, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu, residual=idt)
+            x = o.global_avgpool(x)
+        else:
+            for k, v in p.features:
+                if k == "conv":
+                    x = o.conv2d(x, v.w, v.b, v.kh, v.kw, v.stride, v.pad, v.relu)
+                else:
+                    x = o.maxpool2d(x, *v)
+            x = x.reshape(x.shape[0], -1)
+        for i, fc in enumerate(p.fcs):
+            last = i == len(p.fcs) - 1
+            x = o.linear(x, fc.w, fc.b, relu=fc.relu, out_f32=last)
+        return x
+
+    def forward(self, img_u8: torch.Tensor):
+        return self.ops.softmax_top1(self.logits(img_u8))
+
+    __call__ = forward
+
+    # -- hipGraph -------------------------------------------------------------
+    def capture(self, batch: int, hw: int = 224):
+        """Capture forward for a fixed batch; returns (static_in, replay_fn)."""
+        if batch in self._graphs:
+            g, sin, sout = self._graphs[batch]
+            return sin, (lambda: (g.replay(), sout)[1])
+        sin = torch.zeros(batch, hw, hw, 3, dtype=torch.uint8, device=self.device)
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self.forward(sin)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            sout = self.forward(sin)
+        self._graphs[batch] = (g, sin, sout)
+        return sin, (lambda: (g.replay(), sout)[1])
+
+    def flops_per_image(self) -> float:
+        """Useful (unpadded) FLOPs for one 224x224 image."""
+        return program_flops(self.p)
+
+
+def program_flops(p: Program, hw: int = 224) -> float:
+    """Analytic forward FLOPs per image (2*MAC, convs + FCs)."""
+    tot = 0.0
+
+    def out_hw(h, c):
+        return (h + 2 * c.pad - c.kh) // c.stride + 1
+
+    if p.kind == "resnet":
+        h = out_hw(hw, p.stem)
+        tot += h * h * p.stem.flops_per_out_pixel
+        h = (h + 2 - 3) // 2 + 1
+        for blk in p.blocks:
+            hin = h
+            for c in blk.convs:
+                h = out_hw(h, c)
+                tot += h * h * c.flops_per_out_pixel
+            if blk.down is not None:
+                hd = out_hw(hin, blk.down)
+                tot += hd * hd * blk.down.flops_per_out_pixel
+    else:
+        h = hw
+        for k, v in p.features:
+            if k == "conv":
+                h = out_hw(h, v)
+                tot += h * h * v.flops_per_out_pixel
+            else:
+                kk, s, pp = v
+                h = (h + 2 * pp - kk) // s + 1
+    for fc in p.fcs:
+        tot += fc.flops_per_out_pixel
+    return tot

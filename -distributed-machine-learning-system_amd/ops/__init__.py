@@ -1,0 +1,55 @@
+"""Functional wrappers around the gfx950 HIP kernels (``idunno._C``).
+
+Tensors are NHWC fp16 activations on the current GPU.  Every function runs on
+PyTorch's current HIP stream, so sequences of these ops can be captured into a
+hipGraph with ``torch.cuda.graph``.
+"""
+from __future__ import annotations
+
+from ._ext import available, load, so_path
+
+__all__ = [
+    "available", "load", "so_path", "conv2d", "linear", "preprocess", "resize_crop",
+    "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile",
+]
+
+
+def conv2d(x, w, bias, kh: int, kw: int, stride: int, pad: int, relu: bool,
+           residual=None, out_f32: bool = False, tile: int = -1):
+    """Implicit-GEMM MFMA convolution with fused bias / residual / ReLU."""
+    return load().conv2d_nhwc(x, w, bias, residual, kh, kw, stride, pad, relu, out_f32, tile)
+
+
+def linear(x, w, bias, relu: bool = False, out_f32: bool = False):
+    """y = x @ w.T + bias via the conv kernel as a 1x1 conv on a 1x1 image."""
+    b, k = x.shape
+    y = load().conv2d_nhwc(x.view(b, 1, 1, k), w, bias, None, 1, 1, 1, 0, relu, out_f32, -1)
+    return y.view(b, w.shape[0])
+
+
+def preprocess(img_u8):
+    """uint8 [B,H,W,3] -> normalised fp16 [B,H,W,4] (4th channel zero)."""
+    return load().preprocess(img_u8)
+
+
+def resize_crop(img_u8, resize: int = 256, crop: int = 224):
+    """Resize(shorter side) + CenterCrop + normalise, fused."""
+    return load().resize_crop(img_u8, resize, crop)
+
+
+def maxpool2d(x, k: int = 3, s: int = 2, pad: int = 1):
+    return load().maxpool2d_nhwc(x, k, s, pad)
+
+
+def global_avgpool(x):
+    return load().global_avgpool_nhwc(x)
+
+
+def softmax_top1(logits):
+    """Returns (class int32 [B], probability fp32 [B])."""
+    cls, prob = load().softmax_top1(logits)
+    return cls, prob
+
+
+def pick_tile(m: int, cout: int) -> int:
+    return int(load().pick_tile(m, cout))

@@ -1,0 +1,121 @@
+"""One-process-per-GPU data plane over RCCL (torch.distributed "nccl" == RCCL
+on ROCm; xGMI between the 8 MI355X of a node).
+
+Replaces the reference's per-chunk TCP messages on the hot path
+(SURVEY.md §2.5):
+  * M9  INFERENCE chunk dispatch (coordinator -> workers)   -> ``dispatch``:
+        one broadcast of a tiny int64 descriptor table [world, 4]
+        (model_id, query_id, start, end) per query round;
+  * M11 RESULT broadcast of stringified tuples to all 10 hosts -> ``gather``:
+        one RCCL gather of packed top-1 results (int32 class + fp32 prob,
+        8 B/image, 3.2 KB for a 400-image chunk) to the coordinator rank
+        (and, optionally, a second one to the standby rank).
+Images never cross the fabric in steady state: every rank owns an HBM-resident
+shard of the dataset (see ``idunno.runtime.staging``).
+
+On CPU (tests) the same code runs over gloo.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+NO_WORK = -1
+
+
+@dataclass
+class Env:
+    rank: int
+    world: int
+    local_rank: int
+    device: torch.device
+    backend: str
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+
+def init_from_env(backend: str | None = None, timeout_s: float = 300.0) -> Env:
+    """Initialise the default process group from torchrun-style env vars."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    gpu = torch.cuda.is_available()
+    if gpu:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    backend = backend or ("nccl" if gpu else "gloo")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        from datetime import timedelta
+
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=timedelta(seconds=timeout_s), **kw)
+    return Env(rank, world, local, device, backend)
+
+
+class QueryPlane:
+    """Collective dispatch / gather between the coordinator rank and workers."""
+
+    def __init__(self, env: Env, coordinator: int = 0, max_chunk: int = 512, group=None):
+        self.env = env
+        self.coord = coordinator
+        self.max_chunk = max_chunk
+        self.group = group
+        dev = env.device
+        self._desc = torch.full((env.world, 4), NO_WORK, dtype=torch.int64, device=dev)
+        self._pack = torch.zeros(max_chunk, 2, dtype=torch.int32, device=dev)
+        self._gathered = [torch.zeros(max_chunk, 2, dtype=torch.int32, device=dev)
+                          for _ in range(env.world)] if env.rank == coordinator else None
+
+    # -- M9 ---------------------------------------------------------------------
+    def dispatch(self, table: list[tuple[int, int, int, int]] | None) -> tuple[int, int, int, int]:
+        """Coordinator passes one (model_id, qid, start, end) row per rank
+        (end = -1 for an idle rank); every rank gets its own row back."""
+        if self.env.rank == self.coord:
+            assert table is not None and len(table) == self.env.world
+            for r, row in enumerate(table):
+                if row[3] != NO_WORK and row[3] - row[2] + 1 > self.max_chunk:
+                    raise ValueError(f"chunk {row} larger than max_chunk={self.max_chunk}")
+            self._desc.copy_(torch.tensor(table, dtype=torch.int64), non_blocking=True)
+        if self.env.distributed:
+            dist.broadcast(self._desc, src=self.coord, group=self.group)
+        row = self._desc[self.env.rank].tolist()
+        return tuple(int(v) for v in row)
+
+    # -- M11 --------------------------------------------------------------------
+    def pack(self, cls: torch.Tensor, prob: torch.Tensor) -> torch.Tensor:
+        n = cls.numel()
+        self._pack[:n, 0].copy_(cls.view(-1).to(torch.int32))
+        self._pack[:n, 1].copy_(prob.view(-1).float().view(torch.int32))
+        return self._pack
+
+    def gather(self, cls: torch.Tensor | None, prob: torch.Tensor | None):
+        """Gather packed top-1 results to the coordinator.  Returns, on the
+        coordinator, a list (per rank) of int32 [max_chunk, 2] device tensors."""
+        if cls is not None:
+            self.pack(cls, prob)
+        if not self.env.distributed:
+            self._gathered[0].copy_(self._pack)
+            return self._gathered
+        if self.env.rank == self.coord:
+            dist.gather(self._pack, self._gathered, dst=self.coord, group=self.group)
+            return self._gathered
+        dist.gather(self._pack, None, dst=self.coord, group=self.group)
+        return None
+
+
+def unpack(packed: torch.Tensor, n: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """(cls int32 [n], prob fp32 [n]) from a packed [*, 2] int32 tensor (any device)."""
+    p = packed[:n]
+    return p[:, 0].clone(), p[:, 1].clone().view(torch.float32)

@@ -1,0 +1,305 @@
+"""Coordinator job-state tables and the c1/c2/c4/cq/cvm views.
+
+Table layouts are kept identical to the reference so the shell output and the
+standby snapshot look the same (mp4_machinelearning.py:115-160):
+
+  worker_set        {(model, qnum): [(worker, start, end, 'w'|'f', t_start, t_end), ...]}   (cq)
+  working_vm_set    {worker: [(model, qnum, start, end), ...]}                              (cvm)
+  inference_result_list {"<model> <qnum>": [str([(img, category, prob), ...]), ...]}      (c4 -> result.txt)
+  query_processing_time_meta {model: [mean, q1, q2, q3, std]}                               (c2)
+
+Deliberate fixes:
+  A2  c1/c2 numbers are measured for *every* model (none synthesised from the other)
+  A3  finished-image counts are end - start + 1
+  A4  results are kept as arrays (class id int32, prob fp32) and rendered to
+      the reference's string format lazily, so no 4 KB truncation exists
+  A11 query numbers are coordinator-assigned
+  A13 single writer: every mutation goes through this object under one lock,
+      and result ingestion is idempotent by chunk key (model, qnum, start, end)
+"""
+from __future__ import annotations
+
+import json
+import threading
+import time
+from collections import defaultdict, deque
+from dataclasses import dataclass
+
+import numpy as np
+
+WINDOW_S = 30.0  # reference SLIDING_WINDOW_SECONDS * SLIDING_WINDOW_FACTOR (10 * 3)
+
+DEFAULT_BATCHSIZE = {"resnet18": 400, "alexnet": 500, "resnet50": 1024, "resnet34": 400}
+
+
+def class_names(n: int = 1000, path: str | None = None) -> list[str]:
+    """ImageNet category names if a classes file is available, else synthetic.
+
+    The reference downloads imagenet_classes.txt (alexnet_resnet.py:27-42);
+    there is no network here, so a local file is optional."""
+    import os
+
+    cands = [path] if path else []
+    cands.append(os.environ.get("IDUNNO_CLASSES", ""))
+    for p in cands:
+        if p and os.path.exists(p):
+            with open(p) as f:
+                names = [ln.strip() for ln in f if ln.strip()]
+            if len(names) >= n:
+                return names[:n]
+    return [f"class_{i}" for i in range(n)]
+
+
+@dataclass
+class ChunkResult:
+    start: int
+    end: int
+    cls: np.ndarray      # int32 [n]
+    prob: np.ndarray     # float32 [n]
+    worker: str
+
+    def render(self, names: list[str]) -> str:
+        tup = [(f"test_{self.start + i}.JPEG", names[int(c)] if 0 <= int(c) < len(names) else str(int(c)),
+                float(p)) for i, (c, p) in enumerate(zip(self.cls.tolist(), self.prob.tolist()))]
+        return str(tup)
+
+
+class JobState:
+    def __init__(self, batchsize: dict | None = None, clock=time.time, window_s: float = WINDOW_S,
+                 names: list[str] | None = None):
+        self.lock = threading.RLock()
+        self.clock = clock
+        self.window_s = window_s
+        self.batchsize = dict(DEFAULT_BATCHSIZE, **(batchsize or {}))
+        self.names = names
+        self.worker_set: dict = defaultdict(list)
+        self.working_vm_set: dict = defaultdict(list)
+        self.results: dict = defaultdict(list)          # "model q" -> [ChunkResult]
+        self._done_keys: set = set()
+        self.finished_images: dict = defaultdict(int)
+        self.finished_queries: dict = defaultdict(int)
+        self._rate_win: dict = defaultdict(deque)       # model -> (t_finish, n_images)
+        self._ptime_win: dict = defaultdict(deque)      # model -> (t_finish, normalised query time)
+        self.query_processing_time_meta: dict = {}
+        self.next_qnum: dict = defaultdict(int)
+        self.seq = 0                                    # mutation counter (standby replication)
+        self.query_submit_time: dict = {}
+        self.query_latency: dict = defaultdict(list)    # model -> [end-to-end seconds]
+
+    # -- ids --------------------------------------------------------------------
+    def new_query_number(self, model: str) -> int:
+        """Coordinator-assigned query number (fix A11; the reference counted on the client)."""
+        with self.lock:
+            self.next_qnum[model] += 1
+            return self.next_qnum[model]
+
+    # -- mutations --------------------------------------------------------------
+    def assign(self, model: str, qnum, chunks, now: float | None = None) -> None:
+        """Record a dispatched query: chunks = [(worker, start, end), ...]."""
+        now = self.clock() if now is None else now
+        with self.lock:
+            key = (model, qnum)
+            self.query_submit_time.setdefault(key, now)
+            for w, s, e in chunks:
+                self.worker_set[key].append((w, int(s), int(e), "w", now, now))
+                self.working_vm_set[w].append((model, qnum, int(s), int(e)))
+            self.seq += 1
+
+    def record_result(self, model: str, qnum, worker: str, start: int, end: int, cls, prob,
+                      now: float | None = None) -> bool:
+        """Ingest one finished chunk.  Idempotent: returns False for duplicates
+        (e.g. a re-dispatched chunk whose original worker also answered)."""
+        now = self.clock() if now is None else now
+        start, end = int(start), int(end)
+        with self.lock:
+            ck = (model, qnum, start, end)
+            if ck in self._done_keys:
+                return False
+            key = (model, qnum)
+            entries = self.worker_set.get(key, [])
+            hit = None
+            for i, ent in enumerate(entries):
+                if ent[1] == start and ent[2] == end and ent[3] == "w":
+                    hit = i
+                    break
+            t_start = now
+            if hit is not None:
+                w, s, e, _, t_start, _ = entries[hit]
+                entries[hit] = (w, s, e, "f", t_start, now)
+                try:
+                    self.working_vm_set[w].remove((model, qnum, s, e))
+                except ValueError:
+                    pass
+                if not self.working_vm_set[w]:
+                    self.working_vm_set.pop(w, None)
+            self._done_keys.add(ck)
+            n = end - start + 1                                   # fix A3
+            self.finished_images[model] += n
+            self._rate_win[model].append((now, n))
+            bs = self.batchsize.get(model, n)
+            self._ptime_win[model].append((now, (now - t_start) / n * bs))
+            self._expire(model, now)
+            self._recompute_c2(model)
+            self.results[f"{model} {qnum}"].append(
+                ChunkResult(start, end, np.asarray(cls, dtype=np.int32), np.asarray(prob, dtype=np.float32),
+                            worker))
+            if entries and all(ent[3] == "f" for ent in entries):
+                self.finished_queries[model] += 1
+                t0 = self.query_submit_time.get(key)
+                if t0 is not None:
+                    self.query_latency[model].append(now - t0)
+            self.seq += 1
+            return True
+
+    def chunks_of(self, worker: str) -> list[tuple]:
+        with self.lock:
+            return list(self.working_vm_set.get(worker, []))
+
+    def reassign(self, failed: str, new_worker: str, chunk: tuple, now: float | None = None) -> None:
+        """Move one in-flight chunk of a failed worker to ``new_worker``
+        (reference transfer_failed_inference_work, mp4_machinelearning.py:706-760)."""
+        now = self.clock() if now is None else now
+        model, qnum, s, e = chunk
+        with self.lock:
+            key = (model, qnum)
+            ents = self.worker_set.get(key, [])
+            for i, ent in enumerate(ents):
+                if ent[0] == failed and ent[1] == s and ent[2] == e and ent[3] == "w":
+                    ents.pop(i)
+                    break
+            ents.append((new_worker, s, e, "w", now, now))
+            try:
+                self.working_vm_set[failed].remove(chunk)
+            except (ValueError, KeyError):
+                pass
+            if not self.working_vm_set.get(failed):
+                self.working_vm_set.pop(failed, None)
+            self.working_vm_set[new_worker].append(chunk)
+            self.seq += 1
+
+    def pending(self) -> list[tuple]:
+        """All chunks still marked 'w': [(model, qnum, worker, s, e, t_start)]."""
+        with self.lock:
+            out = []
+            for (model, q), ents in self.worker_set.items():
+                for w, s, e, st, t0, _ in ents:
+                    if st == "w":
+                        out.append((model, q, w, s, e, t0))
+            return out
+
+    # -- metrics ------------------------------------------------------------------
+    def _expire(self, model: str, now: float) -> None:
+        for win in (self._rate_win[model], self._ptime_win[model]):
+            while win and now - win[0][0] > self.window_s:
+                win.popleft()
+
+    def _recompute_c2(self, model: str) -> None:
+        vals = [v for _, v in self._ptime_win[model]]
+        if vals:
+            a = np.asarray(vals, dtype=np.float64)
+            self.query_processing_time_meta[model] = [float(a.mean()), float(np.percentile(a, 25)),
+                                                      float(np.percentile(a, 50)),
+                                                      float(np.percentile(a, 75)), float(a.std())]
+
+    def images_done(self, model: str) -> int:
+        return int(self.finished_images.get(model, 0))
+
+    def rates(self, model: str, now: float | None = None) -> dict:
+        now = self.clock() if now is None else now
+        with self.lock:
+            self._expire(model, now)
+            win = self._rate_win[model]
+            imgs = sum(n for _, n in win)
+            span = self.window_s
+            if win:
+                span = max(min(self.window_s, now - win[0][0]), 1e-9)
+            ips = imgs / span if win else 0.0
+            return {"images_per_s": ips, "queries_per_s": ips / self.batchsize.get(model, 1),
+                    "finished_images": self.images_done(model),
+                    "finished_queries": int(self.finished_queries.get(model, 0))}
+
+    def models(self) -> list[str]:
+        with self.lock:
+            ms = set(self.finished_images) | {m for m, _ in self.worker_set}
+            return sorted(ms) or ["resnet18", "alexnet"]
+
+    # -- shell views ------------------------------------------------------------
+    def c1(self) -> str:
+        """Query rate + finished count per model, reference labels (:1257-1267)."""
+        label = {"resnet18": "Resnet18", "alexnet": "AlexNet"}
+        lines = []
+        for m in self.models():
+            r = self.rates(m)
+            L = label.get(m, m)
+            lines.append(f"{L} query rate is {r['images_per_s']}")
+            lines.append(f"{L} finished inference is {r['finished_images']}")
+            lines.append(f"{L} finished batchsize query rare is {r['queries_per_s']}")
+        return "\n".join(lines)
+
+    def c2(self) -> str:
+        """Processing-time stats per model over the sliding window (:1232-1253)."""
+        lines = []
+        with self.lock:
+            for m, v in sorted(self.query_processing_time_meta.items()):
+                lines += [f"model {m} processing time", f"average {v[0]}", f"q1 {v[1]}", f"q2 {v[2]}",
+                          f"q3 {v[3]}", f"stddev {v[4]}"]
+        return "\n".join(lines)
+
+    def inference_result_list(self) -> dict:
+        names = self.names or class_names()
+        with self.lock:
+            return {k: [c.render(names) for c in sorted(v, key=lambda c: c.start)]
+                    for k, v in self.results.items()}
+
+    def c4(self, path: str = "result.txt") -> str:
+        d = self.inference_result_list()
+        with open(path, "w") as f:
+            f.write(json.dumps(d))
+        return str(d)
+
+    def cq(self) -> str:
+        with self.lock:
+            return str(dict(self.worker_set))
+
+    def cvm(self) -> str:
+        with self.lock:
+            return str(dict(self.working_vm_set))
+
+    # -- replication (hot standby) --------------------------------------------------
+    def snapshot(self) -> dict:
+        """Structured, JSON/msgpack-able snapshot (fix A12: no raw str() dumps)."""
+        with self.lock:
+            return {
+                "seq": self.seq,
+                "worker_set": [[list(k), [list(e) for e in v]] for k, v in self.worker_set.items()],
+                "working_vm_set": {w: [list(c) for c in v] for w, v in self.working_vm_set.items()},
+                "results": {k: [[c.start, c.end, c.cls.tolist(), c.prob.tolist(), c.worker] for c in v]
+                            for k, v in self.results.items()},
+                "finished_images": dict(self.finished_images),
+                "finished_queries": dict(self.finished_queries),
+                "next_qnum": dict(self.next_qnum),
+                "meta": dict(self.query_processing_time_meta),
+                "submit": [[list(k), t] for k, t in self.query_submit_time.items()],
+            }
+
+    def restore(self, snap: dict) -> None:
+        with self.lock:
+            self.seq = snap["seq"]
+            self.worker_set = defaultdict(list)
+            for k, v in snap["worker_set"]:
+                self.worker_set[(k[0], k[1])] = [tuple(e) for e in v]
+            self.working_vm_set = defaultdict(list, {w: [tuple(c) for c in v]
+                                                     for w, v in snap["working_vm_set"].items()})
+            self.results = defaultdict(list)
+            self._done_keys = set()
+            for k, v in snap["results"].items():
+                model, q = k.rsplit(" ", 1)
+                qn = int(q) if q.lstrip("-").isdigit() else q
+                for s, e, c, p, w in v:
+                    self.results[k].append(ChunkResult(s, e, np.asarray(c, np.int32), np.asarray(p, np.float32), w))
+                    self._done_keys.add((model, qn, s, e))
+            self.finished_images = defaultdict(int, snap["finished_images"])
+            self.finished_queries = defaultdict(int, snap["finished_queries"])
+            self.next_qnum = defaultdict(int, snap["next_qnum"])
+            self.query_processing_time_meta = dict(snap["meta"])
+            self.query_submit_time = {(k[0], k[1]): t for k, t in snap.get("submit", [])}

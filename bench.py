@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet18 bs=400 image-classification queries on 1..8 MI355X.
+
+Metric (BASELINE.json): images/sec for the whole node + p50 query latency,
+ResNet18, 400 images per query per GPU, synthetic 224x224x3 uint8 images and
+random-init weights (no datasets or checkpoints are reachable).
+
+One *step* is one round of the cluster's query path, end to end:
+  1. the coordinator (rank 0) splits the round's image range over the alive
+     ranks with the fair-time scheduler's split rule and dispatches the chunk
+     descriptors (RCCL broadcast);
+  2. every rank takes its 400-image chunk from its HBM-resident dataset shard,
+     runs preprocess + the HIP ResNet18 forward + fused softmax-top1 (one
+     hipGraph replay of hand-written gfx950 kernels);
+  3. top-1 (class, prob) pairs are gathered to the coordinator over RCCL,
+     copied to host and recorded in the job-state tables (worker_set 'f' marks,
+     result store, c1/c2 statistics).
+Weak scaling: per-GPU work is fixed (400 images per GPU per step).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+BASELINE_IMG_PER_S = 41.0          # 400 img / 9.749 s (ResNet18, 5 workers)
+BASELINE_P50_S = 9.749             # p50 ResNet18 400-image query latency
+METRIC = "images/sec (whole node) + p50 query latency, ResNet18 bs=400 at 1/2/4/8 GPU"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="resnet18")
+    ap.add_argument("--batch", type=int, default=400, help="images per query chunk per GPU")
+    ap.add_argument("--shard-images", type=int, default=2000, help="HBM-resident images per rank")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    a = parse(argv)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from idunno.models import HipRunner, build_program, program_flops
+    from idunno.parallel.dataplane import QueryPlane, init_from_env, unpack
+    from idunno.runtime.jobstate import JobState
+    from idunno.runtime.scheduler import split_range
+
+    env = init_from_env()
+    if env.device.type != "cuda":
+        print(json.dumps({"error": "bench.py needs a GPU (MI355X)"}))
+        return 2
+    if env.world != a.gpus:
+        a.gpus = env.world
+    coord = env.rank == 0
+    B = a.batch
+
+    program = build_program(a.model, seed=a.seed)
+    runner = HipRunner(program, env.device)
+
+    # HBM-resident synthetic dataset shard (uint8 224x224x3), generated on-device.
+    g = torch.Generator(device=env.device)
+    g.manual_seed(1000 + env.rank)
+    n_shard = max(a.shard_images, B)
+    shard = torch.randint(0, 256, (n_shard, 224, 224, 3), dtype=torch.uint8, device=env.device,
+                          generator=g)
+    shard_base = env.rank * n_shard   # global image index of shard[0]
+
+    if a.no_graph:
+        static_in = torch.empty(B, 224, 224, 3, dtype=torch.uint8, device=env.device)
+
+        def run():
+            return runner.forward(static_in)
+    else:
+        static_in, run = runner.capture(B)
+
+    plane = QueryPlane(env, coordinator=0, max_chunk=B)
+    state = JobState() if coord else None
+    host_res = torch.empty(env.world, B, 2, dtype=torch.int32, pin_memory=True) if coord else None
+    model_id = 1 if a.model.startswith("resnet") else 0
+    lat = []
+
+    def step(q: int):
+        t0 = time.perf_counter()
+        table = None
+        if coord:
+            off = (q * B) % (n_shard - B + 1)
+            # the round's images: B consecutive images in every rank's shard
+            table = []
+            for r in range(env.world):
+                s = r * n_shard + off
+                (s0, e0), = split_range(s, s + B - 1, 1)
+                table.append((model_id, q * env.world + r, s0, e0))
+                state.assign(a.model, q * env.world + r, [(f"rank{r}", s0, e0)], t0)
+        _, qid, s, e = plane.dispatch(table)
+        ls = s - shard_base
+        static_in.copy_(shard[ls:ls + (e - s + 1)])
+        cls, prob = run()
+        gathered = plane.gather(cls, prob)
+        if coord:
+            for r in range(env.world):
+                host_res[r].copy_(gathered[r], non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            t1 = time.perf_counter()
+            for r in range(env.world):
+                row = table[r]
+                c, p = unpack(host_res[r], row[3] - row[2] + 1)
+                state.record_result(a.model, row[1], f"rank{r}", row[2], row[3], c.numpy(), p.numpy(), t1)
+            lat.append(time.perf_counter() - t0)
+
+    def barrier():
+        if env.distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for q in range(a.warmup):
+        step(q)
+    barrier()
+    lat.clear()
+    t_start = time.perf_counter()
+    for q in range(a.warmup, a.warmup + a.steps):
+        step(q)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if env.distributed:
+        t = torch.tensor([elapsed], device=env.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if coord:
+        imgs = env.world * B * a.steps
+        ips = imgs / elapsed
+        p50 = statistics.median(lat) if lat else None
+        flops = program_flops(runner.p)
+        out = {
+            "metric": METRIC,
+            "value": round(ips, 2),
+            "unit": "images/sec",
+            "n_gpus": env.world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000 * elapsed / a.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(ips / BASELINE_IMG_PER_S, 2),
+            "dtype": "fp16",
+            "data": "synthetic uint8 224x224x3 images (HBM-resident shard per GPU), random-init weights",
+            "config": {"model": a.model, "global_batch": env.world * B, "seq_len": None,
+                       "image_hw": 224, "batch_per_gpu": B,
+                       "parallelism": f"dp{env.world}", "graph": not a.no_graph},
+            "p50_query_latency_s": round(p50, 6) if p50 else None,
+            "p50_vs_baseline_speedup": round(BASELINE_P50_S / p50, 1) if p50 else None,
+            "model_tflops": round(flops * ips / 1e12, 2),
+            "results_recorded": state.images_done(a.model),
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if env.distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

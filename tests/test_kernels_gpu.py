@@ -1,0 +1,203 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference.
+
+Shapes follow SURVEY.md §2.4 (ResNet18 / AlexNet / ResNet50 layer list) at a
+small batch; inputs are random and asymmetric so a transposed store or a
+swapped fragment map cannot pass.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from idunno import ops as o
+
+    o.load()
+    return o
+
+
+def _ref_conv(x_nhwc, w, b, stride, pad, relu, res=None):
+    x = x_nhwc.float().permute(0, 3, 1, 2)
+    y = F.conv2d(x, w.float(), b.float(), stride, pad)
+    if res is not None:
+        y = y + res.float().permute(0, 3, 1, 2)
+    if relu:
+        y = F.relu(y)
+    return y.permute(0, 2, 3, 1)
+
+
+def _check(y, ref, tol=1e-2):
+    y = y.float()
+    scale = ref.abs().max().item() + 1e-6
+    err = (y - ref).abs().max().item()
+    assert err <= tol * scale + 1e-3, f"max err {err} vs scale {scale}"
+
+
+CONV_CASES = [
+    # (B, H, Cin, Cout, k, stride, pad)
+    (2, 56, 64, 64, 3, 1, 1),      # resnet layer1
+    (2, 56, 64, 128, 3, 2, 1),     # layer2 first conv
+    (2, 56, 64, 128, 1, 2, 0),     # layer2 downsample
+    (2, 28, 128, 128, 3, 1, 1),
+    (2, 14, 256, 256, 3, 1, 1),
+    (3, 7, 512, 512, 3, 1, 1),     # layer4, M = 147 (not a tile multiple)
+    (2, 27, 64, 192, 5, 1, 2),     # alexnet conv2
+    (2, 13, 192, 384, 3, 1, 1),    # alexnet conv3
+    (2, 56, 256, 64, 1, 1, 0),     # resnet50 1x1 reduce
+    (2, 14, 1024, 256, 1, 1, 0),
+]
+
+
+@pytest.mark.parametrize("B,H,Cin,Cout,k,s,p", CONV_CASES)
+def test_conv_big(ops, B, H, Cin, Cout, k, s, p):
+    from idunno.models.packed import pack_conv_weight
+
+    torch.manual_seed(B * 1000 + H + Cin + Cout + k)
+    x = torch.randn(B, H, H, Cin, device=DEV).half()
+    w = (torch.randn(Cout, Cin, k, k) / (Cin * k * k) ** 0.5)
+    b = torch.randn(Cout) * 0.1
+    pw, small = pack_conv_weight(w)
+    assert not small
+    wq = w.half().float()
+    y = ops.conv2d(x, pw.to(DEV), b.to(DEV), k, k, s, p, True)
+    ref = _ref_conv(x, wq.to(DEV), b.to(DEV), s, p, True)
+    assert y.shape == ref.shape
+    _check(y, ref)
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+def test_conv_all_tiles_with_residual(ops, tile):
+    from idunno.models.packed import pack_conv_weight
+
+    torch.manual_seed(tile)
+    B, H, Cin, Cout = 2, 14, 128, 128
+    x = torch.randn(B, H, H, Cin, device=DEV).half()
+    w = torch.randn(Cout, Cin, 3, 3) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    res = torch.randn(B, H, H, Cout, device=DEV).half()
+    pw, _ = pack_conv_weight(w)
+    y = ops.conv2d(x, pw.to(DEV), b.to(DEV), 3, 3, 1, 1, True, residual=res, tile=tile)
+    ref = _ref_conv(x, w.half().float().to(DEV), b.to(DEV), 1, 1, True, res)
+    _check(y, ref)
+
+
+@pytest.mark.parametrize("k,s,p,H", [(7, 2, 3, 224), (11, 4, 2, 224), (7, 2, 3, 37)])
+def test_conv_small_c_stem(ops, k, s, p, H):
+    from idunno.models.packed import pack_conv_weight
+
+    torch.manual_seed(k * 7 + H)
+    B, Cout = 2, 64
+    x3 = torch.randn(B, H, H, 3, device=DEV).half()
+    x4 = torch.zeros(B, H, H, 4, device=DEV).half()
+    x4[..., :3] = x3
+    w = torch.randn(Cout, 3, k, k) / (3 * k * k) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    pw, small = pack_conv_weight(w)
+    assert small
+    y = ops.conv2d(x4, pw.to(DEV), b.to(DEV), k, k, s, p, True)
+    ref = _ref_conv(x3, w.half().float().to(DEV), b.to(DEV), s, p, True)
+    _check(y, ref)
+
+
+@pytest.mark.parametrize("B,K,N", [(5, 512, 1000), (7, 9216, 4096), (16, 2048, 1000)])
+def test_linear_fp32_out(ops, B, K, N):
+    torch.manual_seed(B + K + N)
+    x = torch.randn(B, K, device=DEV).half()
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).half()
+    b = torch.randn(N, device=DEV)
+    y = ops.linear(x, w, b, relu=False, out_f32=True)
+    assert y.dtype == torch.float32 and y.shape == (B, N)
+    ref = x.float() @ w.float().t() + b
+    _check(y, ref, tol=5e-3)
+
+
+def test_maxpool_and_avgpool(ops):
+    torch.manual_seed(3)
+    x = torch.randn(3, 112, 112, 64, device=DEV).half()
+    y = ops.maxpool2d(x, 3, 2, 1)
+    ref = F.max_pool2d(x.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    assert torch.equal(y.float(), ref)
+    x2 = torch.randn(2, 13, 13, 256, device=DEV).half()
+    y2 = ops.maxpool2d(x2, 3, 2, 0)
+    ref2 = F.max_pool2d(x2.float().permute(0, 3, 1, 2), 3, 2, 0).permute(0, 2, 3, 1)
+    assert torch.equal(y2.float(), ref2)
+    x3 = torch.randn(4, 7, 7, 512, device=DEV).half()
+    a = ops.global_avgpool(x3)
+    _check(a, x3.float().mean(dim=(1, 2)), tol=2e-3)
+
+
+def test_preprocess_and_resize_crop(ops):
+    from idunno.models.reference import preprocess_u8
+
+    torch.manual_seed(4)
+    img = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device=DEV)
+    y = ops.preprocess(img)
+    ref = preprocess_u8(img).permute(0, 2, 3, 1)
+    assert y.shape == (2, 224, 224, 4)
+    assert (y[..., :3].float() - ref).abs().max().item() < 5e-3
+    assert y[..., 3].abs().max().item() == 0
+    big = torch.randint(0, 256, (2, 300, 400, 3), dtype=torch.uint8, device=DEV)
+    z = ops.resize_crop(big, 256, 224)
+    assert z.shape == (2, 224, 224, 4)
+    # reference: bilinear (align_corners=False, no antialias) + centre crop
+    f = big.permute(0, 3, 1, 2).float()
+    r = F.interpolate(f, size=(256, 341), mode="bilinear", align_corners=False)
+    top, left = (256 - 224 + 1) // 2, (341 - 224 + 1) // 2
+    r = r[:, :, top:top + 224, left:left + 224].clamp(0, 255)
+    mean = torch.tensor([0.485, 0.456, 0.406], device=DEV).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225], device=DEV).view(1, 3, 1, 1)
+    r = ((r / 255 - mean) / std).permute(0, 2, 3, 1)
+    assert (z[..., :3].float() - r).abs().max().item() < 2e-2
+
+
+def test_softmax_top1(ops):
+    torch.manual_seed(5)
+    logits = torch.randn(37, 1000, device=DEV) * 3
+    logits[3, 10] = logits[3, 20] = 100.0  # tie -> lowest index
+    cls, prob = ops.softmax_top1(logits)
+    p = torch.softmax(logits, dim=1)
+    v, i = p.max(dim=1)
+    assert torch.equal(cls.long(), i)
+    assert cls[3].item() == 10
+    assert torch.allclose(prob, v, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["resnet18", "alexnet", "resnet50"])
+def test_model_end_to_end_vs_fp32_oracle(ops, name):
+    from idunno.models import HipRunner, compile_model
+    from idunno.models import reference as ref
+
+    m = ref.build(name, seed=7, randomize_bn=True)
+    prog = compile_model(m, name)
+    runner = HipRunner(prog)
+    torch.manual_seed(8)
+    img = torch.randint(0, 256, (8, 224, 224, 3), dtype=torch.uint8, device=DEV)
+    logits = runner.logits(img)
+    with torch.no_grad():
+        r = m.to(DEV)(ref.preprocess_u8(img))
+    scale = r.abs().max().item()
+    err = (logits - r).abs().max().item()
+    assert err < 0.03 * scale, f"{name}: logits err {err} vs scale {scale}"
+    cls, prob = runner.forward(img)
+    agree = (cls.long() == r.argmax(1)).float().mean().item()
+    assert agree >= 0.85, f"top-1 agreement {agree}"
+
+
+def test_hipgraph_replay_matches_eager(ops):
+    from idunno.models import HipRunner, build_program
+
+    runner = HipRunner(build_program("resnet18", seed=3))
+    torch.manual_seed(9)
+    img = torch.randint(0, 256, (16, 224, 224, 3), dtype=torch.uint8, device=DEV)
+    c0, p0 = runner.forward(img)
+    sin, run = runner.capture(16)
+    sin.copy_(img)
+    c1, p1 = run()
+    torch.cuda.synchronize()
+    assert torch.equal(c0, c1)
+    assert torch.allclose(p0, p1)

@@ -1,0 +1,44 @@
+"""BN folding + MFMA weight packing, checked on CPU by re-running the packed
+program with fp32 torch ops (idunno.models.packed.emulate)."""
+import pytest
+import torch
+
+from idunno.models import packed
+from idunno.models import reference as ref
+
+
+@pytest.mark.parametrize("name", ["resnet18", "alexnet", "resnet50"])
+def test_packed_program_matches_reference(name):
+    m = ref.build(name, seed=1, randomize_bn=True)
+    p = packed.compile_model(m, name)
+    torch.manual_seed(0)
+    img = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        r = m(ref.preprocess_u8(img))
+    e = packed.emulate(p, img)
+    assert (r - e).abs().max().item() < 2e-3 * r.abs().max().item()
+    assert torch.equal(r.argmax(1), e.argmax(1))
+
+
+def test_pack_unpack_roundtrip_small_and_big():
+    for shape in [(64, 3, 7, 7), (64, 3, 11, 11), (128, 64, 3, 3), (256, 128, 1, 1)]:
+        w = torch.randn(*shape)
+        pw, small = packed.pack_conv_weight(w)
+        c = packed.Conv(pw, torch.zeros(shape[0]), shape[1], shape[0], shape[2], shape[3], 1, 0, False, small)
+        assert small == (shape[1] == 3)
+        assert torch.equal(packed.unpack_conv_weight(c), w.half().float())
+    assert packed.pack_conv_weight(torch.randn(64, 3, 7, 7))[0].shape == (64, 7 * 32)
+    assert packed.pack_conv_weight(torch.randn(64, 3, 11, 11))[0].shape == (64, 11 * 64)
+
+
+def test_flops():
+    p = packed.build_program("resnet18")
+    assert abs(packed.program_flops(p) / 1e9 - 3.63) < 0.02
+    p = packed.build_program("alexnet")
+    assert abs(packed.program_flops(p) / 1e9 - 1.43) < 0.02
+
+
+def test_alias():
+    assert ref.canonical("resnet") == "resnet18"
+    with pytest.raises(ValueError):
+        ref.canonical("vgg")
