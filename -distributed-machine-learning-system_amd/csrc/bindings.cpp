@@ -160,6 +160,14 @@ std::vector<torch::Tensor> softmax_top1(torch::Tensor logits) {
   return {cls, prob};
 }
 
+torch::Tensor synth_images(int64_t seed, int64_t start, int64_t n, int64_t hw, torch::Device dev) {
+  TORCH_CHECK(dev.is_cuda(), "synth_images needs a GPU device");
+  TORCH_CHECK(n >= 0 && start >= 0 && (hw * hw * 3) % 8 == 0, "bad synth_images args");
+  auto out = torch::empty({n, hw, hw, 3}, torch::TensorOptions().dtype(torch::kUInt8).device(dev));
+  if (n) synth_images_launch(out.data_ptr<uint8_t>(), (uint64_t)seed, start, n, hw * hw * 3, cur_stream());
+  return out;
+}
+
 int64_t pick_tile(int64_t M, int64_t Cout) { return conv_pick_tile((int)M, (int)Cout); }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -172,5 +180,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool2d_nhwc", &maxpool2d_nhwc, "NHWC max pool");
   m.def("global_avgpool_nhwc", &global_avgpool_nhwc, "NHWC global average pool");
   m.def("softmax_top1", &softmax_top1, "fused row softmax + argmax");
+  m.def("synth_images", &synth_images, "deterministic synthetic uint8 images [n,hw,hw,3]");
   m.def("pick_tile", &pick_tile, "tile id the conv heuristic picks for (M, Cout)");
 }

@@ -32,6 +32,8 @@ void resize_crop_launch(const uint8_t* img, half_t* out, int B, int Hi, int Wi, 
 void maxpool_launch(const half_t* x, half_t* y, int B, int H, int W, int C, int Ho, int Wo, int k,
                     int s, int pad, hipStream_t st);
 void avgpool_launch(const half_t* x, half_t* y, int B, int HW, int C, hipStream_t st);
+void synth_images_launch(uint8_t* out, uint64_t seed, long start, long n, long bytes_per_img,
+                         hipStream_t st);
 void softmax_top1_launch(const float* logits, int ld, int N, int rows, int* cls, float* prob,
                          hipStream_t st);
 

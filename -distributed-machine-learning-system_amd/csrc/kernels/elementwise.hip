@@ -191,4 +191,34 @@ void softmax_top1_launch(const float* logits, int ld, int N, int rows, int* cls,
                      prob);
 }
 
+// Deterministic synthetic images: byte group g (8 bytes) of image `idx` is the
+// little-endian splitmix64 hash of (seed << 32) ^ (idx * 18816 + g), where
+// 18816 = 224*224*3 / 8.  The CPU generator (idunno.runtime.data) computes the
+// same function with numpy, so any worker (GPU or CPU) produces bit-identical
+// image `idx` without moving bytes - the synthetic stand-in for the
+// reference's ./<model>/test_<i>.JPEG files.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ void synth_images_kernel(uint64_t* __restrict__ out, uint64_t seed, long start, long n,
+                                    long groups_per_img) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * groups_per_img) return;
+  const long i = t / groups_per_img, g = t - i * groups_per_img;
+  out[t] = splitmix64((seed << 32) ^ (uint64_t)((start + i) * groups_per_img + g));
+}
+
+void synth_images_launch(uint8_t* out, uint64_t seed, long start, long n, long bytes_per_img,
+                         hipStream_t st) {
+  const long gpi = bytes_per_img / 8;
+  const long total = n * gpi;
+  const int bs = 256;
+  hipLaunchKernelGGL(synth_images_kernel, dim3((unsigned)((total + bs - 1) / bs)), dim3(bs), 0, st,
+                     reinterpret_cast<uint64_t*>(out), seed, start, n, gpi);
+}
+
 }  // namespace idunno

@@ -10,7 +10,7 @@ from ._ext import available, load, so_path
 
 __all__ = [
     "available", "load", "so_path", "conv2d", "linear", "preprocess", "resize_crop",
-    "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile",
+    "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile", "synth_images",
 ]
 
 
@@ -53,3 +53,11 @@ def softmax_top1(logits):
 
 def pick_tile(m: int, cout: int) -> int:
     return int(load().pick_tile(m, cout))
+
+
+def synth_images(seed: int, start: int, n: int, device, hw: int = 224):
+    """Deterministic synthetic uint8 images [n, hw, hw, 3] generated on the GPU
+    (bit-identical to ``idunno.runtime.data.synth_images_cpu``)."""
+    import torch
+
+    return load().synth_images(int(seed), int(start), int(n), int(hw), torch.device(device))

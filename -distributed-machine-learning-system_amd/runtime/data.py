@@ -1,0 +1,158 @@
+"""Image data path: where a worker's chunk of images comes from.
+
+The reference worker reads ``./<model>/test_<i>.JPEG`` from local disk, one
+PIL image per forward, and overwrites non-RGB files in place
+(alexnet_resnet.py:24, 48-54).  Here a chunk ``[start, end]``
+is served as one uint8 tensor ``[n, 224, 224, 3]`` already resident on the
+worker's device:
+
+  * ``SyntheticSource``  deterministic per-index images (bit-identical on CPU
+    numpy and on the GPU kernel ``ops.synth_images``), so any worker produces
+    the same image ``i`` and results do not depend on placement;
+  * ``SdfsSource``       images stored in SDFS as raw uint8 shards
+    (``images/shard_<k>``, ``shard_images`` per shard).  A worker reads the
+    shards covering its chunk from its own replica when it holds one (else
+    from a replica over the control plane) and keeps them in an HBM cache, so
+    each shard crosses PCIe once: ``HbmStager`` copies through a pinned host
+    buffer with a non-blocking H2D on a dedicated side stream
+    (hipMemcpyAsync), overlapping compute on the default stream.
+"""
+from __future__ import annotations
+
+import threading
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+HW = 224
+IMG_BYTES = HW * HW * 3
+GROUPS = IMG_BYTES // 8
+
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+
+
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = x + _GOLD
+        x = (x ^ (x >> np.uint64(30))) * _M1
+        x = (x ^ (x >> np.uint64(27))) * _M2
+        return x ^ (x >> np.uint64(31))
+
+
+def synth_images_cpu(seed: int, start: int, n: int) -> np.ndarray:
+    """uint8 [n, 224, 224, 3]; same bytes as the GPU kernel."""
+    idx = (np.arange(n, dtype=np.uint64)[:, None] + np.uint64(start)) * np.uint64(GROUPS) + \
+        np.arange(GROUPS, dtype=np.uint64)[None, :]
+    h = _splitmix64((np.uint64(seed) << np.uint64(32)) ^ idx)
+    return h.astype("<u8").view(np.uint8).reshape(n, HW, HW, 3)
+
+
+class SyntheticSource:
+    def __init__(self, seed: int, device: torch.device | str = "cpu"):
+        self.seed = int(seed)
+        self.device = torch.device(device)
+
+    def get(self, start: int, end: int) -> torch.Tensor:
+        n = end - start + 1
+        if self.device.type == "cuda":
+            from .. import ops
+
+            return ops.synth_images(self.seed, start, n, self.device)
+        return torch.from_numpy(synth_images_cpu(self.seed, start, n))
+
+
+class HbmStager:
+    """Host -> HBM staging through pinned memory on a side stream."""
+
+    def __init__(self, device: torch.device, pinned_bytes: int = 64 << 20):
+        self.device = torch.device(device)
+        self.gpu = self.device.type == "cuda"
+        self.stream = torch.cuda.Stream(device=self.device) if self.gpu else None
+        self.pinned = torch.empty(pinned_bytes, dtype=torch.uint8, pin_memory=self.gpu)
+        self.lock = threading.Lock()
+
+    def stage(self, data: bytes | np.ndarray, shape: tuple) -> torch.Tensor:
+        """Copy host bytes to a new device tensor of ``shape`` (uint8)."""
+        src = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) \
+            else np.ascontiguousarray(data).reshape(-1).view(np.uint8)
+        if not self.gpu:
+            return torch.from_numpy(src.copy()).view(*shape)
+        out = torch.empty(src.size, dtype=torch.uint8, device=self.device)
+        step = self.pinned.numel()
+        with self.lock:
+            for off in range(0, src.size, step):
+                n = min(step, src.size - off)
+                # wait until the previous async copy out of `pinned` has drained
+                self.stream.synchronize()
+                self.pinned[:n].numpy()[:] = src[off:off + n]
+                with torch.cuda.stream(self.stream):
+                    out[off:off + n].copy_(self.pinned[:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        torch.cuda.current_stream(self.device).wait_event(ev)
+        return out.view(*shape)
+
+
+def shard_name(k: int) -> str:
+    return f"images/shard_{k:05d}"
+
+
+class SdfsSource:
+    """Images from SDFS shards, cached in HBM (LRU by bytes)."""
+
+    def __init__(self, sdfs, device, shard_images: int = 500, cache_bytes: int = 32 << 30):
+        self.sdfs = sdfs
+        self.device = torch.device(device)
+        self.S = int(shard_images)
+        self.stager = HbmStager(self.device)
+        self.cache: OrderedDict[int, torch.Tensor] = OrderedDict()
+        self.cache_bytes = cache_bytes
+        self.lock = threading.Lock()
+        self.fetches = 0
+
+    def _shard(self, k: int) -> torch.Tensor:
+        with self.lock:
+            t = self.cache.get(k)
+            if t is not None:
+                self.cache.move_to_end(k)
+                return t
+        data = self.sdfs.get_bytes(shard_name(k))
+        if data is None:
+            raise KeyError(f"missing SDFS shard {shard_name(k)}")
+        n = len(data) // IMG_BYTES
+        t = self.stager.stage(data, (n, HW, HW, 3))
+        with self.lock:
+            self.fetches += 1
+            self.cache[k] = t
+            tot = sum(v.numel() for v in self.cache.values())
+            while tot > self.cache_bytes and len(self.cache) > 1:
+                _, old = self.cache.popitem(last=False)
+                tot -= old.numel()
+        return t
+
+    def get(self, start: int, end: int) -> torch.Tensor:
+        parts = []
+        i = start
+        while i <= end:
+            k = i // self.S
+            sh = self._shard(k)
+            lo = i - k * self.S
+            hi = min(end - k * self.S, sh.shape[0] - 1)
+            if hi < lo:
+                raise KeyError(f"image {i} beyond shard {k}")
+            parts.append(sh[lo:hi + 1])
+            i = k * self.S + hi + 1
+        return parts[0] if len(parts) == 1 else torch.cat(parts, 0)
+
+
+def put_synthetic_dataset(sdfs, n_images: int, seed: int, shard_images: int = 500) -> int:
+    """Upload a deterministic synthetic dataset into SDFS as uint8 shards."""
+    k = 0
+    for s in range(0, n_images, shard_images):
+        n = min(shard_images, n_images - s)
+        sdfs.put_bytes(synth_images_cpu(seed, s, n).tobytes(), shard_name(k))
+        k += 1
+    return k

@@ -1,0 +1,131 @@
+"""Inference executors (layer L4; reference ``alexnet_resnet.deeplearning``,
+alexnet_resnet.py:12-92).
+
+The reference reloads the model from torch.hub on every chunk and runs batch-1
+forwards (A6).  An executor here holds each model resident (weights built
+once, BN-folded, in HBM) and runs the whole chunk as one batch:
+
+  * ``HipExecutor``   the MI355X path: HIP kernels, one hipGraph per
+                      (model, batch) replayed for every chunk;
+  * ``TorchExecutor`` fp32 PyTorch reference modules (CPU hosts, tests);
+  * ``FakeExecutor``  deterministic answers from the image index, no compute
+                      (control-plane tests).
+All return ``(cls int32 [n], prob float32 [n])`` numpy arrays.
+"""
+from __future__ import annotations
+
+import threading
+import time
+
+import numpy as np
+import torch
+
+from ..models import reference as ref
+
+
+class Executor:
+    device = torch.device("cpu")
+
+    def run(self, model: str, images: torch.Tensor | None, start: int, end: int):
+        raise NotImplementedError
+
+    def warmup(self, model: str, batch: int) -> None:
+        pass
+
+
+class FakeExecutor(Executor):
+    def __init__(self, delay_per_image_s: float = 0.0):
+        self.delay = delay_per_image_s
+        self.calls = 0
+
+    def run(self, model, images, start, end):
+        self.calls += 1
+        n = end - start + 1
+        if self.delay:
+            time.sleep(self.delay * n)
+        idx = np.arange(start, end + 1, dtype=np.int64)
+        salt = 7 if ref.canonical(model) == "alexnet" else 13
+        return ((idx * 7919 + salt) % 1000).astype(np.int32), np.full(n, 0.5, dtype=np.float32)
+
+
+class TorchExecutor(Executor):
+    def __init__(self, device="cpu", seed: int = 0):
+        self.device = torch.device(device)
+        self.seed = seed
+        self.models: dict[str, torch.nn.Module] = {}
+        self.lock = threading.Lock()
+
+    def _model(self, name):
+        name = ref.canonical(name)
+        with self.lock:
+            m = self.models.get(name)
+            if m is None:
+                m = ref.build(name, seed=self.seed).to(self.device)
+                self.models[name] = m
+        return m
+
+    @torch.no_grad()
+    def run(self, model, images, start, end):
+        m = self._model(model)
+        x = ref.preprocess_u8(images.to(self.device))
+        p = torch.softmax(m(x), dim=1)
+        prob, cls = p.max(dim=1)
+        return cls.to(torch.int32).cpu().numpy(), prob.float().cpu().numpy()
+
+
+class HipExecutor(Executor):
+    """gfx950 kernels; per-(model, batch) hipGraphs, weights resident in HBM."""
+
+    def __init__(self, device="cuda", seed: int = 0, use_graphs: bool = True, max_graphs: int = 16):
+        from .. import ops
+        from ..models import HipRunner, build_program
+
+        ops.load()  # loud failure if the extension is missing on a GPU host
+        self.device = torch.device(device)
+        self.seed = seed
+        self.use_graphs = use_graphs
+        self.max_graphs = max_graphs
+        self._HipRunner, self._build = HipRunner, build_program
+        self.runners: dict[str, object] = {}
+        self.lock = threading.Lock()
+
+    def runner(self, name):
+        name = ref.canonical(name)
+        with self.lock:
+            r = self.runners.get(name)
+            if r is None:
+                with torch.cuda.device(self.device):
+                    r = self._HipRunner(self._build(name, seed=self.seed), self.device)
+                self.runners[name] = r
+        return r
+
+    def warmup(self, model, batch):
+        if self.use_graphs:
+            with torch.cuda.device(self.device):
+                self.runner(model).capture(batch)
+
+    def run(self, model, images, start, end):
+        r = self.runner(model)
+        n = images.shape[0]
+        with torch.cuda.device(self.device):
+            if self.use_graphs and len(r._graphs) < self.max_graphs or n in r._graphs:
+                sin, replay = r.capture(n)
+                sin.copy_(images)
+                cls, prob = replay()
+            else:
+                cls, prob = r.forward(images.contiguous())
+            out = torch.stack([cls, prob.view(torch.int32)], dim=1).cpu()
+        return out[:, 0].numpy().copy(), out[:, 1].contiguous().view(torch.float32).numpy().copy()
+
+
+def make_executor(kind: str, device=None, seed: int = 0) -> Executor:
+    kind = kind.lower()
+    if kind == "auto":
+        kind = "hip" if torch.cuda.is_available() else "torch"
+    if kind == "hip":
+        return HipExecutor(device or "cuda", seed=seed)
+    if kind == "torch":
+        return TorchExecutor(device or "cpu", seed=seed)
+    if kind == "fake":
+        return FakeExecutor()
+    raise ValueError(f"unknown executor {kind!r}")

@@ -266,15 +266,18 @@ class JobState:
             return str(dict(self.working_vm_set))
 
     # -- replication (hot standby) --------------------------------------------------
-    def snapshot(self) -> dict:
-        """Structured, JSON/msgpack-able snapshot (fix A12: no raw str() dumps)."""
+    def snapshot(self, include_results: bool = True) -> dict:
+        """Structured, JSON/msgpack-able snapshot (fix A12: no raw str() dumps).
+
+        The coordinator's periodic push to the standby omits results: workers
+        send every RESULT to the standby directly."""
         with self.lock:
             return {
                 "seq": self.seq,
                 "worker_set": [[list(k), [list(e) for e in v]] for k, v in self.worker_set.items()],
                 "working_vm_set": {w: [list(c) for c in v] for w, v in self.working_vm_set.items()},
-                "results": {k: [[c.start, c.end, c.cls.tolist(), c.prob.tolist(), c.worker] for c in v]
-                            for k, v in self.results.items()},
+                "results": ({k: [[c.start, c.end, c.cls.tolist(), c.prob.tolist(), c.worker] for c in v]
+                             for k, v in self.results.items()} if include_results else None),
                 "finished_images": dict(self.finished_images),
                 "finished_queries": dict(self.finished_queries),
                 "next_qnum": dict(self.next_qnum),
@@ -282,24 +285,45 @@ class JobState:
                 "submit": [[list(k), t] for k, t in self.query_submit_time.items()],
             }
 
-    def restore(self, snap: dict) -> None:
+    def restore(self, snap: dict, keep_results: bool = False) -> None:
+        """Adopt a snapshot.  With ``keep_results`` (standby mirror) the locally
+        received results and counters are kept and chunks already answered
+        stay marked 'f' even if the snapshot predates their RESULT."""
         with self.lock:
-            self.seq = snap["seq"]
+            if snap["seq"] < self.seq and not keep_results:
+                return
+            self.seq = max(self.seq, snap["seq"])
             self.worker_set = defaultdict(list)
             for k, v in snap["worker_set"]:
                 self.worker_set[(k[0], k[1])] = [tuple(e) for e in v]
             self.working_vm_set = defaultdict(list, {w: [tuple(c) for c in v]
                                                      for w, v in snap["working_vm_set"].items()})
-            self.results = defaultdict(list)
-            self._done_keys = set()
-            for k, v in snap["results"].items():
-                model, q = k.rsplit(" ", 1)
-                qn = int(q) if q.lstrip("-").isdigit() else q
-                for s, e, c, p, w in v:
-                    self.results[k].append(ChunkResult(s, e, np.asarray(c, np.int32), np.asarray(p, np.float32), w))
-                    self._done_keys.add((model, qn, s, e))
-            self.finished_images = defaultdict(int, snap["finished_images"])
-            self.finished_queries = defaultdict(int, snap["finished_queries"])
-            self.next_qnum = defaultdict(int, snap["next_qnum"])
-            self.query_processing_time_meta = dict(snap["meta"])
-            self.query_submit_time = {(k[0], k[1]): t for k, t in snap.get("submit", [])}
+            if snap.get("results") is not None:
+                self.results = defaultdict(list)
+                self._done_keys = set()
+                for k, v in snap["results"].items():
+                    model, q = k.rsplit(" ", 1)
+                    qn = int(q) if q.lstrip("-").isdigit() else q
+                    for s, e, c, p, w in v:
+                        self.results[k].append(ChunkResult(s, e, np.asarray(c, np.int32),
+                                                           np.asarray(p, np.float32), w))
+                        self._done_keys.add((model, qn, s, e))
+            if not keep_results:
+                self.finished_images = defaultdict(int, snap["finished_images"])
+                self.finished_queries = defaultdict(int, snap["finished_queries"])
+            # reconcile: chunks we already hold a result for are finished
+            for (model, q), ents in self.worker_set.items():
+                for i, (w, s, e, st, t0, t1) in enumerate(ents):
+                    if st == "w" and (model, q, s, e) in self._done_keys:
+                        ents[i] = (w, s, e, "f", t0, t1)
+                        try:
+                            self.working_vm_set[w].remove((model, q, s, e))
+                        except ValueError:
+                            pass
+            for w in [w for w, v in self.working_vm_set.items() if not v]:
+                self.working_vm_set.pop(w)
+            for m, n in snap["next_qnum"].items():
+                self.next_qnum[m] = max(self.next_qnum.get(m, 0), n)
+            self.query_processing_time_meta.update(snap["meta"])
+            for k, t in snap.get("submit", []):
+                self.query_submit_time.setdefault((k[0], k[1]), t)

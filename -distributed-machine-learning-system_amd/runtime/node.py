@@ -1,0 +1,378 @@
+"""One cluster node = one rank process (one MI355X GPU) — layers L2-L6.
+
+Re-design of the reference's monolithic ``Server`` class
+(mp4_machinelearning.py:114-1334).  Every node runs the same program; roles
+come from the membership state, not from host names:
+
+  * worker       runs JOB chunks one at a time on its executor and sends each
+                 RESULT to the acting coordinator *and* the hot standby
+                 (instead of broadcasting to all 10 hosts, :603-613);
+  * coordinator  (the acting master) accepts INFERENCE queries, splits them
+                 with the fair-time scheduler, dispatches JOBs, ingests
+                 RESULTs into the job-state tables, re-dispatches the chunks of
+                 failed workers (:706-760), re-replicates SDFS files (:852-874)
+                 and pushes structured METADATA to the standby every second;
+  * hot standby  mirrors job state; when the coordinator's PINGs stop for
+                 ``failure_timeout_s`` it promotes itself (new epoch), takes
+                 over scheduling, re-dispatches chunks that were running on
+                 dead nodes and keeps serving queries (the reference's standby
+                 only ever ran whole queries locally, :592-613);
+  * client       the shell: ``inference`` submits queries to the coordinator
+                 with fallback to the standby (:947-969), ``c1/c2/c4/cq/cvm``
+                 query the coordinator's tables.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import queue
+import re
+import threading
+import time
+from logging.handlers import RotatingFileHandler
+
+import numpy as np
+
+from ..models.reference import canonical
+from .jobstate import JobState
+from .membership import Membership
+from .messages import Type
+from .scheduler import FairTimeScheduler
+from .sdfs import Sdfs
+from .transport import TransportError
+
+log = logging.getLogger("idunno.node")
+
+
+class Node:
+    def __init__(self, cfg, name: str, transport, executor, source=None, clock=time.time):
+        self.cfg = cfg
+        self.name = name
+        self.transport = transport
+        self.executor = executor
+        self.source = source
+        self.clock = clock
+        self.membership = Membership(name, cfg, transport, master=cfg.coordinator_name)
+        self.sdfs = Sdfs(self, os.path.join(cfg.store_root, name, "sdfs"))
+        self.state = JobState(batchsize=cfg.batch_size, clock=clock)
+        self.sched = FairTimeScheduler(budget=cfg.worker_budget)
+        self.jobs: queue.Queue = queue.Queue()
+        self.extra_delay_s = 0.0                   # fault injection: slow worker
+        self.standby = cfg.standby_name
+        self.alive_flag = True
+        self.meta_seq = -1
+        self.chunks_done = 0
+        self.logger = self._make_logger()
+        self._stop = threading.Event()
+        self._threads: list[threading.Thread] = []
+        self.promotions = 0
+        self.membership.on_failure.append(self._on_node_failure)
+        self.membership.on_master_failure.append(self._on_master_failure)
+        self.membership.on_master_change.append(self._on_master_change)
+
+    # -- infra --------------------------------------------------------------------
+    def _make_logger(self):
+        lg = logging.getLogger(f"idunno.node.{self.name}")
+        lg.setLevel(logging.DEBUG)
+        self.log_path = None
+        if self.cfg.log_dir:
+            os.makedirs(self.cfg.log_dir, exist_ok=True)
+            self.log_path = os.path.join(self.cfg.log_dir, f"{self.name}.log")
+            for h in list(lg.handlers):            # a previous node of this name in-process
+                if isinstance(h, RotatingFileHandler) and h.baseFilename != os.path.abspath(self.log_path):
+                    lg.removeHandler(h)
+                    h.close()
+            if not any(isinstance(h, RotatingFileHandler) for h in lg.handlers):
+                h = RotatingFileHandler(self.log_path, maxBytes=100 << 20, backupCount=1)
+                h.setFormatter(logging.Formatter("%(asctime)s %(levelname)s %(message)s"))
+                lg.addHandler(h)
+        return lg
+
+    @property
+    def is_coordinator(self) -> bool:
+        return self.membership.is_master()
+
+    def start(self, join: bool = True) -> "Node":
+        self.transport.start(self.handle)
+        self.membership.start()
+        for fn, nm in ((self._worker_loop, "worker"), (self._metadata_loop, "meta"),
+                       (self._straggler_loop, "straggler")):
+            th = threading.Thread(target=fn, name=f"{self.name}-{nm}", daemon=True)
+            th.start()
+            self._threads.append(th)
+        if join:
+            self.join_with_retry()
+        self.logger.info("node %s started (master=%s)", self.name, self.membership.master)
+        return self
+
+    def join_with_retry(self, timeout: float = 15.0) -> bool:
+        end = time.monotonic() + timeout
+        delay = 0.05
+        while not self._stop.is_set():
+            if self.membership.join(timeout=2.0):
+                return True
+            if time.monotonic() > end:
+                return False
+            time.sleep(delay)
+            delay = min(delay * 2, 1.0)
+        return False
+
+    def stop(self) -> None:
+        self._stop.set()
+        self.alive_flag = False
+        self.membership.stop()
+        self.jobs.put(None)
+        self.transport.close()
+
+    # -- dispatch of incoming messages ---------------------------------------------------
+    def handle(self, msg: dict):
+        if not self.alive_flag:
+            return None
+        t = msg["t"]
+        if t in (Type.PING, Type.PONG, Type.JOIN, Type.LEAVE, Type.PROMOTE):
+            return self.membership.handle(msg)
+        if t in (Type.REPLICATE, Type.FETCH, Type.UNLINK, Type.PUT, Type.GET, Type.LS, Type.DELETE,
+                 Type.GET_VERSIONS):
+            return self.sdfs.handle(msg)
+        if t == Type.INFERENCE:
+            return self.submit_query(msg["model"], int(msg["start"]), int(msg["end"]),
+                                     client=msg.get("src"))
+        if t == Type.JOB:
+            self.jobs.put(msg)
+            return {"ok": True}
+        if t == Type.RESULT:
+            self._ingest_result(msg)
+            return None
+        if t == Type.METADATA:
+            self._apply_metadata(msg)
+            return None
+        if t == Type.STATS:
+            return self._stats(msg.get("view", "c1"))
+        if t == Type.GREP:
+            return {"ok": True, "lines": self.local_grep(msg["pattern"])}
+        if t == Type.KILL:
+            if msg.get("mode") == "delay":
+                self.extra_delay_s = float(msg.get("seconds", 1.0))
+                return {"ok": True}
+            threading.Thread(target=self.crash, daemon=True).start()
+            return None
+        return {"ok": False, "error": f"unknown message {t}"}
+
+    def crash(self) -> None:
+        """Fault injection: stop answering everything (like a killed VM)."""
+        self.logger.warning("%s crashing (fault injection)", self.name)
+        self.stop()
+
+    # -- coordinator -------------------------------------------------------------------
+    def submit_query(self, model: str, start: int, end: int, client: str | None = None) -> dict:
+        if not self.is_coordinator:
+            if self.name == self.standby and not self.membership.is_alive(self.membership.master):
+                self._promote("query arrived while coordinator is down")
+            else:
+                try:
+                    return self.transport.request(self.membership.master,
+                                                  {"t": Type.INFERENCE, "model": model, "start": start,
+                                                   "end": end}, self.cfg.rpc_timeout_s)
+                except TransportError:
+                    if self.name != self.standby:
+                        return {"ok": False, "error": "coordinator unreachable"}
+                    self._promote("coordinator unreachable on forward")
+        model = canonical(model)
+        if end < start:
+            return {"ok": False, "error": "empty range"}
+        alive = self.membership.alive()
+        qnum = self.state.new_query_number(model)
+        with self.state.lock:
+            busy = {m for (m, _q, _w, _s, _e, _t) in self.state.pending()}
+        self.sched.active_jobs = busy | {model}
+        plan = self.sched.assign(model, start, end, alive)
+        now = self.clock()
+        self.state.assign(model, qnum, plan, now)
+        for w, s, e in plan:
+            self._send_job(w, model, qnum, s, e)
+        self.logger.info("query %s %s [%d,%d] -> %s", model, qnum, start, end, plan)
+        return {"ok": True, "qnum": qnum, "plan": [list(p) for p in plan]}
+
+    def _send_job(self, worker: str, model: str, qnum, s: int, e: int) -> bool:
+        msg = {"t": Type.JOB, "model": model, "qnum": qnum, "start": s, "end": e,
+               "epoch": self.membership.epoch}
+        if worker == self.name:
+            msg["src"] = self.name
+            self.jobs.put(msg)
+            return True
+        ok = self.transport.send(worker, msg)
+        if not ok:
+            self.logger.warning("JOB to %s failed; will re-dispatch on failure detection", worker)
+        return ok
+
+    def _ingest_result(self, msg: dict) -> None:
+        cls = np.frombuffer(msg["cls"], dtype=np.int32)
+        prob = np.frombuffer(msg["prob"], dtype=np.float32)
+        new = self.state.record_result(msg["model"], msg["qnum"], msg["worker"], msg["start"], msg["end"],
+                                       cls, prob)
+        if new and self.is_coordinator:
+            n = msg["end"] - msg["start"] + 1
+            self.sched.observe(msg["model"], msg.get("compute_s", 0.0) / n * self.cfg.batch_for(msg["model"]))
+
+    def pick_replacement(self, failed: str, alive: list[str]) -> str | None:
+        """Least-loaded live worker, ties broken by ring order after the failed node."""
+        cands = [a for a in alive if a != failed]
+        if not cands:
+            return None
+        ring = sorted(set(cands) | {failed})
+        i = ring.index(failed)
+        order = ring[i + 1:] + ring[:i]
+        load = {w: len(self.state.chunks_of(w)) for w in order}
+        return min(order, key=lambda w: (load[w], order.index(w)))
+
+    def _on_node_failure(self, node: str) -> None:
+        if not self.is_coordinator:
+            return
+        t0 = time.monotonic()
+        try:
+            moves = self.sdfs.rereplicate(node)
+        except Exception:  # noqa: BLE001
+            self.logger.exception("re-replication failed")
+            moves = []
+        chunks = self.state.chunks_of(node)
+        alive = self.membership.alive()
+        for ch in chunks:
+            model, qnum, s, e = ch
+            w = self.pick_replacement(node, alive)
+            if w is None:
+                self.logger.error("no live worker for %s", ch)
+                continue
+            self.state.reassign(node, w, ch)
+            self._send_job(w, model, qnum, s, e)
+        self.logger.warning("failure of %s: re-dispatched %d chunks, re-replicated %d files in %.3fs",
+                            node, len(chunks), len(moves), time.monotonic() - t0)
+
+    def _straggler_loop(self) -> None:
+        """Resend chunks running longer than straggler_timeout_s (A7 fixed; off by default)."""
+        while not self._stop.wait(max(0.05, self.cfg.straggler_timeout_s / 4)):
+            if not (self.cfg.straggler_resend and self.is_coordinator):
+                continue
+            now = self.clock()
+            for model, qnum, w, s, e, t0 in self.state.pending():
+                if now - t0 > self.cfg.straggler_timeout_s:
+                    alt = self.pick_replacement(w, self.membership.alive())
+                    if alt:
+                        self.logger.warning("straggler %s %s [%d,%d] on %s -> %s", model, qnum, s, e, w, alt)
+                        self.state.reassign(w, alt, (model, qnum, s, e))
+                        self._send_job(alt, model, qnum, s, e)
+
+    # -- standby replication ------------------------------------------------------------
+    def _metadata_loop(self) -> None:
+        while not self._stop.wait(self.cfg.metadata_period_s):
+            if not self.is_coordinator or self.standby == self.name:
+                continue
+            self.push_metadata()
+
+    def push_metadata(self) -> bool:
+        snap = {"t": Type.METADATA, "seq": self.state.seq, "epoch": self.membership.epoch,
+                "jobs": self.state.snapshot(include_results=False), "sdfs": self.sdfs.snapshot(),
+                "avg_time": dict(self.sched.avg_time)}
+        return self.transport.send(self.standby, snap)
+
+    def _apply_metadata(self, msg: dict) -> None:
+        if self.is_coordinator:
+            return
+        if msg.get("epoch", 0) < self.membership.epoch:
+            return
+        self.state.restore(msg["jobs"], keep_results=True)
+        self.sdfs.restore(msg["sdfs"])
+        self.sched.avg_time.update(msg.get("avg_time", {}))
+        self.meta_seq = msg.get("seq", 0)
+
+    def _on_master_failure(self, old: str) -> None:
+        if self.name == self.standby:
+            self._promote(f"no heartbeat from {old}")
+
+    def _promote(self, why: str) -> None:
+        if self.is_coordinator:
+            return
+        old = self.membership.master
+        epoch = self.membership.epoch + 1
+        t0 = time.monotonic()
+        self.logger.warning("%s promoting to coordinator (epoch %d): %s", self.name, epoch, why)
+        self.membership.become_master(epoch)
+        self.promotions += 1
+        for n in self.membership.alive():
+            if n not in (self.name, old):
+                self.transport.send(n, {"t": Type.PROMOTE, "epoch": epoch})
+        # the old coordinator is gone: its own chunks and replicas must move
+        self.membership.mark_failed(old)
+        # chunks that were dispatched to nodes that are already dead
+        alive = set(self.membership.alive())
+        for model, qnum, w, s, e, _t in self.state.pending():
+            if w not in alive:
+                nw = self.pick_replacement(w, sorted(alive))
+                if nw:
+                    self.state.reassign(w, nw, (model, qnum, s, e))
+                    self._send_job(nw, model, qnum, s, e)
+        self.logger.warning("promotion done in %.3fs", time.monotonic() - t0)
+
+    def _on_master_change(self, new: str, epoch: int) -> None:
+        self.logger.info("master is now %s (epoch %d)", new, epoch)
+
+    # -- worker ---------------------------------------------------------------------------
+    def _worker_loop(self) -> None:
+        while not self._stop.is_set():
+            msg = self.jobs.get()
+            if msg is None or self._stop.is_set():
+                return
+            try:
+                self.run_chunk(msg)
+            except Exception:  # noqa: BLE001
+                self.logger.exception("chunk failed: %s", {k: v for k, v in msg.items() if k != 'data'})
+
+    def run_chunk(self, msg: dict) -> None:
+        delay = self.cfg.worker_start_delay_s + self.extra_delay_s
+        if delay:
+            time.sleep(delay)
+        model, s, e = msg["model"], int(msg["start"]), int(msg["end"])
+        t0 = time.perf_counter()
+        imgs = self.source.get(s, e) if self.source is not None else None
+        cls, prob = self.executor.run(model, imgs, s, e)
+        dt = time.perf_counter() - t0
+        if not self.alive_flag:
+            return
+        res = {"t": Type.RESULT, "model": model, "qnum": msg["qnum"], "start": s, "end": e,
+               "worker": self.name, "cls": np.ascontiguousarray(cls, np.int32).tobytes(),
+               "prob": np.ascontiguousarray(prob, np.float32).tobytes(), "compute_s": dt,
+               "epoch": msg.get("epoch", 0)}
+        self.chunks_done += 1
+        targets = {self.membership.master, self.standby}
+        for dst in targets:
+            if dst == self.name:
+                self._ingest_result(dict(res, src=self.name))
+            else:
+                self.transport.send(dst, dict(res))
+
+    # -- views -----------------------------------------------------------------------------
+    def _stats(self, view: str) -> dict:
+        v = view.lower()
+        if v == "c1":
+            return {"ok": True, "text": self.state.c1()}
+        if v == "c2":
+            return {"ok": True, "text": self.state.c2()}
+        if v == "c4":
+            return {"ok": True, "results": self.state.inference_result_list()}
+        if v == "cq":
+            return {"ok": True, "text": self.state.cq()}
+        if v in ("cvm", "c5"):
+            return {"ok": True, "text": self.state.cvm()}
+        if v == "summary":
+            return {"ok": True, "done": {m: self.state.images_done(m) for m in self.state.models()},
+                    "pending": len(self.state.pending()),
+                    "latency": {m: list(v) for m, v in self.state.query_latency.items()},
+                    "finished_queries": dict(self.state.finished_queries)}
+        return {"ok": False, "error": f"unknown view {view}"}
+
+    def local_grep(self, pattern: str) -> list[str]:
+        """MP1 distributed-grep replacement: regex over this node's log."""
+        if not self.log_path or not os.path.exists(self.log_path):
+            return []
+        rx = re.compile(pattern)
+        with open(self.log_path, errors="replace") as f:
+            return [f"{self.name}: {ln.rstrip()}" for ln in f if rx.search(ln)]

@@ -1,0 +1,148 @@
+"""Unit tests of the control-plane building blocks (CPU, no GPU)."""
+import json
+import os
+import socket
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from idunno.config import ClusterConfig
+from idunno.runtime import messages as M
+from idunno.runtime.jobstate import JobState
+from idunno.runtime.sdfs import VERSION_DELIM, SdfsStore, ring_placement, stable_hash
+from idunno.runtime.transport import InMemoryNetwork, TcpTransport, TransportError, wait_for
+
+
+# -- framing ---------------------------------------------------------------------
+def test_frame_roundtrip_and_partial_reads():
+    msgs = [{"t": M.Type.RESULT, "cls": np.arange(5000, dtype=np.int32).tobytes(), "q": i} for i in range(3)]
+    stream = b"".join(M.encode(m) for m in msgs)
+    rd = M.FrameReader()
+    out = []
+    for i in range(0, len(stream), 777):           # arbitrary fragmentation
+        out += rd.feed(stream[i:i + 777])
+    assert [o["q"] for o in out] == [0, 1, 2]
+    assert np.frombuffer(out[2]["cls"], np.int32)[-1] == 4999  # > 4096 bytes: no truncation (A4)
+
+
+# -- transports -------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_tcp_request_reply_and_unreachable():
+    base = _free_port()
+    cfg = ClusterConfig(base_port=base, num_nodes=2)
+    a = TcpTransport("node00", cfg.address, cfg.address("node00"))
+    b = TcpTransport("node01", cfg.address, cfg.address("node01"))
+    a.start(lambda m: {"echo": m["x"] * 2})
+    b.start(lambda m: None)
+    try:
+        r = b.request("node00", {"t": "X", "x": 21}, timeout=2)
+        assert r["echo"] == 42 and r["src"] == "node00"
+        a.close()
+        with pytest.raises(TransportError):
+            b.request("node00", {"t": "X", "x": 1}, timeout=0.5)
+        # the peer is gone: within a couple of sends the refused reconnect is reported
+        assert wait_for(lambda: not b.send("node00", {"t": "X", "x": 1}), 2)
+    finally:
+        a.close()
+        b.close()
+
+
+def test_inmemory_faults():
+    net = InMemoryNetwork()
+    got = []
+    a, b = net.transport("a"), net.transport("b")
+    a.start(lambda m: None)
+    b.start(lambda m: got.append(m["i"]))
+    assert a.send("b", {"t": "X", "i": 1})
+    net.partition("a", "b")
+    assert a.send("b", {"t": "X", "i": 2})          # silently lost
+    net.heal()
+    net.crash("b")
+    assert not a.send("b", {"t": "X", "i": 3})      # refused
+    assert wait_for(lambda: got == [1], 1)
+
+
+# -- SDFS store / placement ----------------------------------------------------------
+def test_stable_placement():
+    ring = [f"node{i:02d}" for i in range(8)]
+    p1 = ring_placement("images/shard_00001", ring, 4)
+    assert p1 == ring_placement("images/shard_00001", ring, 4)   # stable across processes (A8)
+    assert len(set(p1)) == 4
+    assert stable_hash("a") == 3904355907                          # crc32
+
+
+def test_store_versions(tmp_path):
+    st = SdfsStore(str(tmp_path))
+    st.write("dir/f.txt", 1, b"a")
+    st.write("dir/f.txt", 2, b"bb")
+    assert st.versions("dir/f.txt") == [1, 2]
+    assert st.read("dir/f.txt") == b"bb" and st.read("dir/f.txt", 1) == b"a"
+    assert st.files() == ["dir/f.txt"]
+    assert st.unlink("dir/f.txt") == 2 and st.files() == []
+    with pytest.raises(ValueError):
+        st.write("../etc/passwd", 1, b"x")
+
+
+# -- job state --------------------------------------------------------------------------
+def test_jobstate_tables_and_views(tmp_path):
+    clock = [100.0]
+    js = JobState(clock=lambda: clock[0])
+    q = js.new_query_number("resnet18")
+    js.assign("resnet18", q, [("node01", 0, 79), ("node02", 80, 159)])
+    assert js.cvm().startswith("{'node01': [('resnet18', 1, 0, 79)]")
+    clock[0] = 101.0
+    assert js.record_result("resnet18", q, "node01", 0, 79, np.arange(80) % 1000, np.full(80, 0.25))
+    assert not js.record_result("resnet18", q, "node01", 0, 79, np.zeros(80), np.zeros(80))  # idempotent
+    assert js.images_done("resnet18") == 80                                              # A3: end-start+1
+    assert ("node01", 0, 79, "f", 100.0, 101.0) in js.worker_set[("resnet18", 1)]
+    assert "node01" not in js.working_vm_set
+    clock[0] = 102.0
+    js.record_result("resnet18", q, "node02", 80, 159, np.ones(80), np.full(80, 0.5))
+    assert js.finished_queries["resnet18"] == 1
+    assert js.query_latency["resnet18"] == [2.0]
+    c1 = js.c1()
+    assert "Resnet18 finished inference is 160" in c1
+    c2 = js.c2()
+    assert c2.startswith("model resnet18 processing time") and "average" in c2
+    path = tmp_path / "result.txt"
+    js.c4(str(path))
+    d = json.loads(path.read_text())
+    first = d["resnet18 1"][0]
+    assert first.startswith("[('test_0.JPEG', 'class_0', 0.25)")
+    # snapshot / restore round trip through msgpack
+    import msgpack
+
+    snap = msgpack.unpackb(msgpack.packb(js.snapshot()), raw=False, strict_map_key=False)
+    js2 = JobState()
+    js2.restore(snap)
+    assert js2.images_done("resnet18") == 160
+    assert js2.inference_result_list() == js.inference_result_list()
+
+
+def test_jobstate_reassign_and_pending():
+    js = JobState()
+    js.assign("alexnet", 1, [("node03", 0, 99)])
+    js.reassign("node03", "node04", ("alexnet", 1, 0, 99))
+    assert js.chunks_of("node04") == [("alexnet", 1, 0, 99)] and js.chunks_of("node03") == []
+    assert [p[2] for p in js.pending()] == ["node04"]
+
+
+def test_config_env_and_file(tmp_path):
+    p = tmp_path / "c.json"
+    p.write_text(json.dumps({"num_nodes": 4, "heartbeat_period_s": 0.1}))
+    cfg = ClusterConfig.load(str(p), env={"IDUNNO_FAILURE_TIMEOUT_S": "0.7", "IDUNNO_REPLICATION": "3"},
+                             base_port=20000)
+    assert cfg.num_nodes == 4 and cfg.heartbeat_period_s == 0.1 and cfg.failure_timeout_s == 0.7
+    assert cfg.replication == 3 and cfg.base_port == 20000
+    assert cfg.standby_name == "node03" and cfg.address("node02") == ("127.0.0.1", 20002)
+    with pytest.raises(KeyError):
+        cfg.update(bogus=1)
