@@ -13,6 +13,16 @@ using namespace idunno;
 
 static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// 256 zero bytes per device: the DMA source of padding taps / masked rows.
+static torch::Tensor zero_buffer(const torch::Device& dev) {
+  static std::vector<torch::Tensor> bufs(64);
+  const int i = dev.index() < 0 ? 0 : dev.index();
+  TORCH_CHECK(i < 64, "device index out of range");
+  if (!bufs[i].defined())
+    bufs[i] = torch::zeros({256}, torch::TensorOptions().dtype(torch::kUInt8).device(dev));
+  return bufs[i];
+}
+
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 #define CHECK_DT(t, dt) TORCH_CHECK((t).scalar_type() == (dt), #t " has wrong dtype")
@@ -83,9 +93,18 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   a.Kpad = Kpad;
   a.relu = relu ? 1 : 0;
   if (M == 0) return y;
-  const int t = tile >= 0 ? (int)tile : conv_pick_tile(a.M, Cout);
-  TORCH_CHECK(t >= 0 && t <= 3, "tile id out of range");
-  conv_igemm_launch(a, small, out_f32, t, cur_stream());
+  if (small) {
+    const int t = (tile >= 0 && tile <= 3) ? (int)tile : conv_pick_tile(a.M, Cout);
+    conv_igemm_launch(a, small, out_f32, t, cur_stream());
+    return y;
+  }
+  if (tile >= 0 && tile <= 3) {          // v1 register-staged loop (kept for A/B)
+    conv_igemm_launch(a, small, out_f32, (int)tile, cur_stream());
+    return y;
+  }
+  a.zero = zero_buffer(x.device()).data_ptr();
+  const int t = tile >= 10 ? (int)tile : conv_glds_pick(a.M, Cout);
+  TORCH_CHECK(conv_glds_launch(a, out_f32, t, cur_stream()), "unknown conv tile id ", t);
   return y;
 }
 
@@ -168,7 +187,7 @@ torch::Tensor synth_images(int64_t seed, int64_t start, int64_t n, int64_t hw, t
   return out;
 }
 
-int64_t pick_tile(int64_t M, int64_t Cout) { return conv_pick_tile((int)M, (int)Cout); }
+int64_t pick_tile(int64_t M, int64_t Cout) { return conv_glds_pick((int)M, (int)Cout); }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "IDunno-MI355X native HIP kernels (gfx950)";

@@ -22,10 +22,13 @@ struct ConvArgs {
   int relu;
   int tiles_n;  // ceil(Cout / BN)
   int tiles_m;  // ceil(M / BM)
+  const void* zero;  // >= 16 zero bytes (DMA source for padding taps)
 };
 
 void conv_igemm_launch(ConvArgs a, bool small, bool out_f32, int tile, hipStream_t st);
 int conv_pick_tile(int M, int Cout);
+bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
+int conv_glds_pick(int M, int Cout);
 void preprocess_launch(const uint8_t* img, half_t* out, long npix, hipStream_t st);
 void resize_crop_launch(const uint8_t* img, half_t* out, int B, int Hi, int Wi, int Hr, int Wr,
                         int crop, hipStream_t st);

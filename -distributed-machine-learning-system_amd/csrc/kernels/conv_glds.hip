@@ -1,0 +1,278 @@
+// Implicit-GEMM convolution, v2 main loop: global->LDS DMA (global_load_lds_dwordx4)
+// with an NS-deep LDS ring and counted vmcnt waits (cdna_hip_programming §5
+// "Pipelining across barriers", T3/T4).  Used for every conv with C % 64 == 0
+// (all ResNet / AlexNet convs after the stem, and the FC layers as 1x1 convs).
+//
+// Why: the v1 register-staged loop (conv_igemm.hip) keeps one K stage in
+// flight; at 2-3 waves/SIMD the L2 latency of the im2col gathers is exposed
+// every stage and the MFMA pipe idles (~20 % of peak on MI355X, see
+// profiles/).  Here NS-1 stages are in flight while the MFMAs of the current
+// one run, no VGPRs are spent on staging, and the LDS image is written by the
+// DMA engine directly.
+//
+// LDS image: per stage, A (weights, BN rows) then B (pixels, BM rows), each
+// row BK halfs, 16-byte chunks XOR-swizzled per row.  glds writes lane-linear
+// (base + lane*16), so the swizzle is applied to the *source* address: the
+// lane that lands in slot s of row r loads global chunk s ^ swz(r), and the
+// fragment read uses the same XOR (rule 21).  Out-of-image taps (padding) and
+// rows past M / Cout load from a 16-byte zero buffer instead of branching.
+#include "../kernels.h"
+
+namespace idunno {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+__device__ __forceinline__ int swz_r(int row, int cpr) {
+  if (cpr == 8) return (row >> 1) & 7;
+  const int q = (row >> 2) & 3;
+  return (0x78 >> (2 * q)) & 3;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most n (runtime, multiple of G) DMA ops of this wave are pending
+template <int G, int NS>
+__device__ __forceinline__ void wait_stages(int pending_stages) {
+  if constexpr (NS >= 4) {
+    if (pending_stages >= 2) { wait_vmcnt<2 * G>(); return; }
+  }
+  if constexpr (NS >= 3) {
+    if (pending_stages >= 1) { wait_vmcnt<G>(); return; }
+  }
+  wait_vmcnt<0>();
+}
+
+template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32>
+__global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs a) {
+  constexpr int NW = WN * WM;
+  constexpr int NT = 64 * NW;
+  constexpr int TN = BN / WN, TM = BM / WM;
+  constexpr int FN = TN / 16, FM = TM / 16;
+  constexpr int CPR = BK / 8;                 // 16-byte chunks per row
+  constexpr int RB = BK * 2;                  // bytes per row
+  constexpr int RPI = 64 / CPR;               // rows per DMA instruction (1 KiB)
+  constexpr int A_INS = BN / RPI, B_INS = BM / RPI;
+  static_assert(A_INS % NW == 0 && B_INS % NW == 0, "DMA instructions must split evenly over waves");
+  constexpr int GA = A_INS / NW, GB = B_INS / NW, G = GA + GB;
+  constexpr int A_BYTES = BN * RB, STAGE = (BN + BM) * RB;
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  static_assert(G * (NS - 2) < 64, "vmcnt immediate");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave / WM, wm = wave % WM;
+
+  const int nwg = a.tiles_n * a.tiles_m;
+  const int lid = xcd_remap(blockIdx.x, nwg);
+  const int tm = lid / a.tiles_n, tn = lid % a.tiles_n;
+  const int n0 = tn * BN, m0 = tm * BM;
+
+  const half_t* zero = reinterpret_cast<const half_t*>(a.zero);
+  const int lrow = lane / CPR, lslot = lane % CPR;
+
+  // A sources: per DMA instruction j of this wave, a row base pointer (or zero)
+  const half_t* a_src[GA];
+  int a_ch[GA];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int row = (wave + NW * j) * RPI + lrow;
+    const int n = n0 + row;
+    a_ch[j] = (lslot ^ swz_r(row, CPR)) * 8;
+    a_src[j] = n < a.Cout ? a.w + (size_t)n * a.Kpad + a_ch[j] : nullptr;
+  }
+  // B sources: pixel decomposition per instruction
+  int b_base[GB], b_ih0[GB], b_iw0[GB], b_ch[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int row = (wave + NW * j) * RPI + lrow;
+    const int m = m0 + row;
+    b_ch[j] = (lslot ^ swz_r(row, CPR)) * 8;
+    if (m < a.M) {
+      const int hw = a.Ho * a.Wo;
+      const int b = m / hw, r = m - b * hw;
+      const int oh = r / a.Wo, ow = r - oh * a.Wo;
+      b_base[j] = b * a.H * a.W * a.C + b_ch[j];
+      b_ih0[j] = oh * a.stride - a.pad;
+      b_iw0[j] = ow * a.stride - a.pad;
+    } else {
+      b_base[j] = -1;
+      b_ih0[j] = -100000;
+      b_iw0[j] = -100000;
+    }
+  }
+
+  // issue-side K coordinates (run NS-1 stages ahead of compute)
+  int i_s = 0, i_cb = 0, i_kw = 0, i_kh = 0;
+  auto issue = [&](int buf) {
+    char* base = smem + buf * STAGE;
+    const int koff = i_s * BK;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const half_t* src = a_src[j] ? a_src[j] + koff : zero;
+      __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(base + (wave + NW * j) * 1024), 16, 0, 0);
+    }
+    const int coff = i_cb * BK;
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int ih = b_ih0[j] + i_kh, iw = b_iw0[j] + i_kw;
+      const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const half_t* src = ok ? a.x + b_base[j] + (ih * a.W + iw) * a.C + coff : zero;
+      __builtin_amdgcn_global_load_lds((glb_void_t*)src,
+                                       (lds_void_t*)(base + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
+    }
+    // advance (cb fastest, then kw, then kh) == weight K order (kh, kw, c)
+    ++i_s;
+    if (++i_cb == a.cblk) {
+      i_cb = 0;
+      if (++i_kw == a.KW) {
+        i_kw = 0;
+        ++i_kh;
+      }
+    }
+  };
+
+  float4v acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  const int nK = a.nK;
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nK) issue(p);
+
+  const int frow = lane & 15, fch = lane >> 4;
+  for (int s = 0; s < nK; ++s) {
+    const int ahead = min(NS - 2, nK - 1 - s);
+    wait_stages<G, NS>(ahead);
+    __builtin_amdgcn_s_barrier();
+    if (s + NS - 1 < nK) issue((s + NS - 1) % NS);
+
+    const char* base = smem + (s % NS) * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int ch = fch + 4 * kk;
+      half8v fa[FN], fb[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int row = wn * TN + i * 16 + frow;
+        fa[i] = *reinterpret_cast<const half8v*>(base + row * RB + ((ch ^ swz_r(row, CPR)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int row = wm * TM + j * 16 + frow;
+        fb[j] = *reinterpret_cast<const half8v*>(base + A_BYTES + row * RB + ((ch ^ swz_r(row, CPR)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: bias (+residual) (+ReLU), NHWC store --------------------
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int n = n0 + wn * TN + i * 16 + (lane >> 4) * 4;
+    if (n >= a.Cout) continue;
+    const float4v bv = *reinterpret_cast<const float4v*>(a.bias + n);
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int m = m0 + wm * TM + j * 16 + (lane & 15);
+      if (m >= a.M) continue;
+      float4v v = acc[i][j] + bv;
+      if constexpr (HAS_RES) {
+        const half4v r = *reinterpret_cast<const half4v*>(a.res + (size_t)m * a.Cout + n);
+        v[0] += (float)r[0];
+        v[1] += (float)r[1];
+        v[2] += (float)r[2];
+        v[3] += (float)r[3];
+      }
+      if (a.relu) {
+        v[0] = fmaxf(v[0], 0.f);
+        v[1] = fmaxf(v[1], 0.f);
+        v[2] = fmaxf(v[2], 0.f);
+        v[3] = fmaxf(v[3], 0.f);
+      }
+      if constexpr (OUT_F32) {
+        *reinterpret_cast<float4v*>(static_cast<float*>(a.y) + (size_t)m * a.ldy + n) = v;
+      } else {
+        half4v o;
+        o[0] = (half_t)v[0];
+        o[1] = (half_t)v[1];
+        o[2] = (half_t)v[2];
+        o[3] = (half_t)v[3];
+        *reinterpret_cast<half4v*>(static_cast<half_t*>(a.y) + (size_t)m * a.ldy + n) = o;
+      }
+    }
+  }
+}
+
+template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32>
+static void glds_cfg(ConvArgs a, hipStream_t st) {
+  a.tiles_n = (a.Cout + BN - 1) / BN;
+  a.tiles_m = (a.M + BM - 1) / BM;
+  a.cblk = a.C / BK;
+  a.nK = a.KH * a.KW * a.cblk;
+  const int grid = a.tiles_n * a.tiles_m;
+  const size_t lds = (size_t)NS * (BN + BM) * BK * 2;
+  auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WN * WM), lds, st, a);
+}
+
+// Tile table (id -> config).  Exposed ids are stable: tests sweep all of them.
+//   10: 128x128, BK 64, 4 waves (2x2), 3 stages   96 KiB LDS
+//   11: 128x128, BK 32, 4 waves (2x2), 4 stages   64 KiB
+//   12: 64x256,  BK 64, 4 waves (1x4), 3 stages   120 KiB
+//   13: 64x256,  BK 32, 4 waves (1x4), 4 stages   80 KiB
+//   14: 128x256, BK 64, 8 waves (2x4), 3 stages   144 KiB
+//   15: 64x128,  BK 64, 4 waves (1x4), 3 stages   72 KiB
+//   16: 128x64,  BK 64, 4 waves (2x2), 3 stages   72 KiB
+//   17: 256x128, BK 64, 8 waves (4x2), 3 stages   144 KiB
+template <bool R, bool F>
+static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
+  switch (tile) {
+    case 10: glds_cfg<128, 128, 64, 2, 2, 3, R, F>(a, st); return true;
+    case 11: glds_cfg<128, 128, 32, 2, 2, 4, R, F>(a, st); return true;
+    case 12: glds_cfg<64, 256, 64, 1, 4, 3, R, F>(a, st); return true;
+    case 13: glds_cfg<64, 256, 32, 1, 4, 4, R, F>(a, st); return true;
+    case 14: glds_cfg<128, 256, 64, 2, 4, 3, R, F>(a, st); return true;
+    case 15: glds_cfg<64, 128, 64, 1, 4, 3, R, F>(a, st); return true;
+    case 16: glds_cfg<128, 64, 64, 2, 2, 3, R, F>(a, st); return true;
+    case 17: glds_cfg<256, 128, 64, 4, 2, 3, R, F>(a, st); return true;
+    default: return false;
+  }
+}
+
+bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
+  const bool res = a.res != nullptr;
+  if (res) return out_f32 ? glds_dispatch<true, true>(a, tile, st) : glds_dispatch<true, false>(a, tile, st);
+  return out_f32 ? glds_dispatch<false, true>(a, tile, st) : glds_dispatch<false, false>(a, tile, st);
+}
+
+int conv_glds_pick(int M, int Cout) {
+  auto blocks = [&](int bn, int bm) { return ((Cout + bn - 1) / bn) * ((M + bm - 1) / bm); };
+  if (Cout % 128 == 0) {
+    if (blocks(128, 256) >= 768) return 14;
+    if (blocks(128, 128) >= 384) return 10;
+    return 16;
+  }
+  if (blocks(64, 256) >= 768) return 12;
+  return 15;
+}
+
+}  // namespace idunno

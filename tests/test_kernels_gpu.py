@@ -70,12 +70,13 @@ def test_conv_big(ops, B, H, Cin, Cout, k, s, p):
     _check(y, ref)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3])
-def test_conv_all_tiles_with_residual(ops, tile):
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 10, 11, 12, 13, 14, 15, 16, 17])
+@pytest.mark.parametrize("H", [14, 9])
+def test_conv_all_tiles_with_residual(ops, tile, H):
     from idunno.models.packed import pack_conv_weight
 
-    torch.manual_seed(tile)
-    B, H, Cin, Cout = 2, 14, 128, 128
+    torch.manual_seed(tile * 31 + H)
+    B, Cin, Cout = 2, 128, 128 if tile not in (17,) else 256
     x = torch.randn(B, H, H, Cin, device=DEV).half()
     w = torch.randn(Cout, Cin, 3, 3) / (Cin * 9) ** 0.5
     b = torch.randn(Cout) * 0.1
