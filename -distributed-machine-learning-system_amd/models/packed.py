@@ -18,6 +18,7 @@ without a GPU).
 """
 from __future__ import annotations
 
+import threading
 from dataclasses import dataclass, field
 
 import torch
@@ -235,6 +236,9 @@ def emulate(p: Program, img_u8: torch.Tensor) -> torch.Tensor:
 # HIP runner
 # ---------------------------------------------------------------------------
 
+_CAPTURE_LOCK = threading.Lock()
+
+
 class HipRunner:
     """Runs a packed Program through the gfx950 kernels.
 
@@ -300,15 +304,16 @@ class HipRunner:
             g, sin, sout = self._graphs[batch]
             return sin, (lambda: (g.replay(), sout)[1])
         sin = torch.zeros(batch, hw, hw, 3, dtype=torch.uint8, device=self.device)
-        s = torch.cuda.Stream(device=self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                self.forward(sin)
-        torch.cuda.current_stream(self.device).wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            sout = self.forward(sin)
+        with _CAPTURE_LOCK:  # one capture at a time per process; other threads keep launching
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self.forward(sin)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                sout = self.forward(sin)
         self._graphs[batch] = (g, sin, sout)
         return sin, (lambda: (g.replay(), sout)[1])
 

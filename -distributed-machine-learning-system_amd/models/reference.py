@@ -149,9 +149,20 @@ def preprocess_u8(img_u8: torch.Tensor) -> torch.Tensor:
     """uint8 [B,H,W,3] -> normalised fp32 NCHW (ToTensor + Normalize, reference
     alexnet_resnet.py:60-61)."""
     x = img_u8.permute(0, 3, 1, 2).float().div_(255.0)
-    mean = torch.tensor(IMAGENET_MEAN, device=x.device).view(1, 3, 1, 1)
-    std = torch.tensor(IMAGENET_STD, device=x.device).view(1, 3, 1, 1)
+    mean, std = _norm_consts(x.device)
     return (x - mean) / std
+
+
+_NORM: dict = {}
+
+
+def _norm_consts(device):
+    """Per-device cached mean/std (no H2D copy inside a graph capture)."""
+    key = str(device)
+    if key not in _NORM:
+        _NORM[key] = (torch.tensor(IMAGENET_MEAN, device=device).view(1, 3, 1, 1),
+                      torch.tensor(IMAGENET_STD, device=device).view(1, 3, 1, 1))
+    return _NORM[key]
 
 
 def build(name: str, seed: int = 0, randomize_bn: bool = False) -> nn.Module:

@@ -88,6 +88,7 @@ class HipExecutor(Executor):
         self._HipRunner, self._build = HipRunner, build_program
         self.runners: dict[str, object] = {}
         self.lock = threading.Lock()
+        self.stream = None      # private HIP stream: nodes sharing a GPU overlap
 
     def runner(self, name):
         name = ref.canonical(name)
@@ -108,13 +109,19 @@ class HipExecutor(Executor):
         r = self.runner(model)
         n = images.shape[0]
         with torch.cuda.device(self.device):
-            if self.use_graphs and len(r._graphs) < self.max_graphs or n in r._graphs:
-                sin, replay = r.capture(n)
-                sin.copy_(images)
-                cls, prob = replay()
-            else:
-                cls, prob = r.forward(images.contiguous())
-            out = torch.stack([cls, prob.view(torch.int32)], dim=1).cpu()
+            if self.stream is None:
+                self.stream = torch.cuda.Stream(device=self.device)
+            s = self.stream
+            s.wait_stream(torch.cuda.current_stream(self.device))   # images were produced there
+            images.record_stream(s)
+            with torch.cuda.stream(s):
+                if (self.use_graphs and len(r._graphs) < self.max_graphs) or n in r._graphs:
+                    sin, replay = r.capture(n)
+                    sin.copy_(images)
+                    cls, prob = replay()
+                else:
+                    cls, prob = r.forward(images.contiguous())
+                out = torch.stack([cls, prob.view(torch.int32)], dim=1).cpu()
         return out[:, 0].numpy().copy(), out[:, 1].contiguous().view(torch.float32).numpy().copy()
 
 

@@ -96,15 +96,17 @@ class Membership:
         with self.lock:
             self.left = False
             self.members[self.name] = [now, Status_RUNNING]
-            self.joined = True
         self.last_master_ping = self.clock()
         if self.is_master():
+            self.joined = True
             return True
         try:
             rep = self.t.request(self.master, {"t": Type.JOIN, "entry": [now, Status_RUNNING]}, timeout)
         except Exception as e:  # noqa: BLE001
             log.warning("%s: join via %s failed: %s", self.name, self.master, e)
             return False
+        self.last_master_ping = self.clock()
+        self.joined = True
         self._merge(rep.get("members", {}))
         with self.lock:
             if rep.get("epoch", 0) >= self.epoch:

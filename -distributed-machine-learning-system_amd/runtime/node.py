@@ -66,6 +66,7 @@ class Node:
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self.promotions = 0
+        self._retries: dict = {}
         self.membership.on_failure.append(self._on_node_failure)
         self.membership.on_master_failure.append(self._on_master_failure)
         self.membership.on_master_change.append(self._on_master_change)
@@ -206,6 +207,9 @@ class Node:
         return ok
 
     def _ingest_result(self, msg: dict) -> None:
+        if "error" in msg:
+            self._chunk_error(msg)
+            return
         cls = np.frombuffer(msg["cls"], dtype=np.int32)
         prob = np.frombuffer(msg["prob"], dtype=np.float32)
         new = self.state.record_result(msg["model"], msg["qnum"], msg["worker"], msg["start"], msg["end"],
@@ -213,6 +217,25 @@ class Node:
         if new and self.is_coordinator:
             n = msg["end"] - msg["start"] + 1
             self.sched.observe(msg["model"], msg.get("compute_s", 0.0) / n * self.cfg.batch_for(msg["model"]))
+
+    MAX_CHUNK_RETRIES = 3
+
+    def _chunk_error(self, msg: dict) -> None:
+        """A worker reported an executor failure: retry the chunk elsewhere."""
+        if not self.is_coordinator:
+            return
+        key = (msg["model"], msg["qnum"], int(msg["start"]), int(msg["end"]))
+        n = self._retries.get(key, 0) + 1
+        self._retries[key] = n
+        self.logger.error("chunk %s failed on %s (%s), attempt %d", key, msg["worker"], msg["error"], n)
+        if n > self.MAX_CHUNK_RETRIES:
+            return
+        alive = [w for w in self.membership.alive() if w != msg["worker"]] or self.membership.alive()
+        w = self.pick_replacement(msg["worker"], alive + [msg["worker"]])
+        if w is None:
+            return
+        self.state.reassign(msg["worker"], w, key)
+        self._send_job(w, *key)
 
     def pick_replacement(self, failed: str, alive: list[str]) -> str | None:
         """Least-loaded live worker, ties broken by ring order after the failed node."""
@@ -323,8 +346,14 @@ class Node:
                 return
             try:
                 self.run_chunk(msg)
-            except Exception:  # noqa: BLE001
-                self.logger.exception("chunk failed: %s", {k: v for k, v in msg.items() if k != 'data'})
+            except Exception as e:  # noqa: BLE001
+                self.logger.exception("chunk failed: %s", msg)
+                err = {"t": Type.RESULT, "model": msg["model"], "qnum": msg["qnum"], "start": msg["start"],
+                       "end": msg["end"], "worker": self.name, "error": f"{type(e).__name__}: {e}"}
+                if self.membership.master == self.name:
+                    self._ingest_result(dict(err, src=self.name))
+                else:
+                    self.transport.send(self.membership.master, err)
 
     def run_chunk(self, msg: dict) -> None:
         delay = self.cfg.worker_start_delay_s + self.extra_delay_s

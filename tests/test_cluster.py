@@ -188,3 +188,21 @@ def test_tcp_cluster_small():
         check_results(cl, "alexnet", 0, 299)
     finally:
         c.stop()
+
+
+def test_executor_failure_retried_elsewhere():
+    from idunno.runtime.executor import FakeExecutor
+
+    class Broken(FakeExecutor):
+        def run(self, *a, **k):
+            raise RuntimeError("simulated HIP error")
+
+    c = LocalCluster(num_nodes=4, executor_factory=lambda i: Broken() if i == 2 else FakeExecutor(), **FAST).start()
+    try:
+        cl = c.client()
+        cl.inference(0, 399, "resnet18")
+        s = cl.wait_idle(10, {"resnet18": 400})
+        assert s["done"]["resnet18"] == 400
+        check_results(cl, "resnet18", 0, 399)
+    finally:
+        c.stop()
