@@ -108,6 +108,32 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   return y;
 }
 
+// uint8 [B,H,W,3] -> maxpool3x3/2(relu(conv7x7/2(normalise(img)) + bias)) : fp16 [B,Hp,Wp,64]
+torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias) {
+  CHECK_DEV(img);
+  CHECK_DEV(w);
+  CHECK_DEV(bias);
+  CHECK_CONTIG(img);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(bias);
+  CHECK_DT(img, torch::kUInt8);
+  CHECK_DT(w, torch::kHalf);
+  CHECK_DT(bias, torch::kFloat);
+  TORCH_CHECK(img.dim() == 4 && img.size(3) == 3, "img must be [B, H, W, 3] uint8");
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == 64 && w.size(1) == 7 * 32, "stem weight must be [64, 7*32] (small-C packing)");
+  TORCH_CHECK(bias.numel() == 64, "bias must have 64 entries");
+  const int B = img.size(0), H = img.size(1), W = img.size(2);
+  TORCH_CHECK(H >= 7 && W >= 7, "image too small");
+  TORCH_CHECK((long)B * H * W * 3 < (1L << 31), "batch too large");
+  const int Hc = (H + 6 - 7) / 2 + 1, Wc = (W + 6 - 7) / 2 + 1;
+  const int Hp = (Hc + 2 - 3) / 2 + 1, Wp = (Wc + 2 - 3) / 2 + 1;
+  auto y = torch::empty({B, Hp, Wp, 64}, img.options().dtype(torch::kHalf));
+  if (B)
+    stem_fused_launch(img.data_ptr<uint8_t>(), reinterpret_cast<const half_t*>(w.data_ptr()), bias.data_ptr<float>(),
+                      reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, cur_stream());
+  return y;
+}
+
 torch::Tensor preprocess(torch::Tensor img) {
   CHECK_DEV(img);
   CHECK_CONTIG(img);
@@ -195,6 +221,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("relu"), py::arg("out_f32") = false, py::arg("tile") = -1);
   m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 NHWC4");
+  m.def("stem_fused", &stem_fused, "fused normalise + conv7x7/2 + bias + relu + maxpool3x3/2 (ResNet stem)");
   m.def("resize_crop", &resize_crop, "bilinear resize + centre crop + normalise");
   m.def("maxpool2d_nhwc", &maxpool2d_nhwc, "NHWC max pool");
   m.def("global_avgpool_nhwc", &global_avgpool_nhwc, "NHWC global average pool");

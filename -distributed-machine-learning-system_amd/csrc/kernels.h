@@ -29,6 +29,8 @@ void conv_igemm_launch(ConvArgs a, bool small, bool out_f32, int tile, hipStream
 int conv_pick_tile(int M, int Cout);
 bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 int conv_glds_pick(int M, int Cout);
+void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, half_t* y, int B, int H, int W,
+                       hipStream_t st);
 void preprocess_launch(const uint8_t* img, half_t* out, long npix, hipStream_t st);
 void resize_crop_launch(const uint8_t* img, half_t* out, int B, int Hi, int Wi, int Hr, int Wr,
                         int crop, hipStream_t st);

@@ -243,6 +243,9 @@ static void glds_cfg(ConvArgs a, hipStream_t st) {
 //   15: 64x128,  BK 64, 4 waves (1x4), 3 stages   72 KiB
 //   16: 128x64,  BK 64, 4 waves (2x2), 3 stages   72 KiB
 //   17: 256x128, BK 64, 8 waves (4x2), 3 stages   144 KiB
+//   18: 128x128, BK 32, 4 waves, 3 stages 48 KiB   19: 128x64, BK 32, 4 stages 48 KiB
+//   20: 64x128,  BK 32, 4 stages 48 KiB            21: 256x128, BK 32, 8 waves, 4 stages 96 KiB
+//   22: 128x256, BK 32, 8 waves, 4 stages 96 KiB   23: 64x64, BK 64, 4 waves (2x2), 3 stages 48 KiB
 template <bool R, bool F>
 static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
   switch (tile) {
@@ -254,6 +257,12 @@ static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
     case 15: glds_cfg<64, 128, 64, 1, 4, 3, R, F>(a, st); return true;
     case 16: glds_cfg<128, 64, 64, 2, 2, 3, R, F>(a, st); return true;
     case 17: glds_cfg<256, 128, 64, 4, 2, 3, R, F>(a, st); return true;
+    case 18: glds_cfg<128, 128, 32, 2, 2, 3, R, F>(a, st); return true;
+    case 19: glds_cfg<128, 64, 32, 2, 2, 4, R, F>(a, st); return true;
+    case 20: glds_cfg<64, 128, 32, 1, 4, 4, R, F>(a, st); return true;
+    case 21: glds_cfg<256, 128, 32, 4, 2, 4, R, F>(a, st); return true;
+    case 22: glds_cfg<128, 256, 32, 2, 4, 4, R, F>(a, st); return true;
+    case 23: glds_cfg<64, 64, 64, 2, 2, 3, R, F>(a, st); return true;
     default: return false;
   }
 }
@@ -264,14 +273,11 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
   return out_f32 ? glds_dispatch<false, true>(a, tile, st) : glds_dispatch<false, false>(a, tile, st);
 }
 
+// Default tile per shape, from the per-layer sweep on MI355X (tools/bench_layers.py,
+// profiles/r1_layer_sweep.md): 2 blocks/CU with a 4-deep BK=32 ring wins where
+// M is large; 128x64 tiles keep >= 2 waves of blocks when M is small (layer4).
 int conv_glds_pick(int M, int Cout) {
-  auto blocks = [&](int bn, int bm) { return ((Cout + bn - 1) / bn) * ((M + bm - 1) / bm); };
-  if (Cout % 128 == 0) {
-    if (blocks(128, 256) >= 768) return 14;
-    if (blocks(128, 128) >= 384) return 10;
-    return 16;
-  }
-  if (blocks(64, 256) >= 768) return 12;
+  if (Cout % 128 == 0) return M >= 50000 ? 11 : 16;
   return 15;
 }
 

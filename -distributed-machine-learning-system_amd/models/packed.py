@@ -248,11 +248,12 @@ class HipRunner:
     static input buffer, removing per-kernel launch overhead.
     """
 
-    def __init__(self, program: Program, device=None):
+    def __init__(self, program: Program, device=None, fuse_stem: bool = True):
         from .. import ops
 
         ops.load()
         self.ops = ops
+        self.fuse_stem = fuse_stem
         self.device = torch.device(device or "cuda")
         self.p = program.to(self.device)
         self._graphs: dict[int, tuple] = {}
@@ -261,14 +262,18 @@ class HipRunner:
     def logits(self, img_u8: torch.Tensor) -> torch.Tensor:
         o = self.ops
         p = self.p
-        if img_u8.shape[1:3] == (224, 224):
-            x = o.preprocess(img_u8)
-        else:
-            x = o.resize_crop(img_u8, 256, 224)
+        native = tuple(img_u8.shape[1:3]) == (224, 224)
+        s = p.stem
+        fused = (self.fuse_stem and native and p.kind == "resnet" and s.small and s.kh == 7 and s.kw == 7
+                 and s.stride == 2 and s.pad == 3 and s.cout == 64)
+        if not fused:
+            x = o.preprocess(img_u8) if native else o.resize_crop(img_u8, 256, 224)
         if p.kind == "resnet":
-            s = p.stem
-            x = o.conv2d(x, s.w, s.b, s.kh, s.kw, s.stride, s.pad, s.relu)
-            x = o.maxpool2d(x, 3, 2, 1)
+            if fused:
+                x = o.stem_fused(img_u8, s.w, s.b)
+            else:
+                x = o.conv2d(x, s.w, s.b, s.kh, s.kw, s.stride, s.pad, s.relu)
+                x = o.maxpool2d(x, 3, 2, 1)
             for blk in p.blocks:
                 idt = x
                 if blk.down is not None:

@@ -37,6 +37,11 @@ def resize_crop(img_u8, resize: int = 256, crop: int = 224):
     return load().resize_crop(img_u8, resize, crop)
 
 
+def stem_fused(img_u8, w, bias):
+    """ResNet stem in one kernel: uint8 [B,H,W,3] -> fp16 [B,H/4,W/4,64]."""
+    return load().stem_fused(img_u8, w, bias)
+
+
 def maxpool2d(x, k: int = 3, s: int = 2, pad: int = 1):
     return load().maxpool2d_nhwc(x, k, s, pad)
 

@@ -61,7 +61,7 @@ def main():
     ap.add_argument("--batch", type=int, default=400)
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--tiles", default="auto,0,1,2,3,10,11,12,13,14,15,16,17")
+    ap.add_argument("--tiles", default="auto,0,1,2,3,10,11,12,13,14,15,16,17,18,19,20,21,22,23")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     from idunno import ops
@@ -70,6 +70,23 @@ def main():
     dev = "cuda"
     rows = []
     tiles = [t for t in a.tiles.split(",")]
+    # stem: unfused (preprocess + conv + maxpool) vs fused kernel vs torch
+    from idunno.models import build_program
+    from idunno.models.reference import preprocess_u8
+    p = build_program(a.model)
+    s = p.stem
+    if a.model.startswith("resnet"):
+        img = torch.randint(0, 256, (a.batch, 224, 224, 3), dtype=torch.uint8, device=dev)
+        w, b = s.w.to(dev), s.b.to(dev)
+        t_unf = min(timeit(lambda: ops.maxpool2d(ops.conv2d(ops.preprocess(img), w, b, 7, 7, 2, 3, True), 3, 2, 1))
+                    for _ in range(a.rounds))
+        t_fus = min(timeit(lambda: ops.stem_fused(img, w, b)) for _ in range(a.rounds))
+        from idunno.models.packed import unpack_conv_weight
+        wr = unpack_conv_weight(s).half().to(dev)
+        t_tor = min(timeit(lambda: F.max_pool2d(F.relu(F.conv2d(preprocess_u8(img).half(), wr, b.half(), 2, 3)), 3, 2, 1))
+                    for _ in range(a.rounds))
+        print(f"stem+pool  unfused {t_unf:8.1f}us  fused {t_fus:8.1f}us  torch {t_tor:8.1f}us", flush=True)
+        rows.append({"layer": "stem+maxpool", "us": {"unfused": t_unf, "fused": t_fus, "torch": t_tor}})
     for name, B, h, c in layer_shapes(a.model, a.batch):
         cin = 4 if c.small else c.cin
         x = torch.randn(B, h, h, cin, device=dev).half()
