@@ -148,6 +148,68 @@ class SdfsSource:
         return parts[0] if len(parts) == 1 else torch.cat(parts, 0)
 
 
+def load_image_u8(data: bytes, resize: int = 256, crop: int = 224) -> np.ndarray:
+    """Decode one image and apply the reference's Resize(256) + CenterCrop(224)
+    (alexnet_resnet.py:50-59) with PIL, returning uint8 [crop, crop, 3].
+    Non-RGB images are converted in memory; the source file is never
+    rewritten (the reference overwrites it on disk)."""
+    import io
+
+    from PIL import Image
+
+    im = Image.open(io.BytesIO(data))
+    if im.mode != "RGB":
+        im = im.convert("RGB")
+    w, h = im.size
+    if w <= h:
+        nw, nh = resize, int(resize * h / w)
+    else:
+        nh, nw = resize, int(resize * w / h)
+    im = im.resize((nw, nh), Image.BILINEAR)
+    left, top = int(round((nw - crop) / 2.0)), int(round((nh - crop) / 2.0))
+    im = im.crop((left, top, left + crop, top + crop))
+    return np.asarray(im, dtype=np.uint8)
+
+
+class JpegSource:
+    """Real image files ``test_<i>.JPEG`` (the reference's dataset naming,
+    alexnet_resnet.py:49) read from a local directory or from SDFS, decoded and
+    resized on host threads, staged to HBM in one copy per chunk.  A missing
+    image becomes an all-zero image and is reported in ``missing``."""
+
+    def __init__(self, device, root: str | None = None, sdfs=None, prefix: str = "", workers: int = 8):
+        from concurrent.futures import ThreadPoolExecutor
+
+        self.device = torch.device(device)
+        self.root, self.sdfs, self.prefix = root, sdfs, prefix
+        self.pool = ThreadPoolExecutor(max_workers=workers)
+        self.stager = HbmStager(self.device)
+        self.missing: list[int] = []
+
+    def _read(self, i: int) -> bytes | None:
+        name = f"{self.prefix}test_{i}.JPEG"
+        if self.sdfs is not None:
+            return self.sdfs.get_bytes(name)
+        import os
+
+        p = os.path.join(self.root, name)
+        if not os.path.exists(p):
+            return None
+        with open(p, "rb") as f:
+            return f.read()
+
+    def _one(self, i: int) -> np.ndarray:
+        data = self._read(i)
+        if data is None:
+            self.missing.append(i)
+            return np.zeros((HW, HW, 3), np.uint8)
+        return load_image_u8(data)
+
+    def get(self, start: int, end: int) -> torch.Tensor:
+        arr = np.stack(list(self.pool.map(self._one, range(start, end + 1))))
+        return self.stager.stage(arr, arr.shape)
+
+
 def put_synthetic_dataset(sdfs, n_images: int, seed: int, shard_images: int = 500) -> int:
     """Upload a deterministic synthetic dataset into SDFS as uint8 shards."""
     k = 0

@@ -37,6 +37,7 @@ from ..models.reference import canonical
 from .jobstate import JobState
 from .membership import Membership
 from .messages import Type
+from .ring import replica_neighbors
 from .scheduler import FairTimeScheduler
 from .sdfs import Sdfs
 from .transport import TransportError
@@ -242,9 +243,8 @@ class Node:
         cands = [a for a in alive if a != failed]
         if not cands:
             return None
-        ring = sorted(set(cands) | {failed})
-        i = ring.index(failed)
-        order = ring[i + 1:] + ring[:i]
+        # ring successors of the failed node (reference :717-721), least loaded first
+        order = [n for n in replica_neighbors(failed, cands) if n != failed]
         load = {w: len(self.state.chunks_of(w)) for w in order}
         return min(order, key=lambda w: (load[w], order.index(w)))
 

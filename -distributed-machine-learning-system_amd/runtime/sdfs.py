@@ -27,6 +27,7 @@ import zlib
 from pathlib import Path
 
 from .messages import Type
+from .ring import file_neighbors
 
 log = logging.getLogger("idunno.sdfs")
 
@@ -38,12 +39,11 @@ def stable_hash(name: str) -> int:
 
 
 def ring_placement(name: str, ring: list[str], r: int) -> list[str]:
-    """R consecutive ring nodes starting at crc32(name) % len(ring)."""
+    """R consecutive ring nodes starting at crc32(name) % len(ring)
+    (reference get_file_neighbors(abs(hash(name)) % 10), :361 / utils.py:48-55)."""
     if not ring:
         return []
-    k = stable_hash(name) % len(ring)
-    r = min(r, len(ring))
-    return [ring[(k + i) % len(ring)] for i in range(r)]
+    return file_neighbors(stable_hash(name) % len(ring), ring, r)
 
 
 def _safe(name: str) -> str:

@@ -65,15 +65,21 @@ def test_cluster_hip_vs_fp32_oracle_and_sdfs_path():
         got = _collect(cl, "resnet18", 200)
     finally:
         c.stop()
+    from idunno.models import HipRunner, build_program
+
     imgs = torch.from_numpy(synth_images_cpu(c.cfg.data_seed, 0, 200)).cuda()
+    # the cluster path (split, dispatch, graphs per chunk size, gather) must give
+    # exactly what one direct forward of the same kernels gives
+    dc, dp = HipRunner(build_program("resnet18", seed=0)).forward(imgs)
+    assert all(got[i][0] == dc[i].item() for i in range(200))
+    # and the probabilities must match the fp32 oracle's probability of that class
+    # (default-init ResNet18 on noise has near-tied logits, so argmax equality
+    # with the oracle is not a meaningful check here; kernel tests cover it)
     m = ref.build("resnet18", seed=0).cuda()
     with torch.no_grad():
         p = torch.softmax(m(ref.preprocess_u8(imgs)), 1)
-    pv, pc = p.max(1)
-    agree = np.mean([got[i][0] == pc[i].item() for i in range(200)])
-    perr = max(abs(got[i][1] - pv[i].item()) for i in range(200))
-    assert agree >= 0.8, agree
-    assert perr < 0.02, perr
+    perr = max(abs(got[i][1] - p[i, got[i][0]].item()) for i in range(200))
+    assert perr < 0.02 * p.max().item() + 1e-4, perr
 
     c2 = _cluster("sdfs")
     try:

@@ -1,0 +1,56 @@
+"""Image sources on the CPU: deterministic synthetic images, JPEG files
+(reference naming / Resize+CenterCrop), SDFS shards; ring helpers."""
+import io
+
+import numpy as np
+import torch
+
+from idunno.runtime.data import JpegSource, SyntheticSource, load_image_u8, synth_images_cpu
+from idunno.runtime.executor import TorchExecutor
+from idunno.runtime.ring import file_neighbors, neighbors, replica_neighbors
+
+
+def test_synthetic_deterministic_and_index_addressed():
+    a = synth_images_cpu(7, 10, 3)
+    b = synth_images_cpu(7, 11, 1)
+    assert a.shape == (3, 224, 224, 3) and a.dtype == np.uint8
+    assert np.array_equal(a[1], b[0])                     # image i is the same from any chunk
+    assert not np.array_equal(a[0], a[1])
+    assert abs(a.mean() - 127.5) < 1.0                    # ~uniform bytes
+    t = SyntheticSource(7).get(10, 12)
+    assert torch.equal(t, torch.from_numpy(a))
+
+
+def test_jpeg_source_resize_crop(tmp_path):
+    from PIL import Image
+
+    rng = np.random.default_rng(0)
+    for i, (w, h) in enumerate([(300, 400), (500, 256), (256, 256)]):
+        Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8)).save(tmp_path / f"test_{i}.JPEG")
+    Image.fromarray(rng.integers(0, 256, (260, 280), dtype=np.uint8), mode="L").save(tmp_path / "test_3.JPEG")
+    before = (tmp_path / "test_3.JPEG").read_bytes()
+    src = JpegSource("cpu", root=str(tmp_path))
+    x = src.get(0, 4)
+    assert x.shape == (5, 224, 224, 3) and x.dtype == torch.uint8
+    assert src.missing == [4] and x[4].sum() == 0
+    assert (tmp_path / "test_3.JPEG").read_bytes() == before   # A14: file not rewritten
+    buf = io.BytesIO()
+    Image.fromarray(np.full((256, 320, 3), 200, np.uint8)).save(buf, format="PNG")
+    y = load_image_u8(buf.getvalue())
+    assert y.shape == (224, 224, 3) and int(y[100, 100, 0]) == 200
+
+
+def test_torch_executor_on_synthetic():
+    ex = TorchExecutor("cpu", seed=0)
+    imgs = SyntheticSource(3).get(0, 1)
+    cls, prob = ex.run("alexnet", imgs, 0, 1)
+    assert cls.shape == (2,) and cls.dtype == np.int32 and np.all((prob > 0) & (prob <= 1))
+    cls2, _ = ex.run("alexnet", imgs, 0, 1)
+    assert np.array_equal(cls, cls2)
+
+
+def test_ring_helpers_reference_semantics():
+    ring = [f"h{i:02d}" for i in range(1, 11)]
+    assert replica_neighbors("h05", ring) == ["h06", "h07", "h08", "h09", "h10", "h01", "h02", "h03", "h04", "h05"]
+    assert "h03" not in neighbors("h03", ring) and len(neighbors("h03", ring)) == 9
+    assert file_neighbors(8, ring, 4) == ["h09", "h10", "h01", "h02"]
