@@ -61,6 +61,10 @@ class Client:
                 time.sleep(interval)
         return out
 
+    def submit_job(self, start: int, end: int, model: str) -> dict:
+        """Send the whole range once; the coordinator batches it (C28 variant)."""
+        return self._call({"t": Type.INFERENCE, "model": model, "start": start, "end": end, "job": True})
+
     def inference_async(self, start: int, end: int, model: str) -> threading.Thread:
         th = threading.Thread(target=self.inference, args=(start, end, model), daemon=True)
         th.start()

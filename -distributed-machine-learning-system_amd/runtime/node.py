@@ -137,6 +137,8 @@ class Node:
                  Type.GET_VERSIONS):
             return self.sdfs.handle(msg)
         if t == Type.INFERENCE:
+            if msg.get("job"):
+                return self.submit_job(msg["model"], int(msg["start"]), int(msg["end"]))
             return self.submit_query(msg["model"], int(msg["start"]), int(msg["end"]),
                                      client=msg.get("src"))
         if t == Type.JOB:
@@ -194,6 +196,30 @@ class Node:
             self._send_job(w, model, qnum, s, e)
         self.logger.info("query %s %s [%d,%d] -> %s", model, qnum, start, end, plan)
         return {"ok": True, "qnum": qnum, "plan": [list(p) for p in plan]}
+
+    def submit_job(self, model: str, start: int, end: int) -> dict:
+        """Coordinator-side batching (the reference's two-tier variant,
+        mp4_machinelearning_work_inference_separate.py:611-640):
+        the client sends one whole range, the coordinator cuts it into
+        batch-size queries and schedules them, paced by client_query_interval_s."""
+        if not self.is_coordinator:
+            return self.transport.request(self.membership.master,
+                                          {"t": Type.INFERENCE, "model": model, "start": start, "end": end,
+                                           "job": True}, self.cfg.rpc_timeout_s)
+        model = canonical(model)
+        bs = self.cfg.batch_for(model)
+        ranges = [(i, min(i + bs - 1, end)) for i in range(start, end + 1, bs)]
+
+        def run():
+            for k, (s, e) in enumerate(ranges):
+                if self._stop.is_set() or not self.is_coordinator:
+                    return
+                self.submit_query(model, s, e)
+                if self.cfg.client_query_interval_s and k + 1 < len(ranges):
+                    time.sleep(self.cfg.client_query_interval_s)
+
+        threading.Thread(target=run, name=f"{self.name}-job", daemon=True).start()
+        return {"ok": True, "queries": len(ranges)}
 
     def _send_job(self, worker: str, model: str, qnum, s: int, e: int) -> bool:
         msg = {"t": Type.JOB, "model": model, "qnum": qnum, "start": s, "end": e,

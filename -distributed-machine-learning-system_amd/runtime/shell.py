@@ -30,6 +30,7 @@ c2 current processing time of a query for each model (mean, q1, q2, q3, stddev)
 c4 query results (also written to result.txt)
 cvm (c5) tasks running on each node
 cq how each query is distributed: (node, start, end, state, t_start, t_end)
+job <start> <end> <model>: send the whole range; the coordinator cuts it into batch-size queries
 dataset <n_images> [shard_images]: put a synthetic 224x224x3 dataset into SDFS
 kill <node> | delay <node> <seconds>: fault injection
 exit"""
@@ -98,6 +99,10 @@ class Shell:
                 need(3)
                 self.client.inference_async(int(args[0]), int(args[1]), args[2])
                 return f"submitting {args[2]} queries for [{args[0]}, {args[1]}]"
+            if cmd == "job":
+                need(3)
+                r = self.client.submit_job(int(args[0]), int(args[1]), args[2])
+                return f"coordinator batching {r.get('queries')} {args[2]} queries"
             if cmd == "c4":
                 res = self.client.c4("result.txt")
                 return str(res)

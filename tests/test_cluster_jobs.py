@@ -1,0 +1,33 @@
+"""Coordinator-side batching (reference two-tier variant) and
+straggler resend (A7), on the in-memory fake cluster."""
+from idunno.runtime.cluster import LocalCluster
+from idunno.runtime.shell import Shell
+
+FAST = dict(heartbeat_period_s=0.05, failure_timeout_s=0.4, metadata_period_s=0.1, rpc_timeout_s=2.0)
+
+
+def test_job_submission_batched_by_coordinator():
+    c = LocalCluster(num_nodes=4, **FAST).start()
+    try:
+        cl = c.client()
+        sh = Shell(c.nodes["node03"], cl)
+        assert sh.execute("job 0 1049 alexnet") == "coordinator batching 3 alexnet queries"
+        s = cl.wait_idle(10, {"alexnet": 1050})
+        assert s["done"]["alexnet"] == 1050
+        assert s["finished_queries"]["alexnet"] == 3
+        qs = c.coordinator().state.worker_set
+        assert sorted(q for (m, q) in qs if m == "alexnet") == [1, 2, 3]
+    finally:
+        c.stop()
+
+
+def test_straggler_resend():
+    c = LocalCluster(num_nodes=4, straggler_resend=True, straggler_timeout_s=0.3, **FAST).start()
+    try:
+        c.nodes["node02"].extra_delay_s = 3.0       # alive (answers pings) but very slow
+        cl = c.client()
+        cl.inference(0, 399, "resnet18")
+        s = cl.wait_idle(2.5, {"resnet18": 400})
+        assert s["done"]["resnet18"] == 400, s      # finished before the straggler would have
+    finally:
+        c.stop()

@@ -63,7 +63,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--tiles", default="auto,0,1,2,3,10,11,12,13,14,15,16,17,18,19,20,21,22,23")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--layers", default=None, help="comma list of layer names to run (default all)")
+    ap.add_argument("--no-stem", action="store_true")
     a = ap.parse_args()
+    only = set(a.layers.split(",")) if a.layers else None
     from idunno import ops
 
     ops.load()
@@ -75,7 +78,7 @@ def main():
     from idunno.models.reference import preprocess_u8
     p = build_program(a.model)
     s = p.stem
-    if a.model.startswith("resnet"):
+    if a.model.startswith("resnet") and not a.no_stem:
         img = torch.randint(0, 256, (a.batch, 224, 224, 3), dtype=torch.uint8, device=dev)
         w, b = s.w.to(dev), s.b.to(dev)
         t_unf = min(timeit(lambda: ops.maxpool2d(ops.conv2d(ops.preprocess(img), w, b, 7, 7, 2, 3, True), 3, 2, 1))
@@ -88,6 +91,8 @@ def main():
         print(f"stem+pool  unfused {t_unf:8.1f}us  fused {t_fus:8.1f}us  torch {t_tor:8.1f}us", flush=True)
         rows.append({"layer": "stem+maxpool", "us": {"unfused": t_unf, "fused": t_fus, "torch": t_tor}})
     for name, B, h, c in layer_shapes(a.model, a.batch):
+        if only is not None and name not in only:
+            continue
         cin = 4 if c.small else c.cin
         x = torch.randn(B, h, h, cin, device=dev).half()
         if c.small:
