@@ -263,6 +263,14 @@ static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
     case 21: glds_cfg<256, 128, 32, 4, 2, 4, R, F>(a, st); return true;
     case 22: glds_cfg<128, 256, 32, 2, 4, 4, R, F>(a, st); return true;
     case 23: glds_cfg<64, 64, 64, 2, 2, 3, R, F>(a, st); return true;
+    case 24: glds_cfg<128, 128, 64, 2, 4, 3, R, F>(a, st); return true;   // 8 waves, 96 KiB
+    case 25: glds_cfg<256, 128, 64, 4, 2, 2, R, F>(a, st); return true;   // 8 waves, 96 KiB, dbuf
+    case 26: glds_cfg<128, 128, 64, 2, 2, 2, R, F>(a, st); return true;   // 64 KiB dbuf, 2 blk/CU
+    case 27: glds_cfg<64, 128, 64, 1, 4, 2, R, F>(a, st); return true;    // 48 KiB dbuf, 3 blk/CU
+    case 28: glds_cfg<64, 256, 32, 1, 4, 3, R, F>(a, st); return true;    // 60 KiB, 2 blk/CU
+    case 29: glds_cfg<64, 256, 64, 1, 8, 3, R, F>(a, st); return true;    // 8 waves, 120 KiB
+    case 30: glds_cfg<128, 256, 64, 2, 4, 2, R, F>(a, st); return true;   // 8 waves, 96 KiB dbuf
+    case 31: glds_cfg<64, 128, 32, 1, 4, 3, R, F>(a, st); return true;    // 36 KiB, 4 blk/CU
     default: return false;
   }
 }

@@ -50,6 +50,12 @@ __device__ __forceinline__ int swz64s(int row) {
   return (0x78 >> (2 * q)) & 3;
 }
 
+// Byte offset of 16-byte channel chunk c (0..7) of conv pixel p in the LDS conv
+// tile.  Rows are 128 B (64 fp16 channels); the chunk is XOR-swizzled by p & 7 so
+// the epilogue's 16 lanes (16 consecutive pixels, one channel chunk) hit 8
+// different 16-byte slots instead of one bank (16-way -> 2-way).
+__device__ __forceinline__ int conv_off(int p, int c) { return p * 128 + ((c ^ (p & 7)) << 4); }
+
 struct StemGeom {
   int B, H, W, Hc, Wc, Hp, Wp, tiles_x, tiles_y, ntiles;
 };
@@ -206,7 +212,7 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
           half4v o;
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = (half_t)(valid ? fmaxf(acc[i][r] + bv[i][r], 0.f) : 0.f);
-          *reinterpret_cast<half4v*>(conv + p * 128 + (i * 16 + fch * 4) * 2) = o;
+          *reinterpret_cast<half4v*>(conv + conv_off(p, i * 2 + (fch >> 1)) + (fch & 1) * 8) = o;
         }
       }
     }
@@ -224,12 +230,12 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
       const int c8 = i & 7, pp = i >> 3;
       const int py = pp / PT, px = pp - py * PT;
       if (py0 + py >= g.Hp || px0 + px >= g.Wp) continue;
-      half8v m = *reinterpret_cast<const half8v*>(conv + ((2 * py) * CR + 2 * px) * 128 + c8 * 16);
+      half8v m = *reinterpret_cast<const half8v*>(conv + conv_off((2 * py) * CR + 2 * px, c8));
 #pragma unroll
       for (int dy = 0; dy < PK; ++dy)
 #pragma unroll
         for (int dx = 0; dx < PK; ++dx) {
-          const half8v v = *reinterpret_cast<const half8v*>(conv + ((2 * py + dy) * CR + 2 * px + dx) * 128 + c8 * 16);
+          const half8v v = *reinterpret_cast<const half8v*>(conv + conv_off((2 * py + dy) * CR + 2 * px + dx, c8));
 #pragma unroll
           for (int j = 0; j < 8; ++j) m[j] = v[j] > m[j] ? v[j] : m[j];
         }

@@ -88,6 +88,12 @@ class Node:
                 h = RotatingFileHandler(self.log_path, maxBytes=100 << 20, backupCount=1)
                 h.setFormatter(logging.Formatter("%(asctime)s %(levelname)s %(message)s"))
                 lg.addHandler(h)
+            # full DEBUG log to the node's file (reference host.log); only ERROR to the console
+            lg.propagate = False
+            if not any(type(h) is logging.StreamHandler for h in lg.handlers):
+                sh = logging.StreamHandler()
+                sh.setLevel(logging.ERROR)
+                lg.addHandler(sh)
         return lg
 
     @property
