@@ -271,6 +271,13 @@ static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
     case 29: glds_cfg<64, 256, 64, 1, 8, 3, R, F>(a, st); return true;    // 8 waves, 120 KiB
     case 30: glds_cfg<128, 256, 64, 2, 4, 2, R, F>(a, st); return true;   // 8 waves, 96 KiB dbuf
     case 31: glds_cfg<64, 128, 32, 1, 4, 3, R, F>(a, st); return true;    // 36 KiB, 4 blk/CU
+    case 32: glds_cfg<128, 128, 32, 2, 2, 2, R, F>(a, st); return true;   // 32 KiB dbuf
+    case 33: glds_cfg<64, 256, 64, 1, 4, 2, R, F>(a, st); return true;    // 80 KiB dbuf
+    case 34: glds_cfg<128, 64, 64, 2, 2, 2, R, F>(a, st); return true;    // 48 KiB dbuf
+    case 35: glds_cfg<64, 64, 64, 2, 2, 2, R, F>(a, st); return true;     // 32 KiB dbuf, 5 blk/CU
+    case 36: glds_cfg<128, 128, 64, 2, 4, 2, R, F>(a, st); return true;   // 8 waves, 64 KiB dbuf
+    case 37: glds_cfg<64, 128, 64, 1, 8, 2, R, F>(a, st); return true;    // 8 waves, 48 KiB dbuf
+    case 38: glds_cfg<128, 64, 64, 2, 4, 2, R, F>(a, st); return true;    // 8 waves (32x16 wave tile)
     default: return false;
   }
 }
@@ -285,8 +292,9 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
 // profiles/r1_layer_sweep.md): 2 blocks/CU with a 4-deep BK=32 ring wins where
 // M is large; 128x64 tiles keep >= 2 waves of blocks when M is small (layer4).
 int conv_glds_pick(int M, int Cout) {
-  if (Cout % 128 == 0) return M >= 50000 ? 11 : 16;
-  return 15;
+  // sweep r1 #3: BK=64 double buffering with 2-3 workgroups/CU beats deeper rings
+  if (Cout % 128 == 0 && M >= 50000) return 26;   // 128x128, 64 KiB
+  return 27;                                       // 64x128, 48 KiB
 }
 
 }  // namespace idunno
