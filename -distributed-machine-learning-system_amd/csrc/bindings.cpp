@@ -109,7 +109,28 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
 }
 
 // uint8 [B,H,W,3] -> maxpool3x3/2(relu(conv7x7/2(normalise(img)) + bias)) : fp16 [B,Hp,Wp,64]
-torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias) {
+// Optional device-side window: with `start` (int64 GPU scalar) and batch > 0,
+// `img` is a whole image shard [N,H,W,3] and images [*start, *start + batch)
+// are used; the kernel clamps *start into [0, N - batch] so a bad descriptor
+// can never read outside the shard.
+static const long long* window_args(const torch::Tensor& img, const c10::optional<torch::Tensor>& start, int64_t batch,
+                                    int& B, long long& max_start) {
+  B = img.size(0);
+  max_start = 0;
+  if (!start.has_value() || !start->defined()) return nullptr;
+  const auto& s = *start;
+  CHECK_DEV(s);
+  CHECK_DT(s, torch::kLong);
+  TORCH_CHECK(s.numel() == 1, "start must be a 1-element int64 tensor");
+  TORCH_CHECK(s.device() == img.device(), "start must live on the image device");
+  TORCH_CHECK(batch > 0 && batch <= img.size(0), "window batch out of range");
+  B = (int)batch;
+  max_start = img.size(0) - batch;
+  return reinterpret_cast<const long long*>(s.data_ptr());
+}
+
+torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias, c10::optional<torch::Tensor> start,
+                         int64_t batch) {
   CHECK_DEV(img);
   CHECK_DEV(w);
   CHECK_DEV(bias);
@@ -122,7 +143,10 @@ torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias)
   TORCH_CHECK(img.dim() == 4 && img.size(3) == 3, "img must be [B, H, W, 3] uint8");
   TORCH_CHECK(w.dim() == 2 && w.size(0) == 64 && w.size(1) == 7 * 32, "stem weight must be [64, 7*32] (small-C packing)");
   TORCH_CHECK(bias.numel() == 64, "bias must have 64 entries");
-  const int B = img.size(0), H = img.size(1), W = img.size(2);
+  const int H = img.size(1), W = img.size(2);
+  int B;
+  long long max_start;
+  const long long* sp = window_args(img, start, batch, B, max_start);
   TORCH_CHECK(H >= 7 && W >= 7, "image too small");
   TORCH_CHECK((long)B * H * W * 3 < (1L << 31), "batch too large");
   const int Hc = (H + 6 - 7) / 2 + 1, Wc = (W + 6 - 7) / 2 + 1;
@@ -130,18 +154,23 @@ torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias)
   auto y = torch::empty({B, Hp, Wp, 64}, img.options().dtype(torch::kHalf));
   if (B)
     stem_fused_launch(img.data_ptr<uint8_t>(), reinterpret_cast<const half_t*>(w.data_ptr()), bias.data_ptr<float>(),
-                      reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, cur_stream());
+                      reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp, max_start, cur_stream());
   return y;
 }
 
-torch::Tensor preprocess(torch::Tensor img) {
+torch::Tensor preprocess(torch::Tensor img, c10::optional<torch::Tensor> start, int64_t batch) {
   CHECK_DEV(img);
   CHECK_CONTIG(img);
   CHECK_DT(img, torch::kUInt8);
   TORCH_CHECK(img.dim() == 4 && img.size(3) == 3, "img must be [B, H, W, 3] uint8");
-  auto out = torch::empty({img.size(0), img.size(1), img.size(2), 4}, img.options().dtype(torch::kHalf));
-  const long npix = img.size(0) * img.size(1) * img.size(2);
-  if (npix) preprocess_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), npix, cur_stream());
+  int B;
+  long long max_start;
+  const long long* sp = window_args(img, start, batch, B, max_start);
+  auto out = torch::empty({B, img.size(1), img.size(2), 4}, img.options().dtype(torch::kHalf));
+  const long npix = (long)B * img.size(1) * img.size(2);
+  if (npix)
+    preprocess_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), npix, sp, max_start,
+                      (long)img.size(1) * img.size(2), cur_stream());
   return out;
 }
 
@@ -220,8 +249,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_nhwc", &conv2d_nhwc, "implicit-GEMM MFMA conv + bias (+res) (+relu)", py::arg("x"), py::arg("w"),
         py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("relu"), py::arg("out_f32") = false, py::arg("tile") = -1);
-  m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 NHWC4");
-  m.def("stem_fused", &stem_fused, "fused normalise + conv7x7/2 + bias + relu + maxpool3x3/2 (ResNet stem)");
+  m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 NHWC4", py::arg("img"),
+        py::arg("start") = py::none(), py::arg("batch") = -1);
+  m.def("stem_fused", &stem_fused, "fused normalise + conv7x7/2 + bias + relu + maxpool3x3/2 (ResNet stem)",
+        py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("start") = py::none(), py::arg("batch") = -1);
   m.def("resize_crop", &resize_crop, "bilinear resize + centre crop + normalise");
   m.def("maxpool2d_nhwc", &maxpool2d_nhwc, "NHWC max pool");
   m.def("global_avgpool_nhwc", &global_avgpool_nhwc, "NHWC global average pool");

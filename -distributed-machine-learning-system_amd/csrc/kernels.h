@@ -30,8 +30,9 @@ int conv_pick_tile(int M, int Cout);
 bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 int conv_glds_pick(int M, int Cout);
 void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, half_t* y, int B, int H, int W,
-                       hipStream_t st);
-void preprocess_launch(const uint8_t* img, half_t* out, long npix, hipStream_t st);
+                       const long long* start_idx, long long max_start, hipStream_t st);
+void preprocess_launch(const uint8_t* img, half_t* out, long npix, const long long* start_idx,
+                       long long max_start, long pix_per_img, hipStream_t st);
 void resize_crop_launch(const uint8_t* img, half_t* out, int B, int Hi, int Wi, int Hr, int Wr,
                         int crop, hipStream_t st);
 void maxpool_launch(const half_t* x, half_t* y, int B, int H, int W, int C, int Ho, int Wo, int k,

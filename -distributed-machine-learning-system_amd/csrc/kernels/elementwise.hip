@@ -18,10 +18,18 @@ __constant__ float kMean[3] = {0.485f, 0.456f, 0.406f};
 __constant__ float kInvStd[3] = {1.0f / 0.229f, 1.0f / 0.224f, 1.0f / 0.225f};
 
 // One thread per pixel: 3 bytes in, 8 bytes (4 halfs) out.
+// Optional device-side window: images start at *start_idx (clamped to
+// [0, max_start]) of the shard `img`.
 __global__ void preprocess_kernel(const uint8_t* __restrict__ img, half_t* __restrict__ out,
-                                  long npix) {
+                                  long npix, const long long* __restrict__ start_idx, long long max_start,
+                                  long pix_per_img) {
   const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npix) return;
+  if (start_idx != nullptr) {
+    long long s0 = *start_idx;
+    s0 = s0 < 0 ? 0 : (s0 > max_start ? max_start : s0);
+    img += (size_t)s0 * pix_per_img * 3;
+  }
   const uint8_t* s = img + p * 3;
   half4v o;
   o[0] = (half_t)(((float)s[0] * (1.f / 255.f) - kMean[0]) * kInvStd[0]);
@@ -31,10 +39,12 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ img, half_t* __res
   *reinterpret_cast<half4v*>(out + p * 4) = o;
 }
 
-void preprocess_launch(const uint8_t* img, half_t* out, long npix, hipStream_t st) {
+void preprocess_launch(const uint8_t* img, half_t* out, long npix, const long long* start_idx,
+                       long long max_start, long pix_per_img, hipStream_t st) {
   const int bs = 256;
   const long grid = (npix + bs - 1) / bs;
-  hipLaunchKernelGGL(preprocess_kernel, dim3((unsigned)grid), dim3(bs), 0, st, img, out, npix);
+  hipLaunchKernelGGL(preprocess_kernel, dim3((unsigned)grid), dim3(bs), 0, st, img, out, npix, start_idx,
+                     max_start, pix_per_img);
 }
 
 // Bilinear resize of an (Hi x Wi) uint8 HWC image so that its shorter side is

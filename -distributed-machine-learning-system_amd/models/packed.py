@@ -259,18 +259,23 @@ class HipRunner:
         self._graphs: dict[int, tuple] = {}
 
     # -- eager forward ------------------------------------------------------
-    def logits(self, img_u8: torch.Tensor) -> torch.Tensor:
+    def logits(self, img_u8: torch.Tensor, start: torch.Tensor | None = None, batch: int = -1) -> torch.Tensor:
+        """fp32 logits.  With ``start`` (int64 GPU scalar) and ``batch``,
+        ``img_u8`` is a whole HBM-resident shard and the images
+        [*start, *start + batch) are classified (device-side window)."""
         o = self.ops
         p = self.p
         native = tuple(img_u8.shape[1:3]) == (224, 224)
+        if start is not None and not native:
+            raise ValueError("device-side windows need 224x224 shards")
         s = p.stem
         fused = (self.fuse_stem and native and p.kind == "resnet" and s.small and s.kh == 7 and s.kw == 7
                  and s.stride == 2 and s.pad == 3 and s.cout == 64)
         if not fused:
-            x = o.preprocess(img_u8) if native else o.resize_crop(img_u8, 256, 224)
+            x = o.preprocess(img_u8, start, batch) if native else o.resize_crop(img_u8, 256, 224)
         if p.kind == "resnet":
             if fused:
-                x = o.stem_fused(img_u8, s.w, s.b)
+                x = o.stem_fused(img_u8, s.w, s.b, start, batch)
             else:
                 x = o.conv2d(x, s.w, s.b, s.kh, s.kw, s.stride, s.pad, s.relu)
                 x = o.maxpool2d(x, 3, 2, 1)
@@ -297,10 +302,35 @@ class HipRunner:
             x = o.linear(x, fc.w, fc.b, relu=fc.relu, out_f32=last)
         return x
 
-    def forward(self, img_u8: torch.Tensor):
-        return self.ops.softmax_top1(self.logits(img_u8))
+    def forward(self, img_u8: torch.Tensor, start: torch.Tensor | None = None, batch: int = -1):
+        return self.ops.softmax_top1(self.logits(img_u8, start, batch))
 
     __call__ = forward
+
+    def capture_window(self, shard: torch.Tensor, batch: int):
+        """hipGraph of forward over a device-side window of ``shard``.
+
+        Returns (start, replay): write the first image index into the int64
+        GPU scalar ``start`` (a stream-ordered device op, e.g. from an RCCL
+        broadcast of the query descriptor), then ``replay()`` -> (cls, prob).
+        No host round trip and no staging copy of the images."""
+        key = ("win", shard.data_ptr(), tuple(shard.shape), batch)
+        if key in self._graphs:
+            g, start, sout = self._graphs[key]
+            return start, (lambda: (g.replay(), sout)[1])
+        start = torch.zeros(1, dtype=torch.int64, device=self.device)
+        with _CAPTURE_LOCK:
+            st = torch.cuda.Stream(device=self.device)
+            st.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(st):
+                for _ in range(2):
+                    self.forward(shard, start, batch)
+            torch.cuda.current_stream(self.device).wait_stream(st)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                sout = self.forward(shard, start, batch)
+        self._graphs[key] = (g, start, sout)
+        return start, (lambda: (g.replay(), sout)[1])
 
     # -- hipGraph -------------------------------------------------------------
     def capture(self, batch: int, hw: int = 224):

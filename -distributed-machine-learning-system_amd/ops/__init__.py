@@ -27,9 +27,11 @@ def linear(x, w, bias, relu: bool = False, out_f32: bool = False):
     return y.view(b, w.shape[0])
 
 
-def preprocess(img_u8):
-    """uint8 [B,H,W,3] -> normalised fp16 [B,H,W,4] (4th channel zero)."""
-    return load().preprocess(img_u8)
+def preprocess(img_u8, start=None, batch: int = -1):
+    """uint8 [B,H,W,3] -> normalised fp16 [B,H,W,4] (4th channel zero).
+    With ``start`` (int64 GPU scalar) and ``batch``, reads images
+    [*start, *start+batch) of the shard ``img_u8`` (device-side window)."""
+    return load().preprocess(img_u8, start, batch)
 
 
 def resize_crop(img_u8, resize: int = 256, crop: int = 224):
@@ -37,9 +39,10 @@ def resize_crop(img_u8, resize: int = 256, crop: int = 224):
     return load().resize_crop(img_u8, resize, crop)
 
 
-def stem_fused(img_u8, w, bias):
-    """ResNet stem in one kernel: uint8 [B,H,W,3] -> fp16 [B,H/4,W/4,64]."""
-    return load().stem_fused(img_u8, w, bias)
+def stem_fused(img_u8, w, bias, start=None, batch: int = -1):
+    """ResNet stem in one kernel: uint8 [B,H,W,3] -> fp16 [B,H/4,W/4,64]
+    (optionally a device-side window of a shard, see ``preprocess``)."""
+    return load().stem_fused(img_u8, w, bias, start, batch)
 
 
 def maxpool2d(x, k: int = 3, s: int = 2, pad: int = 1):

@@ -93,6 +93,27 @@ class QueryPlane:
         row = self._desc[self.env.rank].tolist()
         return tuple(int(v) for v in row)
 
+    def dispatch_device(self, table: list[tuple[int, int, int, int]] | None, slot: int = 0) -> torch.Tensor:
+        """Asynchronous dispatch: no host synchronisation anywhere.
+
+        The coordinator stages the table in pinned host memory (``slot`` picks
+        one of two buffers so a table is never overwritten while its copy is
+        in flight), copies it to the device and broadcasts it; every rank gets
+        back a *device* view of its own row, which the forward graph consumes
+        directly (e.g. as the shard window start)."""
+        if not hasattr(self, "_desc_host"):
+            pin = self.env.device.type == "cuda"
+            self._desc_host = [torch.full((self.env.world, 4), NO_WORK, dtype=torch.int64, pin_memory=pin)
+                               for _ in range(2)]
+        if self.env.rank == self.coord:
+            assert table is not None and len(table) == self.env.world
+            h = self._desc_host[slot % 2]
+            h.copy_(torch.tensor(table, dtype=torch.int64))
+            self._desc.copy_(h, non_blocking=True)
+        if self.env.distributed:
+            dist.broadcast(self._desc, src=self.coord, group=self.group)
+        return self._desc[self.env.rank]
+
     # -- M11 --------------------------------------------------------------------
     def pack(self, cls: torch.Tensor, prob: torch.Tensor) -> torch.Tensor:
         n = cls.numel()

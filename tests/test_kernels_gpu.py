@@ -204,6 +204,22 @@ def test_hipgraph_replay_matches_eager(ops):
     assert torch.allclose(p0, p1)
 
 
+@pytest.mark.parametrize("fuse", [True, False])
+def test_device_window_graph_matches_slices(ops, fuse):
+    from idunno.models import HipRunner, build_program
+
+    runner = HipRunner(build_program("resnet18", seed=5), fuse_stem=fuse)
+    shard = ops.synth_images(99, 0, 40, "cuda")
+    start, run = runner.capture_window(shard, 8)
+    for s0 in (0, 13, 32, 35):     # 35 > 40 - 8: clamped to 32 on the device
+        start.fill_(s0)
+        c1, p1 = run()
+        s = min(s0, 32)
+        c0, p0 = runner.forward(shard[s:s + 8].contiguous())
+        torch.cuda.synchronize()
+        assert torch.equal(c0, c1) and torch.allclose(p0, p1)
+
+
 @pytest.mark.parametrize("B,H", [(3, 224), (2, 64), (1, 100)])
 def test_stem_fused_vs_fp32(ops, B, H):
     from idunno.models.packed import pack_conv_weight
