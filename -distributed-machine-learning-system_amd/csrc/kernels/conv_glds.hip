@@ -292,9 +292,10 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
 // profiles/r1_layer_sweep.md): 2 blocks/CU with a 4-deep BK=32 ring wins where
 // M is large; 128x64 tiles keep >= 2 waves of blocks when M is small (layer4).
 int conv_glds_pick(int M, int Cout) {
-  // sweep r1 #3: BK=64 double buffering with 2-3 workgroups/CU beats deeper rings
-  if (Cout % 128 == 0 && M >= 50000) return 26;   // 128x128, 64 KiB
-  return 27;                                       // 64x128, 48 KiB
+  // sweeps r1 #3/#4: BK=64 double buffering with 2-3 workgroups/CU beats deeper
+  // rings; 8 waves per 128x128 tile (4 waves/SIMD) best where M is large
+  if (Cout % 128 == 0) return M >= 50000 ? 36 : 34;   // 128x128 8-wave | 128x64
+  return 27;                                           // 64x128, 48 KiB
 }
 
 }  // namespace idunno

@@ -154,6 +154,14 @@ def main(argv=None) -> int:
         t = torch.tensor([elapsed], device=env.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    p50_loaded = statistics.median(lat) if lat else None
+
+    # Unloaded query latency (outside the timed throughput region): one round at
+    # a time, each submitted only after the previous one's results were ingested.
+    lat.clear()
+    for q in range(a.warmup + a.steps, a.warmup + a.steps + max(5, min(a.steps, 20))):
+        step(q)
+        barrier()
 
     if coord:
         imgs = env.world * B * a.steps
@@ -177,6 +185,7 @@ def main(argv=None) -> int:
                        "image_hw": 224, "batch_per_gpu": B,
                        "parallelism": f"dp{env.world}", "graph": not a.no_graph},
             "p50_query_latency_s": round(p50, 6) if p50 else None,
+            "p50_query_latency_loaded_s": round(p50_loaded, 6) if p50_loaded else None,
             "p50_vs_baseline_speedup": round(BASELINE_P50_S / p50, 1) if p50 else None,
             "model_tflops": round(flops * ips / 1e12, 2),
             "results_recorded": state.images_done(a.model),

@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Full-cluster benchmark through the node runtime (control plane + HIP executors),
+the analogue of the reference report's experiments (BASELINE.json
+configs 3 and 4):
+
+  * two concurrent jobs, AlexNet (500-image queries) and ResNet18 (400-image
+    queries), over `--nodes` nodes with the fair-time scheduler;
+  * per-model query latency (p50 / mean), whole-cluster images/s, workers per
+    query, and the c1/c2 views;
+  * optional coordinator kill mid-job (`--kill-coordinator-after S`): the
+    standby must promote itself and finish both jobs.
+
+Nodes are in-process over localhost TCP; node i uses cuda:(i % ngpus), so on
+a 1-GPU box all nodes share the GPU (throughput is then the single GPU's).
+
+usage: python tools/bench_cluster.py [--nodes 8] [--images 10000] [--kill-coordinator-after 0]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=8)
+    ap.add_argument("--images", type=int, default=10000)
+    ap.add_argument("--executor", default="hip", choices=["hip", "fake", "torch"])
+    ap.add_argument("--kill-coordinator-after", type=float, default=0.0)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    import logging
+
+    import torch
+
+    logging.basicConfig(level=logging.ERROR)
+    from bench_recovery import free_base
+    from idunno.runtime.cluster import LocalCluster
+    from idunno.runtime.data import SyntheticSource
+    from idunno.runtime.executor import FakeExecutor, HipExecutor, TorchExecutor
+
+    ngpu = max(1, torch.cuda.device_count()) if a.executor == "hip" else 1
+
+    def exf(i):
+        if a.executor == "hip":
+            return HipExecutor(f"cuda:{i % ngpu}", seed=0)
+        if a.executor == "torch":
+            return TorchExecutor("cpu")
+        return FakeExecutor()
+
+    def srcf(i, node):
+        if a.executor == "hip":
+            return SyntheticSource(node.cfg.data_seed, f"cuda:{i % ngpu}")
+        if a.executor == "torch":
+            return SyntheticSource(node.cfg.data_seed, "cpu")
+        return None
+
+    c = LocalCluster(num_nodes=a.nodes, transport="tcp", base_port=free_base(a.nodes), executor_factory=exf,
+                     source_factory=srcf, heartbeat_period_s=0.3, failure_timeout_s=2.0,
+                     metadata_period_s=0.5, rpc_timeout_s=30.0).start()
+    out = {"nodes": a.nodes, "gpus": ngpu, "executor": a.executor, "images_per_job": a.images}
+    try:
+        cl = c.client(c.cfg.node_name(a.nodes - 2))
+        # warm-up: capture graphs for the chunk sizes the fair-time split will produce
+        cl.inference(10 ** 6, 10 ** 6 + 400 * 2 - 1, "resnet18")
+        cl.inference(10 ** 6, 10 ** 6 + 500 * 2 - 1, "alexnet")
+        cl.wait_idle(600)
+        coord = c.coordinator()
+        base = {m: coord.state.images_done(m) for m in ("alexnet", "resnet18")}
+        t0 = time.perf_counter()
+        ta = cl.submit_job(0, a.images - 1, "alexnet")
+        t_second = time.perf_counter()
+        tr = cl.submit_job(0, a.images - 1, "resnet18")
+        out["second_job_start_s"] = time.perf_counter() - t_second
+        killed = False
+        want = {m: base[m] + a.images for m in base}
+        while True:
+            if a.kill_coordinator_after and not killed and time.perf_counter() - t0 > a.kill_coordinator_after:
+                c.crash(c.cfg.coordinator_name)
+                killed = True
+                t_kill = time.perf_counter()
+            try:
+                s = cl.view("summary")
+            except Exception:  # noqa: BLE001  (during failover)
+                time.sleep(0.05)
+                continue
+            if all(s["done"].get(m, 0) >= want[m] for m in want) and s["pending"] == 0:
+                break
+            if time.perf_counter() - t0 > 1800:
+                raise TimeoutError(s)
+            time.sleep(0.01)
+        wall = time.perf_counter() - t0
+        coord = c.coordinator()
+        lat = {m: coord.state.query_latency.get(m, [])[-(a.images // coord.cfg.batch_for(m)):] for m in want}
+        workers = {}
+        for (m, q), ents in coord.state.worker_set.items():
+            workers.setdefault(m, []).append(len({e[0] for e in ents}))
+        out.update({
+            "wall_s": round(wall, 3),
+            "images_per_s": round(2 * a.images / wall, 1),
+            "query_latency_p50_s": {m: round(statistics.median(v), 4) for m, v in lat.items() if v},
+            "query_latency_mean_s": {m: round(statistics.mean(v), 4) for m, v in lat.items() if v},
+            "workers_per_query_median": {m: statistics.median(v) for m, v in workers.items()},
+            "coordinator_killed": killed,
+            "final_coordinator": coord.name,
+            "c1": cl.view("c1")["text"],
+            "c2": cl.view("c2")["text"],
+            "job_replies": [ta, tr],
+        })
+        if killed:
+            out["failover_to_done_s"] = round(time.perf_counter() - t_kill, 3)
+    finally:
+        c.stop()
+    print(json.dumps(out, indent=1, default=str))
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1, default=str)
+
+
+if __name__ == "__main__":
+    main()
