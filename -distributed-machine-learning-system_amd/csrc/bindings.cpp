@@ -7,6 +7,8 @@
 #include <ATen/hip/HIPContext.h>
 #include <torch/extension.h>
 
+#include <mutex>
+
 #include "kernels.h"
 
 using namespace idunno;
@@ -14,14 +16,29 @@ using namespace idunno;
 static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
 // 256 zero bytes per device: the DMA source of padding taps / masked rows.
+// Created once per device under a lock and never freed: several node threads
+// share one GPU, and a buffer replaced by a racing thread would go back to the
+// caching allocator while kernels still read it as "zeros".
 static torch::Tensor zero_buffer(const torch::Device& dev) {
-  static std::vector<torch::Tensor> bufs(64);
+  static std::mutex mu;
+  static std::vector<torch::Tensor>* bufs = new std::vector<torch::Tensor>(64);
   const int i = dev.index() < 0 ? 0 : dev.index();
   TORCH_CHECK(i < 64, "device index out of range");
-  if (!bufs[i].defined())
-    bufs[i] = torch::zeros({256}, torch::TensorOptions().dtype(torch::kUInt8).device(dev));
-  return bufs[i];
+  std::lock_guard<std::mutex> lk(mu);
+  auto& b = (*bufs)[i];
+  if (!b.defined()) {
+    b = torch::zeros({256}, torch::TensorOptions().dtype(torch::kUInt8).device(dev));
+    // other threads' streams will read it: make the fill complete before publishing
+    (void)hipStreamSynchronize(cur_stream());
+  }
+  return b;
 }
+
+// Whether auto tile selection routes 3x3/s1 convs to the LDS-patch kernel
+// (set_conv3x3_patch_default from Python; off until the per-layer sweep says so).
+static bool g_patch_default = false;
+static bool conv3x3_patch_default() { return g_patch_default; }
+void set_conv3x3_patch_default(bool on) { g_patch_default = on; }
 
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
@@ -103,6 +120,14 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     return y;
   }
   a.zero = zero_buffer(x.device()).data_ptr();
+  const bool patch_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 &&
+                        conv3x3_patch_supported(H, W, C, Cout);
+  if (tile == 40 || (tile < 0 && patch_ok && conv3x3_patch_default())) {
+    TORCH_CHECK(patch_ok, "tile 40 (LDS-patch 3x3 conv) does not support this shape");
+    conv3x3_patch_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W, C, Cout,
+                         a.relu, cur_stream());
+    return y;
+  }
   const int t = tile >= 10 ? (int)tile : conv_glds_pick(a.M, Cout);
   TORCH_CHECK(conv_glds_launch(a, out_f32, t, cur_stream()), "unknown conv tile id ", t);
   return y;
@@ -259,4 +284,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_top1", &softmax_top1, "fused row softmax + argmax");
   m.def("synth_images", &synth_images, "deterministic synthetic uint8 images [n,hw,hw,3]");
   m.def("pick_tile", &pick_tile, "tile id the conv heuristic picks for (M, Cout)");
+  m.def("set_conv3x3_patch_default", &set_conv3x3_patch_default,
+        "route auto-tiled 3x3/s1 convs to the LDS-patch kernel (tile 40)");
 }

@@ -28,6 +28,9 @@ struct ConvArgs {
 void conv_igemm_launch(ConvArgs a, bool small, bool out_f32, int tile, hipStream_t st);
 int conv_pick_tile(int M, int Cout);
 bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
+bool conv3x3_patch_supported(int H, int W, int C, int Cout);
+void conv3x3_patch_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
+                          const void* zero, int B, int H, int W, int C, int Cout, int relu, hipStream_t st);
 int conv_glds_pick(int M, int Cout);
 void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, half_t* y, int B, int H, int W,
                        const long long* start_idx, long long max_start, hipStream_t st);

@@ -85,6 +85,33 @@ class JobState:
         self.seq = 0                                    # mutation counter (standby replication)
         self.query_submit_time: dict = {}
         self.query_latency: dict = defaultdict(list)    # model -> [end-to-end seconds]
+        self.jobs: dict = {}                            # job id -> {model, start, end, next}
+
+    # -- coordinator-side jobs (C28 variant), replicated to the standby ----------
+    def add_job(self, model: str, start: int, end: int) -> int:
+        with self.lock:
+            jid = len(self.jobs) + 1
+            self.jobs[jid] = {"model": model, "start": int(start), "end": int(end), "next": int(start)}
+            self.seq += 1
+            return jid
+
+    def advance_job(self, jid: int, nxt: int) -> None:
+        with self.lock:
+            self.jobs[jid]["next"] = int(nxt)
+            self.seq += 1
+
+    def unfinished_jobs(self) -> list[int]:
+        with self.lock:
+            return [j for j, v in self.jobs.items() if v["next"] <= v["end"]]
+
+    def range_submitted(self, model: str, s: int, e: int) -> bool:
+        """True if some query of ``model`` already covers exactly [s, e] chunks
+        (used when a promoted standby resumes a job from a lagging snapshot)."""
+        with self.lock:
+            for (m, _q), ents in self.worker_set.items():
+                if m == model and ents and min(x[1] for x in ents) == s and max(x[2] for x in ents) == e:
+                    return True
+            return False
 
     # -- ids --------------------------------------------------------------------
     def new_query_number(self, model: str) -> int:
@@ -283,6 +310,7 @@ class JobState:
                 "next_qnum": dict(self.next_qnum),
                 "meta": dict(self.query_processing_time_meta),
                 "submit": [[list(k), t] for k, t in self.query_submit_time.items()],
+                "jobs": [[j, v] for j, v in self.jobs.items()],
             }
 
     def restore(self, snap: dict, keep_results: bool = False) -> None:
@@ -327,3 +355,7 @@ class JobState:
             self.query_processing_time_meta.update(snap["meta"])
             for k, t in snap.get("submit", []):
                 self.query_submit_time.setdefault((k[0], k[1]), t)
+            for j, v in snap.get("jobs", []):
+                cur = self.jobs.get(j)
+                if cur is None or v["next"] > cur["next"]:
+                    self.jobs[j] = dict(v)

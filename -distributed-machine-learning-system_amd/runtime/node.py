@@ -68,6 +68,7 @@ class Node:
         self._threads: list[threading.Thread] = []
         self.promotions = 0
         self._retries: dict = {}
+        self.transport.dead_check = self._peer_dead
         self.membership.on_failure.append(self._on_node_failure)
         self.membership.on_master_failure.append(self._on_master_failure)
         self.membership.on_master_change.append(self._on_master_change)
@@ -168,6 +169,15 @@ class Node:
             return None
         return {"ok": False, "error": f"unknown message {t}"}
 
+    def _peer_dead(self, dst: str) -> bool:
+        """Failure-detector view used to abandon in-flight requests early."""
+        m = self.membership
+        if dst == m.master and m.master_suspected:
+            return True
+        with m.lock:
+            e = m.members.get(dst)
+        return e is not None and e[1] != "RUNNING"
+
     def crash(self) -> None:
         """Fault injection: stop answering everything (like a killed VM)."""
         self.logger.warning("%s crashing (fault injection)", self.name)
@@ -214,18 +224,30 @@ class Node:
                                            "job": True}, self.cfg.rpc_timeout_s)
         model = canonical(model)
         bs = self.cfg.batch_for(model)
-        ranges = [(i, min(i + bs - 1, end)) for i in range(start, end + 1, bs)]
+        jid = self.state.add_job(model, start, end)
+        self._start_job_runner(jid)
+        return {"ok": True, "job": jid, "queries": (end - start) // bs + 1}
+
+    def _start_job_runner(self, jid: int) -> None:
+        """Submit the job's remaining batch-size queries.  The job cursor lives in
+        the replicated job state, so a promoted standby resumes it (skipping a
+        range the old coordinator had already dispatched)."""
 
         def run():
-            for k, (s, e) in enumerate(ranges):
-                if self._stop.is_set() or not self.is_coordinator:
+            while not self._stop.is_set() and self.is_coordinator:
+                with self.state.lock:
+                    job = dict(self.state.jobs[jid])
+                s = job["next"]
+                if s > job["end"]:
                     return
-                self.submit_query(model, s, e)
-                if self.cfg.client_query_interval_s and k + 1 < len(ranges):
+                e = min(s + self.cfg.batch_for(job["model"]) - 1, job["end"])
+                if not self.state.range_submitted(job["model"], s, e):
+                    self.submit_query(job["model"], s, e)
+                self.state.advance_job(jid, e + 1)
+                if self.cfg.client_query_interval_s and e < job["end"]:
                     time.sleep(self.cfg.client_query_interval_s)
 
-        threading.Thread(target=run, name=f"{self.name}-job", daemon=True).start()
-        return {"ok": True, "queries": len(ranges)}
+        threading.Thread(target=run, name=f"{self.name}-job{jid}", daemon=True).start()
 
     def _send_job(self, worker: str, model: str, qnum, s: int, e: int) -> bool:
         msg = {"t": Type.JOB, "model": model, "qnum": qnum, "start": s, "end": e,
@@ -365,6 +387,8 @@ class Node:
                 if nw:
                     self.state.reassign(w, nw, (model, qnum, s, e))
                     self._send_job(nw, model, qnum, s, e)
+        for jid in self.state.unfinished_jobs():      # coordinator-side jobs carry on here
+            self._start_job_runner(jid)
         self.logger.warning("promotion done in %.3fs", time.monotonic() - t0)
 
     def _on_master_change(self, new: str, epoch: int) -> None:

@@ -44,6 +44,7 @@ class BaseTransport:
         self._pending: dict[int, Future] = {}
         self._plock = threading.Lock()
         self.closed = False
+        self.dead_check = None          # optional f(dst) -> True once the FD declares dst dead
 
     # subclasses implement _send_raw(dst, msg) -> bool
     def _send_raw(self, dst: str, msg: dict) -> bool:  # pragma: no cover
@@ -67,7 +68,18 @@ class BaseTransport:
         try:
             if not self._send_raw(dst, msg):
                 raise TransportError(f"{dst} unreachable")
-            return fut.result(timeout=timeout)
+            # wait in slices so a peer the failure detector declares dead fails
+            # the call at once instead of holding the caller for the full timeout
+            end = time.monotonic() + timeout
+            while True:
+                left = end - time.monotonic()
+                if left <= 0:
+                    raise FuturesTimeout()
+                try:
+                    return fut.result(timeout=min(left, 0.05))
+                except (TimeoutError, FuturesTimeout):
+                    if self.dead_check is not None and self.dead_check(dst):
+                        raise TransportError(f"{dst} declared dead while waiting for {msg.get('t')}")
         except (TimeoutError, FuturesTimeout) as e:
             raise TransportError(f"request {msg.get('t')} to {dst} timed out") from e
         finally:

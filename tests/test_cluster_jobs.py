@@ -21,6 +21,25 @@ def test_job_submission_batched_by_coordinator():
         c.stop()
 
 
+def test_job_resumed_by_promoted_standby():
+    """A coordinator-side job that is still being cut into queries when the
+    coordinator dies is resumed by the standby from the replicated job cursor."""
+    c = LocalCluster(num_nodes=5, client_query_interval_s=0.05, **FAST).start()
+    try:
+        cl = c.client("node03")
+        r = cl.submit_job(0, 3999, "resnet18")          # 10 queries, 50 ms apart
+        assert r["queries"] == 10
+        import time
+
+        time.sleep(0.22)                                  # a few queries dispatched
+        c.crash("node00")
+        s = cl.wait_idle(15, {"resnet18": 4000})
+        assert s["done"]["resnet18"] == 4000, s           # nothing lost, nothing double counted
+        assert c.coordinator().name == "node04"
+    finally:
+        c.stop()
+
+
 def test_straggler_resend():
     c = LocalCluster(num_nodes=4, straggler_resend=True, straggler_timeout_s=0.3, **FAST).start()
     try:
