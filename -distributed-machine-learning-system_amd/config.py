@@ -50,6 +50,10 @@ class ClusterConfig:
     replication: int = 4                     # reference places 4-5 replicas (utils.py:48-55)
     store_root: str = "/tmp/idunno"
 
+    # -- checkpoint / resume ----------------------------------------------------
+    checkpoint_period_s: float = 0.0         # coordinator writes state to disk (0 = off)
+    resume: bool = False                     # coordinator restarts from its checkpoint
+
     # -- misc -------------------------------------------------------------------
     log_dir: str = ""
     rpc_timeout_s: float = 5.0

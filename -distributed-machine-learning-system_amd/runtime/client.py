@@ -111,6 +111,25 @@ class Client:
                 lines.append(f"{n}: <unreachable>")
         return lines
 
+    def trace(self, path: str) -> int:
+        """Collect every live node's spans into one Chrome trace file."""
+        from ..utils.tracing import write_chrome_trace
+
+        lists = []
+        for n in self.node.membership.alive():
+            try:
+                if n == self.node.name:
+                    lists.append(self.node.tracer.export())
+                else:
+                    lists.append(self.node.transport.request(n, {"t": Type.STATS, "view": "trace"},
+                                                             self.cfg.rpc_timeout_s).get("events", []))
+            except TransportError:
+                pass
+        return write_chrome_trace(path, lists)
+
+    def checkpoint(self) -> dict:
+        return self._call({"t": Type.STATS, "view": "checkpoint"})
+
     def kill(self, node: str, mode: str = "crash", seconds: float = 1.0) -> bool:
         if node == self.node.name:
             self.node.handle({"t": Type.KILL, "mode": mode, "seconds": seconds, "src": self.node.name})

@@ -41,6 +41,7 @@ from .ring import replica_neighbors
 from .scheduler import FairTimeScheduler
 from .sdfs import Sdfs
 from .transport import TransportError
+from ..utils.tracing import Tracer
 
 log = logging.getLogger("idunno.node")
 
@@ -68,6 +69,7 @@ class Node:
         self._threads: list[threading.Thread] = []
         self.promotions = 0
         self._retries: dict = {}
+        self.tracer = Tracer(name)
         self.transport.dead_check = self._peer_dead
         self.membership.on_failure.append(self._on_node_failure)
         self.membership.on_master_failure.append(self._on_master_failure)
@@ -111,6 +113,12 @@ class Node:
             self._threads.append(th)
         if join:
             self.join_with_retry()
+        if self.cfg.resume and self.is_coordinator:
+            def resume():   # let the workers join first
+                time.sleep(self.cfg.failure_timeout_s)
+                n = self.resume_from_checkpoint()
+                self.logger.warning("resumed: re-sent %d chunks", n)
+            threading.Thread(target=resume, name=f"{self.name}-resume", daemon=True).start()
         self.logger.info("node %s started (master=%s)", self.name, self.membership.master)
         return self
 
@@ -169,6 +177,59 @@ class Node:
             return None
         return {"ok": False, "error": f"unknown message {t}"}
 
+    # -- checkpoint / resume ------------------------------------------
+    def checkpoint_path(self) -> str:
+        return os.path.join(self.cfg.store_root, self.name, "checkpoint.msgpack")
+
+    def save_checkpoint(self, path: str | None = None) -> str:
+        """Atomically write the coordinator state (job tables incl. results, job
+        cursors, SDFS metadata, scheduler averages) to disk."""
+        import msgpack
+
+        path = path or self.checkpoint_path()
+        snap = {"epoch": self.membership.epoch, "node": self.name, "time": time.time(),
+                "jobs": self.state.snapshot(include_results=True), "sdfs": self.sdfs.snapshot(),
+                "avg_time": dict(self.sched.avg_time)}
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(msgpack.packb(snap, use_bin_type=True))
+        os.replace(tmp, path)
+        return path
+
+    def load_checkpoint(self, path: str | None = None) -> bool:
+        import msgpack
+
+        path = path or self.checkpoint_path()
+        if not os.path.exists(path):
+            return False
+        with open(path, "rb") as f:
+            snap = msgpack.unpackb(f.read(), raw=False, strict_map_key=False)
+        self.state.restore(snap["jobs"])
+        self.sdfs.restore(snap["sdfs"])
+        self.sched.avg_time.update(snap.get("avg_time", {}))
+        self.logger.warning("restored checkpoint %s (seq %s)", path, snap["jobs"].get("seq"))
+        return True
+
+    def resume_from_checkpoint(self, path: str | None = None) -> int:
+        """Coordinator restart: reload state, re-send every unfinished chunk to a
+        live worker, restart unfinished coordinator-side jobs.  Returns #chunks."""
+        if not self.load_checkpoint(path):
+            return 0
+        alive = self.membership.alive()
+        n = 0
+        for model, qnum, w, s, e, _t in self.state.pending():
+            nw = w if w in alive else self.pick_replacement(w, alive)
+            if nw is None:
+                continue
+            if nw != w:
+                self.state.reassign(w, nw, (model, qnum, s, e))
+            self._send_job(nw, model, qnum, s, e)
+            n += 1
+        for jid in self.state.unfinished_jobs():
+            self._start_job_runner(jid)
+        return n
+
     def _peer_dead(self, dst: str) -> bool:
         """Failure-detector view used to abandon in-flight requests early."""
         m = self.membership
@@ -208,6 +269,7 @@ class Node:
         plan = self.sched.assign(model, start, end, alive)
         now = self.clock()
         self.state.assign(model, qnum, plan, now)
+        self.tracer.instant("query.submit", model=model, q=qnum, start=start, end=end, workers=len(plan))
         for w, s, e in plan:
             self._send_job(w, model, qnum, s, e)
         self.logger.info("query %s %s [%d,%d] -> %s", model, qnum, start, end, plan)
@@ -269,6 +331,8 @@ class Node:
         prob = np.frombuffer(msg["prob"], dtype=np.float32)
         new = self.state.record_result(msg["model"], msg["qnum"], msg["worker"], msg["start"], msg["end"],
                                        cls, prob)
+        self.tracer.instant("result.ingest", model=msg["model"], q=msg["qnum"], start=msg["start"],
+                            worker=msg["worker"], new=new)
         if new and self.is_coordinator:
             n = msg["end"] - msg["start"] + 1
             self.sched.observe(msg["model"], msg.get("compute_s", 0.0) / n * self.cfg.batch_for(msg["model"]))
@@ -340,10 +404,18 @@ class Node:
 
     # -- standby replication ------------------------------------------------------------
     def _metadata_loop(self) -> None:
+        last_ckpt = time.monotonic()
         while not self._stop.wait(self.cfg.metadata_period_s):
-            if not self.is_coordinator or self.standby == self.name:
+            if not self.is_coordinator:
                 continue
-            self.push_metadata()
+            if self.standby != self.name:
+                self.push_metadata()
+            if self.cfg.checkpoint_period_s > 0 and time.monotonic() - last_ckpt >= self.cfg.checkpoint_period_s:
+                try:
+                    self.save_checkpoint()
+                except OSError:
+                    self.logger.exception("checkpoint failed")
+                last_ckpt = time.monotonic()
 
     def push_metadata(self) -> bool:
         snap = {"t": Type.METADATA, "seq": self.state.seq, "epoch": self.membership.epoch,
@@ -417,8 +489,11 @@ class Node:
             time.sleep(delay)
         model, s, e = msg["model"], int(msg["start"]), int(msg["end"])
         t0 = time.perf_counter()
-        imgs = self.source.get(s, e) if self.source is not None else None
-        cls, prob = self.executor.run(model, imgs, s, e)
+        tags = dict(model=model, q=msg["qnum"], start=s, end=e)
+        with self.tracer.span("chunk.stage", **tags):
+            imgs = self.source.get(s, e) if self.source is not None else None
+        with self.tracer.span("chunk.compute", **tags):
+            cls, prob = self.executor.run(model, imgs, s, e)
         dt = time.perf_counter() - t0
         if not self.alive_flag:
             return
@@ -447,6 +522,10 @@ class Node:
             return {"ok": True, "text": self.state.cq()}
         if v in ("cvm", "c5"):
             return {"ok": True, "text": self.state.cvm()}
+        if v == "trace":
+            return {"ok": True, "events": self.tracer.export()}
+        if v == "checkpoint":
+            return {"ok": True, "path": self.save_checkpoint()}
         if v == "summary":
             return {"ok": True, "done": {m: self.state.images_done(m) for m in self.state.models()},
                     "pending": len(self.state.pending()),

@@ -32,6 +32,8 @@ cvm (c5) tasks running on each node
 cq how each query is distributed: (node, start, end, state, t_start, t_end)
 job <start> <end> <model>: send the whole range; the coordinator cuts it into batch-size queries
 dataset <n_images> [shard_images]: put a synthetic 224x224x3 dataset into SDFS
+trace <file.json>: write every node's query/chunk spans as a Chrome trace
+checkpoint: write the coordinator's job state to disk (restart with IDUNNO_RESUME=1)
 kill <node> | delay <node> <seconds>: fault injection
 exit"""
 
@@ -114,6 +116,11 @@ class Shell:
                 k = put_synthetic_dataset(n.sdfs, int(args[0]), n.cfg.data_seed,
                                           int(args[1]) if len(args) > 1 else 500)
                 return f"put {k} shards"
+            if cmd == "trace":
+                need(1)
+                return f"wrote {self.client.trace(args[0])} trace events to {args[0]}"
+            if cmd == "checkpoint":
+                return f"checkpoint written to {self.client.checkpoint().get('path')}"
             if cmd == "kill":
                 need(1)
                 return "sent" if self.client.kill(args[0]) else "unreachable"
