@@ -15,6 +15,12 @@ using namespace idunno;
 
 static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// Every launch is checked ("HIP error checking on every call").
+static void check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, what, ": HIP launch failed: ", hipGetErrorString(e));
+}
+
 // 256 zero bytes per device: the DMA source of padding taps / masked rows.
 // Created once per device under a lock and never freed: several node threads
 // share one GPU, and a buffer replaced by a racing thread would go back to the
@@ -112,11 +118,11 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   if (M == 0) return y;
   if (small) {
     const int t = (tile >= 0 && tile <= 3) ? (int)tile : conv_pick_tile(a.M, Cout);
-    conv_igemm_launch(a, small, out_f32, t, cur_stream());
+    conv_igemm_launch(a, small, out_f32, t, cur_stream()); check_launch("conv_igemm");
     return y;
   }
   if (tile >= 0 && tile <= 3) {          // v1 register-staged loop (kept for A/B)
-    conv_igemm_launch(a, small, out_f32, (int)tile, cur_stream());
+    conv_igemm_launch(a, small, out_f32, (int)tile, cur_stream()); check_launch("conv_igemm");
     return y;
   }
   a.zero = zero_buffer(x.device()).data_ptr();
@@ -125,11 +131,12 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   if (tile == 40 || (tile < 0 && patch_ok && conv3x3_patch_default())) {
     TORCH_CHECK(patch_ok, "tile 40 (LDS-patch 3x3 conv) does not support this shape");
     conv3x3_patch_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W, C, Cout,
-                         a.relu, cur_stream());
+                         a.relu, cur_stream()); check_launch("conv3x3_patch");
     return y;
   }
   const int t = tile >= 10 ? (int)tile : conv_glds_pick(a.M, Cout);
   TORCH_CHECK(conv_glds_launch(a, out_f32, t, cur_stream()), "unknown conv tile id ", t);
+  check_launch("conv_glds");
   return y;
 }
 
@@ -179,7 +186,7 @@ torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias,
   auto y = torch::empty({B, Hp, Wp, 64}, img.options().dtype(torch::kHalf));
   if (B)
     stem_fused_launch(img.data_ptr<uint8_t>(), reinterpret_cast<const half_t*>(w.data_ptr()), bias.data_ptr<float>(),
-                      reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp, max_start, cur_stream());
+                      reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp, max_start, cur_stream()); check_launch("stem_fused");
   return y;
 }
 
@@ -195,7 +202,7 @@ torch::Tensor preprocess(torch::Tensor img, c10::optional<torch::Tensor> start, 
   const long npix = (long)B * img.size(1) * img.size(2);
   if (npix)
     preprocess_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), npix, sp, max_start,
-                      (long)img.size(1) * img.size(2), cur_stream());
+                      (long)img.size(1) * img.size(2), cur_stream()); check_launch("preprocess");
   return out;
 }
 
@@ -216,7 +223,7 @@ torch::Tensor resize_crop(torch::Tensor img, int64_t resize, int64_t crop) {
   TORCH_CHECK(Hr >= crop && Wr >= crop, "crop larger than resized image");
   auto out = torch::empty({B, crop, crop, 4}, img.options().dtype(torch::kHalf));
   if (B) resize_crop_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), B, Hi, Wi, Hr, Wr,
-                            crop, cur_stream());
+                            crop, cur_stream()); check_launch("resize_crop");
   return out;
 }
 
@@ -231,7 +238,7 @@ torch::Tensor maxpool2d_nhwc(torch::Tensor x, int64_t k, int64_t s, int64_t pad)
   TORCH_CHECK(Ho > 0 && Wo > 0, "empty output");
   auto y = torch::empty({B, Ho, Wo, C}, x.options());
   if (B) maxpool_launch(reinterpret_cast<const half_t*>(x.data_ptr()), reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, C,
-                        Ho, Wo, k, s, pad, cur_stream());
+                        Ho, Wo, k, s, pad, cur_stream()); check_launch("maxpool");
   return y;
 }
 
@@ -243,7 +250,7 @@ torch::Tensor global_avgpool_nhwc(torch::Tensor x) {
   const int B = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
   auto y = torch::empty({B, C}, x.options());
   if (B) avgpool_launch(reinterpret_cast<const half_t*>(x.data_ptr()), reinterpret_cast<half_t*>(y.data_ptr()), B, HW, C,
-                        cur_stream());
+                        cur_stream()); check_launch("avgpool");
   return y;
 }
 
@@ -255,7 +262,7 @@ std::vector<torch::Tensor> softmax_top1(torch::Tensor logits) {
   auto cls = torch::empty({rows}, logits.options().dtype(torch::kInt));
   auto prob = torch::empty({rows}, logits.options());
   if (rows) softmax_top1_launch(logits.data_ptr<float>(), ld, N, rows, cls.data_ptr<int>(), prob.data_ptr<float>(),
-                                cur_stream());
+                                cur_stream()); check_launch("softmax_top1");
   return {cls, prob};
 }
 
@@ -263,7 +270,7 @@ torch::Tensor synth_images(int64_t seed, int64_t start, int64_t n, int64_t hw, t
   TORCH_CHECK(dev.is_cuda(), "synth_images needs a GPU device");
   TORCH_CHECK(n >= 0 && start >= 0 && (hw * hw * 3) % 8 == 0, "bad synth_images args");
   auto out = torch::empty({n, hw, hw, 3}, torch::TensorOptions().dtype(torch::kUInt8).device(dev));
-  if (n) synth_images_launch(out.data_ptr<uint8_t>(), (uint64_t)seed, start, n, hw * hw * 3, cur_stream());
+  if (n) synth_images_launch(out.data_ptr<uint8_t>(), (uint64_t)seed, start, n, hw * hw * 3, cur_stream()); check_launch("synth_images");
   return out;
 }
 
