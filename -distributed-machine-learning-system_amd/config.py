@@ -50,6 +50,11 @@ class ClusterConfig:
     replication: int = 4                     # reference places 4-5 replicas (utils.py:48-55)
     store_root: str = "/tmp/idunno"
 
+    # -- collective data plane (one node per process only) ----------------------
+    collective_rounds: bool = False          # run queries as RCCL/gloo rounds when the group is healthy
+    collective_port_offset: int = 500        # TCPStore port = base_port + offset + epoch % 100
+    collective_timeout_s: float = 30.0
+
     # -- checkpoint / resume ----------------------------------------------------
     checkpoint_period_s: float = 0.0         # coordinator writes state to disk (0 = off)
     resume: bool = False                     # coordinator restarts from its checkpoint

@@ -37,6 +37,7 @@ class Type:
     GREP = "GREP"                    # distributed log grep (MP1 replacement)
     REPLY = "REPLY"                  # response to a request (carries "rid")
     KILL = "KILL"                    # fault injection
+    GROUP_FORM = "GROUP_FORM"        # coordinator -> members: join collective-group epoch N
 
 
 Status_RUNNING = "RUNNING"

@@ -70,10 +70,13 @@ class Node:
         self.promotions = 0
         self._retries: dict = {}
         self.tracer = Tracer(name)
+        self.device = getattr(executor, "device", None)  # GPU of this node (None = CPU)
+        self.rounds = None                          # collective round plane (cfg.collective_rounds)
         self.transport.dead_check = self._peer_dead
         self.membership.on_failure.append(self._on_node_failure)
         self.membership.on_master_failure.append(self._on_master_failure)
         self.membership.on_master_change.append(self._on_master_change)
+        self.membership.on_join.append(self._on_node_join)
 
     # -- infra --------------------------------------------------------------------
     def _make_logger(self):
@@ -104,6 +107,14 @@ class Node:
         return self.membership.is_master()
 
     def start(self, join: bool = True) -> "Node":
+        if self.cfg.collective_rounds and self.rounds is None:
+            import torch
+
+            from .rounds import RoundPlane
+
+            self.rounds = RoundPlane(self, torch.device(self.device) if self.device is not None else
+                                     torch.device("cpu"))
+            self.rounds.start()
         self.transport.start(self.handle)
         self.membership.start()
         for fn, nm in ((self._worker_loop, "worker"), (self._metadata_loop, "meta"),
@@ -138,6 +149,8 @@ class Node:
         self._stop.set()
         self.alive_flag = False
         self.membership.stop()
+        if self.rounds is not None:
+            self.rounds.stop()
         self.jobs.put(None)
         self.transport.close()
 
@@ -169,6 +182,10 @@ class Node:
             return self._stats(msg.get("view", "c1"))
         if t == Type.GREP:
             return {"ok": True, "lines": self.local_grep(msg["pattern"])}
+        if t == Type.GROUP_FORM:
+            if self.rounds is not None:
+                self.rounds.on_group_form(msg)
+            return None
         if t == Type.KILL:
             if msg.get("mode") == "delay":
                 self.extra_delay_s = float(msg.get("seconds", 1.0))
@@ -270,6 +287,9 @@ class Node:
         now = self.clock()
         self.state.assign(model, qnum, plan, now)
         self.tracer.instant("query.submit", model=model, q=qnum, start=start, end=end, workers=len(plan))
+        if self.rounds is not None and self.rounds.try_enqueue(model, qnum, plan):
+            self.logger.info("query %s %s [%d,%d] -> collective round %s", model, qnum, start, end, plan)
+            return {"ok": True, "qnum": qnum, "plan": [list(p) for p in plan], "round": True}
         for w, s, e in plan:
             self._send_job(w, model, qnum, s, e)
         self.logger.info("query %s %s [%d,%d] -> %s", model, qnum, start, end, plan)
@@ -366,9 +386,15 @@ class Node:
         load = {w: len(self.state.chunks_of(w)) for w in order}
         return min(order, key=lambda w: (load[w], order.index(w)))
 
+    def _on_node_join(self, node: str) -> None:
+        if self.rounds is not None and self.is_coordinator:
+            self.rounds.schedule_reform(f"{node} joined")
+
     def _on_node_failure(self, node: str) -> None:
         if not self.is_coordinator:
             return
+        if self.rounds is not None:
+            self.rounds.schedule_reform(f"{node} failed")
         t0 = time.monotonic()
         try:
             moves = self.sdfs.rereplicate(node)
@@ -465,6 +491,8 @@ class Node:
 
     def _on_master_change(self, new: str, epoch: int) -> None:
         self.logger.info("master is now %s (epoch %d)", new, epoch)
+        if self.rounds is not None and new == self.name:
+            self.rounds.schedule_reform(f"promoted (epoch {epoch})", delay=0.5)
 
     # -- worker ---------------------------------------------------------------------------
     def _worker_loop(self) -> None:

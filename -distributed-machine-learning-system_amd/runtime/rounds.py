@@ -1,0 +1,254 @@
+"""Collective query rounds inside the fault-tolerant node runtime.
+
+When ``cfg.collective_rounds`` is on (one node per process, e.g. one per GPU
+via ``idunno.launch``), a query whose plan puts at most one chunk on each
+group member runs as ONE collective round on the ``ElasticGroup`` (RCCL
+broadcast of the descriptor table + gather of packed top-1 results, the same
+``QueryPlane`` bench.py drives) instead of per-chunk TCP JOB/RESULT messages.
+The reference has no equivalent (every chunk is a TCP message,
+mp4_machinelearning.py:560-613); the TCP path stays as the fallback:
+
+  * a round whose collectives fail is abandoned and its chunks are re-sent as
+    TCP JOBs (results are idempotent by chunk key);
+  * every membership change (failure, join, standby promotion) makes the
+    coordinator re-form the group under a new epoch over the live members.
+
+Each node runs ONE driver thread that owns the process group, so forming,
+rounds and teardown never race: as coordinator it forms epochs and serves the
+round queue, as a member it follows the latest GROUP_FORM it was sent.
+"""
+from __future__ import annotations
+
+import logging
+import queue
+import threading
+import time
+
+import numpy as np
+
+from ..parallel.dataplane import NO_WORK
+from ..parallel.elastic import MODEL_IDS, STOP, ElasticGroup
+from .messages import Type
+
+log = logging.getLogger("idunno.rounds")
+
+
+class RoundPlane:
+    def __init__(self, node, device):
+        self.node = node
+        self.cfg = node.cfg
+        self.group = ElasticGroup(device, timeout_s=self.cfg.collective_timeout_s, max_chunk=self.cfg.max_chunk)
+        self.q: queue.Queue = queue.Queue()
+        self.lock = threading.Lock()
+        self.epoch = 0                      # last epoch formed or announced
+        self.members: list[str] = []
+        self.healthy = False                # coordinator: rounds may be queued
+        self.rounds_done = 0
+        self.rounds_failed = 0
+        self._reform_at: float | None = None
+        self._pending_form: dict | None = None
+        self._wake = threading.Event()
+        self._thread: threading.Thread | None = None
+
+    def start(self) -> None:
+        self._thread = threading.Thread(target=self._driver, name=f"{self.node.name}-rounds", daemon=True)
+        self._thread.start()
+
+    def stop(self) -> None:
+        self._wake.set()
+
+    # -- triggers (any thread) ----------------------------------------------------------
+    def schedule_reform(self, reason: str, delay: float = 0.2) -> None:
+        """Coordinator: re-form the group over the live members after ``delay``
+        (several triggers inside the window collapse into one re-form)."""
+        with self.lock:
+            self.healthy = False
+            at = time.monotonic() + delay
+            self._reform_at = at if self._reform_at is None else min(self._reform_at, at)
+        log.info("%s: re-form scheduled (%s)", self.node.name, reason)
+        self._wake.set()
+
+    def on_group_form(self, msg: dict) -> None:
+        with self.lock:
+            if int(msg["epoch"]) <= self.epoch:
+                return
+            self._pending_form = dict(msg)
+        self._wake.set()
+
+    def try_enqueue(self, model: str, qnum, plan) -> bool:
+        """Coordinator: queue a query as one collective round if the group covers
+        its plan (one chunk per member at most)."""
+        with self.lock:
+            if not self.healthy:
+                return False
+            members = list(self.members)
+        workers = [w for w, _, _ in plan]
+        if len(set(workers)) != len(workers) or not set(workers) <= set(members):
+            return False
+        if any(e - s + 1 > self.cfg.max_chunk for _, s, e in plan):
+            return False
+        mid = MODEL_IDS.get(model)
+        if mid is None:
+            return False
+        by = {w: (s, e) for w, s, e in plan}
+        table = [(mid, int(qnum), by[m][0], by[m][1]) if m in by else (mid, int(qnum), 0, NO_WORK)
+                 for m in members]
+        self.q.put((model, qnum, table, members))
+        self._wake.set()
+        return True
+
+    # -- driver thread ---------------------------------------------------------------------
+    def _run_chunk(self, model: str, s: int, e: int):
+        n = self.node
+        delay = self.cfg.worker_start_delay_s + n.extra_delay_s
+        if delay:
+            time.sleep(delay)
+        t0 = time.perf_counter()
+        tags = dict(model=model, start=s, end=e, epoch=self.group.epoch)
+        with n.tracer.span("round.stage", **tags):
+            imgs = n.source.get(s, e) if n.source is not None else None
+        with n.tracer.span("round.compute", **tags):
+            cls, prob = n.executor.run(model, imgs, s, e)
+        n.chunks_done += 1
+        self._last_compute = time.perf_counter() - t0
+        return np.ascontiguousarray(cls, np.int32), np.ascontiguousarray(prob, np.float32)
+
+    def _driver(self) -> None:
+        n = self.node
+        while n.alive_flag:
+            self._wake.wait(0.1)
+            self._wake.clear()
+            if not n.alive_flag:
+                break
+            try:
+                if n.is_coordinator:
+                    self._coordinator_step()
+                else:
+                    self._member_step()
+            except Exception:  # noqa: BLE001
+                log.exception("%s: round driver error", n.name)
+                self._drop_group()
+        self._drop_group()
+
+    def _drop_group(self) -> None:
+        with self.lock:
+            self.healthy = False
+        self.group.teardown()
+
+    # coordinator -------------------------------------------------------------------------
+    def _coordinator_step(self) -> None:
+        n = self.node
+        with self.lock:
+            due = self._reform_at is not None and time.monotonic() >= self._reform_at
+            if due:
+                self._reform_at = None
+        if due:
+            self._reform()
+            return
+        if self._reform_at is not None:
+            self._wake.set()                       # keep polling until it is due
+        if not self.group.formed:
+            self._flush_queue_to_tcp()
+            return
+        while n.alive_flag and self._reform_at is None:
+            try:
+                model, qnum, table, members = self.q.get(timeout=0.05)
+            except queue.Empty:
+                return
+            if members != self.group.members:
+                self._fallback(model, qnum, table, members)
+                continue
+            try:
+                out = self.group.round(table, self._run_chunk)
+            except Exception as e:  # noqa: BLE001
+                self.rounds_failed += 1
+                log.warning("%s: round failed in epoch %d (%s); falling back to TCP", n.name, self.group.epoch, e)
+                n.tracer.instant("round.failed", epoch=self.group.epoch, q=qnum)
+                self._drop_group()
+                self._fallback(model, qnum, table, members)
+                self._flush_queue_to_tcp()
+                # the failure detector re-forms on a death; re-form anyway in case it was transient
+                self.schedule_reform("round failure", delay=self.cfg.failure_timeout_s * 1.5)
+                return
+            self.rounds_done += 1
+            now = time.time()
+            for row, cls, prob in out:
+                w = members[table.index(row)]
+                res = {"t": Type.RESULT, "model": model, "qnum": qnum, "start": row[2], "end": row[3],
+                       "worker": w, "cls": cls.tobytes(), "prob": prob.tobytes(), "compute_s": 0.0,
+                       "epoch": n.membership.epoch, "t_done": now}
+                n._ingest_result(dict(res, src=n.name))
+                if n.standby != n.name and n.membership.is_alive(n.standby):
+                    n.transport.send(n.standby, res)
+
+    def _reform(self) -> None:
+        n = self.node
+        if self.group.formed:
+            try:                                   # let members leave the old epoch cleanly
+                self.group.round([(0, 0, STOP, NO_WORK)] * len(self.group.members), self._run_chunk)
+            except Exception:  # noqa: BLE001
+                pass
+        self._drop_group()
+        self._flush_queue_to_tcp()
+        members = [n.name] + [m for m in n.membership.alive() if m != n.name]
+        with self.lock:
+            self.epoch = max(self.epoch + 1, n.membership.epoch * 1000 + 1)
+            epoch = self.epoch
+            self.members = members
+        if len(members) < 2:
+            return                                 # nothing to collect from; TCP path only
+        port = self.cfg.base_port + self.cfg.collective_port_offset + epoch % 100
+        log.warning("%s: forming collective epoch %d over %s", n.name, epoch, members)
+        n.tracer.instant("round.form", epoch=epoch, members=len(members))
+        for m in members[1:]:
+            n.transport.send(m, {"t": Type.GROUP_FORM, "epoch": epoch, "members": members, "port": port})
+        ok = self.group.form(n.name, members, epoch, self.cfg.host, port)
+        with self.lock:
+            self.healthy = ok and self._reform_at is None and epoch == self.epoch
+        if not ok:
+            log.warning("%s: epoch %d rendezvous failed; TCP path until the next re-form", n.name, epoch)
+            self.schedule_reform("rendezvous failed", delay=self.cfg.failure_timeout_s * 1.5)
+
+    def _flush_queue_to_tcp(self) -> None:
+        while True:
+            try:
+                model, qnum, table, members = self.q.get_nowait()
+            except queue.Empty:
+                return
+            self._fallback(model, qnum, table, members)
+
+    def _fallback(self, model, qnum, table, members) -> None:
+        """Re-send a round's chunks as TCP JOBs.  Chunks of dead members are
+        re-dispatched by the failure handler (it owns the reassignment)."""
+        n = self.node
+        alive = set(n.membership.alive())
+        for m, row in zip(members, table):
+            if row[3] != NO_WORK and m in alive:
+                n._send_job(m, model, qnum, row[2], row[3])
+
+    # member ---------------------------------------------------------------------------------
+    def _member_step(self) -> None:
+        n = self.node
+        with self.lock:
+            msg, self._pending_form = self._pending_form, None
+        if msg is None:
+            return
+        epoch, members, port = int(msg["epoch"]), list(msg["members"]), int(msg["port"])
+        with self.lock:
+            if epoch < self.epoch:
+                return
+            self.epoch, self.members = epoch, members
+        if not self.group.form(n.name, members, epoch, self.cfg.host, port):
+            return
+        while n.alive_flag:
+            try:
+                r = self.group.round(None, self._run_chunk)
+            except Exception as e:  # noqa: BLE001
+                log.info("%s: left epoch %d (%s)", n.name, epoch, e)
+                break
+            if r == "stop":
+                break
+            self.rounds_done += 1
+        self._drop_group()
+        if self._pending_form is not None:
+            self._wake.set()

@@ -35,7 +35,10 @@ def _worker(rank, world, port, q):
             chunks = split_range(step * 100, step * 100 + 99, world)
             table = [(1, step, s, e) for s, e in chunks]
             table += [(1, step, 0, NO_WORK)] * (world - len(table))
-        mid, qid, s, e = plane.dispatch(table)
+        if step % 2:
+            mid, qid, s, e = plane.dispatch(table)
+        else:                                   # the asynchronous (device-row) variant bench.py uses
+            mid, qid, s, e = (int(v) for v in plane.dispatch_device(table, slot=step).tolist())
         cls, prob = ex.run("resnet18", None, s, e)
         g = plane.gather(torch.from_numpy(cls), torch.from_numpy(prob))
         if env.rank == 0:

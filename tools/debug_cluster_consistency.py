@@ -35,6 +35,32 @@ def main():
     c_g, p_g = run()
     torch.cuda.synchronize()
     print("graph n=67 mismatches:", int((c_g != c_all[:67]).sum().item()), "max|dp|", (p_g - p_all[:67]).abs().max().item())
+    # concurrency: 3 executors in 3 threads on one GPU, like 3 nodes of a LocalCluster
+    import threading
+
+    for use_graphs in (False, True):
+        exs = [HipExecutor("cuda", seed=0, use_graphs=use_graphs) for _ in range(3)]
+        chunks = [(0, 66), (67, 133), (134, 199)]
+        res = {}
+
+        def work(k):
+            s, e = chunks[k]
+            for rep in range(3):
+                imgs_k = src.get(s, e)
+                res[(k, rep)] = exs[k].run("resnet18", imgs_k, s, e)
+
+        ths = [threading.Thread(target=work, args=(k,)) for k in range(3)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        bad = 0
+        for (k, rep), (cls, prob) in sorted(res.items()):
+            s, e = chunks[k]
+            mism = int((cls != c_all[s:e + 1].cpu().numpy()).sum())
+            bad += mism
+            print(f"threads graphs={use_graphs} chunk {k} rep {rep}: mismatches={mism}")
+        print(f"threads graphs={use_graphs}: total mismatches {bad}")
     top2 = torch.topk(l_all, 2, dim=1).values
     print("median top1-top2 logit margin:", (top2[:, 0] - top2[:, 1]).median().item(),
           "logit scale:", l_all.abs().max().item())
