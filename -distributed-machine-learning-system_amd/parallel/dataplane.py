@@ -10,8 +10,13 @@ Replaces the reference's per-chunk TCP messages on the hot path
         one RCCL gather of packed top-1 results (int32 class + fp32 prob,
         8 B/image, 3.2 KB for a 400-image chunk) to the coordinator rank
         (and, optionally, a second one to the standby rank).
-Images never cross the fabric in steady state: every rank owns an HBM-resident
-shard of the dataset (see ``idunno.runtime.staging``).
+  * M9  data variant -> ``scatter``: the coordinator holds a query's images in
+        HBM and sends every rank its chunk with one grouped point-to-point
+        send per peer, so the 7 xGMI links of the root carry the shards
+        concurrently (60 MB for a 400-image query, 7.5 MB per rank at 8).
+In steady state images do not cross the fabric at all: every rank stages its
+own shard host->HBM (``idunno.runtime.data.HbmStager`` / ``SdfsSource``) and
+``scatter`` is used only when the images live on the coordinator.
 
 On CPU (tests) the same code runs over gloo.
 """
@@ -113,6 +118,33 @@ class QueryPlane:
         if self.env.distributed:
             dist.broadcast(self._desc, src=self.coord, group=self.group)
         return self._desc[self.env.rank]
+
+    def scatter(self, images: torch.Tensor | None, table, row, img_shape=(224, 224, 3)):
+        """Send every rank its chunk of the coordinator's images.
+
+        ``images`` (coordinator only) holds the query's images ``[B, *img_shape]``
+        with row 0 = the smallest start in ``table``; ``row`` is this rank's
+        descriptor from ``dispatch``.  Returns this rank's ``[n, *img_shape]``
+        images (a view on the coordinator, a reused receive buffer elsewhere) or
+        None for an idle rank."""
+        s, e = int(row[2]), int(row[3])
+        n = 0 if e == NO_WORK else e - s + 1
+        if self.env.rank == self.coord:
+            base = min(r[2] for r in table if r[3] != NO_WORK)
+            ops = [dist.P2POp(dist.isend, images[r[2] - base:r[3] - base + 1].contiguous(), peer, self.group)
+                   for peer, r in enumerate(table) if peer != self.coord and r[3] != NO_WORK]
+            if ops and self.env.distributed:
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+            return images[s - base:e + 1 - base] if n else None
+        if n == 0:
+            return None
+        if getattr(self, "_recv", None) is None or tuple(self._recv.shape[1:]) != tuple(img_shape):
+            self._recv = torch.empty((self.max_chunk, *img_shape), dtype=torch.uint8, device=self.env.device)
+        buf = self._recv[:n]
+        for req in dist.batch_isend_irecv([dist.P2POp(dist.irecv, buf, self.coord, self.group)]):
+            req.wait()
+        return buf
 
     # -- M11 --------------------------------------------------------------------
     def pack(self, cls: torch.Tensor, prob: torch.Tensor) -> torch.Tensor:

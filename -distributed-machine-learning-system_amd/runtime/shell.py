@@ -34,7 +34,8 @@ job <start> <end> <model>: send the whole range; the coordinator cuts it into ba
 dataset <n_images> [shard_images]: put a synthetic 224x224x3 dataset into SDFS
 trace <file.json>: write every node's query/chunk spans as a Chrome trace
 checkpoint: write the coordinator's job state to disk (restart with IDUNNO_RESUME=1)
-kill <node> | delay <node> <seconds>: fault injection
+kill-rank <node|rank> | kill-coordinator | delay-rank <node|rank> <seconds>: fault injection
+  (kill / delay are aliases of kill-rank / delay-rank)
 exit"""
 
 ARITY_ERR = "Error: missing or too many {} parameter ."
@@ -121,12 +122,16 @@ class Shell:
                 return f"wrote {self.client.trace(args[0])} trace events to {args[0]}"
             if cmd == "checkpoint":
                 return f"checkpoint written to {self.client.checkpoint().get('path')}"
-            if cmd == "kill":
+            if cmd in ("kill", "kill-rank"):
                 need(1)
-                return "sent" if self.client.kill(args[0]) else "unreachable"
-            if cmd == "delay":
+                return "sent" if self.client.kill(self._node_arg(args[0])) else "unreachable"
+            if cmd == "kill-coordinator":
+                need(0)
+                return "sent" if self.client.kill(n.membership.master) else "unreachable"
+            if cmd in ("delay", "delay-rank"):
                 need(2)
-                return "sent" if self.client.kill(args[0], "delay", float(args[1])) else "unreachable"
+                return ("sent" if self.client.kill(self._node_arg(args[0]), "delay", float(args[1]))
+                        else "unreachable")
             if cmd in ("help", "menu"):
                 return MENU
             if cmd == "exit":
@@ -136,6 +141,10 @@ class Shell:
             return ARITY_ERR.format(e.cmd)
         except Exception as e:  # noqa: BLE001
             return f"Error: {type(e).__name__}: {e}"
+
+    def _node_arg(self, a: str) -> str:
+        """A node name, or a rank index (``kill-rank 3`` -> node03)."""
+        return self.node.cfg.node_name(int(a)) if a.isdigit() else a
 
     def repl(self) -> None:
         print(MENU)

@@ -164,8 +164,16 @@ def test_shell_commands(cluster, tmp_path, monkeypatch):
     c4 = sh.execute("c4")
     assert "test_0.JPEG" in c4 and json.loads((tmp_path / "result.txt").read_text())
     assert sh.execute("get-versions x 0 y").startswith("Error")
-    assert "put 1 shards" == sh.execute("dataset 10 10") or True
+    assert sh.execute("dataset 10 10") == "put 1 shards"
     assert "started" in sh.execute("grep started")
+    # fault injection by rank index or name
+    assert sh.execute("delay-rank 3 0.25") == "sent"
+    assert wait_for(lambda: cluster.nodes["node03"].extra_delay_s == 0.25, 3)
+    assert sh.execute("delay node03 0") == "sent"
+    assert wait_for(lambda: cluster.nodes["node03"].extra_delay_s == 0.0, 3)
+    assert sh.execute("kill-rank 4") == "sent"
+    assert wait_for(lambda: "node04" not in cluster.coordinator().membership.alive(), 3)
+    assert sh.execute("kill-coordinator x") == "Error: missing or too many kill-coordinator parameter ."
     assert sh.execute("leave") == "left"
     assert wait_for(lambda: "node02" not in cluster.coordinator().membership.alive(), 3)
     assert sh.execute("join") == "joined"

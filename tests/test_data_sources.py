@@ -54,3 +54,25 @@ def test_ring_helpers_reference_semantics():
     assert replica_neighbors("h05", ring) == ["h06", "h07", "h08", "h09", "h10", "h01", "h02", "h03", "h04", "h05"]
     assert "h03" not in neighbors("h03", ring) and len(neighbors("h03", ring)) == 9
     assert file_neighbors(8, ring, 4) == ["h09", "h10", "h01", "h02"]
+
+
+def test_deeplearning_api_bs1_cpu_path(tmp_path):
+    """Reference L4 API (alexnet_resnet.py:12-92) on the CPU: AlexNet, batch 1
+    per forward (BASELINE.json config 1), tuples in the reference format."""
+    from PIL import Image
+
+    from idunno.inference import deeplearning
+
+    res, dt = deeplearning("nope", "alexnet", 5, 7, device="cpu", batch=1, root=str(tmp_path))
+    assert [r[0] for r in res] == ["test_5.JPEG", "test_6.JPEG", "test_7.JPEG"] and dt > 0
+    assert all(isinstance(c, str) and 0 < p <= 1 for _, c, p in res)
+    # batched forward gives the same answers as batch 1
+    res_b, _ = deeplearning("nope", "alexnet", 5, 7, device="cpu", root=str(tmp_path))
+    assert [r[1] for r in res_b] == [r[1] for r in res]
+    assert max(abs(a[2] - b[2]) for a, b in zip(res, res_b)) < 1e-4
+    # a ./<filename>/test_<i>.JPEG directory is used when it exists
+    d = tmp_path / "resnet"
+    d.mkdir()
+    Image.fromarray(np.full((256, 256, 3), 90, np.uint8)).save(d / "test_0.JPEG")
+    res_j, _ = deeplearning("resnet", "resnet", 0, 0, device="cpu", root=str(tmp_path))
+    assert len(res_j) == 1 and res_j[0][0] == "test_0.JPEG"

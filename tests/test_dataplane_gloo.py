@@ -67,3 +67,48 @@ def test_dispatch_gather_over_gloo(world):
     assert sorted(out) == list(range(300))
     for i, (c, p) in out.items():
         assert c == (i * 7919 + 13) % 1000 and abs(p - 0.5) < 1e-7
+
+
+def _scatter_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import numpy as np
+    import torch.distributed as dist
+
+    from idunno.parallel.dataplane import NO_WORK, QueryPlane, init_from_env
+    from idunno.runtime.data import synth_images_cpu
+    from idunno.runtime.scheduler import split_range
+
+    env = init_from_env(backend="gloo")
+    plane = QueryPlane(env, coordinator=0, max_chunk=16)
+    ok = True
+    for step, (s0, e0) in enumerate([(100, 129), (7, 8)]):
+        table = imgs = None
+        if env.rank == 0:
+            chunks = split_range(s0, e0, world)
+            table = [(1, step, s, e) for s, e in chunks] + [(1, step, 0, NO_WORK)] * (world - len(chunks))
+            imgs = torch.from_numpy(synth_images_cpu(5, s0, e0 - s0 + 1))
+        row = plane.dispatch(table)
+        got = plane.scatter(imgs, table, row)
+        if row[3] == NO_WORK:
+            ok &= got is None
+        else:
+            ok &= np.array_equal(got.numpy(), synth_images_cpu(5, row[2], row[3] - row[2] + 1))
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_scatter_images_over_gloo():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res == {r: True for r in range(world)}
