@@ -15,6 +15,8 @@ gamma=1/beta=0, running stats (0, 1); Linear default init.
 """
 from __future__ import annotations
 
+import threading
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -165,6 +167,9 @@ def _norm_consts(device):
     return _NORM[key]
 
 
+_BUILD_LOCK = threading.Lock()
+
+
 def build(name: str, seed: int = 0, randomize_bn: bool = False) -> nn.Module:
     """Random-init model of the named architecture, in eval mode.
 
@@ -173,7 +178,10 @@ def build(name: str, seed: int = 0, randomize_bn: bool = False) -> nn.Module:
     """
     name = canonical(name)
     g = torch.Generator().manual_seed(seed)
-    with torch.random.fork_rng(devices=[]):
+    # nn.init draws from the process-global CPU generator: nodes of one process
+    # building models concurrently (LocalCluster threads) would interleave their
+    # draws and get different weights for the same seed, so builds serialise.
+    with _BUILD_LOCK, torch.random.fork_rng(devices=[]):
         torch.manual_seed(seed)
         m = BUILDERS[name]()
     if randomize_bn:

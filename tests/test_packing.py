@@ -42,3 +42,24 @@ def test_alias():
     assert ref.canonical("resnet") == "resnet18"
     with pytest.raises(ValueError):
         ref.canonical("vgg")
+
+
+def test_concurrent_builds_give_identical_weights():
+    """Nodes of one process build their models on their own threads; the
+    global-RNG init must not interleave (was: wrong answers in LocalCluster)."""
+    import threading
+
+    from idunno.models import reference as ref
+
+    out = [None] * 4
+
+    def work(i):
+        out[i] = ref.build("resnet18", seed=0).state_dict()
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for sd in out[1:]:
+        assert all(torch.equal(sd[k], out[0][k]) for k in out[0])
