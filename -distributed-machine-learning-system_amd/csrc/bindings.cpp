@@ -45,6 +45,12 @@ static torch::Tensor zero_buffer(const torch::Device& dev) {
 static bool g_patch_default = false;
 static bool conv3x3_patch_default() { return g_patch_default; }
 void set_conv3x3_patch_default(bool on) { g_patch_default = on; }
+// Whether auto tile selection routes 3x3/s1 64->64 convs to the resident-weight
+// kernel (tile 50, conv3x3_c64.hip): on by default since sweep r1 #6 (ResNet18
+// layer1 at B=400: 112 / 153 us vs 178 / 207 us for the best im2col tile,
+// profiles/r1_v6_layer1_c64.log).
+static bool g_c64_default = true;
+void set_conv3x3_c64_default(bool on) { g_c64_default = on; }
 
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
@@ -132,6 +138,13 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     TORCH_CHECK(patch_ok, "tile 40 (LDS-patch 3x3 conv) does not support this shape");
     conv3x3_patch_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W, C, Cout,
                          a.relu, cur_stream()); check_launch("conv3x3_patch");
+    return y;
+  }
+  const bool c64_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 && conv3x3_c64_supported(C, Cout);
+  if (tile == 50 || (tile < 0 && c64_ok && g_c64_default)) {
+    TORCH_CHECK(c64_ok, "tile 50 (resident-weight 3x3 64->64 conv) does not support this shape");
+    conv3x3_c64_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W, a.relu,
+                       cur_stream()); check_launch("conv3x3_c64");
     return y;
   }
   const int t = tile >= 10 ? (int)tile : conv_glds_pick(a.M, Cout);
@@ -291,6 +304,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_top1", &softmax_top1, "fused row softmax + argmax");
   m.def("synth_images", &synth_images, "deterministic synthetic uint8 images [n,hw,hw,3]");
   m.def("pick_tile", &pick_tile, "tile id the conv heuristic picks for (M, Cout)");
+  m.def("set_conv3x3_c64_default", &set_conv3x3_c64_default,
+        "route auto-tiled 3x3/s1 64->64 convs to the resident-weight kernel (tile 50)");
   m.def("set_conv3x3_patch_default", &set_conv3x3_patch_default,
         "route auto-tiled 3x3/s1 convs to the LDS-patch kernel (tile 40)");
 }

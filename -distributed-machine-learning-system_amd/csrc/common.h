@@ -50,4 +50,39 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// ---- LDS reads the compiler does not see ------------------------------------------
+// While a global_load_lds (LDS-DMA) is in flight, hipcc's wait-count pass puts
+// an `s_waitcnt vmcnt(0)` in front of the next ds_read it emits (it cannot tell
+// that the read does not touch the DMA's destination), draining the prefetch
+// the kernel just issued.  Fragment reads issued from inline asm are invisible
+// to that pass; the kernel then orders them itself: a counted
+// `s_waitcnt lgkmcnt(N)` (lds_waitcnt) followed by lds_tie() of every fragment
+// register it covers (volatile asm keeps its order, and each MFMA consumes the
+// tied value, so none can be scheduled above the wait).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+__device__ __forceinline__ half8v lds_read_b128(uint32_t addr) {
+  half8v v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+
+template <int N>
+__device__ __forceinline__ void lds_waitcnt() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void lds_tie(half8v& r) { asm volatile("" : "+v"(r)); }
+
+// 8-byte global load the wait-count pass does not track (same reason as above:
+// a tracked load beside an LDS-DMA prefetch gets a vmcnt(0) at its first use).
+// The caller retires it with an explicit counted `s_waitcnt vmcnt(N)`.
+__device__ __forceinline__ half4v gload_b64_untracked(const void* p) {
+  half4v v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
 }  // namespace idunno

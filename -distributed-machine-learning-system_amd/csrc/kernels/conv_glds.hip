@@ -155,27 +155,46 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
     __builtin_amdgcn_s_barrier();
     if (s + NS - 1 < nK) issue((s + NS - 1) % NS);
 
-    const char* base = smem + (s % NS) * STAGE;
+    // fragment reads through inline asm (common.h lds_read_b128): a compiler-
+    // emitted ds_read here gets an `s_waitcnt vmcnt(0)` in front of it that
+    // drains the stage just issued above, and the ring never overlaps loads
+    // with MFMAs.  All reads of the stage go out first; each K-chunk of 32 then
+    // waits (counted lgkmcnt) only for its own fragments.
+    const uint32_t base = lds_addr(smem) + (s % NS) * STAGE;
+    constexpr int KK = BK / 32, NR = FN + FM;
+    half8v fa[KK][FN], fb[KK][FM];
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
+    for (int kk = 0; kk < KK; ++kk) {
       const int ch = fch + 4 * kk;
-      half8v fa[FN], fb[FM];
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
         const int row = wn * TN + i * 16 + frow;
-        fa[i] = *reinterpret_cast<const half8v*>(base + row * RB + ((ch ^ swz_r(row, CPR)) << 4));
+        fa[kk][i] = lds_read_b128(base + row * RB + ((ch ^ swz_r(row, CPR)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
         const int row = wm * TM + j * 16 + frow;
-        fb[j] = *reinterpret_cast<const half8v*>(base + A_BYTES + row * RB + ((ch ^ swz_r(row, CPR)) << 4));
+        fb[kk][j] = lds_read_b128(base + A_BYTES + row * RB + ((ch ^ swz_r(row, CPR)) << 4));
       }
+    }
+    auto mfma_chunk = [&](int kk) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i) lds_tie(fa[kk][i]);
+#pragma unroll
+      for (int j = 0; j < FM; ++j) lds_tie(fb[kk][j]);
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int j = 0; j < FM; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+    };
+    static_assert(KK == 1 || KK == 2, "BK 32 or 64");
+    if constexpr (KK == 2) {
+      lds_waitcnt<NR>();                         // chunk 0 landed, chunk 1 may be in flight
+      mfma_chunk(0);
     }
+    lds_waitcnt<0>();
+    mfma_chunk(KK - 1);
   }
 
   // ---- epilogue: bias (+residual) (+ReLU), NHWC store --------------------
