@@ -189,6 +189,33 @@ def test_model_end_to_end_vs_fp32_oracle(ops, name):
     assert agree >= 0.85, f"top-1 agreement {agree}"
 
 
+@pytest.mark.parametrize("name,B", [("resnet18", 1), ("resnet18", 80), ("resnet18", 400), ("alexnet", 1),
+                                    ("alexnet", 500), ("resnet50", 1024)])
+def test_model_batch_sizes_vs_fp32_oracle(ops, name, B):
+    """whole-model forward at B in {1, 80, 400, 1024} (and the
+    AlexNet query size 500) against the fp32 PyTorch oracle on identical
+    weights: logits within 3 % of their scale, and the same top-1 class on every
+    image whose oracle top-1/top-2 margin exceeds 2 % of that scale."""
+    from idunno.models import HipRunner, compile_model
+    from idunno.models import reference as ref
+
+    m = ref.build(name, seed=11, randomize_bn=True)
+    runner = HipRunner(compile_model(m, name))
+    g = torch.Generator(device=DEV).manual_seed(B)
+    img = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=DEV, generator=g)
+    logits = runner.logits(img)
+    with torch.no_grad():
+        r = torch.cat([m.to(DEV)(ref.preprocess_u8(img[i:i + 128])) for i in range(0, B, 128)])
+    scale = r.abs().max().item()
+    assert (logits - r).abs().max().item() < 0.03 * scale
+    cls, prob = runner.forward(img)
+    top2 = r.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 0.02 * scale
+    assert torch.equal(cls.long()[clear], r.argmax(1)[clear])
+    p_ref = torch.softmax(r, 1).gather(1, cls.long().view(-1, 1)).view(-1)
+    assert (prob - p_ref).abs().max().item() < 0.02
+
+
 def test_hipgraph_replay_matches_eager(ops):
     from idunno.models import HipRunner, build_program
 
