@@ -304,6 +304,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_top1", &softmax_top1, "fused row softmax + argmax");
   m.def("synth_images", &synth_images, "deterministic synthetic uint8 images [n,hw,hw,3]");
   m.def("pick_tile", &pick_tile, "tile id the conv heuristic picks for (M, Cout)");
+  m.def("set_stem_ablation", &set_stem_ablation,
+        "profiling only: 1 skip pool, 2 skip conv MFMAs, 4 skip patch normalise (wrong outputs)");
   m.def("set_conv3x3_c64_default", &set_conv3x3_c64_default,
         "route auto-tiled 3x3/s1 64->64 convs to the resident-weight kernel (tile 50)");
   m.def("set_conv3x3_patch_default", &set_conv3x3_patch_default,

@@ -58,7 +58,11 @@ __device__ __forceinline__ int conv_off(int p, int c) { return p * 128 + ((c ^ (
 
 struct StemGeom {
   int B, H, W, Hc, Wc, Hp, Wp, tiles_x, tiles_y, ntiles;
+  int ablate;   // profiling only (set_stem_ablation): 1 skip pool, 2 skip MFMAs, 4 skip patch normalise
 };
+
+static int g_stem_ablate = 0;
+void set_stem_ablation(int mode) { g_stem_ablate = mode; }
 
 struct Quads {
   uint32_t d[stem::QPT][3];
@@ -216,11 +220,13 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
       float4v acc[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[i] = float4v{0.f, 0.f, 0.f, 0.f};
+      if (!(g.ablate & 2)) {
 #pragma unroll
-      for (int kh = 0; kh < KH; ++kh) {
-        const half8v fb = *reinterpret_cast<const half8v*>(pb + kh * IPC * 8);
+        for (int kh = 0; kh < KH; ++kh) {
+          const half8v fb = *reinterpret_cast<const half8v*>(pb + kh * IPC * 8);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[kh][i], fb, acc[i], 0, 0, 0);
+          for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[kh][i], fb, acc[i], 0, 0, 0);
+        }
       }
       if (p < NPIX) {
         const int oy = oy0 + cy, ox = ox0 + cx;
@@ -239,13 +245,13 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
 
     const int tnext = tn;
     if (tnext < g.ntiles) {
-      store_patch(patch, g, tnext, tid, q);        // uses the quads prefetched one tile ago
+      if (!(g.ablate & 4)) store_patch(patch, g, tnext, tid, q);   // uses the quads prefetched one tile ago
       tn = tnext + gridDim.x;
       if (tn < g.ntiles) load_quads(img, g, tn, tid, q);
     }
 
     // ---- 3x3/2 max-pool from the LDS tile -> global ---------------------------
-    for (int i = tid; i < PT * PT * 8; i += 256) {
+    for (int i = tid; i < ((g.ablate & 1) ? 0 : PT * PT * 8); i += 256) {
       const int c8 = i & 7, pp = i >> 3;
       const int py = pp / PT, px = pp - py * PT;
       if (py0 + py >= g.Hp || px0 + px >= g.Wp) continue;
@@ -281,6 +287,7 @@ void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, h
   g.tiles_x = (g.Wp + PT - 1) / PT;
   g.tiles_y = (g.Hp + PT - 1) / PT;
   g.ntiles = B * g.tiles_x * g.tiles_y;
+  g.ablate = g_stem_ablate;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_fused_kernel),

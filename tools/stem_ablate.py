@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Time the fused stem with parts of its work ablated (profiling only; the
+ablated outputs are wrong): where does a tile's time go?"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from idunno import ops
+    from idunno.models import build_program
+
+    ext = ops.load()
+    p = build_program("resnet18")
+    s = p.stem
+    img = torch.randint(0, 256, (400, 224, 224, 3), dtype=torch.uint8, device="cuda")
+    w, b = s.w.cuda(), s.b.cuda()
+    names = {0: "full", 1: "no pool", 2: "no MFMA", 4: "no patch normalise", 3: "no pool+MFMA", 7: "none (loads, sync)"}
+    for rnd in range(2):
+        for mode, name in names.items():
+            ext.set_stem_ablation(mode)
+            ops.stem_fused(img, w, b)
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st.record()
+            for _ in range(10):
+                ops.stem_fused(img, w, b)
+            en.record()
+            torch.cuda.synchronize()
+            if rnd:
+                print(f"{name:22s} {st.elapsed_time(en) / 10 * 1000:8.1f} us", flush=True)
+    ext.set_stem_ablation(0)
+
+
+if __name__ == "__main__":
+    main()
