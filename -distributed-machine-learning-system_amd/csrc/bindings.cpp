@@ -148,6 +148,11 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     return y;
   }
   const int t = tile >= 10 ? (int)tile : conv_glds_pick(a.M, Cout);
+  if (t >= 60 && t < 70) {             // v3 large-tile loop (conv_big.hip)
+    TORCH_CHECK(conv_big_launch(a, out_f32, t, cur_stream()), "unknown conv tile id ", t);
+    check_launch("conv_big");
+    return y;
+  }
   TORCH_CHECK(conv_glds_launch(a, out_f32, t, cur_stream()), "unknown conv tile id ", t);
   check_launch("conv_glds");
   return y;

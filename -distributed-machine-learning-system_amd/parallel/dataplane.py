@@ -80,8 +80,12 @@ class QueryPlane:
         dev = env.device
         self._desc = torch.full((env.world, 4), NO_WORK, dtype=torch.int64, device=dev)
         self._pack = torch.zeros(max_chunk, 2, dtype=torch.int32, device=dev)
-        self._gathered = [torch.zeros(max_chunk, 2, dtype=torch.int32, device=dev)
-                          for _ in range(env.world)] if env.rank == coordinator else None
+        # one contiguous [world, max_chunk, 2] buffer on the coordinator; the
+        # per-rank gather outputs are views of it, so the whole round's results
+        # come to the host with ONE device->host copy (``gathered_all``)
+        self.gathered_all = torch.zeros(env.world, max_chunk, 2, dtype=torch.int32, device=dev) \
+            if env.rank == coordinator else None
+        self._gathered = list(self.gathered_all.unbind(0)) if env.rank == coordinator else None
 
     # -- M9 ---------------------------------------------------------------------
     def dispatch(self, table: list[tuple[int, int, int, int]] | None) -> tuple[int, int, int, int]:

@@ -125,8 +125,7 @@ def main(argv=None) -> int:
         gathered = plane.gather(cls, prob)                  # RCCL gather of top-1 to rank 0
         if coord:
             slot = q % 2
-            for r in range(env.world):
-                host_res[slot][r].copy_(gathered[r], non_blocking=True)
+            host_res[slot].copy_(plane.gathered_all, non_blocking=True)   # one D2H copy per round
             ev = torch.cuda.Event()
             ev.record()
             if pending:

@@ -87,6 +87,35 @@ def test_conv_all_tiles_with_residual(ops, tile, H):
     _check(y, ref)
 
 
+BIG_TILES = [60, 61, 62, 63, 65, 66, 67]
+
+
+@pytest.mark.parametrize("tile", BIG_TILES)
+@pytest.mark.parametrize("B,H,Cin,Cout,k,s,res", [
+    (3, 28, 128, 128, 3, 1, True),    # layer2 3x3 + residual, M = 2352 (not a tile multiple)
+    (2, 28, 64, 128, 3, 2, False),    # layer2 first conv, stride 2
+    (2, 14, 256, 256, 3, 1, True),    # layer3
+    (3, 7, 512, 512, 3, 1, False),    # layer4, M = 147 < one tile
+    (2, 13, 192, 384, 3, 1, False),   # alexnet conv3: Cout not a multiple of 256
+    (2, 9, 64, 192, 1, 1, True),      # 1x1, one K stage; Cout 192 masks part of a 128/256 tile
+])
+def test_conv_big_tiles(ops, tile, B, H, Cin, Cout, k, s, res):
+    """v3 large-tile loop (conv_big.hip) vs fp32 torch, with masked rows / columns."""
+    from idunno.models.packed import pack_conv_weight
+
+    torch.manual_seed(tile * 7 + H + Cout)
+    p = k // 2
+    x = torch.randn(B, H, H, Cin, device=DEV).half()
+    w = torch.randn(Cout, Cin, k, k) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    Ho = (H + 2 * p - k) // s + 1
+    r = torch.randn(B, Ho, Ho, Cout, device=DEV).half() if res else None
+    pw, _ = pack_conv_weight(w)
+    y = ops.conv2d(x, pw.to(DEV), b.to(DEV), k, k, s, p, True, residual=r, tile=tile)
+    ref = _ref_conv(x, w.half().float().to(DEV), b.to(DEV), s, p, True, r)
+    _check(y, ref)
+
+
 @pytest.mark.parametrize("k,s,p,H", [(7, 2, 3, 224), (11, 4, 2, 224), (7, 2, 3, 37)])
 def test_conv_small_c_stem(ops, k, s, p, H):
     from idunno.models.packed import pack_conv_weight
