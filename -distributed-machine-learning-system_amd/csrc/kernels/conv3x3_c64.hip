@@ -122,21 +122,17 @@ __device__ __forceinline__ void c64_tile(const C64Args& a, int t, bool prefetch,
   using namespace c64;
   const int lrow = lane >> 3, lslot = lane & 7;
   const int frow = lane & 15, fch = lane >> 4;
-  constexpr int NRES = HAS_RES ? FN * FM : 0;    // residual loads per tile
-  __builtin_amdgcn_s_barrier();                  // every wave is done reading nxt (tile t-1)
+  // One barrier per tile.  Every wave reaches it after (a) its MFMAs of tile
+  // t-1 (so `nxt`, tile t-1's patch, is free) and (b) its `vmcnt(0)` behind
+  // those MFMAs (so its DMAs of tile t's patch, issued a whole tile earlier,
+  // have landed).  The wait sits AFTER the MFMAs, not before them: vmcnt also
+  // counts the epilogue stores of the previous tile, and a wait in front of
+  // the MFMAs would expose their write latency on every tile.
+  __builtin_amdgcn_s_barrier();
   if (prefetch) {
-    // tile t+1's patch and residual go in flight; what tile t needs (its patch,
-    // its residual, the weights, older stores) was issued before them
     c64_issue_patch(a, t + 1, nxt, wave, lrow, lslot);
     if constexpr (HAS_RES) c64_load_res(a, t + 1, rv_next, wn, wm, lane);
-    if (wave < P_HI)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P_INS + NRES) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P_INS - 1 + NRES) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  __builtin_amdgcn_s_barrier();
 
   float4v acc[FN][FM];
 #pragma unroll
@@ -195,6 +191,10 @@ __device__ __forceinline__ void c64_tile(const C64Args& a, int t, bool prefetch,
       for (int f = 0; f < FM; ++f)
         acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ca[i], cb[f], acc[i][f], 0, 0, 0);
   }
+  __builtin_amdgcn_sched_barrier(0);
+  // patch and residual of tile t+1 (issued before the MFMAs), this tile's
+  // residual and the previous tile's stores: all had a tile of MFMAs to land
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // ---- epilogue: bias (+residual) (+ReLU), NHWC 8-byte stores -------------------
   const int per = a.tiles_x * a.tiles_y;
@@ -278,6 +278,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_c64_kernel(const C64Args a) {
   half4v rA[FN][FM], rB[FN][FM];                 // residual of the current / next tile
   c64_issue_patch(a, t_begin, p0, wave, lrow, lslot);
   if constexpr (HAS_RES) c64_load_res(a, t_begin, rA, wn, wm, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // weights + first patch (+ residual) landed
   // two tiles per trip so the buffers and residual registers swap statically
   for (int t = t_begin; t < t_end; t += 2) {
     c64_tile<HAS_RES>(a, t, t + 1 < t_end, smem, p0, p1, bvr, pbase, rA, rB, wave, wn, wm, lane);

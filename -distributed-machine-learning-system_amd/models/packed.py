@@ -317,7 +317,7 @@ class HipRunner:
         key = ("win", shard.data_ptr(), tuple(shard.shape), batch)
         if key in self._graphs:
             g, start, sout = self._graphs[key]
-            return start, (lambda: (g.replay(), sout)[1])
+            return start, self._replayer(g, sout, shard)
         start = torch.zeros(1, dtype=torch.int64, device=self.device)
         with _CAPTURE_LOCK:
             st = torch.cuda.Stream(device=self.device)
@@ -330,14 +330,25 @@ class HipRunner:
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 sout = self.forward(shard, start, batch)
         self._graphs[key] = (g, start, sout)
-        return start, (lambda: (g.replay(), sout)[1])
+        return start, self._replayer(g, sout, shard)
+
+    def _replayer(self, g, sout, *keep):
+        """Replay closure that keeps this runner (its HBM-resident weights) and
+        the captured inputs alive: the graph holds raw device pointers, so a
+        caller that drops the runner and keeps only the closure must not let
+        the weights go back to the allocator."""
+        def replay():
+            g.replay()
+            return sout
+        replay._keep = (self, keep)
+        return replay
 
     # -- hipGraph -------------------------------------------------------------
     def capture(self, batch: int, hw: int = 224):
         """Capture forward for a fixed batch; returns (static_in, replay_fn)."""
         if batch in self._graphs:
             g, sin, sout = self._graphs[batch]
-            return sin, (lambda: (g.replay(), sout)[1])
+            return sin, self._replayer(g, sout)
         sin = torch.zeros(batch, hw, hw, 3, dtype=torch.uint8, device=self.device)
         with _CAPTURE_LOCK:  # one capture at a time per process; other threads keep launching
             s = torch.cuda.Stream(device=self.device)
@@ -350,7 +361,7 @@ class HipRunner:
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 sout = self.forward(sin)
         self._graphs[batch] = (g, sin, sout)
-        return sin, (lambda: (g.replay(), sout)[1])
+        return sin, self._replayer(g, sout)
 
     def flops_per_image(self) -> float:
         """Useful (unpadded) FLOPs for one 224x224 image."""

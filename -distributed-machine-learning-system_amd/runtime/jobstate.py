@@ -64,6 +64,26 @@ class ChunkResult:
         return str(tup)
 
 
+def _add_interval(ivs: list, s: int, e: int) -> int:
+    """Merge [s, e] into the sorted, disjoint interval list ``ivs`` (in place);
+    returns how many of its integers were not already covered."""
+    new = e - s + 1
+    out, i = [], 0
+    while i < len(ivs) and ivs[i][1] < s - 1:
+        out.append(ivs[i])
+        i += 1
+    lo, hi = s, e
+    while i < len(ivs) and ivs[i][0] <= e + 1:
+        a, b = ivs[i]
+        new -= max(0, min(b, e) - max(a, s) + 1)
+        lo, hi = min(lo, a), max(hi, b)
+        i += 1
+    out.append([lo, hi])
+    out.extend(ivs[i:])
+    ivs[:] = out
+    return new
+
+
 class JobState:
     def __init__(self, batchsize: dict | None = None, clock=time.time, window_s: float = WINDOW_S,
                  names: list[str] | None = None):
@@ -76,6 +96,7 @@ class JobState:
         self.working_vm_set: dict = defaultdict(list)
         self.results: dict = defaultdict(list)          # "model q" -> [ChunkResult]
         self._done_keys: set = set()
+        self._done_imgs: dict = defaultdict(list)       # (model, qnum) -> merged finished [s, e] ranges
         self.finished_images: dict = defaultdict(int)
         self.finished_queries: dict = defaultdict(int)
         self._rate_win: dict = defaultdict(deque)       # model -> (t_finish, n_images)
@@ -89,12 +110,28 @@ class JobState:
         self.jobs: dict = {}                            # job id -> {model, start, end, next}
 
     # -- coordinator-side jobs (C28 variant), replicated to the standby ----------
-    def add_job(self, model: str, start: int, end: int) -> int:
+    def add_job(self, model: str, start: int, end: int, bs: int | None = None) -> int:
+        """Register a coordinator-side job and reserve the query numbers of all
+        its batch-size queries up front (query k of the job is ``qbase + k``).
+        A promoted standby that resumes the job from a lagging snapshot then
+        re-issues a query the dead coordinator had already dispatched under the
+        SAME number, and ``record_result``'s per-query image dedupe keeps the
+        late results of the original dispatch from being counted twice."""
+        bs = int(bs or self.batchsize.get(model, 1))
         with self.lock:
             jid = len(self.jobs) + 1
-            self.jobs[jid] = {"model": model, "start": int(start), "end": int(end), "next": int(start)}
+            nq = (int(end) - int(start)) // bs + 1
+            qbase = self.next_qnum[model] + 1
+            self.next_qnum[model] += nq
+            self.jobs[jid] = {"model": model, "start": int(start), "end": int(end), "next": int(start),
+                              "bs": bs, "qbase": qbase}
             self.seq += 1
             return jid
+
+    def job_query_number(self, jid: int, s: int) -> int:
+        with self.lock:
+            j = self.jobs[jid]
+            return j["qbase"] + (int(s) - j["start"]) // j["bs"]
 
     def advance_job(self, jid: int, nxt: int) -> None:
         with self.lock:
@@ -145,6 +182,7 @@ class JobState:
                 return False
             key = (model, qnum)
             entries = self.worker_set.get(key, [])
+            was_done = bool(entries) and all(ent[3] == "f" for ent in entries)
             hit = None
             for i, ent in enumerate(entries):
                 if ent[1] == start and ent[2] == end and ent[3] == "w":
@@ -161,7 +199,17 @@ class JobState:
                 if not self.working_vm_set[w]:
                     self.working_vm_set.pop(w, None)
             self._done_keys.add(ck)
-            n = end - start + 1                                   # fix A3
+            if entries and not was_done and all(ent[3] == "f" for ent in entries):
+                self.finished_queries[model] += 1
+                t0 = self.query_submit_time.get(key)
+                if t0 is not None:
+                    self.query_latency[model].append(now - t0)
+            # images of this query already answered under another chunk split
+            # (re-dispatch after a failure / a resumed job) are not counted again
+            n = _add_interval(self._done_imgs[key], start, end)   # fix A3: end - start + 1 when new
+            if n == 0:
+                self.seq += 1
+                return False
             self.finished_images[model] += n
             self._rate_win[model].append((now, n))
             bs = self.batchsize.get(model, n)
@@ -171,11 +219,6 @@ class JobState:
             self.results[f"{model} {qnum}"].append(
                 ChunkResult(start, end, np.asarray(cls, dtype=np.int32), np.asarray(prob, dtype=np.float32),
                             worker))
-            if entries and all(ent[3] == "f" for ent in entries):
-                self.finished_queries[model] += 1
-                t0 = self.query_submit_time.get(key)
-                if t0 is not None:
-                    self.query_latency[model].append(now - t0)
             self.seq += 1
             return True
 
@@ -342,6 +385,7 @@ class JobState:
             if snap.get("results") is not None:
                 self.results = defaultdict(list)
                 self._done_keys = set()
+                self._done_imgs = defaultdict(list)
                 for k, v in snap["results"].items():
                     model, q = k.rsplit(" ", 1)
                     qn = int(q) if q.lstrip("-").isdigit() else q
@@ -349,6 +393,7 @@ class JobState:
                         self.results[k].append(ChunkResult(s, e, np.asarray(c, np.int32),
                                                            np.asarray(p, np.float32), w))
                         self._done_keys.add((model, qn, s, e))
+                        _add_interval(self._done_imgs[(model, qn)], s, e)
             if not keep_results:
                 self.finished_images = defaultdict(int, snap["finished_images"])
                 self.finished_queries = defaultdict(int, snap["finished_queries"])

@@ -262,7 +262,8 @@ class Node:
         self.stop()
 
     # -- coordinator -------------------------------------------------------------------
-    def submit_query(self, model: str, start: int, end: int, client: str | None = None) -> dict:
+    def submit_query(self, model: str, start: int, end: int, client: str | None = None,
+                     qnum: int | None = None) -> dict:
         if not self.is_coordinator:
             if self.name == self.standby and not self.membership.is_alive(self.membership.master):
                 self._promote("query arrived while coordinator is down")
@@ -279,7 +280,8 @@ class Node:
         if end < start:
             return {"ok": False, "error": "empty range"}
         alive = self.membership.alive()
-        qnum = self.state.new_query_number(model)
+        if qnum is None:
+            qnum = self.state.new_query_number(model)
         with self.state.lock:
             busy = {m for (m, _q, _w, _s, _e, _t) in self.state.pending()}
         self.sched.active_jobs = busy | {model}
@@ -306,7 +308,7 @@ class Node:
                                            "job": True}, self.cfg.rpc_timeout_s)
         model = canonical(model)
         bs = self.cfg.batch_for(model)
-        jid = self.state.add_job(model, start, end)
+        jid = self.state.add_job(model, start, end, bs)
         self._start_job_runner(jid)
         return {"ok": True, "job": jid, "queries": (end - start) // bs + 1}
 
@@ -324,7 +326,7 @@ class Node:
                     return
                 e = min(s + self.cfg.batch_for(job["model"]) - 1, job["end"])
                 if not self.state.range_submitted(job["model"], s, e):
-                    self.submit_query(job["model"], s, e)
+                    self.submit_query(job["model"], s, e, qnum=self.state.job_query_number(jid, s))
                 self.state.advance_job(jid, e + 1)
                 if self.cfg.client_query_interval_s and e < job["end"]:
                     time.sleep(self.cfg.client_query_interval_s)

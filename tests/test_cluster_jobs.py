@@ -3,7 +3,7 @@ straggler resend (A7), on the in-memory fake cluster."""
 from idunno.runtime.cluster import LocalCluster
 from idunno.runtime.shell import Shell
 
-FAST = dict(heartbeat_period_s=0.05, failure_timeout_s=0.4, metadata_period_s=0.1, rpc_timeout_s=2.0)
+FAST = dict(heartbeat_period_s=0.05, failure_timeout_s=1.0, metadata_period_s=0.1, rpc_timeout_s=2.0)
 
 
 def test_job_submission_batched_by_coordinator():

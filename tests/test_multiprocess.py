@@ -55,7 +55,7 @@ def test_multiprocess_cluster_failures():
              "--base-port", str(base), "--store-root", tmp, "--executor", "fake", "--join-delay", "0.3"],
             cwd=ROOT, env=env, stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
     cfg = ClusterConfig(num_nodes=n, base_port=base, store_root=tmp, heartbeat_period_s=0.05,
-                        failure_timeout_s=0.6, metadata_period_s=0.1, rpc_timeout_s=3.0)
+                        failure_timeout_s=1.2, metadata_period_s=0.1, rpc_timeout_s=3.0)
     me = Node(cfg, "node03", TcpTransport("node03", cfg.address, cfg.address("node03")), FakeExecutor())
     try:
         time.sleep(1.0)

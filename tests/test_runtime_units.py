@@ -136,6 +136,31 @@ def test_jobstate_reassign_and_pending():
     assert [p[2] for p in js.pending()] == ["node04"]
 
 
+def test_jobstate_dedupes_images_across_chunk_splits():
+    """A query re-dispatched with a different chunk split (promoted standby
+    resuming a job under its reserved query number) counts each image once."""
+    js = JobState()
+    jid = js.add_job("resnet18", 0, 999, 400)            # 3 queries -> numbers 1, 2, 3 reserved
+    assert [js.job_query_number(jid, s) for s in (0, 400, 800)] == [1, 2, 3]
+    assert js.new_query_number("resnet18") == 4
+    cls = np.zeros(400, np.int32)
+    prob = np.ones(400, np.float32)
+    js.assign("resnet18", 1, [("a", 0, 199), ("b", 200, 399)])
+    assert js.record_result("resnet18", 1, "a", 0, 199, cls[:200], prob[:200])
+    # the same query re-issued over three workers: only images 200..399 are new
+    js.assign("resnet18", 1, [("c", 0, 132), ("d", 133, 265), ("e", 266, 399)])
+    assert not js.record_result("resnet18", 1, "c", 0, 132, cls[:133], prob[:133])
+    assert js.record_result("resnet18", 1, "d", 133, 265, cls[:133], prob[:133])
+    assert js.record_result("resnet18", 1, "e", 266, 399, cls[:134], prob[:134])
+    assert js.record_result("resnet18", 1, "b", 200, 399, cls[:200], prob[:200]) is False
+    assert js.images_done("resnet18") == 400
+    assert js.finished_queries["resnet18"] == 1
+    # the same images under a NEW query number are new work (repeated queries count)
+    js.assign("resnet18", 5, [("a", 0, 399)])
+    assert js.record_result("resnet18", 5, "a", 0, 399, cls, prob)
+    assert js.images_done("resnet18") == 800
+
+
 def test_config_env_and_file(tmp_path):
     p = tmp_path / "c.json"
     p.write_text(json.dumps({"num_nodes": 4, "heartbeat_period_s": 0.1}))

@@ -6,7 +6,7 @@ from idunno.runtime.cluster import LocalCluster
 from idunno.runtime.shell import Shell
 from idunno.runtime.transport import wait_for
 
-FAST = dict(heartbeat_period_s=0.05, failure_timeout_s=0.4, metadata_period_s=0.1, rpc_timeout_s=2.0)
+FAST = dict(heartbeat_period_s=0.05, failure_timeout_s=1.0, metadata_period_s=0.1, rpc_timeout_s=2.0)
 
 
 def test_chrome_trace_has_query_and_chunk_spans(tmp_path):
