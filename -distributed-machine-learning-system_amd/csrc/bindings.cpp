@@ -148,6 +148,15 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     return y;
   }
   const int t = tile >= 10 ? (int)tile : conv_glds_pick(a.M, Cout);
+  if (t >= 70 && t < 80) {             // persistent loop (conv_pers.hip); 1-stage convs fall back to tile 65
+    if (conv_pers_launch(a, out_f32, t, cur_stream())) {
+      check_launch("conv_pers");
+      return y;
+    }
+    TORCH_CHECK(conv_big_launch(a, out_f32, 65, cur_stream()), "conv_big fallback failed");
+    check_launch("conv_big");
+    return y;
+  }
   if (t >= 60 && t < 70) {             // v3 large-tile loop (conv_big.hip)
     TORCH_CHECK(conv_big_launch(a, out_f32, t, cur_stream()), "unknown conv tile id ", t);
     check_launch("conv_big");

@@ -85,4 +85,13 @@ __device__ __forceinline__ half4v gload_b64_untracked(const void* p) {
   return v;
 }
 
+// 16-byte global load the wait-count pass does not track (see gload_b64_untracked).
+__device__ __forceinline__ float4v gload_f4_untracked(const void* p) {
+  float4v v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+__device__ __forceinline__ void reg_tie(half4v& r) { asm volatile("" : "+v"(r)); }
+
 }  // namespace idunno

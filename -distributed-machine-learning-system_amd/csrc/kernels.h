@@ -29,6 +29,7 @@ void conv_igemm_launch(ConvArgs a, bool small, bool out_f32, int tile, hipStream
 int conv_pick_tile(int M, int Cout);
 bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 bool conv_big_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
+bool conv_pers_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);   // false: shape unsupported
 bool conv3x3_patch_supported(int H, int W, int C, int Cout);
 bool conv3x3_c64_supported(int C, int Cout);
 void set_stem_ablation(int mode);

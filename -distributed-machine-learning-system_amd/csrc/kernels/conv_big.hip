@@ -39,7 +39,8 @@ __device__ __forceinline__ void big_vmcnt() {
 }
 
 template <int BN, int BM, int WN, int WM, int NS, int MINB, bool HAS_RES, bool OUT_F32>
-__global__ void __launch_bounds__(512, MINB) conv_big_kernel(const ConvArgs a) {
+// second launch bound = waves per SIMD (HIP semantics): MINB workgroups of 8 waves per CU
+__global__ void __launch_bounds__(512, 2 * MINB) conv_big_kernel(const ConvArgs a) {
   constexpr int NW = 8;
   static_assert(WN * WM == NW, "8 waves");
   constexpr int TN = BN / WN, TM = BM / WM;

@@ -87,7 +87,7 @@ def test_conv_all_tiles_with_residual(ops, tile, H):
     _check(y, ref)
 
 
-BIG_TILES = [60, 61, 62, 63, 65, 66, 67]
+BIG_TILES = [60, 61, 62, 63, 65, 66, 67, 70, 71, 72, 73]
 
 
 @pytest.mark.parametrize("tile", BIG_TILES)
@@ -113,6 +113,25 @@ def test_conv_big_tiles(ops, tile, B, H, Cin, Cout, k, s, res):
     pw, _ = pack_conv_weight(w)
     y = ops.conv2d(x, pw.to(DEV), b.to(DEV), k, k, s, p, True, residual=r, tile=tile)
     ref = _ref_conv(x, w.half().float().to(DEV), b.to(DEV), s, p, True, r)
+    _check(y, ref)
+
+
+@pytest.mark.parametrize("tile", [70, 71, 72, 73])
+@pytest.mark.parametrize("res", [False, True])
+def test_conv_persistent_many_tiles_per_workgroup(ops, tile, res):
+    """Persistent kernel with several tiles per workgroup (ring crosses tile
+    boundaries, epilogue overlaps the next tile's DMA), last tile partial."""
+    from idunno.models.packed import pack_conv_weight
+
+    torch.manual_seed(tile + 100 * res)
+    B, H, Cin, Cout = 25, 56, 64, 128      # M = 78400: 613 / 1225 tiles > resident workgroups
+    x = torch.randn(B, H, H, Cin, device=DEV).half()
+    w = torch.randn(Cout, Cin, 3, 3) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    r = torch.randn(B, H, H, Cout, device=DEV).half() if res else None
+    pw, _ = pack_conv_weight(w)
+    y = ops.conv2d(x, pw.to(DEV), b.to(DEV), 3, 3, 1, 1, True, residual=r, tile=tile)
+    ref = _ref_conv(x, w.half().float().to(DEV), b.to(DEV), 1, 1, True, r)
     _check(y, ref)
 
 
