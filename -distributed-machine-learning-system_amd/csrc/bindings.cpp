@@ -188,8 +188,11 @@ static const long long* window_args(const torch::Tensor& img, const c10::optiona
   return reinterpret_cast<const long long*>(s.data_ptr());
 }
 
+// `start_offset` is subtracted from *start on the device: the window start may
+// be a GLOBAL image index (e.g. straight from the broadcast query descriptor)
+// and the offset the shard's first global index.
 torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias, c10::optional<torch::Tensor> start,
-                         int64_t batch) {
+                         int64_t batch, int64_t start_offset) {
   CHECK_DEV(img);
   CHECK_DEV(w);
   CHECK_DEV(bias);
@@ -213,11 +216,11 @@ torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias,
   auto y = torch::empty({B, Hp, Wp, 64}, img.options().dtype(torch::kHalf));
   if (B)
     stem_fused_launch(img.data_ptr<uint8_t>(), reinterpret_cast<const half_t*>(w.data_ptr()), bias.data_ptr<float>(),
-                      reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp, max_start, cur_stream()); check_launch("stem_fused");
+                      reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp, start_offset, max_start, cur_stream()); check_launch("stem_fused");
   return y;
 }
 
-torch::Tensor preprocess(torch::Tensor img, c10::optional<torch::Tensor> start, int64_t batch) {
+torch::Tensor preprocess(torch::Tensor img, c10::optional<torch::Tensor> start, int64_t batch, int64_t start_offset) {
   CHECK_DEV(img);
   CHECK_CONTIG(img);
   CHECK_DT(img, torch::kUInt8);
@@ -228,7 +231,7 @@ torch::Tensor preprocess(torch::Tensor img, c10::optional<torch::Tensor> start, 
   auto out = torch::empty({B, img.size(1), img.size(2), 4}, img.options().dtype(torch::kHalf));
   const long npix = (long)B * img.size(1) * img.size(2);
   if (npix)
-    preprocess_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), npix, sp, max_start,
+    preprocess_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), npix, sp, start_offset, max_start,
                       (long)img.size(1) * img.size(2), cur_stream()); check_launch("preprocess");
   return out;
 }
@@ -281,15 +284,27 @@ torch::Tensor global_avgpool_nhwc(torch::Tensor x) {
   return y;
 }
 
-std::vector<torch::Tensor> softmax_top1(torch::Tensor logits) {
+// Optional `packed` [>= rows, 2] int32: also write (class, prob bits) pairs there
+// (the data plane's gather send buffer, so no repack kernel runs afterwards).
+std::vector<torch::Tensor> softmax_top1(torch::Tensor logits, c10::optional<torch::Tensor> packed) {
   CHECK_DEV(logits);
   CHECK_DT(logits, torch::kFloat);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [rows, N] with unit column stride");
   const int rows = logits.size(0), N = logits.size(1), ld = logits.stride(0);
   auto cls = torch::empty({rows}, logits.options().dtype(torch::kInt));
   auto prob = torch::empty({rows}, logits.options());
+  int* pk = nullptr;
+  if (packed.has_value() && packed->defined()) {
+    auto& p = *packed;
+    CHECK_DEV(p);
+    CHECK_CONTIG(p);
+    CHECK_DT(p, torch::kInt);
+    TORCH_CHECK(p.device() == logits.device(), "packed must live on the logits device");
+    TORCH_CHECK(p.dim() == 2 && p.size(1) == 2 && p.size(0) >= rows, "packed must be [>= rows, 2] int32");
+    pk = p.data_ptr<int>();
+  }
   if (rows) softmax_top1_launch(logits.data_ptr<float>(), ld, N, rows, cls.data_ptr<int>(), prob.data_ptr<float>(),
-                                cur_stream()); check_launch("softmax_top1");
+                                pk, cur_stream()); check_launch("softmax_top1");
   return {cls, prob};
 }
 
@@ -309,13 +324,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("relu"), py::arg("out_f32") = false, py::arg("tile") = -1);
   m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 NHWC4", py::arg("img"),
-        py::arg("start") = py::none(), py::arg("batch") = -1);
+        py::arg("start") = py::none(), py::arg("batch") = -1, py::arg("start_offset") = 0);
   m.def("stem_fused", &stem_fused, "fused normalise + conv7x7/2 + bias + relu + maxpool3x3/2 (ResNet stem)",
-        py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("start") = py::none(), py::arg("batch") = -1);
+        py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("start") = py::none(), py::arg("batch") = -1,
+        py::arg("start_offset") = 0);
   m.def("resize_crop", &resize_crop, "bilinear resize + centre crop + normalise");
   m.def("maxpool2d_nhwc", &maxpool2d_nhwc, "NHWC max pool");
   m.def("global_avgpool_nhwc", &global_avgpool_nhwc, "NHWC global average pool");
-  m.def("softmax_top1", &softmax_top1, "fused row softmax + argmax");
+  m.def("softmax_top1", &softmax_top1, "fused row softmax + argmax", py::arg("logits"),
+        py::arg("packed") = py::none());
   m.def("synth_images", &synth_images, "deterministic synthetic uint8 images [n,hw,hw,3]");
   m.def("pick_tile", &pick_tile, "tile id the conv heuristic picks for (M, Cout)");
   m.def("set_stem_ablation", &set_stem_ablation,

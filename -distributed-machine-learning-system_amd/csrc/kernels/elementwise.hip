@@ -21,12 +21,12 @@ __constant__ float kInvStd[3] = {1.0f / 0.229f, 1.0f / 0.224f, 1.0f / 0.225f};
 // Optional device-side window: images start at *start_idx (clamped to
 // [0, max_start]) of the shard `img`.
 __global__ void preprocess_kernel(const uint8_t* __restrict__ img, half_t* __restrict__ out,
-                                  long npix, const long long* __restrict__ start_idx, long long max_start,
-                                  long pix_per_img) {
+                                  long npix, const long long* __restrict__ start_idx, long long start_off,
+                                  long long max_start, long pix_per_img) {
   const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npix) return;
   if (start_idx != nullptr) {
-    long long s0 = *start_idx;
+    long long s0 = *start_idx - start_off;
     s0 = s0 < 0 ? 0 : (s0 > max_start ? max_start : s0);
     img += (size_t)s0 * pix_per_img * 3;
   }
@@ -40,11 +40,11 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ img, half_t* __res
 }
 
 void preprocess_launch(const uint8_t* img, half_t* out, long npix, const long long* start_idx,
-                       long long max_start, long pix_per_img, hipStream_t st) {
+                       long long start_off, long long max_start, long pix_per_img, hipStream_t st) {
   const int bs = 256;
   const long grid = (npix + bs - 1) / bs;
   hipLaunchKernelGGL(preprocess_kernel, dim3((unsigned)grid), dim3(bs), 0, st, img, out, npix, start_idx,
-                     max_start, pix_per_img);
+                     start_off, max_start, pix_per_img);
 }
 
 // Bilinear resize of an (Hi x Wi) uint8 HWC image so that its shorter side is
@@ -161,7 +161,7 @@ void avgpool_launch(const half_t* x, half_t* y, int B, int HW, int C, hipStream_
 // prob(top1) = 1 / sum_j exp(x_j - x_max).  Ties resolve to the lowest index
 // (torch.topk semantics on CPU).
 __global__ void softmax_top1_kernel(const float* __restrict__ logits, int ld, int N, int rows,
-                                    int* __restrict__ cls, float* __restrict__ prob) {
+                                    int* __restrict__ cls, float* __restrict__ prob, int* __restrict__ packed) {
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (wave >= rows) return;
@@ -188,17 +188,22 @@ __global__ void softmax_top1_kernel(const float* __restrict__ logits, int ld, in
   for (int j = lane; j < N; j += 64) s += __expf(r[j] - best);
   s = wave_sum(s);
   if (lane == 0) {
+    const float p = 1.f / s;
     cls[wave] = bidx;
-    prob[wave] = 1.f / s;
+    prob[wave] = p;
+    if (packed != nullptr) {   // (class, prob bits) pairs: the RCCL gather's send buffer
+      packed[2 * wave] = bidx;
+      packed[2 * wave + 1] = __float_as_int(p);
+    }
   }
 }
 
-void softmax_top1_launch(const float* logits, int ld, int N, int rows, int* cls, float* prob,
+void softmax_top1_launch(const float* logits, int ld, int N, int rows, int* cls, float* prob, int* packed,
                          hipStream_t st) {
   const int bs = 256;  // 4 rows per block
   const int grid = (rows + 3) / 4;
   hipLaunchKernelGGL(softmax_top1_kernel, dim3(grid), dim3(bs), 0, st, logits, ld, N, rows, cls,
-                     prob);
+                     prob, packed);
 }
 
 // Deterministic synthetic images: byte group g (8 bytes) of image `idx` is the

@@ -259,10 +259,11 @@ class HipRunner:
         self._graphs: dict[int, tuple] = {}
 
     # -- eager forward ------------------------------------------------------
-    def logits(self, img_u8: torch.Tensor, start: torch.Tensor | None = None, batch: int = -1) -> torch.Tensor:
+    def logits(self, img_u8: torch.Tensor, start: torch.Tensor | None = None, batch: int = -1,
+               start_offset: int = 0) -> torch.Tensor:
         """fp32 logits.  With ``start`` (int64 GPU scalar) and ``batch``,
         ``img_u8`` is a whole HBM-resident shard and the images
-        [*start, *start + batch) are classified (device-side window)."""
+        [*start - start_offset, ... + batch) are classified (device-side window)."""
         o = self.ops
         p = self.p
         native = tuple(img_u8.shape[1:3]) == (224, 224)
@@ -272,10 +273,10 @@ class HipRunner:
         fused = (self.fuse_stem and native and p.kind == "resnet" and s.small and s.kh == 7 and s.kw == 7
                  and s.stride == 2 and s.pad == 3 and s.cout == 64)
         if not fused:
-            x = o.preprocess(img_u8, start, batch) if native else o.resize_crop(img_u8, 256, 224)
+            x = o.preprocess(img_u8, start, batch, start_offset) if native else o.resize_crop(img_u8, 256, 224)
         if p.kind == "resnet":
             if fused:
-                x = o.stem_fused(img_u8, s.w, s.b, start, batch)
+                x = o.stem_fused(img_u8, s.w, s.b, start, batch, start_offset)
             else:
                 x = o.conv2d(x, s.w, s.b, s.kh, s.kw, s.stride, s.pad, s.relu)
                 x = o.maxpool2d(x, 3, 2, 1)
@@ -302,35 +303,46 @@ class HipRunner:
             x = o.linear(x, fc.w, fc.b, relu=fc.relu, out_f32=last)
         return x
 
-    def forward(self, img_u8: torch.Tensor, start: torch.Tensor | None = None, batch: int = -1):
-        return self.ops.softmax_top1(self.logits(img_u8, start, batch))
+    def forward(self, img_u8: torch.Tensor, start: torch.Tensor | None = None, batch: int = -1,
+                start_offset: int = 0, packed: torch.Tensor | None = None):
+        """(class int32 [B], prob fp32 [B]); with ``packed`` the fused
+        softmax-top1 also writes (class, prob bits) pairs into it."""
+        return self.ops.softmax_top1(self.logits(img_u8, start, batch, start_offset), packed)
 
     __call__ = forward
 
-    def capture_window(self, shard: torch.Tensor, batch: int):
+    def capture_window(self, shard: torch.Tensor, batch: int, start: torch.Tensor | None = None,
+                       start_offset: int = 0, packed: torch.Tensor | None = None):
         """hipGraph of forward over a device-side window of ``shard``.
 
         Returns (start, replay): write the first image index into the int64
         GPU scalar ``start`` (a stream-ordered device op, e.g. from an RCCL
         broadcast of the query descriptor), then ``replay()`` -> (cls, prob).
-        No host round trip and no staging copy of the images."""
-        key = ("win", shard.data_ptr(), tuple(shard.shape), batch)
+        No host round trip and no staging copy of the images.  A caller-owned
+        ``start`` (e.g. the start field of this rank's row of the broadcast
+        descriptor table) is read in place, minus ``start_offset``; with
+        ``packed`` the graph also writes (class, prob bits) pairs there (the
+        gather's send buffer)."""
+        key = ("win", shard.data_ptr(), tuple(shard.shape), batch,
+               None if start is None else start.data_ptr(), start_offset,
+               None if packed is None else packed.data_ptr())
         if key in self._graphs:
             g, start, sout = self._graphs[key]
             return start, self._replayer(g, sout, shard)
-        start = torch.zeros(1, dtype=torch.int64, device=self.device)
+        if start is None:
+            start = torch.zeros(1, dtype=torch.int64, device=self.device)
         with _CAPTURE_LOCK:
             st = torch.cuda.Stream(device=self.device)
             st.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(st):
                 for _ in range(2):
-                    self.forward(shard, start, batch)
+                    self.forward(shard, start, batch, start_offset, packed)
             torch.cuda.current_stream(self.device).wait_stream(st)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                sout = self.forward(shard, start, batch)
+                sout = self.forward(shard, start, batch, start_offset, packed)
         self._graphs[key] = (g, start, sout)
-        return start, self._replayer(g, sout, shard)
+        return start, self._replayer(g, sout, shard, packed)
 
     def _replayer(self, g, sout, *keep):
         """Replay closure that keeps this runner (its HBM-resident weights) and

@@ -27,11 +27,13 @@ def linear(x, w, bias, relu: bool = False, out_f32: bool = False):
     return y.view(b, w.shape[0])
 
 
-def preprocess(img_u8, start=None, batch: int = -1):
+def preprocess(img_u8, start=None, batch: int = -1, start_offset: int = 0):
     """uint8 [B,H,W,3] -> normalised fp16 [B,H,W,4] (4th channel zero).
     With ``start`` (int64 GPU scalar) and ``batch``, reads images
-    [*start, *start+batch) of the shard ``img_u8`` (device-side window)."""
-    return load().preprocess(img_u8, start, batch)
+    [*start - start_offset, ... + batch) of the shard ``img_u8`` (device-side
+    window; ``start`` may be a global image index and ``start_offset`` the
+    shard's first global index)."""
+    return load().preprocess(img_u8, start, batch, start_offset)
 
 
 def resize_crop(img_u8, resize: int = 256, crop: int = 224):
@@ -39,10 +41,10 @@ def resize_crop(img_u8, resize: int = 256, crop: int = 224):
     return load().resize_crop(img_u8, resize, crop)
 
 
-def stem_fused(img_u8, w, bias, start=None, batch: int = -1):
+def stem_fused(img_u8, w, bias, start=None, batch: int = -1, start_offset: int = 0):
     """ResNet stem in one kernel: uint8 [B,H,W,3] -> fp16 [B,H/4,W/4,64]
     (optionally a device-side window of a shard, see ``preprocess``)."""
-    return load().stem_fused(img_u8, w, bias, start, batch)
+    return load().stem_fused(img_u8, w, bias, start, batch, start_offset)
 
 
 def maxpool2d(x, k: int = 3, s: int = 2, pad: int = 1):
@@ -53,9 +55,10 @@ def global_avgpool(x):
     return load().global_avgpool_nhwc(x)
 
 
-def softmax_top1(logits):
-    """Returns (class int32 [B], probability fp32 [B])."""
-    cls, prob = load().softmax_top1(logits)
+def softmax_top1(logits, packed=None):
+    """Returns (class int32 [B], probability fp32 [B]); with ``packed`` (int32
+    [>= B, 2]) also writes (class, prob bits) pairs into it."""
+    cls, prob = load().softmax_top1(logits, packed)
     return cls, prob
 
 

@@ -79,13 +79,15 @@ class QueryPlane:
         self.group = group
         dev = env.device
         self._desc = torch.full((env.world, 4), NO_WORK, dtype=torch.int64, device=dev)
-        self._pack = torch.zeros(max_chunk, 2, dtype=torch.int32, device=dev)
         # one contiguous [world, max_chunk, 2] buffer on the coordinator; the
         # per-rank gather outputs are views of it, so the whole round's results
         # come to the host with ONE device->host copy (``gathered_all``)
         self.gathered_all = torch.zeros(env.world, max_chunk, 2, dtype=torch.int32, device=dev) \
             if env.rank == coordinator else None
         self._gathered = list(self.gathered_all.unbind(0)) if env.rank == coordinator else None
+        # send buffer; a single rank's results are already in place (no copy)
+        self._pack = self._gathered[0] if env.world == 1 else \
+            torch.zeros(max_chunk, 2, dtype=torch.int32, device=dev)
 
     # -- M9 ---------------------------------------------------------------------
     def dispatch(self, table: list[tuple[int, int, int, int]] | None) -> tuple[int, int, int, int]:
@@ -151,6 +153,18 @@ class QueryPlane:
         return buf
 
     # -- M11 --------------------------------------------------------------------
+    @property
+    def send_buffer(self) -> torch.Tensor:
+        """[max_chunk, 2] int32 (class, prob bits): a forward that writes its
+        results here directly (``HipRunner.capture_window(packed=...)``)
+        calls ``gather(None, None)``."""
+        return self._pack
+
+    def row_start(self) -> torch.Tensor:
+        """Device view of this rank's descriptor start field (int64 [1]): the
+        forward graph reads its shard window start from it in place."""
+        return self._desc[self.env.rank, 2:3]
+
     def pack(self, cls: torch.Tensor, prob: torch.Tensor) -> torch.Tensor:
         n = cls.numel()
         self._pack[:n, 0].copy_(cls.view(-1).to(torch.int32))
@@ -163,8 +177,7 @@ class QueryPlane:
         if cls is not None:
             self.pack(cls, prob)
         if not self.env.distributed:
-            self._gathered[0].copy_(self._pack)
-            return self._gathered
+            return self._gathered            # _pack IS _gathered[0]
         if self.env.rank == self.coord:
             dist.gather(self._pack, self._gathered, dst=self.coord, group=self.group)
             return self._gathered

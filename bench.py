@@ -79,16 +79,18 @@ def main(argv=None) -> int:
     shard_base = env.rank * n_shard   # global image index of shard[0]
     shard = ops.synth_images(a.seed + 1234, shard_base, n_shard, env.device)
 
+    plane = QueryPlane(env, coordinator=0, max_chunk=B)
+    # the graph reads its window start straight from this rank's row of the
+    # broadcast descriptor table (global image index - shard_base) and writes
+    # the packed top-1 pairs straight into the gather's send buffer
+    start_dev, send = plane.row_start(), plane.send_buffer[:B]
     if a.no_graph:
-        start_dev = torch.zeros(1, dtype=torch.int64, device=env.device)
-
         def run():
-            return runner.forward(shard, start_dev, B)
+            return runner.forward(shard, start_dev, B, shard_base, send)
     else:
         # one hipGraph: device-side shard window -> fused stem -> ... -> softmax-top1
-        start_dev, run = runner.capture_window(shard, B)
+        _, run = runner.capture_window(shard, B, start=start_dev, start_offset=shard_base, packed=send)
 
-    plane = QueryPlane(env, coordinator=0, max_chunk=B)
     state = JobState() if coord else None
     host_res = [torch.empty(env.world, B, 2, dtype=torch.int32, pin_memory=True) for _ in range(2)] if coord else None
     model_id = 1 if a.model.startswith("resnet") else 0
@@ -119,10 +121,9 @@ def main(argv=None) -> int:
                 (s0, e0), = split_range(s, s + B - 1, 1)
                 table.append((model_id, q * env.world + r, s0, e0))
                 state.assign(a.model, q * env.world + r, [(f"rank{r}", s0, e0)], t0)
-        row = plane.dispatch_device(table, slot=q)          # RCCL broadcast of descriptors
-        torch.sub(row[2:3], shard_base, out=start_dev)      # window start, on device
-        cls, prob = run()                                   # hipGraph replay
-        gathered = plane.gather(cls, prob)                  # RCCL gather of top-1 to rank 0
+        plane.dispatch_device(table, slot=q)                # RCCL broadcast of descriptors
+        run()                                               # hipGraph replay (reads the row in place)
+        plane.gather(None, None)                            # RCCL gather of top-1 to rank 0
         if coord:
             slot = q % 2
             host_res[slot].copy_(plane.gathered_all, non_blocking=True)   # one D2H copy per round

@@ -295,6 +295,28 @@ def test_device_window_graph_matches_slices(ops, fuse):
         assert torch.equal(c0, c1) and torch.allclose(p0, p1)
 
 
+@pytest.mark.parametrize("fuse", [True, False])
+def test_window_from_descriptor_row_with_packed_output(ops, fuse):
+    """Graph reads a GLOBAL start index in place (minus the shard's base) and
+    writes (class, prob bits) pairs into a caller buffer (bench / data plane)."""
+    from idunno.models import HipRunner, build_program
+
+    runner = HipRunner(build_program("resnet18", seed=6), fuse_stem=fuse)
+    base = 1000
+    shard = ops.synth_images(7, base, 24, "cuda")
+    desc = torch.zeros(2, 4, dtype=torch.int64, device="cuda")
+    packed = torch.full((8, 2), -1, dtype=torch.int32, device="cuda")
+    _, run = runner.capture_window(shard, 8, start=desc[1, 2:3], start_offset=base, packed=packed)
+    for g0 in (1000, 1009, 1016):
+        desc[1, 2] = g0
+        c1, p1 = run()
+        s = g0 - base
+        c0, p0 = runner.forward(shard[s:s + 8].contiguous())
+        torch.cuda.synchronize()
+        assert torch.equal(c0, c1) and torch.allclose(p0, p1)
+        assert torch.equal(packed[:, 0], c0) and torch.equal(packed[:, 1].view(torch.float32), p1)
+
+
 @pytest.mark.parametrize("B,H", [(3, 224), (2, 64), (1, 100)])
 def test_stem_fused_vs_fp32(ops, B, H):
     from idunno.models.packed import pack_conv_weight
