@@ -39,10 +39,10 @@ __device__ __forceinline__ void big_vmcnt() {
 }
 
 template <int BN, int BM, int WN, int WM, int NS, int MINB, bool HAS_RES, bool OUT_F32>
-// second launch bound = waves per SIMD (HIP semantics): MINB workgroups of 8 waves per CU
-__global__ void __launch_bounds__(512, 2 * MINB) conv_big_kernel(const ConvArgs a) {
-  constexpr int NW = 8;
-  static_assert(WN * WM == NW, "8 waves");
+// second launch bound = waves per SIMD (HIP semantics): MINB workgroups of WN*WM waves per CU
+__global__ void __launch_bounds__(64 * WN * WM, WN * WM / 4 * MINB) conv_big_kernel(const ConvArgs a) {
+  constexpr int NW = WN * WM;
+  static_assert(NW == 8 || NW == 16, "8 or 16 waves");
   constexpr int TN = BN / WN, TM = BM / WM;
   constexpr int FN = TN / 16, FM = TM / 16;
   constexpr int A_INS = BN / 8, B_INS = BM / 8;           // 1 KiB DMA instructions per stage
@@ -267,7 +267,7 @@ static void big_cfg(ConvArgs a, hipStream_t st) {
                               (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WN * WM), lds, st, a);
 }
 
 // Tile table (ids 60-67; 512 threads, BK = 64):
@@ -279,6 +279,9 @@ static void big_cfg(ConvArgs a, hipStream_t st) {
 //   65: 128x128,             waves 2x4 (64x32),      2 stages  64 KiB, 2 blocks/CU
 //   66: 128x128,             waves 2x4 (64x32),      3 stages  96 KiB
 //   67: 64x256,              waves 1x8 (64x32),      2 stages  80 KiB, 2 blocks/CU
+//   68: 256x128, 16 waves 4x4 (64x32), 2 stages 96 KiB: the bytes per FLOP of a 256-row
+//       tile (0.75x of 128x128) at the wave count of two 128x128 workgroups
+//   69: 128x256, 16 waves 2x8 (64x32), 2 stages 96 KiB
 template <bool R, bool F>
 static bool big_dispatch(ConvArgs a, int tile, hipStream_t st) {
   switch (tile) {
@@ -289,6 +292,8 @@ static bool big_dispatch(ConvArgs a, int tile, hipStream_t st) {
     case 65: big_cfg<128, 128, 2, 4, 2, 2, R, F>(a, st); return true;
     case 66: big_cfg<128, 128, 2, 4, 3, 1, R, F>(a, st); return true;
     case 67: big_cfg<64, 256, 1, 8, 2, 2, R, F>(a, st); return true;
+    case 68: big_cfg<256, 128, 4, 4, 2, 1, R, F>(a, st); return true;   // 16 waves (64x32 each)
+    case 69: big_cfg<128, 256, 2, 8, 2, 1, R, F>(a, st); return true;   // 16 waves (64x32 each)
     default: return false;
   }
 }
