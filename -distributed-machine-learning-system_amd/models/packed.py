@@ -350,10 +350,24 @@ class HipRunner:
         caller that drops the runner and keeps only the closure must not let
         the weights go back to the allocator."""
         def replay():
-            g.replay()
+            # several nodes may share a process (and a GPU): a replay while another
+            # thread is capturing fails on ROCm ("prepare for replay during
+            # capturing stage"), so replays and captures are mutually exclusive
+            with _CAPTURE_LOCK:
+                g.replay()
             return sout
         replay._keep = (self, keep)
         return replay
+
+    def close(self) -> None:
+        """Destroy the captured graphs now, under the capture lock (a graph
+        destroyed by another thread's garbage collection while a capture is
+        active aborts the process: hipErrorStreamCaptureUnsupported)."""
+        with _CAPTURE_LOCK:
+            self._graphs.clear()
+            import gc
+
+            gc.collect()
 
     # -- hipGraph -------------------------------------------------------------
     def capture(self, batch: int, hw: int = 224):

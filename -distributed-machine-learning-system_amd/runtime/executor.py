@@ -89,6 +89,7 @@ class HipExecutor(Executor):
         self.runners: dict[str, object] = {}
         self.lock = threading.Lock()
         self.stream = None      # private HIP stream: nodes sharing a GPU overlap
+        self.closed = False
 
     def runner(self, name):
         name = ref.canonical(name)
@@ -115,7 +116,7 @@ class HipExecutor(Executor):
             s.wait_stream(torch.cuda.current_stream(self.device))   # images were produced there
             images.record_stream(s)
             with torch.cuda.stream(s):
-                if (self.use_graphs and len(r._graphs) < self.max_graphs) or n in r._graphs:
+                if not self.closed and ((self.use_graphs and len(r._graphs) < self.max_graphs) or n in r._graphs):
                     sin, replay = r.capture(n)
                     sin.copy_(images)
                     cls, prob = replay()
@@ -123,6 +124,16 @@ class HipExecutor(Executor):
                     cls, prob = r.forward(images.contiguous())
                 out = torch.stack([cls, prob.view(torch.int32)], dim=1).cpu()
         return out[:, 0].numpy().copy(), out[:, 1].contiguous().view(torch.float32).numpy().copy()
+
+
+    def close(self) -> None:
+        """Release the captured graphs (under the process-wide capture lock);
+        a chunk still running afterwards takes the eager path."""
+        self.closed = True
+        with self.lock:
+            runners = list(self.runners.values())
+        for r in runners:
+            r.close()
 
 
 def make_executor(kind: str, device=None, seed: int = 0) -> Executor:

@@ -128,6 +128,11 @@ class JobState:
             self.seq += 1
             return jid
 
+    def images_held(self, model: str, qnum, s: int, e: int) -> bool:
+        """True if results for every image of [s, e] under (model, qnum) are held."""
+        with self.lock:
+            return any(a <= s and e <= b for a, b in self._done_imgs.get((model, qnum), []))
+
     def job_query_number(self, jid: int, s: int) -> int:
         with self.lock:
             j = self.jobs[jid]
@@ -178,8 +183,6 @@ class JobState:
         start, end = int(start), int(end)
         with self.lock:
             ck = (model, qnum, start, end)
-            if ck in self._done_keys:
-                return False
             key = (model, qnum)
             entries = self.worker_set.get(key, [])
             was_done = bool(entries) and all(ent[3] == "f" for ent in entries)
@@ -198,6 +201,9 @@ class JobState:
                     pass
                 if not self.working_vm_set[w]:
                     self.working_vm_set.pop(w, None)
+            # a duplicate still closes a matching 'w' entry (a re-dispatch with the
+            # same chunk boundaries as the answered original) before it is dropped
+            dup = ck in self._done_keys
             self._done_keys.add(ck)
             if entries and not was_done and all(ent[3] == "f" for ent in entries):
                 self.finished_queries[model] += 1
@@ -206,7 +212,7 @@ class JobState:
                     self.query_latency[model].append(now - t0)
             # images of this query already answered under another chunk split
             # (re-dispatch after a failure / a resumed job) are not counted again
-            n = _add_interval(self._done_imgs[key], start, end)   # fix A3: end - start + 1 when new
+            n = 0 if dup else _add_interval(self._done_imgs[key], start, end)   # fix A3: end-start+1 when new
             if n == 0:
                 self.seq += 1
                 return False
@@ -221,6 +227,24 @@ class JobState:
                             worker))
             self.seq += 1
             return True
+
+    def reopen_unheld(self) -> int:
+        """Chunks marked finished in the replicated tables whose images this
+        node never received (their RESULT reached only the old coordinator)
+        go back to 'w', so a promoted standby recomputes them instead of
+        reporting a query done whose results it cannot show (c4)."""
+        with self.lock:
+            n = 0
+            for (m, q), ents in self.worker_set.items():
+                ivs = self._done_imgs.get((m, q), [])
+                for i, (w, s, e, st, t0, t1) in enumerate(ents):
+                    if st == "f" and not any(a <= s and e <= b for a, b in ivs):
+                        ents[i] = (w, s, e, "w", t0, t1)
+                        self.working_vm_set[w].append((m, q, s, e))
+                        n += 1
+            if n:
+                self.seq += 1
+            return n
 
     def chunks_of(self, worker: str) -> list[tuple]:
         with self.lock:

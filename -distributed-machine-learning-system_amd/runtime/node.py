@@ -153,6 +153,9 @@ class Node:
             self.rounds.stop()
         self.jobs.put(None)
         self.transport.close()
+        close = getattr(self.executor, "close", None)
+        if close is not None:
+            close()
 
     # -- dispatch of incoming messages ---------------------------------------------------
     def handle(self, msg: dict):
@@ -309,6 +312,10 @@ class Node:
         model = canonical(model)
         bs = self.cfg.batch_for(model)
         jid = self.state.add_job(model, start, end, bs)
+        # replicate the job before it starts: a coordinator that dies before its
+        # next periodic push would otherwise take the job with it
+        if self.standby != self.name:
+            self.push_metadata()
         self._start_job_runner(jid)
         return {"ok": True, "job": jid, "queries": (end - start) // bs + 1}
 
@@ -325,8 +332,12 @@ class Node:
                 if s > job["end"]:
                     return
                 e = min(s + self.cfg.batch_for(job["model"]) - 1, job["end"])
-                if not self.state.range_submitted(job["model"], s, e):
-                    self.submit_query(job["model"], s, e, qnum=self.state.job_query_number(jid, s))
+                q = self.state.job_query_number(jid, s)
+                # skip a query the old coordinator already dispatched (known from the
+                # replicated tables) or whose results all reached this node directly
+                if not self.state.range_submitted(job["model"], s, e) and \
+                        not self.state.images_held(job["model"], q, s, e):
+                    self.submit_query(job["model"], s, e, qnum=q)
                 self.state.advance_job(jid, e + 1)
                 if self.cfg.client_query_interval_s and e < job["end"]:
                     time.sleep(self.cfg.client_query_interval_s)
@@ -479,7 +490,14 @@ class Node:
                 self.transport.send(n, {"t": Type.PROMOTE, "epoch": epoch})
         # the old coordinator is gone: its own chunks and replicas must move
         self.membership.mark_failed(old)
-        # chunks that were dispatched to nodes that are already dead
+        reopened = self.state.reopen_unheld()
+        if reopened:
+            self.logger.warning("%d chunk(s) finished only at %s: recomputing", reopened, old)
+        # Every chunk still pending in the replicated tables is (re)sent: to a
+        # replacement if its worker is dead, else to the same worker again.  A
+        # chunk the old coordinator recorded (and replicated) but crashed before
+        # sending would otherwise stay pending forever; for one that is already
+        # in flight the duplicate answer is dropped by the idempotent ingest.
         alive = set(self.membership.alive())
         for model, qnum, w, s, e, _t in self.state.pending():
             if w not in alive:
@@ -487,6 +505,8 @@ class Node:
                 if nw:
                     self.state.reassign(w, nw, (model, qnum, s, e))
                     self._send_job(nw, model, qnum, s, e)
+            else:
+                self._send_job(w, model, qnum, s, e)
         for jid in self.state.unfinished_jobs():      # coordinator-side jobs carry on here
             self._start_job_runner(jid)
         self.logger.warning("promotion done in %.3fs", time.monotonic() - t0)

@@ -161,6 +161,26 @@ def test_jobstate_dedupes_images_across_chunk_splits():
     assert js.images_done("resnet18") == 800
 
 
+def test_standby_reopens_chunks_it_holds_no_results_for():
+    coord, standby = JobState(), JobState()
+    cls, prob = np.zeros(80, np.int32), np.ones(80, np.float32)
+    coord.assign("alexnet", 1, [("a", 0, 79), ("b", 80, 159)])
+    standby.record_result("alexnet", 1, "a", 0, 79, cls, prob)        # dual-sent, arrived
+    coord.record_result("alexnet", 1, "a", 0, 79, cls, prob)
+    coord.record_result("alexnet", 1, "b", 80, 159, cls, prob)        # reached the coordinator only
+    standby.restore(coord.snapshot(include_results=False), keep_results=True)
+    assert standby.pending() == []                                    # the snapshot says all done
+    assert standby.reopen_unheld() == 1
+    assert [(w, s, e) for _m, _q, w, s, e, _t in standby.pending()] == [("b", 80, 159)]
+    assert standby.record_result("alexnet", 1, "c", 80, 159, cls, prob)
+    assert standby.images_done("alexnet") == 160 and standby.pending() == []
+    # re-dispatch with the SAME chunk boundaries as an answered original: the
+    # late duplicate answer closes the new entry (and is not counted)
+    standby.assign("alexnet", 1, [("d", 0, 79)])
+    assert standby.record_result("alexnet", 1, "d", 0, 79, cls, prob) is False
+    assert standby.pending() == [] and standby.images_done("alexnet") == 160
+
+
 def test_config_env_and_file(tmp_path):
     p = tmp_path / "c.json"
     p.write_text(json.dumps({"num_nodes": 4, "heartbeat_period_s": 0.1}))

@@ -31,8 +31,16 @@ def main():
     ap.add_argument("--images", type=int, default=10000)
     ap.add_argument("--executor", default="hip", choices=["hip", "fake", "torch"])
     ap.add_argument("--kill-coordinator-after", type=float, default=0.0)
+    ap.add_argument("--kill-coordinator-at-frac", type=float, default=0.0,
+                    help="kill the coordinator once this fraction of both jobs' images is done")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--watchdog", type=float, default=0.0,
+                    help="dump every thread's stack and exit after this many seconds (hang diagnosis)")
     a = ap.parse_args()
+    if a.watchdog:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(a.watchdog, exit=True)
     import logging
 
     import torch
@@ -78,11 +86,16 @@ def main():
         out["second_job_start_s"] = time.perf_counter() - t_second
         killed = False
         want = {m: base[m] + a.images for m in base}
+        out["warmup_images"] = base          # counted in c1 too (the warm-up queries above)
+        done_frac, killed_at_frac = 0.0, None
+        t_log = time.perf_counter()
         while True:
-            if a.kill_coordinator_after and not killed and time.perf_counter() - t0 > a.kill_coordinator_after:
+            if not killed and ((a.kill_coordinator_after and time.perf_counter() - t0 > a.kill_coordinator_after)
+                               or (a.kill_coordinator_at_frac and done_frac >= a.kill_coordinator_at_frac)):
                 c.crash(c.cfg.coordinator_name)
                 killed = True
                 t_kill = time.perf_counter()
+                killed_at_frac = done_frac
             try:
                 s = cl.view("summary")
             except Exception:  # noqa: BLE001  (during failover)
@@ -90,11 +103,34 @@ def main():
                 continue
             if all(s["done"].get(m, 0) >= want[m] for m in want) and s["pending"] == 0:
                 break
+            done_frac = sum(s["done"].get(m, 0) - base[m] for m in want) / (2 * a.images)
             if time.perf_counter() - t0 > 1800:
                 raise TimeoutError(s)
+            if time.perf_counter() - t_log > 5:        # progress (and a trail if it stalls)
+                t_log = time.perf_counter()
+                print(f"[{t_log - t0:7.1f}s] done {s['done']} pending {s['pending']} "
+                      f"coordinator {c.coordinator().name}", file=sys.stderr, flush=True)
+                if t_log - t0 > 20:                     # stalled: per-query image coverage
+                    st = c.coordinator().state
+                    with st.lock:
+                        for (m, q), ents in sorted(st.worker_set.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
+                            got = sum(b - a + 1 for a, b in st._done_imgs.get((m, q), []))
+                            span = (min(e[1] for e in ents), max(e[2] for e in ents)) if ents else None
+                            print(f"   {m} q{q} span {span} imgs {got} chunks "
+                                  f"{[(e[0], e[1], e[2], e[3]) for e in ents]}", file=sys.stderr, flush=True)
+                        print(f"   jobs {st.jobs} next_qnum {dict(st.next_qnum)}", file=sys.stderr, flush=True)
+                    raise SystemExit(3)
             time.sleep(0.01)
         wall = time.perf_counter() - t0
-        coord = c.coordinator()
+        deadline = time.perf_counter() + 30       # a promotion may still be under way
+        while True:
+            try:
+                coord = c.coordinator()
+                break
+            except RuntimeError:
+                if time.perf_counter() > deadline:
+                    raise
+                time.sleep(0.05)
         lat = {m: coord.state.query_latency.get(m, [])[-(a.images // coord.cfg.batch_for(m)):] for m in want}
         workers = {}
         for (m, q), ents in coord.state.worker_set.items():
@@ -113,6 +149,7 @@ def main():
         })
         if killed:
             out["failover_to_done_s"] = round(time.perf_counter() - t_kill, 3)
+            out["killed_at_done_fraction"] = round(killed_at_frac, 3)
     finally:
         c.stop()
     print(json.dumps(out, indent=1, default=str))
