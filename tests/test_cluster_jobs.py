@@ -40,6 +40,29 @@ def test_job_resumed_by_promoted_standby():
         c.stop()
 
 
+def test_job_survives_coordinator_crash_before_any_periodic_snapshot():
+    """The job is replicated when it is created, not only by the periodic push
+    (metadata period >> time to crash here): the promoted standby resumes it,
+    re-sends chunks it has no results for, and counts every image exactly once."""
+    cfg = dict(FAST, metadata_period_s=30.0)
+    c = LocalCluster(num_nodes=5, client_query_interval_s=0.02, **cfg).start()
+    try:
+        for n in c.nodes.values():
+            n.extra_delay_s = 0.05                         # chunks in flight at the crash
+        cl = c.client("node03")
+        r = cl.submit_job(0, 3999, "resnet18")
+        assert r["queries"] == 10
+        import time
+
+        time.sleep(0.12)
+        c.crash("node00")
+        s = cl.wait_idle(20, {"resnet18": 4000})
+        assert s["done"]["resnet18"] == 4000 and s["pending"] == 0, s
+        assert c.coordinator().name == "node04"
+    finally:
+        c.stop()
+
+
 def test_straggler_resend():
     c = LocalCluster(num_nodes=4, straggler_resend=True, straggler_timeout_s=0.3, **FAST).start()
     try:
