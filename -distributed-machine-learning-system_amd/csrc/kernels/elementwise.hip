@@ -129,32 +129,56 @@ void maxpool_launch(const half_t* x, half_t* y, int B, int H, int W, int C, int 
                      B, H, W, C, Ho, Wo, k, s, pad);
 }
 
-// NHWC global average pool -> [B][C] fp16.  One thread = 8 channels of one image.
-__global__ void avgpool_kernel(const half_t* __restrict__ x, half_t* __restrict__ y, int B, int HW,
-                               int C) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+// NHWC global average pool -> [B][C] fp16.  One 256-thread workgroup per image:
+// thread (g, c8) sums pixels g, g+G, ... of 8-channel chunk c8 (16-byte loads),
+// the G partial sums meet in LDS.  (One thread per chunk over all HW pixels ran
+// 400 workgroups' worth of work on 100 workgroups with a 49-long dependent
+// chain: 17 us for the 20 MB ResNet18 layer4 output.)
+__global__ void __launch_bounds__(256) avgpool_kernel(const half_t* __restrict__ x, half_t* __restrict__ y,
+                                                      int B, int HW, int C) {
+  __shared__ float part[256 * 8];
+  const int b = blockIdx.x;
   const int cv = C / 8;
-  if (t >= (long)B * cv) return;
-  const int b = (int)(t / cv), c8 = (int)(t % cv);
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const half_t* p = x + (size_t)b * HW * C + c8 * 8;
-  for (int i = 0; i < HW; ++i) {
-    const half8v v = *reinterpret_cast<const half8v*>(p + (size_t)i * C);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
-  }
+  const int G = cv >= 256 ? 1 : 256 / cv;          // pixel groups per chunk
+  const half_t* p = x + (size_t)b * HW * C;
   const float inv = 1.f / (float)HW;
-  half8v o;
+  for (int c8 = threadIdx.x % cv; c8 < cv; c8 += (cv >= 256 ? 256 : cv)) {
+    const int g = cv >= 256 ? 0 : threadIdx.x / cv;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (g < G) {
+      for (int i = g; i < HW; i += G) {
+        const half8v v = *reinterpret_cast<const half8v*>(p + (size_t)i * C + c8 * 8);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (half_t)(acc[j] * inv);
-  *reinterpret_cast<half8v*>(y + (size_t)b * C + c8 * 8) = o;
+        for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+      }
+    }
+    if (G == 1) {
+      half8v o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (half_t)(acc[j] * inv);
+      *reinterpret_cast<half8v*>(y + (size_t)b * C + c8 * 8) = o;
+      continue;
+    }
+    if (g < G) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part[(g * cv + c8) * 8 + j] = acc[j];
+    }
+    __syncthreads();
+    if (g == 0) {
+      for (int k = 1; k < G; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += part[(k * cv + c8) * 8 + j];
+      half8v o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (half_t)(acc[j] * inv);
+      *reinterpret_cast<half8v*>(y + (size_t)b * C + c8 * 8) = o;
+    }
+    break;                                          // G > 1: every chunk handled in one pass
+  }
 }
 
 void avgpool_launch(const half_t* x, half_t* y, int B, int HW, int C, hipStream_t st) {
-  const long total = (long)B * (C / 8);
-  const int bs = 256;
-  hipLaunchKernelGGL(avgpool_kernel, dim3((unsigned)((total + bs - 1) / bs)), dim3(bs), 0, st, x, y,
-                     B, HW, C);
+  hipLaunchKernelGGL(avgpool_kernel, dim3((unsigned)B), dim3(256), 0, st, x, y, B, HW, C);
 }
 
 // Row softmax + top-1: one 64-lane wave per row of fp32 logits.
