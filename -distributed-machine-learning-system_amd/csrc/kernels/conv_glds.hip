@@ -297,6 +297,7 @@ static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
     case 36: glds_cfg<128, 128, 64, 2, 4, 2, R, F>(a, st); return true;   // 8 waves, 64 KiB dbuf
     case 37: glds_cfg<64, 128, 64, 1, 8, 2, R, F>(a, st); return true;    // 8 waves, 48 KiB dbuf
     case 38: glds_cfg<128, 64, 64, 2, 4, 2, R, F>(a, st); return true;    // 8 waves (32x16 wave tile)
+    case 39: glds_cfg<128, 128, 32, 2, 4, 4, R, F>(a, st); return true;   // 8 waves, 64 KiB, 3 stages in flight
     default: return false;
   }
 }
