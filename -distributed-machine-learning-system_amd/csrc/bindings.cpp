@@ -63,7 +63,7 @@ void set_conv3x3_c64_default(bool on) { g_c64_default = on; }
 //   res : optional [B, Ho, Wo, Cout] fp16
 torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
                           c10::optional<torch::Tensor> res, int64_t KH, int64_t KW, int64_t stride,
-                          int64_t pad, bool relu, bool out_f32, int64_t tile) {
+                          int64_t pad, bool relu, bool out_f32, int64_t tile, c10::optional<torch::Tensor> out) {
   CHECK_DEV(x);
   CHECK_DEV(w);
   CHECK_DEV(bias);
@@ -98,7 +98,18 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   }
   const long M = (long)B * Ho * Wo;
   TORCH_CHECK(M < (1L << 31) && (long)B * H * W * C < (1L << 31), "tensor too large for int32 indexing");
-  torch::Tensor y = torch::empty({B, Ho, Wo, Cout}, x.options().dtype(out_f32 ? torch::kFloat : torch::kHalf));
+  torch::Tensor y;
+  if (out.has_value() && out->defined()) {   // caller-owned output (e.g. a batch slice of a bigger tensor)
+    y = *out;
+    CHECK_DEV(y);
+    CHECK_CONTIG(y);
+    CHECK_DT(y, out_f32 ? torch::kFloat : torch::kHalf);
+    TORCH_CHECK(y.device() == x.device(), "out must live on the input's device");
+    TORCH_CHECK(y.dim() == 4 && y.size(0) == B && y.size(1) == Ho && y.size(2) == Wo && y.size(3) == Cout,
+                "out shape mismatch");
+  } else {
+    y = torch::empty({B, Ho, Wo, Cout}, x.options().dtype(out_f32 ? torch::kFloat : torch::kHalf));
+  }
   const half_t* rp = nullptr;
   if (res.has_value() && res->defined()) {
     auto& r = *res;
@@ -172,8 +183,10 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
 // `img` is a whole image shard [N,H,W,3] and images [*start, *start + batch)
 // are used; the kernel clamps *start into [0, N - batch] so a bad descriptor
 // can never read outside the shard.
+// A window may be processed in parts: `window` (>= batch, default batch) is the
+// clamping window, `sub` this launch's first image inside it (sub + batch <= window).
 static const long long* window_args(const torch::Tensor& img, const c10::optional<torch::Tensor>& start, int64_t batch,
-                                    int& B, long long& max_start) {
+                                    int64_t window, int64_t sub, int& B, long long& max_start) {
   B = img.size(0);
   max_start = 0;
   if (!start.has_value() || !start->defined()) return nullptr;
@@ -183,8 +196,10 @@ static const long long* window_args(const torch::Tensor& img, const c10::optiona
   TORCH_CHECK(s.numel() == 1, "start must be a 1-element int64 tensor");
   TORCH_CHECK(s.device() == img.device(), "start must live on the image device");
   TORCH_CHECK(batch > 0 && batch <= img.size(0), "window batch out of range");
+  if (window <= 0) window = batch;
+  TORCH_CHECK(window <= img.size(0) && sub >= 0 && sub + batch <= window, "window part out of range");
   B = (int)batch;
-  max_start = img.size(0) - batch;
+  max_start = img.size(0) - window;
   return reinterpret_cast<const long long*>(s.data_ptr());
 }
 
@@ -192,7 +207,7 @@ static const long long* window_args(const torch::Tensor& img, const c10::optiona
 // be a GLOBAL image index (e.g. straight from the broadcast query descriptor)
 // and the offset the shard's first global index.
 torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias, c10::optional<torch::Tensor> start,
-                         int64_t batch, int64_t start_offset) {
+                         int64_t batch, int64_t start_offset, int64_t window, int64_t sub) {
   CHECK_DEV(img);
   CHECK_DEV(w);
   CHECK_DEV(bias);
@@ -208,7 +223,7 @@ torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias,
   const int H = img.size(1), W = img.size(2);
   int B;
   long long max_start;
-  const long long* sp = window_args(img, start, batch, B, max_start);
+  const long long* sp = window_args(img, start, batch, window, sub, B, max_start);
   TORCH_CHECK(H >= 7 && W >= 7, "image too small");
   TORCH_CHECK((long)B * H * W * 3 < (1L << 31), "batch too large");
   const int Hc = (H + 6 - 7) / 2 + 1, Wc = (W + 6 - 7) / 2 + 1;
@@ -216,22 +231,23 @@ torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias,
   auto y = torch::empty({B, Hp, Wp, 64}, img.options().dtype(torch::kHalf));
   if (B)
     stem_fused_launch(img.data_ptr<uint8_t>(), reinterpret_cast<const half_t*>(w.data_ptr()), bias.data_ptr<float>(),
-                      reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp, start_offset, max_start, cur_stream()); check_launch("stem_fused");
+                      reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp, start_offset, max_start, sp ? sub : 0, cur_stream()); check_launch("stem_fused");
   return y;
 }
 
-torch::Tensor preprocess(torch::Tensor img, c10::optional<torch::Tensor> start, int64_t batch, int64_t start_offset) {
+torch::Tensor preprocess(torch::Tensor img, c10::optional<torch::Tensor> start, int64_t batch, int64_t start_offset,
+                         int64_t window, int64_t sub) {
   CHECK_DEV(img);
   CHECK_CONTIG(img);
   CHECK_DT(img, torch::kUInt8);
   TORCH_CHECK(img.dim() == 4 && img.size(3) == 3, "img must be [B, H, W, 3] uint8");
   int B;
   long long max_start;
-  const long long* sp = window_args(img, start, batch, B, max_start);
+  const long long* sp = window_args(img, start, batch, window, sub, B, max_start);
   auto out = torch::empty({B, img.size(1), img.size(2), 4}, img.options().dtype(torch::kHalf));
   const long npix = (long)B * img.size(1) * img.size(2);
   if (npix)
-    preprocess_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), npix, sp, start_offset, max_start,
+    preprocess_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), npix, sp, start_offset, max_start, sp ? sub : 0,
                       (long)img.size(1) * img.size(2), cur_stream()); check_launch("preprocess");
   return out;
 }
@@ -322,12 +338,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "IDunno-MI355X native HIP kernels (gfx950)";
   m.def("conv2d_nhwc", &conv2d_nhwc, "implicit-GEMM MFMA conv + bias (+res) (+relu)", py::arg("x"), py::arg("w"),
         py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
-        py::arg("relu"), py::arg("out_f32") = false, py::arg("tile") = -1);
+        py::arg("relu"), py::arg("out_f32") = false, py::arg("tile") = -1, py::arg("out") = py::none());
   m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 NHWC4", py::arg("img"),
-        py::arg("start") = py::none(), py::arg("batch") = -1, py::arg("start_offset") = 0);
+        py::arg("start") = py::none(), py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1,
+        py::arg("sub") = 0);
   m.def("stem_fused", &stem_fused, "fused normalise + conv7x7/2 + bias + relu + maxpool3x3/2 (ResNet stem)",
         py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("start") = py::none(), py::arg("batch") = -1,
-        py::arg("start_offset") = 0);
+        py::arg("start_offset") = 0, py::arg("window") = -1, py::arg("sub") = 0);
   m.def("resize_crop", &resize_crop, "bilinear resize + centre crop + normalise");
   m.def("maxpool2d_nhwc", &maxpool2d_nhwc, "NHWC max pool");
   m.def("global_avgpool_nhwc", &global_avgpool_nhwc, "NHWC global average pool");

@@ -39,9 +39,10 @@ void conv3x3_patch_launch(const half_t* x, const half_t* w, const float* bias, c
                           const void* zero, int B, int H, int W, int C, int Cout, int relu, hipStream_t st);
 int conv_glds_pick(int M, int Cout);
 void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, half_t* y, int B, int H, int W,
-                       const long long* start_idx, long long start_off, long long max_start, hipStream_t st);
+                       const long long* start_idx, long long start_off, long long max_start, long long sub,
+                       hipStream_t st);
 void preprocess_launch(const uint8_t* img, half_t* out, long npix, const long long* start_idx,
-                       long long start_off, long long max_start, long pix_per_img, hipStream_t st);
+                       long long start_off, long long max_start, long long sub, long pix_per_img, hipStream_t st);
 void resize_crop_launch(const uint8_t* img, half_t* out, int B, int Hi, int Wi, int Hr, int Wr,
                         int crop, hipStream_t st);
 void maxpool_launch(const half_t* x, half_t* y, int B, int H, int W, int C, int Ho, int Wo, int k,

@@ -22,12 +22,12 @@ __constant__ float kInvStd[3] = {1.0f / 0.229f, 1.0f / 0.224f, 1.0f / 0.225f};
 // [0, max_start]) of the shard `img`.
 __global__ void preprocess_kernel(const uint8_t* __restrict__ img, half_t* __restrict__ out,
                                   long npix, const long long* __restrict__ start_idx, long long start_off,
-                                  long long max_start, long pix_per_img) {
+                                  long long max_start, long long sub, long pix_per_img) {
   const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npix) return;
   if (start_idx != nullptr) {
     long long s0 = *start_idx - start_off;
-    s0 = s0 < 0 ? 0 : (s0 > max_start ? max_start : s0);
+    s0 = (s0 < 0 ? 0 : (s0 > max_start ? max_start : s0)) + sub;
     img += (size_t)s0 * pix_per_img * 3;
   }
   const uint8_t* s = img + p * 3;
@@ -40,11 +40,12 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ img, half_t* __res
 }
 
 void preprocess_launch(const uint8_t* img, half_t* out, long npix, const long long* start_idx,
-                       long long start_off, long long max_start, long pix_per_img, hipStream_t st) {
+                       long long start_off, long long max_start, long long sub, long pix_per_img,
+                       hipStream_t st) {
   const int bs = 256;
   const long grid = (npix + bs - 1) / bs;
   hipLaunchKernelGGL(preprocess_kernel, dim3((unsigned)grid), dim3(bs), 0, st, img, out, npix, start_idx,
-                     start_off, max_start, pix_per_img);
+                     start_off, max_start, sub, pix_per_img);
 }
 
 // Bilinear resize of an (Hi x Wi) uint8 HWC image so that its shorter side is

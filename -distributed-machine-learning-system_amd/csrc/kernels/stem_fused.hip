@@ -158,14 +158,14 @@ __device__ __forceinline__ void store_patch(char* patch, const StemGeom& g, int 
 __global__ void __launch_bounds__(256, 2)
 stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w, const float* __restrict__ bias,
                   half_t* __restrict__ y, const StemGeom g, const long long* __restrict__ start_idx,
-                  long long start_off, long long max_start) {
+                  long long start_off, long long max_start, long long sub) {
   using namespace stem;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // device-side first-image index: a captured hipGraph reads any window of an
   // HBM-resident image shard without a host round trip or a staging copy
   if (start_idx != nullptr) {
     long long s = *start_idx - start_off;
-    s = s < 0 ? 0 : (s > max_start ? max_start : s);
+    s = (s < 0 ? 0 : (s > max_start ? max_start : s)) + sub;   // sub: this launch's part of the window
     img += (size_t)s * g.H * g.W * 3;
   }
   char* patch = smem;
@@ -274,7 +274,8 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
 }
 
 void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, half_t* y, int B, int H, int W,
-                       const long long* start_idx, long long start_off, long long max_start, hipStream_t st) {
+                       const long long* start_idx, long long start_off, long long max_start, long long sub,
+                       hipStream_t st) {
   using namespace stem;
   StemGeom g;
   g.B = B;
@@ -295,7 +296,7 @@ void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, h
     attr = true;
   }
   const int grid = g.ntiles < 512 ? g.ntiles : 512;   // persistent: 2 workgroups per CU
-  hipLaunchKernelGGL(stem_fused_kernel, dim3(grid), dim3(256), LDS, st, img, w, bias, y, g, start_idx, start_off, max_start);
+  hipLaunchKernelGGL(stem_fused_kernel, dim3(grid), dim3(256), LDS, st, img, w, bias, y, g, start_idx, start_off, max_start, sub);
 }
 
 }  // namespace idunno

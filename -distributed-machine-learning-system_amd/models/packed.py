@@ -248,12 +248,18 @@ class HipRunner:
     static input buffer, removing per-kernel launch overhead.
     """
 
-    def __init__(self, program: Program, device=None, fuse_stem: bool = True):
+    def __init__(self, program: Program, device=None, fuse_stem: bool = True, front_split: int | None = None):
         from .. import ops
 
         ops.load()
         self.ops = ops
         self.fuse_stem = fuse_stem
+        # >1: stem + the full-resolution blocks (ResNet layer1) run on this many
+        # batch parts, each part's activations small enough to stay in the
+        # 256 MiB Infinity Cache between the stem and the end of layer1.
+        # None = measured default (tools/bench_split.py, profiles/r1_v8_front_split.log):
+        # 2 parts for ResNet18/34 at >= 256 images (+1.3 %), else 1 (ResNet50: -0.6 %)
+        self.front_split = front_split
         self.device = torch.device(device or "cuda")
         self.p = program.to(self.device)
         self._graphs: dict[int, tuple] = {}
@@ -275,21 +281,19 @@ class HipRunner:
         if not fused:
             x = o.preprocess(img_u8, start, batch, start_offset) if native else o.resize_crop(img_u8, 256, 224)
         if p.kind == "resnet":
-            if fused:
+            nb = batch if start is not None else img_u8.shape[0]
+            split = self.front_split if self.front_split is not None else \
+                (2 if p.name in ("resnet18", "resnet34") and nb >= 256 else 1)
+            nfront = self._front_blocks() if fused and split > 1 else 0
+            if nfront:
+                x = self._split_front(img_u8, start, batch, start_offset, nfront, split)
+            elif fused:
                 x = o.stem_fused(img_u8, s.w, s.b, start, batch, start_offset)
             else:
                 x = o.conv2d(x, s.w, s.b, s.kh, s.kw, s.stride, s.pad, s.relu)
                 x = o.maxpool2d(x, 3, 2, 1)
-            for blk in p.blocks:
-                idt = x
-                if blk.down is not None:
-                    d = blk.down
-                    idt = o.conv2d(x, d.w, d.b, d.kh, d.kw, d.stride, d.pad, False)
-                y = x
-                for c in blk.convs[:-1]:
-                    y = o.conv2d(y, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu)
-                c = blk.convs[-1]
-                x = o.conv2d(y, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu, residual=idt)
+            for blk in p.blocks[nfront:]:
+                x = self._block(blk, x)
             x = o.global_avgpool(x)
         else:
             for k, v in p.features:
@@ -302,6 +306,52 @@ class HipRunner:
             last = i == len(p.fcs) - 1
             x = o.linear(x, fc.w, fc.b, relu=fc.relu, out_f32=last)
         return x
+
+    def _block(self, blk, x, out=None):
+        """One residual block; the last conv fuses +identity and ReLU (into ``out``)."""
+        o = self.ops
+        idt = x
+        if blk.down is not None:
+            d = blk.down
+            idt = o.conv2d(x, d.w, d.b, d.kh, d.kw, d.stride, d.pad, False)
+        y = x
+        for c in blk.convs[:-1]:
+            y = o.conv2d(y, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu)
+        c = blk.convs[-1]
+        return o.conv2d(y, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu, residual=idt, out=out)
+
+    def _front_blocks(self) -> int:
+        """Leading blocks that keep the stem's resolution (ResNet layer1)."""
+        n = 0
+        for blk in self.p.blocks:
+            if any(c.stride != 1 for c in blk.convs) or (blk.down is not None and blk.down.stride != 1):
+                break
+            n += 1
+        return n
+
+    def _split_front(self, img_u8, start, batch, start_offset, nfront, split):
+        """Stem + the first ``nfront`` blocks on ``split`` batch parts; the last
+        block of each part writes its slice of the full-batch output."""
+        o, s = self.ops, self.p.stem
+        B = batch if start is not None else img_u8.shape[0]
+        n = -(-B // split)
+        out = None
+        for sub in range(0, B, n):
+            nb = min(n, B - sub)
+            if start is not None:
+                x = o.stem_fused(img_u8, s.w, s.b, start, nb, start_offset, window=B, sub=sub)
+            else:
+                x = o.stem_fused(img_u8[sub:sub + nb], s.w, s.b)
+            for bi in range(nfront):
+                blk = self.p.blocks[bi]
+                if bi < nfront - 1:
+                    x = self._block(blk, x)
+                    continue
+                if out is None:
+                    c = blk.convs[-1]
+                    out = torch.empty((B, x.shape[1], x.shape[2], c.cout), dtype=torch.float16, device=x.device)
+                self._block(blk, x, out=out[sub:sub + nb])
+        return out
 
     def forward(self, img_u8: torch.Tensor, start: torch.Tensor | None = None, batch: int = -1,
                 start_offset: int = 0, packed: torch.Tensor | None = None):

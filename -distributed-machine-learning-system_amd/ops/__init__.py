@@ -15,25 +15,27 @@ __all__ = [
 
 
 def conv2d(x, w, bias, kh: int, kw: int, stride: int, pad: int, relu: bool,
-           residual=None, out_f32: bool = False, tile: int = -1):
-    """Implicit-GEMM MFMA convolution with fused bias / residual / ReLU."""
-    return load().conv2d_nhwc(x, w, bias, residual, kh, kw, stride, pad, relu, out_f32, tile)
+           residual=None, out_f32: bool = False, tile: int = -1, out=None):
+    """Implicit-GEMM MFMA convolution with fused bias / residual / ReLU
+    (into ``out`` when given: a contiguous NHWC tensor, e.g. a batch slice)."""
+    return load().conv2d_nhwc(x, w, bias, residual, kh, kw, stride, pad, relu, out_f32, tile, out)
 
 
 def linear(x, w, bias, relu: bool = False, out_f32: bool = False):
     """y = x @ w.T + bias via the conv kernel as a 1x1 conv on a 1x1 image."""
     b, k = x.shape
-    y = load().conv2d_nhwc(x.view(b, 1, 1, k), w, bias, None, 1, 1, 1, 0, relu, out_f32, -1)
+    y = load().conv2d_nhwc(x.view(b, 1, 1, k), w, bias, None, 1, 1, 1, 0, relu, out_f32, -1, None)
     return y.view(b, w.shape[0])
 
 
-def preprocess(img_u8, start=None, batch: int = -1, start_offset: int = 0):
+def preprocess(img_u8, start=None, batch: int = -1, start_offset: int = 0, window: int = -1, sub: int = 0):
     """uint8 [B,H,W,3] -> normalised fp16 [B,H,W,4] (4th channel zero).
     With ``start`` (int64 GPU scalar) and ``batch``, reads images
     [*start - start_offset, ... + batch) of the shard ``img_u8`` (device-side
     window; ``start`` may be a global image index and ``start_offset`` the
-    shard's first global index)."""
-    return load().preprocess(img_u8, start, batch, start_offset)
+    shard's first global index).  A window of ``window`` images may be done
+    in parts: this call covers images [sub, sub + batch) of it."""
+    return load().preprocess(img_u8, start, batch, start_offset, window, sub)
 
 
 def resize_crop(img_u8, resize: int = 256, crop: int = 224):
@@ -41,10 +43,11 @@ def resize_crop(img_u8, resize: int = 256, crop: int = 224):
     return load().resize_crop(img_u8, resize, crop)
 
 
-def stem_fused(img_u8, w, bias, start=None, batch: int = -1, start_offset: int = 0):
+def stem_fused(img_u8, w, bias, start=None, batch: int = -1, start_offset: int = 0, window: int = -1,
+               sub: int = 0):
     """ResNet stem in one kernel: uint8 [B,H,W,3] -> fp16 [B,H/4,W/4,64]
     (optionally a device-side window of a shard, see ``preprocess``)."""
-    return load().stem_fused(img_u8, w, bias, start, batch, start_offset)
+    return load().stem_fused(img_u8, w, bias, start, batch, start_offset, window, sub)
 
 
 def maxpool2d(x, k: int = 3, s: int = 2, pad: int = 1):

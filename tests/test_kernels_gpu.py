@@ -295,6 +295,28 @@ def test_device_window_graph_matches_slices(ops, fuse):
         assert torch.equal(c0, c1) and torch.allclose(p0, p1)
 
 
+@pytest.mark.parametrize("split", [2, 3])
+def test_front_split_bit_identical(ops, split):
+    """Stem + layer1 on batch parts (window parts through the device-side start)
+    give exactly the unsplit results, eager and captured."""
+    from idunno.models import HipRunner, build_program
+
+    prog = build_program("resnet18", seed=4)
+    one, many = HipRunner(prog, front_split=1), HipRunner(prog, front_split=split)
+    shard = ops.synth_images(3, 0, 30, "cuda")
+    c1, p1 = one.forward(shard[:10].contiguous())
+    c2, p2 = many.forward(shard[:10].contiguous())
+    assert torch.equal(c1, c2) and torch.equal(p1, p2)
+    s1, r1 = one.capture_window(shard, 11)
+    s2, r2 = many.capture_window(shard, 11)
+    for s0 in (0, 5, 25):                      # 25 > 30 - 11: clamped to 19 for every part
+        s1.fill_(s0)
+        s2.fill_(s0)
+        a, b = r1(), r2()
+        torch.cuda.synchronize()
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
 @pytest.mark.parametrize("fuse", [True, False])
 def test_window_from_descriptor_row_with_packed_output(ops, fuse):
     """Graph reads a GLOBAL start index in place (minus the shard's base) and
