@@ -112,3 +112,61 @@ def test_scatter_images_over_gloo():
         p.join(60)
         assert p.exitcode == 0
     assert res == {r: True for r in range(world)}
+
+
+def _bench_pattern_worker(rank, world, port, q):
+    """bench.py's round: the forward reads its window start from the broadcast
+    descriptor row in place and writes packed (class, prob bits) straight into
+    the gather send buffer; rank 0 copies ``gathered_all`` once."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from idunno.parallel.dataplane import QueryPlane, init_from_env, unpack
+
+    env = init_from_env(backend="gloo")
+    B, shard_base = 8, rank * 1000
+    plane = QueryPlane(env, coordinator=0, max_chunk=B)
+    start_dev, send = plane.row_start(), plane.send_buffer[:B]
+
+    def fake_forward():                       # stands in for the captured hipGraph
+        s0 = int(start_dev.item()) - shard_base
+        idx = torch.arange(s0, s0 + B, dtype=torch.int32) + shard_base
+        send[:, 0] = (idx * 7919 + 13) % 1000
+        send[:, 1] = torch.full((B,), 0.25).view(torch.int32)
+
+    out = {}
+    for q_ in range(4):
+        table = [(1, q_ * world + r, r * 1000 + 3 * q_, r * 1000 + 3 * q_ + B - 1) for r in range(world)] \
+            if env.rank == 0 else None
+        plane.dispatch_device(table, slot=q_)
+        fake_forward()
+        plane.gather(None, None)
+        if env.rank == 0:
+            host = plane.gathered_all.clone()
+            for r in range(world):
+                c, p = unpack(host[r], B)
+                for i, (cc, pp) in enumerate(zip(c.tolist(), p.tolist())):
+                    out[(q_, table[r][2] + i)] = (cc, pp)
+    if env.rank == 0:
+        q.put(out)
+    if env.distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_bench_round_pattern_over_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_bench_pattern_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert len(out) == 4 * world * 8
+    for (_q, i), (c, p) in out.items():
+        assert c == (i * 7919 + 13) % 1000 and p == 0.25
