@@ -178,6 +178,76 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   return y;
 }
 
+// Per-device fp32 zeros (the bias of split-K partial GEMMs), grown on demand,
+// never freed (same reasoning as zero_buffer).
+static torch::Tensor zero_f32(const torch::Device& dev, int64_t n) {
+  static std::mutex mu;
+  static std::vector<torch::Tensor>* bufs = new std::vector<torch::Tensor>(64);
+  const int i = dev.index() < 0 ? 0 : dev.index();
+  TORCH_CHECK(i < 64, "device index out of range");
+  std::lock_guard<std::mutex> lk(mu);
+  auto& b = (*bufs)[i];
+  if (!b.defined() || b.numel() < n) {
+    b = torch::zeros({std::max<int64_t>(n, 4096)}, torch::TensorOptions().dtype(torch::kFloat).device(dev));
+    (void)hipStreamSynchronize(cur_stream());
+  }
+  return b;
+}
+
+// y = act(x @ w.T + bias) with K split over `splits` partial GEMMs (the conv
+// kernel as a 1x1 conv on a K-slice of each row: ldx = K) into fp32 partials,
+// then one combine kernel.  For FC layers with few output tiles and a long K
+// (AlexNet fc6-fc8 at batch 500: 64-256 tiles, K = 4096-9216) one tile per CU
+// with 64-144 serial K stages cannot hide the DMA latency.
+torch::Tensor linear_splitk(torch::Tensor x, torch::Tensor w, torch::Tensor bias, bool relu, bool out_f32,
+                            int64_t splits, int64_t tile) {
+  CHECK_DEV(x);
+  CHECK_DEV(w);
+  CHECK_DEV(bias);
+  CHECK_CONTIG(x);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(bias);
+  CHECK_DT(x, torch::kHalf);
+  CHECK_DT(w, torch::kHalf);
+  CHECK_DT(bias, torch::kFloat);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && bias.dim() == 1, "bad ranks");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && bias.size(0) == N, "shape mismatch");
+  TORCH_CHECK(N % 4 == 0, "N must be a multiple of 4");
+  TORCH_CHECK(splits >= 1 && splits <= 16 && K % (64 * splits) == 0, "K must split into multiples of 64");
+  TORCH_CHECK(M * N < (1L << 31) && M * K < (1L << 31), "too large for int32 indexing");
+  auto part = torch::empty({splits, M, N}, x.options().dtype(torch::kFloat));
+  auto y = torch::empty({M, N}, x.options().dtype(out_f32 ? torch::kFloat : torch::kHalf));
+  if (M == 0) return y;
+  const int64_t Ks = K / splits;
+  auto zb = zero_f32(x.device(), N);
+  const void* zero = zero_buffer(x.device()).data_ptr();
+  const half_t* xp = reinterpret_cast<const half_t*>(x.data_ptr());
+  const half_t* wp = reinterpret_cast<const half_t*>(w.data_ptr());
+  const int t = tile >= 10 ? (int)tile : conv_glds_pick((int)M, (int)N);
+  for (int64_t s = 0; s < splits; ++s) {
+    ConvArgs a{};
+    a.x = xp + s * Ks;
+    a.w = wp + s * Ks;
+    a.bias = zb.data_ptr<float>();
+    a.res = nullptr;
+    a.y = part.data_ptr<float>() + s * M * N;
+    a.B = (int)M; a.H = 1; a.W = 1; a.C = (int)Ks; a.ldx = (int)K;
+    a.Ho = 1; a.Wo = 1; a.Cout = (int)N; a.ldy = (int)N;
+    a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0;
+    a.M = (int)M;
+    a.Kpad = (int)K;
+    a.relu = 0;
+    a.zero = zero;
+    TORCH_CHECK(conv_glds_launch(a, true, t, cur_stream()), "unknown conv tile id ", t);
+    check_launch("linear_splitk");
+  }
+  splitk_reduce_launch(part.data_ptr<float>(), (int)splits, (long)(M * N), (int)N, bias.data_ptr<float>(),
+                       relu ? 1 : 0, y.data_ptr(), out_f32, cur_stream());
+  check_launch("splitk_reduce");
+  return y;
+}
+
 // uint8 [B,H,W,3] -> maxpool3x3/2(relu(conv7x7/2(normalise(img)) + bias)) : fp16 [B,Hp,Wp,64]
 // Optional device-side window: with `start` (int64 GPU scalar) and batch > 0,
 // `img` is a whole image shard [N,H,W,3] and images [*start, *start + batch)
@@ -339,6 +409,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_nhwc", &conv2d_nhwc, "implicit-GEMM MFMA conv + bias (+res) (+relu)", py::arg("x"), py::arg("w"),
         py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("relu"), py::arg("out_f32") = false, py::arg("tile") = -1, py::arg("out") = py::none());
+  m.def("linear_splitk", &linear_splitk, "FC layer with split-K partial GEMMs + combine", py::arg("x"),
+        py::arg("w"), py::arg("bias"), py::arg("relu"), py::arg("out_f32"), py::arg("splits"), py::arg("tile") = -1);
   m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 NHWC4", py::arg("img"),
         py::arg("start") = py::none(), py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1,
         py::arg("sub") = 0);

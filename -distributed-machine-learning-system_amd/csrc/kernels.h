@@ -23,6 +23,7 @@ struct ConvArgs {
   int tiles_n;  // ceil(Cout / BN)
   int tiles_m;  // ceil(M / BM)
   const void* zero;  // >= 16 zero bytes (DMA source for padding taps)
+  int ldx;           // conv_glds: input pixel stride in halfs (0: C); a K-slice of a wider row
 };
 
 void conv_igemm_launch(ConvArgs a, bool small, bool out_f32, int tile, hipStream_t st);
@@ -50,6 +51,8 @@ void maxpool_launch(const half_t* x, half_t* y, int B, int H, int W, int C, int 
 void avgpool_launch(const half_t* x, half_t* y, int B, int HW, int C, hipStream_t st);
 void synth_images_launch(uint8_t* out, uint64_t seed, long start, long n, long bytes_per_img,
                          hipStream_t st);
+void splitk_reduce_launch(const float* part, int S, long MN, int N, const float* bias, int relu, void* y,
+                          bool out_f32, hipStream_t st);
 void softmax_top1_launch(const float* logits, int ld, int N, int rows, int* cls, float* prob, int* packed,
                          hipStream_t st);
 

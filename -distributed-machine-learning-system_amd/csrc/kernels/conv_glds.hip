@@ -86,7 +86,9 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
     a_ch[j] = (lslot ^ swz_r(row, CPR)) * 8;
     a_src[j] = n < a.Cout ? a.w + (size_t)n * a.Kpad + a_ch[j] : nullptr;
   }
-  // B sources: pixel decomposition per instruction
+  // B sources: pixel decomposition per instruction (pixel stride ldx: a K-slice
+  // of wider rows when the caller splits K, e.g. linear_splitk)
+  const int ldx = a.ldx ? a.ldx : a.C;
   int b_base[GB], b_ih0[GB], b_iw0[GB], b_ch[GB];
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
@@ -97,7 +99,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
       const int hw = a.Ho * a.Wo;
       const int b = m / hw, r = m - b * hw;
       const int oh = r / a.Wo, ow = r - oh * a.Wo;
-      b_base[j] = b * a.H * a.W * a.C + b_ch[j];
+      b_base[j] = b * a.H * a.W * ldx + b_ch[j];
       b_ih0[j] = oh * a.stride - a.pad;
       b_iw0[j] = ow * a.stride - a.pad;
     } else {
@@ -122,7 +124,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
     for (int j = 0; j < GB; ++j) {
       const int ih = b_ih0[j] + i_kh, iw = b_iw0[j] + i_kw;
       const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const half_t* src = ok ? a.x + b_base[j] + (ih * a.W + iw) * a.C + coff : zero;
+      const half_t* src = ok ? a.x + b_base[j] + (ih * a.W + iw) * ldx + coff : zero;
       __builtin_amdgcn_global_load_lds((glb_void_t*)src,
                                        (lds_void_t*)(base + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
     }

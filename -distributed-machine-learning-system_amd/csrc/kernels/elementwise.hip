@@ -182,6 +182,42 @@ void avgpool_launch(const half_t* x, half_t* y, int B, int HW, int C, hipStream_
   hipLaunchKernelGGL(avgpool_kernel, dim3((unsigned)B), dim3(256), 0, st, x, y, B, HW, C);
 }
 
+// Split-K combine: y[m][n] = act(sum_s part[s][m][n] + bias[n]), 4 outputs per
+// thread (16-byte partial loads), fp16 or fp32 out.
+__global__ void splitk_reduce_kernel(const float* __restrict__ part, int S, long MN, int N,
+                                     const float* __restrict__ bias, int relu, void* __restrict__ y, int out_f32) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= MN) return;
+  float4v v = *reinterpret_cast<const float4v*>(part + i);
+  for (int s = 1; s < S; ++s) v += *reinterpret_cast<const float4v*>(part + (long)s * MN + i);
+  const int n = (int)(i % N);
+  v += *reinterpret_cast<const float4v*>(bias + n);
+  if (relu) {
+    v[0] = fmaxf(v[0], 0.f);
+    v[1] = fmaxf(v[1], 0.f);
+    v[2] = fmaxf(v[2], 0.f);
+    v[3] = fmaxf(v[3], 0.f);
+  }
+  if (out_f32) {
+    *reinterpret_cast<float4v*>(static_cast<float*>(y) + i) = v;
+  } else {
+    half4v o;
+    o[0] = (half_t)v[0];
+    o[1] = (half_t)v[1];
+    o[2] = (half_t)v[2];
+    o[3] = (half_t)v[3];
+    *reinterpret_cast<half4v*>(static_cast<half_t*>(y) + i) = o;
+  }
+}
+
+void splitk_reduce_launch(const float* part, int S, long MN, int N, const float* bias, int relu, void* y,
+                          bool out_f32, hipStream_t st) {
+  const int bs = 256;
+  const long threads = (MN + 3) / 4;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + bs - 1) / bs)), dim3(bs), 0, st, part, S, MN, N,
+                     bias, relu, y, out_f32 ? 1 : 0);
+}
+
 // Row softmax + top-1: one 64-lane wave per row of fp32 logits.
 // prob(top1) = 1 / sum_j exp(x_j - x_max).  Ties resolve to the lowest index
 // (torch.topk semantics on CPU).

@@ -21,11 +21,25 @@ def conv2d(x, w, bias, kh: int, kw: int, stride: int, pad: int, relu: bool,
     return load().conv2d_nhwc(x, w, bias, residual, kh, kw, stride, pad, relu, out_f32, tile, out)
 
 
-def linear(x, w, bias, relu: bool = False, out_f32: bool = False):
-    """y = x @ w.T + bias via the conv kernel as a 1x1 conv on a 1x1 image."""
+# Default K split of FC layers.  Measured (tools/ab_linear_split.py,
+# profiles/r1_v8_ab_linear_split.log): splitting never paid on these models --
+# AlexNet b500 -2.8 % (2 splits) .. -9.8 % (8), b1/b8 -20 %; ResNet50 b1024
+# within its run-to-run spread -- the fp32 partials and extra launches cost
+# more than the DMA latency they hide.  Kept selectable for other shapes.
+LINEAR_SPLITS: int = 1
+
+
+def linear(x, w, bias, relu: bool = False, out_f32: bool = False, splits: int | None = None):
+    """y = x @ w.T + bias: the conv kernel as a 1x1 conv on a 1x1 image, or
+    with ``splits`` > 1 as split-K partial GEMMs + one combine kernel."""
     b, k = x.shape
+    n = w.shape[0]
+    if splits is None:
+        splits = LINEAR_SPLITS
+    if splits > 1:
+        return load().linear_splitk(x, w, bias, relu, out_f32, splits, -1)
     y = load().conv2d_nhwc(x.view(b, 1, 1, k), w, bias, None, 1, 1, 1, 0, relu, out_f32, -1, None)
-    return y.view(b, w.shape[0])
+    return y.view(b, n)
 
 
 def preprocess(img_u8, start=None, batch: int = -1, start_offset: int = 0, window: int = -1, sub: int = 0):

@@ -165,6 +165,23 @@ def test_linear_fp32_out(ops, B, K, N):
     _check(y, ref, tol=5e-3)
 
 
+@pytest.mark.parametrize("splits", [1, 2, 4, 8])
+@pytest.mark.parametrize("B,K,N,relu,f32", [(500, 9216, 4096, True, False), (500, 4096, 1000, False, True),
+                                            (130, 2048, 1000, False, True)])
+def test_linear_split_k(ops, B, K, N, relu, f32, splits):
+    """FC through split-K partial GEMMs (K-slices of each row, ldx = K) + combine."""
+    torch.manual_seed(B + K + N + (splits or 0))
+    x = torch.randn(B, K, device=DEV).half()
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).half()
+    b = torch.randn(N, device=DEV)
+    y = ops.linear(x, w, b, relu=relu, out_f32=f32, splits=splits)
+    assert y.dtype == (torch.float32 if f32 else torch.float16) and y.shape == (B, N)
+    ref = x.float() @ w.float().t() + b
+    if relu:
+        ref = torch.relu(ref)
+    _check(y, ref, tol=5e-3)
+
+
 def test_maxpool_and_avgpool(ops):
     torch.manual_seed(3)
     x = torch.randn(3, 112, 112, 64, device=DEV).half()
