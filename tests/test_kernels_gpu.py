@@ -207,6 +207,16 @@ def test_preprocess_and_resize_crop(ops):
     assert y.shape == (2, 224, 224, 4)
     assert (y[..., :3].float() - ref).abs().max().item() < 5e-3
     assert y[..., 3].abs().max().item() == 0
+    # ragged pixel count (105 = 26 quads + 1) and a source 1 byte off alignment:
+    # the per-byte fallback of the 4-pixel kernel
+    for off in (0, 1):
+        buf = torch.randint(0, 256, (off + 3 * 5 * 7 * 3,), dtype=torch.uint8, device=DEV)
+        odd = buf[off:].view(3, 5, 7, 3)
+        yo = ops.preprocess(odd)
+        refo = preprocess_u8(odd).permute(0, 2, 3, 1)
+        assert yo.shape == (3, 5, 7, 4)
+        assert (yo[..., :3].float() - refo).abs().max().item() < 5e-3
+        assert yo[..., 3].abs().max().item() == 0
     big = torch.randint(0, 256, (2, 300, 400, 3), dtype=torch.uint8, device=DEV)
     z = ops.resize_crop(big, 256, 224)
     assert z.shape == (2, 224, 224, 4)
