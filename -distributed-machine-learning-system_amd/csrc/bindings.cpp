@@ -424,6 +424,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("packed") = py::none());
   m.def("synth_images", &synth_images, "deterministic synthetic uint8 images [n,hw,hw,3]");
   m.def("pick_tile", &pick_tile, "tile id the conv heuristic picks for (M, Cout)");
+  m.def("set_stem_workgroups_per_cu", &set_stem_workgroups_per_cu,
+        "fused stem: persistent workgroups per CU (1-3, default 3)");
   m.def("set_stem_ablation", &set_stem_ablation,
         "profiling only: 1 skip pool, 2 skip conv MFMAs, 4 skip patch normalise (wrong outputs)");
   m.def("set_conv3x3_c64_default", &set_conv3x3_c64_default,

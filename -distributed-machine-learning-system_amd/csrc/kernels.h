@@ -34,6 +34,7 @@ bool conv_pers_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);   // 
 bool conv3x3_patch_supported(int H, int W, int C, int Cout);
 bool conv3x3_c64_supported(int C, int Cout);
 void set_stem_ablation(int mode);
+void set_stem_workgroups_per_cu(int n);
 void conv3x3_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
                         const void* zero, int B, int H, int W, int relu, hipStream_t st);
 void conv3x3_patch_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,

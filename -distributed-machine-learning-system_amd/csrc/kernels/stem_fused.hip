@@ -6,55 +6,63 @@
 // alexnet_resnet.py:57-75 -> torchvision resnet18.conv1/bn1/relu/maxpool).
 // The conv activation (642 MB at B=400) never touches HBM.
 //
-// Work item = one 8x8 tile of pooled outputs of one image.  Workgroups are
-// persistent (2 per CU): the 28 KB of packed weights are staged into LDS and
-// the 7x4 MFMA A-fragments into registers ONCE, then every tile
-//   * takes its 39x40 uint8 input patch from registers prefetched one tile
+// Work item = one 8-row x 7-column tile of pooled outputs of one image.  Its
+// 17 x 15 conv outputs are 17 MFMA pixel fragments: fragment f = conv row f,
+// lane&15 = conv column (lane 15 idle), so the C/D tile of
+// v_mfma_f32_16x16x32_f16 has one conv row across each 16-lane DPP row.
+// Workgroups are persistent (2 per CU); the 28 A-fragments (64 couts x K 7x32)
+// are loaded into registers ONCE, then every tile
+//   * takes its 39x38 uint8 input patch from registers prefetched one tile
 //     earlier (12-byte aligned pixel quads), normalises it into LDS as
 //     [row][col][4] fp16 (channel 3 = 0);
-//   * computes the 17x17 conv outputs under its pool windows (289 px, 19
-//     fragments of 16) as an implicit GEMM M=304, N=64, K=7x32 on
-//     v_mfma_f32_16x16x32_f16 — one K stage per kernel row (8 taps x 4 ch;
-//     tap 7 and channel 3 have zero weights); each B-fragment row is 16
-//     contiguous, 16-byte-aligned bytes of the patch;
-//   * writes bias+ReLU outputs (zero outside the image == -inf padding after
-//     ReLU) to an LDS tile, issues the global loads of the next-next patch,
-//     then max-pools 3x3/2 with 16-byte LDS reads and 16-byte stores.
+//   * runs the implicit GEMM M=17x16, N=64, K=7x32 — one K stage per kernel
+//     row (8 taps x 4 ch; tap 7 and channel 3 have zero weights); each
+//     B-fragment row is 16 contiguous, 16-byte-aligned bytes of the patch;
+//   * does the pool's horizontal 3-max IN REGISTERS (two DPP row shifts of the
+//     fp32 accumulators), so only the 7 pooled columns of each conv row are
+//     written to LDS (2.2x fewer bytes than the full conv row);
+//   * issues the global loads of the next-next patch, then finishes the pool
+//     vertically (5 LDS rows per two pooled rows) with 16-byte stores.
+// Bias + ReLU are applied after the max (both commute with it).
 #include "../kernels.h"
 
 namespace idunno {
 
 namespace stem {
-constexpr int KH = 7, CS = 2, CP = 3;      // conv
-constexpr int PK = 3, PS = 2, PP = 1;      // pool
-constexpr int PT = 8;                       // pooled tile edge
-constexpr int CR = (PT - 1) * PS + PK;      // 17 conv rows/cols under the tile
-constexpr int NPIX = CR * CR;               // 289
-constexpr int NFRAG = (NPIX + 15) / 16;     // 19
-constexpr int IPR = (CR - 1) * CS + KH;     // 39 patch rows
-constexpr int IPC = (CR - 1) * CS + 8;      // 40 patch cols (8th tap read, zero weight)
-constexpr int QPR = 11;                     // 4-pixel quads per patch row (44 px cover 40)
+constexpr int KH = 7, CS = 2, CP = 3;       // conv
+constexpr int PK = 3, PS = 2, PP = 1;       // pool
+constexpr int PTX = 7, PTY = 8;             // pooled tile: 7 columns x 8 rows
+constexpr int CRX = (PTX - 1) * PS + PK;    // 15 conv columns (<= 16 lanes)
+constexpr int CRY = (PTY - 1) * PS + PK;    // 17 conv rows = pixel fragments
+constexpr int IPR = (CRY - 1) * CS + KH;    // 39 patch rows
+constexpr int IPC = (16 - 1) * CS + 8;      // 38 patch cols (idle lane 15 + zero-weight tap 7 stay in-row)
+constexpr int QPR = 11;                     // 4-pixel quads per patch row (44 px cover 41)
 constexpr int NQUAD = IPR * QPR;            // 429
 constexpr int QPT = (NQUAD + 255) / 256;    // quads per thread (2)
-constexpr int PATCH_BYTES = IPR * IPC * 8;  // 12480
-constexpr int W_BYTES = KH * 64 * 64;       // [kh][cout 64][32 halfs] = 28672
-constexpr int CONV_BYTES = NPIX * 128;      // [pix][64 ch] fp16 = 36992
-constexpr int LDS = PATCH_BYTES + W_BYTES + CONV_BYTES;
+constexpr int PATCH_BYTES = IPR * IPC * 8;  // 11856
+constexpr int HP_BYTES = CRY * PTX * 128;   // [conv row][pooled col][64 ch] fp16 = 15232
+constexpr int LDS = PATCH_BYTES + HP_BYTES;
+constexpr int NVP = (PTY / 2) * PTX * 8;    // vertical-pool items: 2 pooled rows x 1 col x 8 ch (224)
+static_assert(CRX <= 15, "one conv row per 16-lane fragment, lane 15 idle");
+static_assert(NVP <= 256, "one vertical-pool item per thread");
+constexpr int NIW = 2;                      // 16-cout A fragments per wave (of 4)
+constexpr int NCH = 4 / NIW;                // waves sharing each conv row
+constexpr int WGS_MAX = 4;                  // workgroups per CU the registers allow
 }  // namespace stem
 
-__constant__ float kStemMean[3] = {0.485f, 0.456f, 0.406f};
-__constant__ float kStemInvStd[3] = {1.0f / 0.229f, 1.0f / 0.224f, 1.0f / 0.225f};
+// ToTensor + Normalize as x * s + c per channel: s = 1 / (255 std), c = -mean / std
+typedef float float2v __attribute__((ext_vector_type(2)));
+constexpr float kSR = 1.f / (255.f * 0.229f), kSG = 1.f / (255.f * 0.224f), kSB = 1.f / (255.f * 0.225f);
+constexpr float kCR = -0.485f / 0.229f, kCG = -0.456f / 0.224f, kCB = -0.406f / 0.225f;
+#define kScaleRG (float2v{kSR, kSG})
+#define kShiftRG (float2v{kCR, kCG})
+#define kScaleBB (float2v{kSB, kSB})
+#define kShiftBB (float2v{kCB, kCB})
 
-__device__ __forceinline__ int swz64s(int row) {
-  const int q = (row >> 2) & 3;
-  return (0x78 >> (2 * q)) & 3;
-}
-
-// Byte offset of 16-byte channel chunk c (0..7) of conv pixel p in the LDS conv
-// tile.  Rows are 128 B (64 fp16 channels); the chunk is XOR-swizzled by p & 7 so
-// the epilogue's 16 lanes (16 consecutive pixels, one channel chunk) hit 8
-// different 16-byte slots instead of one bank (16-way -> 2-way).
-__device__ __forceinline__ int conv_off(int p, int c) { return p * 128 + ((c ^ (p & 7)) << 4); }
+// Byte offset of 16-byte channel chunk c (0..7) of (conv row r, pooled col px)
+// in the LDS tile.  Rows of 128 B; the chunk is XOR-swizzled by px so the
+// epilogue's 8-byte writes (7 pooled columns of one chunk) spread over banks.
+__device__ __forceinline__ int hp_off(int r, int px, int c) { return (r * stem::PTX + px) * 128 + ((c ^ px) << 4); }
 
 struct StemGeom {
   int B, H, W, Hc, Wc, Hp, Wp, tiles_x, tiles_y, ntiles;
@@ -63,6 +71,9 @@ struct StemGeom {
 
 static int g_stem_ablate = 0;
 void set_stem_ablation(int mode) { g_stem_ablate = mode; }
+// persistent workgroups per CU (A/B knob)
+static int g_stem_wgs = stem::WGS_MAX;
+void set_stem_workgroups_per_cu(int n) { g_stem_wgs = n < 1 ? 1 : (n > stem::WGS_MAX ? stem::WGS_MAX : n); }
 
 struct Quads {
   uint32_t d[stem::QPT][3];
@@ -73,8 +84,8 @@ __device__ __forceinline__ void tile_coords(const StemGeom& g, int t, int& b, in
   const int per = g.tiles_x * g.tiles_y;
   b = t / per;
   const int r = t - b * per;
-  py0 = (r / g.tiles_x) * stem::PT;
-  px0 = (r % g.tiles_x) * stem::PT;
+  py0 = (r / g.tiles_x) * stem::PTY;
+  px0 = (r % g.tiles_x) * stem::PTX;
 }
 
 // global -> registers: this thread's quads of tile t's input patch
@@ -84,7 +95,7 @@ __device__ __forceinline__ void load_quads(const uint8_t* __restrict__ img, cons
   int b, py0, px0;
   tile_coords(g, t, b, py0, px0);
   const int iy0 = (py0 * PS - PP) * CS - CP;
-  const int ixa = (px0 * PS - PP) * CS - CP - 3;     // 4px0 - 8: quad-aligned first column
+  const int ixa = (px0 * PS - PP) * CS - CP - 3;     // 4px0 - 8: a multiple of 4 -> 12-byte quads 4-byte aligned
 #pragma unroll
   for (int k = 0; k < QPT; ++k) {
     const int i = tid + 256 * k;
@@ -96,7 +107,7 @@ __device__ __forceinline__ void load_quads(const uint8_t* __restrict__ img, cons
     if ((unsigned)iy >= (unsigned)g.H) continue;
     const uint8_t* p = img + (((size_t)b * g.H + iy) * g.W + ix) * 3;
     if (ix >= 0 && ix + 3 < g.W) {
-      const uint32_t* pd = reinterpret_cast<const uint32_t*>(p);   // 12-byte quads are 4-byte aligned
+      const uint32_t* pd = reinterpret_cast<const uint32_t*>(p);
       q.d[k][0] = pd[0];
       q.d[k][1] = pd[1];
       q.d[k][2] = pd[2];
@@ -127,23 +138,30 @@ __device__ __forceinline__ void store_patch(char* patch, const StemGeom& g, int 
     const int i = tid + 256 * k;
     if (i >= NQUAD) continue;
     const int r = i / QPR, qc = i - r * QPR;
+    // byte -> f32 (v_cvt_f32_ubyteN), x * s + c on f32 pairs (v_pk_fma_f32),
+    // pairs -> packed fp16: ~26 VALU per quad of 4 pixels
+    float f[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) f[j] = (float)((q.d[k][j >> 2] >> (8 * (j & 3))) & 0xFFu);
+    const float2v b01 = float2v{f[2], f[5]} * kScaleBB + kShiftBB;
+    const float2v b23 = float2v{f[8], f[11]} * kScaleBB + kShiftBB;
+    const float bl[4] = {b01[0], b01[1], b23[0], b23[1]};
     half4v px[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      half4v o = {(half_t)0.f, (half_t)0.f, (half_t)0.f, (half_t)0.f};
-      const int x = ixa + 4 * qc + j;
-      if (q.ok[k] && (unsigned)x < (unsigned)g.W) {
+      const float2v rg = float2v{f[3 * j], f[3 * j + 1]} * kScaleRG + kShiftRG;
+      const half2v lo = {(half_t)rg[0], (half_t)rg[1]};     // v_cvt_pk_f16_f32
+      const half2v hi = {(half_t)bl[j], (half_t)0.f};
+      px[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3);
+    }
+    const int x0 = ixa + 4 * qc;
+    if (!(q.ok[k] && x0 >= 0 && x0 + 3 < g.W)) {       // image edge: zero the pixels outside
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-          const int byte = 3 * j + ch;
-          const uint32_t u = (q.d[k][byte >> 2] >> (8 * (byte & 3))) & 0xFFu;
-          o[ch] = (half_t)(((float)u * (1.f / 255.f) - kStemMean[ch]) * kStemInvStd[ch]);
-        }
-      }
-      px[j] = o;
+      for (int j = 0; j < 4; ++j)
+        if (!q.ok[k] || (unsigned)(x0 + j) >= (unsigned)g.W) px[j] = half4v{0, 0, 0, 0};
     }
     // write pixel (t + lane) & 3 in step t: neighbouring lanes' 8-byte stores are
-    // then 40 B apart instead of 32 B, i.e. 16 distinct bank pairs (4-way -> none)
+    // then 40 B apart instead of 32 B, i.e. distinct bank pairs
 #pragma unroll
     for (int t2 = 0; t2 < 4; ++t2) {
       const int j = (t2 + tid) & 3;
@@ -155,7 +173,14 @@ __device__ __forceinline__ void store_patch(char* patch, const StemGeom& g, int 
   }
 }
 
-__global__ void __launch_bounds__(256, 2)
+// packed fp16 pair of lane l + N of the same 16-lane row (DPP row_shl:N; lanes
+// past the row read 0 -- only lanes cx <= 12 are consumed)
+template <int N>
+__device__ __forceinline__ half2v row_shl_h2(half2v v) {
+  return __builtin_bit_cast(half2v, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x100 | N, 0xF, 0xF, true));
+}
+
+__global__ void __launch_bounds__(256, stem::WGS_MAX)
 stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w, const float* __restrict__ bias,
                   half_t* __restrict__ y, const StemGeom g, const long long* __restrict__ start_idx,
                   long long start_off, long long max_start, long long sub) {
@@ -169,8 +194,7 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
     img += (size_t)s * g.H * g.W * 3;
   }
   char* patch = smem;
-  char* wl = smem + PATCH_BYTES;
-  char* conv = smem + PATCH_BYTES + W_BYTES;
+  char* hp = smem + PATCH_BYTES;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
   int t = blockIdx.x;
@@ -179,69 +203,78 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
   Quads q;
   load_quads(img, g, t, tid, q);
 
-  // ---- weights -> LDS [kh][cout][32] (swizzled 16-byte chunks), once ---------
-  for (int i = tid; i < 64 * KH * 4; i += 256) {
-    const int ch = i & 3, kh = (i >> 2) % KH, co = i / (4 * KH);
-    const vec16 v = *reinterpret_cast<const vec16*>(w + (size_t)co * (KH * 32) + kh * 32 + ch * 8);
-    *reinterpret_cast<vec16*>(wl + kh * 4096 + co * 64 + ((ch ^ swz64s(co)) << 4)) = v;
-  }
+  // ---- A fragments (weights [cout][kh][32]) straight into registers, once ----
+  const int frow = lane & 15, fch = lane >> 4;
+  const int ch0 = (wave % NCH) * NIW;   // first 16-cout fragment of this wave
+  half8v fa[KH][NIW];
+#pragma unroll
+  for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+    for (int i = 0; i < NIW; ++i)
+      fa[kh][i] = *reinterpret_cast<const half8v*>(w + (size_t)((ch0 + i) * 16 + frow) * (KH * 32) + kh * 32 + fch * 8);
+  // bias + ReLU after the max-pool, once per pooled output; each pooling
+  // thread owns one fixed 8-channel chunk
+  half8v pb8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pb8[j] = (half_t)bias[(tid & 7) * 8 + j];
+
   store_patch(patch, g, t, tid, q);
   int tn = t + gridDim.x;
   if (tn < g.ntiles) load_quads(img, g, tn, tid, q);
   __syncthreads();
 
-  const int frow = lane & 15, fch = lane >> 4;
-  half8v fa[KH][4];
-#pragma unroll
-  for (int kh = 0; kh < KH; ++kh)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = i * 16 + frow;
-      fa[kh][i] = *reinterpret_cast<const half8v*>(wl + kh * 4096 + row * 64 + ((fch ^ swz64s(row)) << 4));
-    }
-  // bias + ReLU are applied AFTER the max-pool (both commute with max:
-  // relu(max(x) + b) == max(relu(x + b))), once per pooled output instead of once
-  // per conv output (4.5x fewer); each thread pools one fixed 8-channel chunk
-  half8v pb8;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) pb8[j] = (half_t)bias[(tid & 7) * 8 + j];
+  // vertical-pool item of this thread: chunk c8, pooled column vpx, pooled rows 2*vpy2 and 2*vpy2+1
+  const int c8 = tid & 7, vpx = (tid >> 3) % PTX, vpy2 = tid / (8 * PTX);
+  const int cx = frow;   // conv column of this lane in every fragment
 
   while (true) {
     int b, py0, px0;
     tile_coords(g, t, b, py0, px0);
     const int oy0 = py0 * PS - PP, ox0 = px0 * PS - PP;
+    const bool colv = cx < CRX && (unsigned)(ox0 + cx) < (unsigned)g.Wc;
+    const bool interior = ox0 >= 0 && ox0 + CRX <= g.Wc;   // no column of this tile needs masking
 
-    // ---- conv GEMM over the 19 pixel fragments, round-robin over 4 waves -----
-    for (int f = wave; f < NFRAG; f += 4) {
-      const int p = f * 16 + frow;
-      const int pc = min(p, NPIX - 1);
-      const int cy = pc / CR, cx = pc - cy * CR;
-      const char* pb = patch + ((2 * cy) * IPC + 2 * cx + 2 * fch) * 8;
-      float4v acc[4];
+    // ---- conv GEMM, one conv row per fragment, round-robin over 4 waves ------
+    for (int f = wave / NCH; f < CRY; f += 4 / NCH) {
+      const char* pb = patch + ((2 * f) * IPC + 2 * cx + 2 * fch) * 8;
+      float4v acc[NIW];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = float4v{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < NIW; ++i) acc[i] = float4v{0.f, 0.f, 0.f, 0.f};
       if (!(g.ablate & 2)) {
 #pragma unroll
         for (int kh = 0; kh < KH; ++kh) {
           const half8v fb = *reinterpret_cast<const half8v*>(pb + kh * IPC * 8);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[kh][i], fb, acc[i], 0, 0, 0);
+          for (int i = 0; i < NIW; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[kh][i], fb, acc[i], 0, 0, 0);
         }
       }
-      if (p < NPIX) {
-        const int oy = oy0 + cy, ox = ox0 + cx;
-        const bool valid = (unsigned)oy < (unsigned)g.Hc && (unsigned)ox < (unsigned)g.Wc;
-        // raw conv sums; outside the image -65504 (the pool's -inf padding)
+      // lane = (conv column cx; couts i*16 + fch*4 + r).  Outside the image the
+      // conv output is the pool's -inf padding (-65504); the 3-wide horizontal
+      // max takes lanes cx+1, cx+2 of the same DPP row, on packed fp16 pairs
+      // (VALU issue is this phase's cost: 4 cycles per wave instruction).
+      half4v o[NIW];
+      if ((unsigned)(oy0 + f) < (unsigned)g.Hc) {          // wave-uniform
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          half4v o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = valid ? (half_t)acc[i][r] : (half_t)(-65504.f);
-          *reinterpret_cast<half4v*>(conv + conv_off(p, i * 2 + (fch >> 1)) + (fch & 1) * 8) = o;
+        for (int i = 0; i < NIW; ++i) {
+          half2v p0 = {(half_t)acc[i][0], (half_t)acc[i][1]};
+          half2v p1 = {(half_t)acc[i][2], (half_t)acc[i][3]};
+          if (!interior && !colv) p0 = p1 = half2v{(half_t)-65504.f, (half_t)-65504.f};
+          p0 = __builtin_elementwise_max(p0, __builtin_elementwise_max(row_shl_h2<1>(p0), row_shl_h2<2>(p0)));
+          p1 = __builtin_elementwise_max(p1, __builtin_elementwise_max(row_shl_h2<1>(p1), row_shl_h2<2>(p1)));
+          o[i] = half4v{p0[0], p0[1], p1[0], p1[1]};
         }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NIW; ++i) o[i] = half4v{(half_t)-65504.f, (half_t)-65504.f, (half_t)-65504.f, (half_t)-65504.f};
+      }
+      if (!(cx & 1) && cx < 2 * PTX) {
+        const int px = cx >> 1;
+#pragma unroll
+        for (int i = 0; i < NIW; ++i)
+          *reinterpret_cast<half4v*>(hp + hp_off(f, px, 2 * (ch0 + i) + (fch >> 1)) + (fch & 1) * 8) = o[i];
       }
     }
-    __syncthreads();   // conv tile complete; patch(t) no longer read
+    __syncthreads();   // pooled-column tile complete; patch(t) no longer read
 
     const int tnext = tn;
     if (tnext < g.ntiles) {
@@ -250,24 +283,27 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
       if (tn < g.ntiles) load_quads(img, g, tn, tid, q);
     }
 
-    // ---- 3x3/2 max-pool from the LDS tile -> global ---------------------------
-    for (int i = tid; i < ((g.ablate & 1) ? 0 : PT * PT * 8); i += 256) {
-      const int c8 = i & 7, pp = i >> 3;
-      const int py = pp / PT, px = pp - py * PT;
-      if (py0 + py >= g.Hp || px0 + px >= g.Wp) continue;
-      half8v m = *reinterpret_cast<const half8v*>(conv + conv_off((2 * py) * CR + 2 * px, c8));
-#pragma unroll
-      for (int dy = 0; dy < PK; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < PK; ++dx) {
-          if (dy == 0 && dx == 0) continue;
-          const half8v v = *reinterpret_cast<const half8v*>(conv + conv_off((2 * py + dy) * CR + 2 * px + dx, c8));
-          m = __builtin_elementwise_max(m, v);
-        }
-      m = __builtin_elementwise_max(m + pb8, half8v{0, 0, 0, 0, 0, 0, 0, 0});
-      *reinterpret_cast<half8v*>(y + (((size_t)b * g.Hp + py0 + py) * g.Wp + px0 + px) * 64 + c8 * 8) = m;
+    // ---- vertical 3-max over conv rows 4*vpy2 .. 4*vpy2+4 -> 2 pooled rows ----
+    if (tid < NVP && !(g.ablate & 1)) {
+      const int r0 = 4 * vpy2;
+      const half8v a0 = *reinterpret_cast<const half8v*>(hp + hp_off(r0 + 0, vpx, c8));
+      const half8v a1 = *reinterpret_cast<const half8v*>(hp + hp_off(r0 + 1, vpx, c8));
+      const half8v a2 = *reinterpret_cast<const half8v*>(hp + hp_off(r0 + 2, vpx, c8));
+      const half8v a3 = *reinterpret_cast<const half8v*>(hp + hp_off(r0 + 3, vpx, c8));
+      const half8v a4 = *reinterpret_cast<const half8v*>(hp + hp_off(r0 + 4, vpx, c8));
+      const half8v zero = {0, 0, 0, 0, 0, 0, 0, 0};
+      half8v lo = __builtin_elementwise_max(__builtin_elementwise_max(a0, a1), a2);
+      half8v hi = __builtin_elementwise_max(__builtin_elementwise_max(a2, a3), a4);
+      lo = __builtin_elementwise_max(lo + pb8, zero);
+      hi = __builtin_elementwise_max(hi + pb8, zero);
+      const int ox = px0 + vpx, oy = py0 + 2 * vpy2;
+      if (ox < g.Wp) {
+        half_t* dst = y + (((size_t)b * g.Hp + oy) * g.Wp + ox) * 64 + c8 * 8;
+        if (oy < g.Hp) *reinterpret_cast<half8v*>(dst) = lo;
+        if (oy + 1 < g.Hp) *reinterpret_cast<half8v*>(dst + (size_t)g.Wp * 64) = hi;
+      }
     }
-    __syncthreads();   // conv tile reads done; patch(tnext) visible
+    __syncthreads();   // tile reads done; patch(tnext) visible
     if (tnext >= g.ntiles) break;
     t = tnext;
   }
@@ -285,18 +321,20 @@ void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, h
   g.Wc = (W + 2 * CP - KH) / CS + 1;
   g.Hp = (g.Hc + 2 * PP - PK) / PS + 1;
   g.Wp = (g.Wc + 2 * PP - PK) / PS + 1;
-  g.tiles_x = (g.Wp + PT - 1) / PT;
-  g.tiles_y = (g.Hp + PT - 1) / PT;
+  g.tiles_x = (g.Wp + PTX - 1) / PTX;
+  g.tiles_y = (g.Hp + PTY - 1) / PTY;
   g.ntiles = B * g.tiles_x * g.tiles_y;
   g.ablate = g_stem_ablate;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_fused_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    attr = true;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
-  const int grid = g.ntiles < 512 ? g.ntiles : 512;   // persistent: 2 workgroups per CU
-  hipLaunchKernelGGL(stem_fused_kernel, dim3(grid), dim3(256), LDS, st, img, w, bias, y, g, start_idx, start_off, max_start, sub);
+  const int per = g_stem_wgs * ncu;   // persistent: g_stem_wgs workgroups per CU
+  const int grid = g.ntiles < per ? g.ntiles : per;
+  hipLaunchKernelGGL(stem_fused_kernel, dim3(grid), dim3(256), LDS, st, img, w, bias, y, g, start_idx, start_off,
+                     max_start, sub);
 }
 
 }  // namespace idunno

@@ -366,7 +366,7 @@ def test_window_from_descriptor_row_with_packed_output(ops, fuse):
         assert torch.equal(packed[:, 0], c0) and torch.equal(packed[:, 1].view(torch.float32), p1)
 
 
-@pytest.mark.parametrize("B,H", [(3, 224), (2, 64), (1, 100)])
+@pytest.mark.parametrize("B,H", [(3, 224), (2, 64), (1, 100), (2, 37)])
 def test_stem_fused_vs_fp32(ops, B, H):
     from idunno.models.packed import pack_conv_weight
     from idunno.models.reference import preprocess_u8
