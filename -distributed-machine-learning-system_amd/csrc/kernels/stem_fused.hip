@@ -35,16 +35,23 @@ constexpr int PTX = 7, PTY = 8;             // pooled tile: 7 columns x 8 rows
 constexpr int CRX = (PTX - 1) * PS + PK;    // 15 conv columns (<= 16 lanes)
 constexpr int CRY = (PTY - 1) * PS + PK;    // 17 conv rows = pixel fragments
 constexpr int IPR = (CRY - 1) * CS + KH;    // 39 patch rows
-constexpr int IPC = (16 - 1) * CS + 8;      // 38 patch cols (idle lane 15 + zero-weight tap 7 stay in-row)
-constexpr int QPR = 11;                     // 4-pixel quads per patch row (44 px cover 41)
+// LDS patch column of input-patch column c is c + PCO: every pixel of the 11
+// loaded quads then has a slot (no range checks), the middle two pixels of a
+// quad form one aligned 16-byte store, and B-fragment rows stay 16-byte aligned
+constexpr int PCO = 4;
+constexpr int IPC = 46;                     // >= 4*QPR + PCO - 3 + 1 and >= (16-1)*CS + 8 + PCO; even
+constexpr int QPR = 11;                     // 4-pixel quads per patch row (44 px cover the 38 read)
 constexpr int NQUAD = IPR * QPR;            // 429
 constexpr int QPT = (NQUAD + 255) / 256;    // quads per thread (2)
-constexpr int PATCH_BYTES = IPR * IPC * 8;  // 11856
+constexpr int PATCH_BYTES = IPR * IPC * 8;  // 14352
 constexpr int HP_BYTES = CRY * PTX * 128;   // [conv row][pooled col][64 ch] fp16 = 15232
 constexpr int LDS = PATCH_BYTES + HP_BYTES;
 constexpr int NVP = (PTY / 2) * PTX * 8;    // vertical-pool items: 2 pooled rows x 1 col x 8 ch (224)
 static_assert(CRX <= 15, "one conv row per 16-lane fragment, lane 15 idle");
 static_assert(NVP <= 256, "one vertical-pool item per thread");
+static_assert(PCO >= 3 && 4 * (QPR - 1) + PCO < IPC, "every quad pixel has an LDS column");
+static_assert((16 - 1) * CS + 8 + PCO <= IPC, "B-fragment rows stay inside the patch row");
+static_assert(IPC % 2 == 0 && PCO % 2 == 0, "16-byte aligned B rows and middle-pair stores");
 constexpr int NIW = 2;                      // 16-cout A fragments per wave (of 4)
 constexpr int NCH = 4 / NIW;                // waves sharing each conv row
 constexpr int WGS_MAX = 4;                  // workgroups per CU the registers allow
@@ -66,7 +73,7 @@ __device__ __forceinline__ int hp_off(int r, int px, int c) { return (r * stem::
 
 struct StemGeom {
   int B, H, W, Hc, Wc, Hp, Wp, tiles_x, tiles_y, ntiles;
-  int ablate;   // profiling only (set_stem_ablation): 1 skip pool, 2 skip MFMAs, 4 skip patch normalise
+  int ablate;   // profiling only (set_stem_ablation): skip 1 pool, 2 MFMAs, 4 patch normalise, 8 conv epilogue, 16 patch loads
 };
 
 static int g_stem_ablate = 0;
@@ -160,16 +167,11 @@ __device__ __forceinline__ void store_patch(char* patch, const StemGeom& g, int 
       for (int j = 0; j < 4; ++j)
         if (!q.ok[k] || (unsigned)(x0 + j) >= (unsigned)g.W) px[j] = half4v{0, 0, 0, 0};
     }
-    // write pixel (t + lane) & 3 in step t: neighbouring lanes' 8-byte stores are
-    // then 40 B apart instead of 32 B, i.e. distinct bank pairs
-#pragma unroll
-    for (int t2 = 0; t2 < 4; ++t2) {
-      const int j = (t2 + tid) & 3;
-      const half4v o = j == 0 ? px[0] : (j == 1 ? px[1] : (j == 2 ? px[2] : px[3]));
-      const int c = 4 * qc + j - 3;                    // patch column of pixel j
-      if (c < 0 || c >= IPC) continue;
-      *reinterpret_cast<half4v*>(patch + (r * IPC + c) * 8) = o;
-    }
+    // pixel j -> LDS column 4qc + j - 3 + PCO: 8 + 16 + 8 bytes
+    char* d = patch + (r * IPC + 4 * qc + PCO - 3) * 8;
+    *reinterpret_cast<half4v*>(d) = px[0];
+    *reinterpret_cast<half8v*>(d + 8) = __builtin_shufflevector(px[1], px[2], 0, 1, 2, 3, 4, 5, 6, 7);
+    *reinterpret_cast<half4v*>(d + 24) = px[3];
   }
 }
 
@@ -236,7 +238,7 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
 
     // ---- conv GEMM, one conv row per fragment, round-robin over 4 waves ------
     for (int f = wave / NCH; f < CRY; f += 4 / NCH) {
-      const char* pb = patch + ((2 * f) * IPC + 2 * cx + 2 * fch) * 8;
+      const char* pb = patch + ((2 * f) * IPC + 2 * cx + 2 * fch + PCO) * 8;
       float4v acc[NIW];
 #pragma unroll
       for (int i = 0; i < NIW; ++i) acc[i] = float4v{0.f, 0.f, 0.f, 0.f};
@@ -252,6 +254,7 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
       // conv output is the pool's -inf padding (-65504); the 3-wide horizontal
       // max takes lanes cx+1, cx+2 of the same DPP row, on packed fp16 pairs
       // (VALU issue is this phase's cost: 4 cycles per wave instruction).
+      if (g.ablate & 8) continue;
       half4v o[NIW];
       if ((unsigned)(oy0 + f) < (unsigned)g.Hc) {          // wave-uniform
 #pragma unroll
@@ -259,8 +262,10 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
           half2v p0 = {(half_t)acc[i][0], (half_t)acc[i][1]};
           half2v p1 = {(half_t)acc[i][2], (half_t)acc[i][3]};
           if (!interior && !colv) p0 = p1 = half2v{(half_t)-65504.f, (half_t)-65504.f};
-          p0 = __builtin_elementwise_max(p0, __builtin_elementwise_max(row_shl_h2<1>(p0), row_shl_h2<2>(p0)));
-          p1 = __builtin_elementwise_max(p1, __builtin_elementwise_max(row_shl_h2<1>(p1), row_shl_h2<2>(p1)));
+          // llvm.maximum (NaN-propagating) lowers to one v_pk_maximum3_f16 and
+          // needs no canonicalising max(x, x) of the DPP results, unlike maxnum
+          p0 = __builtin_elementwise_maximum(p0, __builtin_elementwise_maximum(row_shl_h2<1>(p0), row_shl_h2<2>(p0)));
+          p1 = __builtin_elementwise_maximum(p1, __builtin_elementwise_maximum(row_shl_h2<1>(p1), row_shl_h2<2>(p1)));
           o[i] = half4v{p0[0], p0[1], p1[0], p1[1]};
         }
       } else {
@@ -280,7 +285,7 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
     if (tnext < g.ntiles) {
       if (!(g.ablate & 4)) store_patch(patch, g, tnext, tid, q);   // uses the quads prefetched one tile ago
       tn = tnext + gridDim.x;
-      if (tn < g.ntiles) load_quads(img, g, tn, tid, q);
+      if (tn < g.ntiles && !(g.ablate & 16)) load_quads(img, g, tn, tid, q);
     }
 
     // ---- vertical 3-max over conv rows 4*vpy2 .. 4*vpy2+4 -> 2 pooled rows ----
@@ -292,10 +297,10 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
       const half8v a3 = *reinterpret_cast<const half8v*>(hp + hp_off(r0 + 3, vpx, c8));
       const half8v a4 = *reinterpret_cast<const half8v*>(hp + hp_off(r0 + 4, vpx, c8));
       const half8v zero = {0, 0, 0, 0, 0, 0, 0, 0};
-      half8v lo = __builtin_elementwise_max(__builtin_elementwise_max(a0, a1), a2);
-      half8v hi = __builtin_elementwise_max(__builtin_elementwise_max(a2, a3), a4);
-      lo = __builtin_elementwise_max(lo + pb8, zero);
-      hi = __builtin_elementwise_max(hi + pb8, zero);
+      half8v lo = __builtin_elementwise_maximum(__builtin_elementwise_maximum(a0, a1), a2);
+      half8v hi = __builtin_elementwise_maximum(__builtin_elementwise_maximum(a2, a3), a4);
+      lo = __builtin_elementwise_maximum(lo + pb8, zero);
+      hi = __builtin_elementwise_maximum(hi + pb8, zero);
       const int ox = px0 + vpx, oy = py0 + 2 * vpy2;
       if (ox < g.Wp) {
         half_t* dst = y + (((size_t)b * g.Hp + oy) * g.Wp + ox) * 64 + c8 * 8;

@@ -18,7 +18,9 @@ def main():
     s = p.stem
     img = torch.randint(0, 256, (400, 224, 224, 3), dtype=torch.uint8, device="cuda")
     w, b = s.w.cuda(), s.b.cuda()
-    names = {0: "full", 1: "no pool", 2: "no MFMA", 4: "no patch normalise", 3: "no pool+MFMA", 7: "none (loads, sync)"}
+    names = {0: "full", 1: "no pool", 2: "no MFMA", 4: "no patch normalise", 8: "no conv epilogue",
+             16: "no patch loads", 3: "no pool+MFMA", 7: "no pool+MFMA+normalise", 15: "+ no epilogue",
+             31: "none (tile loop, barriers)"}
     for rnd in range(2):
         for mode, name in names.items():
             ext.set_stem_ablation(mode)
