@@ -145,6 +145,25 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
 
+  // residual of this tile -> registers before the ring's first DMA: untracked
+  // loads (common.h) older than every DMA, so the ring's counted vmcnt waits
+  // retire them long before the epilogue, whose own load would otherwise expose
+  // a full memory latency per tile (30 us of 138 on ResNet layer2 conv2,
+  // profiles/r1_v8_conv_big_sweep.log)
+  half4v rv[HAS_RES ? FN : 1][HAS_RES ? FM : 1];
+  if constexpr (HAS_RES) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int n = n0 + wn * TN + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int m = m0 + wm * TM + j * 16 + (lane & 15);
+        const size_t off = (m < a.M && n < a.Cout) ? (size_t)m * a.Cout + n : 0;
+        rv[i][j] = gload_b64_untracked(a.res + off);
+      }
+    }
+  }
+
   const int nK = a.nK;
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
@@ -200,6 +219,13 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
   }
 
   // ---- epilogue: bias (+residual) (+ReLU), NHWC store --------------------
+  if constexpr (HAS_RES) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (already retired by the ring's last wait)
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) reg_tie(rv[i][j]);
+  }
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
     const int n = n0 + wn * TN + i * 16 + (lane >> 4) * 4;
@@ -211,7 +237,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
       if (m >= a.M) continue;
       float4v v = acc[i][j] + bv;
       if constexpr (HAS_RES) {
-        const half4v r = *reinterpret_cast<const half4v*>(a.res + (size_t)m * a.Cout + n);
+        const half4v r = rv[i][j];
         v[0] += (float)r[0];
         v[1] += (float)r[1];
         v[2] += (float)r[2];
