@@ -49,6 +49,8 @@ void set_conv3x3_patch_default(bool on) { g_patch_default = on; }
 // kernel (tile 50, conv3x3_c64.hip): on by default since sweep r1 #6 (ResNet18
 // layer1 at B=400: 112 / 153 us vs 178 / 207 us for the best im2col tile,
 // profiles/r1_v6_layer1_c64.log).
+static int g_conv_ablate = 0;
+void set_conv_ablation(int mode) { g_conv_ablate = mode; }
 static bool g_c64_default = true;
 void set_conv3x3_c64_default(bool on) { g_c64_default = on; }
 
@@ -132,6 +134,7 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   a.M = (int)M;
   a.Kpad = Kpad;
   a.relu = relu ? 1 : 0;
+  a.ablate = g_conv_ablate;
   if (M == 0) return y;
   if (small) {
     const int t = (tile >= 0 && tile <= 3) ? (int)tile : conv_pick_tile(a.M, Cout);
@@ -426,6 +429,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pick_tile", &pick_tile, "tile id the conv heuristic picks for (M, Cout)");
   m.def("set_stem_workgroups_per_cu", &set_stem_workgroups_per_cu,
         "fused stem: persistent workgroups per CU (1-3, default 3)");
+  m.def("set_conv_ablation", &set_conv_ablation,
+        "profiling only: conv_glds epilogue ablation (1 skip stores, 2 skip residual loads); outputs are wrong");
   m.def("set_stem_ablation", &set_stem_ablation,
         "profiling only: 1 skip pool, 2 skip conv MFMAs, 4 skip patch normalise (wrong outputs)");
   m.def("set_conv3x3_c64_default", &set_conv3x3_c64_default,

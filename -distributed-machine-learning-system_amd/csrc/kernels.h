@@ -24,6 +24,7 @@ struct ConvArgs {
   int tiles_m;  // ceil(M / BM)
   const void* zero;  // >= 16 zero bytes (DMA source for padding taps)
   int ldx;           // conv_glds: input pixel stride in halfs (0: C); a K-slice of a wider row
+  int ablate;        // profiling only (set_conv_ablation), conv_glds: 1 skip epilogue stores, 2 skip residual loads
 };
 
 void conv_igemm_launch(ConvArgs a, bool small, bool out_f32, int tile, hipStream_t st);

@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
       for (int j = 0; j < FM; ++j) {
         const int m = m0 + wm * TM + j * 16 + (lane & 15);
         const size_t off = (m < a.M && n < a.Cout) ? (size_t)m * a.Cout + n : 0;
-        rv[i][j] = gload_b64_untracked(a.res + off);
+        rv[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : gload_b64_untracked(a.res + off);
       }
     }
   }
@@ -249,7 +249,9 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
         v[2] = fmaxf(v[2], 0.f);
         v[3] = fmaxf(v[3], 0.f);
       }
-      if constexpr (OUT_F32) {
+      if (a.ablate & 1) {
+        if (v[0] == 12345.f) *reinterpret_cast<float*>(a.y) = v[1] + v[2] + v[3];   // keep the math alive
+      } else if constexpr (OUT_F32) {
         *reinterpret_cast<float4v*>(static_cast<float*>(a.y) + (size_t)m * a.ldy + n) = v;
       } else {
         half4v o;
