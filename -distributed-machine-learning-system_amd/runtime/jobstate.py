@@ -20,12 +20,13 @@ Deliberate fixes:
 from __future__ import annotations
 
 import json
-import threading
 import time
 from collections import defaultdict, deque
 from dataclasses import dataclass
 
 import numpy as np
+
+from ..utils import racecheck
 
 WINDOW_S = 30.0  # reference SLIDING_WINDOW_SECONDS * SLIDING_WINDOW_FACTOR (10 * 3)
 
@@ -85,9 +86,13 @@ def _add_interval(ivs: list, s: int, e: int) -> int:
 
 
 class JobState:
+    # tables the race detector watches (all mutated only under self.lock)
+    _TABLES = ("worker_set", "working_vm_set", "results", "finished_images", "finished_queries",
+               "next_qnum", "jobs", "query_latency", "query_submit_time")
+
     def __init__(self, batchsize: dict | None = None, clock=time.time, window_s: float = WINDOW_S,
                  names: list[str] | None = None):
-        self.lock = threading.RLock()
+        self.lock = racecheck.make_lock("jobstate", reentrant=True)
         self.clock = clock
         self.window_s = window_s
         self.batchsize = dict(DEFAULT_BATCHSIZE, **(batchsize or {}))
@@ -108,6 +113,7 @@ class JobState:
         self.query_submit_time: dict = {}
         self.query_latency: dict = defaultdict(list)    # model -> [end-to-end seconds]
         self.jobs: dict = {}                            # job id -> {model, start, end, next}
+        racecheck.instrument(self, self._TABLES)
 
     # -- coordinator-side jobs (C28 variant), replicated to the standby ----------
     def add_job(self, model: str, start: int, end: int, bs: int | None = None) -> int:
@@ -307,7 +313,17 @@ class JobState:
                                                       float(np.percentile(a, 75)), float(a.std())]
 
     def images_done(self, model: str) -> int:
-        return int(self.finished_images.get(model, 0))
+        with self.lock:
+            return int(self.finished_images.get(model, 0))
+
+    def summary(self) -> dict:
+        """Consistent view for the ``summary`` stats request (one lock hold: the
+        tables are appended to by the result-ingest threads meanwhile)."""
+        with self.lock:
+            return {"ok": True, "done": {m: self.images_done(m) for m in self.models()},
+                    "pending": len(self.pending()),
+                    "latency": {m: list(v) for m, v in self.query_latency.items()},
+                    "finished_queries": dict(self.finished_queries)}
 
     def rates(self, model: str, now: float | None = None) -> dict:
         now = self.clock() if now is None else now
@@ -441,3 +457,4 @@ class JobState:
                 cur = self.jobs.get(j)
                 if cur is None or v["next"] > cur["next"]:
                     self.jobs[j] = dict(v)
+            racecheck.instrument(self, self._TABLES)

@@ -26,6 +26,7 @@ import logging
 import threading
 import time
 
+from ..utils import racecheck
 from .messages import Status_LEAVE, Status_RUNNING, Type
 
 log = logging.getLogger("idunno.membership")
@@ -39,7 +40,7 @@ class Membership:
         self.t = transport
         self.clock = clock
         self.wall = wall
-        self.lock = threading.RLock()
+        self.lock = racecheck.make_lock("membership", reentrant=True)
         self.members: dict[str, list] = {}
         self.master = master
         self.epoch = 0
@@ -54,6 +55,7 @@ class Membership:
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self.master_suspected = False
+        racecheck.instrument(self, ("members", "last_ack"), f"Membership[{name}]")
 
     # -- views ----------------------------------------------------------------
     def is_master(self) -> bool:

@@ -577,10 +577,7 @@ class Node:
         if v == "checkpoint":
             return {"ok": True, "path": self.save_checkpoint()}
         if v == "summary":
-            return {"ok": True, "done": {m: self.state.images_done(m) for m in self.state.models()},
-                    "pending": len(self.state.pending()),
-                    "latency": {m: list(v) for m, v in self.state.query_latency.items()},
-                    "finished_queries": dict(self.state.finished_queries)}
+            return self.state.summary()
         return {"ok": False, "error": f"unknown view {view}"}
 
     def local_grep(self, pattern: str) -> list[str]:

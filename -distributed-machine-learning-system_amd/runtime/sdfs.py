@@ -22,10 +22,10 @@ from __future__ import annotations
 import logging
 import os
 import re
-import threading
 import zlib
 from pathlib import Path
 
+from ..utils import racecheck
 from .messages import Type
 from .ring import file_neighbors
 
@@ -60,7 +60,7 @@ class SdfsStore:
     def __init__(self, root: str):
         self.root = Path(root)
         self.root.mkdir(parents=True, exist_ok=True)
-        self.lock = threading.Lock()
+        self.lock = racecheck.make_lock("sdfs.store")
 
     def _path(self, name: str, ver: int) -> Path:
         return self.root / f"{_safe(name)}.v{ver}"
@@ -127,10 +127,11 @@ class Sdfs:
     def __init__(self, node, store_root: str):
         self.node = node                       # the owning Node (name, transport, membership, cfg)
         self.store = SdfsStore(store_root)
-        self.lock = threading.RLock()
+        self.lock = racecheck.make_lock("sdfs", reentrant=True)
         # master metadata (reference sdfs_file_version / sdfs_file_process / sdfs_store_dict)
         self.file_version: dict[str, int] = {}
         self.file_replicas: dict[str, list[str]] = {}
+        racecheck.instrument(self, ("file_version", "file_replicas"), f"Sdfs[{node.name}]")
 
     # -- metadata (master) --------------------------------------------------------
     def store_dict(self) -> dict[str, list[str]]:

@@ -15,7 +15,9 @@ def test_job_submission_batched_by_coordinator():
         s = cl.wait_idle(10, {"alexnet": 1050})
         assert s["done"]["alexnet"] == 1050
         assert s["finished_queries"]["alexnet"] == 3
-        qs = c.coordinator().state.worker_set
+        st = c.coordinator().state
+        with st.lock:
+            qs = list(st.worker_set)
         assert sorted(q for (m, q) in qs if m == "alexnet") == [1, 2, 3]
     finally:
         c.stop()

@@ -45,6 +45,8 @@ def test_checkpoint_and_resume_after_full_restart(tmp_path):
         cl2 = c2.client()
         s = cl2.wait_idle(10, {"resnet18": 300})
         assert s["done"]["resnet18"] == 300
-        assert c2.coordinator().state.next_qnum["resnet18"] == 1   # same query, not re-submitted
+        st = c2.coordinator().state
+        with st.lock:
+            assert st.next_qnum["resnet18"] == 1   # same query, not re-submitted
     finally:
         c2.stop()
