@@ -43,7 +43,8 @@ def _torch_paths():
 
 
 def sources() -> list[Path]:
-    return sorted([*CSRC.rglob("*.hip"), *CSRC.rglob("*.cpp")])
+    # csrc/tests/ holds standalone host programs (sanitizer checks), not extension code
+    return sorted(p for p in [*CSRC.rglob("*.hip"), *CSRC.rglob("*.cpp")] if "tests" not in p.relative_to(CSRC).parts)
 
 
 def headers() -> list[Path]:

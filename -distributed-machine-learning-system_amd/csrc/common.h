@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tile_math.h"
+
 namespace idunno {
 
 typedef _Float16 half_t;
@@ -39,16 +41,6 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming
-// §5 "XCD swizzle must be bijective"): consecutive *logical* tiles land on
-// the same XCD so neighbouring tiles share that XCD's L2.
-__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
-  const int nxcd = 8;
-  if (nwg < nxcd * 2) return orig;
-  const int q = nwg / nxcd, r = nwg % nxcd;
-  const int xcd = orig % nxcd, idx = orig / nxcd;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-}
 
 // ---- LDS reads the compiler does not see ------------------------------------------
 // While a global_load_lds (LDS-DMA) is in flight, hipcc's wait-count pass puts

@@ -65,7 +65,6 @@ struct C64Args {
   int relu;
 };
 
-__device__ __forceinline__ int c64_swz(int row) { return row & 6; }
 
 // Patch DMA of tile t into dst: 8 patch rows per instruction, rows past the
 // patch or outside the image load the zero buffer.

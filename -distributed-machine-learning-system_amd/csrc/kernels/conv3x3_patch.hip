@@ -53,7 +53,6 @@ struct C3Args {
   int relu;
 };
 
-__device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
 
 template <bool HAS_RES>
 __global__ void __launch_bounds__(256, 2) conv3x3_patch_kernel(const C3Args a) {

@@ -30,7 +30,6 @@ typedef __attribute__((address_space(1))) void glb_void_b;
 
 // 128-byte rows: chunk slot XOR (row >> 1) & 7 (conflict-free for the
 // ds_read_b128 lane groups of a 16-row fragment, docs/KERNELS.md)
-__device__ __forceinline__ int big_swz(int row) { return (row >> 1) & 7; }
 
 template <int N>
 __device__ __forceinline__ void big_vmcnt() {
@@ -72,7 +71,7 @@ __global__ void __launch_bounds__(64 * WN * WM, WN * WM / 4 * MINB) conv_big_ker
   for (int j = 0; j < GA; ++j) {
     const int row = (wave + NW * j) * 8 + lrow;
     const int n = n0 + row;
-    a_src[j] = n < a.Cout ? a.w + (size_t)n * a.Kpad + ((lslot ^ big_swz(row)) << 3) : nullptr;
+    a_src[j] = n < a.Cout ? a.w + (size_t)n * a.Kpad + ((lslot ^ swz8(row)) << 3) : nullptr;
   }
   // B (pixels) DMA sources: image base + top-left input coordinate per instruction
   int b_base[GB], b_ih0[GB], b_iw0[GB];
@@ -80,7 +79,7 @@ __global__ void __launch_bounds__(64 * WN * WM, WN * WM / 4 * MINB) conv_big_ker
   for (int j = 0; j < GB; ++j) {
     const int row = (wave + NW * j) * 8 + lrow;
     const int m = m0 + row;
-    const int ch = (lslot ^ big_swz(row)) << 3;
+    const int ch = (lslot ^ swz8(row)) << 3;
     if (m < a.M) {
       const int hw = a.Ho * a.Wo;
       const int b = m / hw, r = m - b * hw;
@@ -133,12 +132,12 @@ __global__ void __launch_bounds__(64 * WN * WM, WN * WM / 4 * MINB) conv_big_ker
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
       const int row = wn * TN + i * 16 + frow;
-      fa[i] = lds_read_b128(base + row * 128 + ((ch ^ big_swz(row)) << 4));
+      fa[i] = lds_read_b128(base + row * 128 + ((ch ^ swz8(row)) << 4));
     }
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
       const int row = wm * TM + j * 16 + frow;
-      fb[j] = lds_read_b128(base + A_BYTES + row * 128 + ((ch ^ big_swz(row)) << 4));
+      fb[j] = lds_read_b128(base + A_BYTES + row * 128 + ((ch ^ swz8(row)) << 4));
     }
   };
 

@@ -23,11 +23,6 @@ namespace idunno {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
-__device__ __forceinline__ int swz_r(int row, int cpr) {
-  if (cpr == 8) return (row >> 1) & 7;
-  const int q = (row >> 2) & 3;
-  return (0x78 >> (2 * q)) & 3;
-}
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {

@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--kill-coordinator-at-frac", type=float, default=0.0,
                     help="kill the coordinator once this fraction of both jobs' images is done")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--reference-pacing", action="store_true",
+                    help="the reference's sleeps: 20 s between a job's queries (:1109), 3 s before each "
+                         "chunk (:594), for apples-to-apples query latency (SURVEY.md §7.2 step 7)")
     ap.add_argument("--watchdog", type=float, default=0.0,
                     help="dump every thread's stack and exit after this many seconds (hang diagnosis)")
     a = ap.parse_args()
@@ -70,6 +73,8 @@ def main():
     c = LocalCluster(num_nodes=a.nodes, transport="tcp", base_port=free_base(a.nodes), executor_factory=exf,
                      source_factory=srcf, heartbeat_period_s=0.3, failure_timeout_s=2.0,
                      metadata_period_s=0.5, rpc_timeout_s=30.0).start()
+    if a.reference_pacing:        # after the cluster is up: the warm-up below runs unpaced
+        pacing = dict(client_query_interval_s=20.0, worker_start_delay_s=3.0)
     out = {"nodes": a.nodes, "gpus": ngpu, "executor": a.executor, "images_per_job": a.images}
     try:
         cl = c.client(c.cfg.node_name(a.nodes - 2))
@@ -79,6 +84,10 @@ def main():
         cl.wait_idle(600)
         coord = c.coordinator()
         base = {m: coord.state.images_done(m) for m in ("alexnet", "resnet18")}
+        if a.reference_pacing:
+            for k, v in pacing.items():     # every node reads the cluster's one config object
+                setattr(c.cfg, k, v)
+            out["pacing"] = pacing
         t0 = time.perf_counter()
         ta = cl.submit_job(0, a.images - 1, "alexnet")
         t_second = time.perf_counter()
@@ -110,7 +119,7 @@ def main():
                 t_log = time.perf_counter()
                 print(f"[{t_log - t0:7.1f}s] done {s['done']} pending {s['pending']} "
                       f"coordinator {c.coordinator().name}", file=sys.stderr, flush=True)
-                if t_log - t0 > 20:                     # stalled: per-query image coverage
+                if t_log - t0 > (20 if not a.reference_pacing else 600):   # stalled: per-query image coverage
                     st = c.coordinator().state
                     with st.lock:
                         for (m, q), ents in sorted(st.worker_set.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
