@@ -155,7 +155,7 @@ def _bench_pattern_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])      # 8: the driver's full-node bench topology
 def test_bench_round_pattern_over_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
