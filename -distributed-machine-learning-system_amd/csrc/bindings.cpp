@@ -181,6 +181,88 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   return y;
 }
 
+// fp32 (reference precision) conv: y = act(conv(x, w) + bias (+ res)), all f32.
+//   x   : [B, H, W, C] f32 NHWC, C == 4 (RGB+0 stem) or C % 16 == 0
+//   w   : [Cout, Kpad] f32: big (kh, kw, c), Kpad = KH*KW*C;
+//         small (kh, tap, c4) with taps padded to ceil(KW/4)*4, Kpad = KH*ceil(KW/4)*16
+torch::Tensor conv2d_nhwc_f32(torch::Tensor x, torch::Tensor w, torch::Tensor bias, c10::optional<torch::Tensor> res,
+                              int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool relu, int64_t tile,
+                              c10::optional<torch::Tensor> out) {
+  CHECK_DEV(x);
+  CHECK_DEV(w);
+  CHECK_DEV(bias);
+  CHECK_CONTIG(x);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(bias);
+  CHECK_DT(x, torch::kFloat);
+  CHECK_DT(w, torch::kFloat);
+  CHECK_DT(bias, torch::kFloat);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 2 && bias.dim() == 1, "bad ranks");
+  TORCH_CHECK(w.device() == x.device() && bias.device() == x.device(), "operands on different devices");
+  TORCH_CHECK(KH >= 1 && KW >= 1 && stride >= 1 && pad >= 0, "bad conv geometry");
+  const int B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Cout = w.size(0), Kpad = w.size(1);
+  TORCH_CHECK(bias.size(0) == Cout, "bias/Cout mismatch");
+  TORCH_CHECK(Cout % 4 == 0, "Cout must be a multiple of 4");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty output");
+  const bool small = (C == 4);
+  ConvF32Args a{};
+  if (small) {
+    a.nsub = (KW + 3) / 4;
+    TORCH_CHECK(Kpad == KH * a.nsub * 16, "small-C f32 weight must be [Cout, KH*ceil(KW/4)*16]");
+  } else {
+    TORCH_CHECK(C % 16 == 0, "C must be 4 or a multiple of 16, got ", C);
+    TORCH_CHECK(Kpad == KH * KW * C, "weight must be [Cout, KH*KW*C]");
+    a.nsub = 1;
+  }
+  const long M = (long)B * Ho * Wo;
+  TORCH_CHECK(M < (1L << 31) && (long)B * H * W * C < (1L << 31) && M * Cout < (1L << 40),
+              "tensor too large for int32 indexing");
+  torch::Tensor y;
+  if (out.has_value() && out->defined()) {
+    y = *out;
+    CHECK_DEV(y);
+    CHECK_CONTIG(y);
+    CHECK_DT(y, torch::kFloat);
+    TORCH_CHECK(y.device() == x.device(), "out must live on the input's device");
+    TORCH_CHECK(y.dim() == 4 && y.size(0) == B && y.size(1) == Ho && y.size(2) == Wo && y.size(3) == Cout,
+                "out shape mismatch");
+  } else {
+    y = torch::empty({B, Ho, Wo, Cout}, x.options());
+  }
+  const float* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    auto& r = *res;
+    CHECK_DEV(r);
+    CHECK_CONTIG(r);
+    CHECK_DT(r, torch::kFloat);
+    TORCH_CHECK(r.device() == x.device(), "residual on a different device");
+    TORCH_CHECK(r.dim() == 4 && r.size(0) == B && r.size(1) == Ho && r.size(2) == Wo && r.size(3) == Cout,
+                "residual shape mismatch");
+    rp = r.data_ptr<float>();
+  }
+  a.x = x.data_ptr<float>();
+  a.w = w.data_ptr<float>();
+  a.bias = bias.data_ptr<float>();
+  a.res = rp;
+  a.y = y.data_ptr<float>();
+  a.B = B; a.H = H; a.W = W; a.C = C;
+  a.Ho = Ho; a.Wo = Wo; a.Cout = Cout; a.ldy = Cout;
+  a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
+  a.M = (int)M;
+  a.Kpad = Kpad;
+  a.relu = relu ? 1 : 0;
+  if (M == 0) return y;
+  a.zero = zero_buffer(x.device()).data_ptr();
+  const int t = tile >= 0 ? (int)tile : conv_f32_pick(a.M, Cout, C);
+  TORCH_CHECK(conv_f32_launch(a, small, t, cur_stream()), "unknown / unsupported f32 conv tile id ", t);
+  check_launch("conv_f32");
+  return y;
+}
+
+int64_t pick_tile_f32(int64_t M, int64_t Cout, int64_t C) { return conv_f32_pick((int)M, (int)Cout, (int)C); }
+
 // Per-device fp32 zeros (the bias of split-K partial GEMMs), grown on demand,
 // never freed (same reasoning as zero_buffer).
 static torch::Tensor zero_f32(const torch::Device& dev, int64_t n) {
@@ -309,7 +391,7 @@ torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias,
 }
 
 torch::Tensor preprocess(torch::Tensor img, c10::optional<torch::Tensor> start, int64_t batch, int64_t start_offset,
-                         int64_t window, int64_t sub) {
+                         int64_t window, int64_t sub, bool f32) {
   CHECK_DEV(img);
   CHECK_CONTIG(img);
   CHECK_DT(img, torch::kUInt8);
@@ -317,11 +399,17 @@ torch::Tensor preprocess(torch::Tensor img, c10::optional<torch::Tensor> start, 
   int B;
   long long max_start;
   const long long* sp = window_args(img, start, batch, window, sub, B, max_start);
-  auto out = torch::empty({B, img.size(1), img.size(2), 4}, img.options().dtype(torch::kHalf));
+  auto out = torch::empty({B, img.size(1), img.size(2), 4}, img.options().dtype(f32 ? torch::kFloat : torch::kHalf));
   const long npix = (long)B * img.size(1) * img.size(2);
-  if (npix)
-    preprocess_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), npix, sp, start_offset, max_start, sp ? sub : 0,
-                      (long)img.size(1) * img.size(2), cur_stream()); check_launch("preprocess");
+  if (!npix) return out;
+  if (f32) {
+    preprocess_f32_launch(img.data_ptr<uint8_t>(), out.data_ptr<float>(), npix, sp, start_offset, max_start,
+                          sp ? sub : 0, (long)img.size(1) * img.size(2), cur_stream());
+    check_launch("preprocess_f32");
+    return out;
+  }
+  preprocess_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), npix, sp, start_offset, max_start, sp ? sub : 0,
+                    (long)img.size(1) * img.size(2), cur_stream()); check_launch("preprocess");
   return out;
 }
 
@@ -349,27 +437,41 @@ torch::Tensor resize_crop(torch::Tensor img, int64_t resize, int64_t crop) {
 torch::Tensor maxpool2d_nhwc(torch::Tensor x, int64_t k, int64_t s, int64_t pad) {
   CHECK_DEV(x);
   CHECK_CONTIG(x);
-  CHECK_DT(x, torch::kHalf);
-  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "x must be [B,H,W,C] with C % 8 == 0");
+  const bool f32 = x.scalar_type() == torch::kFloat;
+  TORCH_CHECK(f32 || x.scalar_type() == torch::kHalf, "x must be fp16 or fp32");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % (f32 ? 4 : 8) == 0, "x must be [B,H,W,C] with C % 8 (fp16) / 4 (fp32) == 0");
   TORCH_CHECK(k >= 1 && s >= 1 && pad >= 0 && 2 * pad <= k, "bad pool geometry");
   const int B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int Ho = (H + 2 * pad - k) / s + 1, Wo = (W + 2 * pad - k) / s + 1;
   TORCH_CHECK(Ho > 0 && Wo > 0, "empty output");
   auto y = torch::empty({B, Ho, Wo, C}, x.options());
-  if (B) maxpool_launch(reinterpret_cast<const half_t*>(x.data_ptr()), reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, C,
-                        Ho, Wo, k, s, pad, cur_stream()); check_launch("maxpool");
+  if (!B) return y;
+  if (f32) {
+    maxpool_f32_launch(x.data_ptr<float>(), y.data_ptr<float>(), B, H, W, C, Ho, Wo, k, s, pad, cur_stream());
+    check_launch("maxpool_f32");
+    return y;
+  }
+  maxpool_launch(reinterpret_cast<const half_t*>(x.data_ptr()), reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, C,
+                 Ho, Wo, k, s, pad, cur_stream()); check_launch("maxpool");
   return y;
 }
 
 torch::Tensor global_avgpool_nhwc(torch::Tensor x) {
   CHECK_DEV(x);
   CHECK_CONTIG(x);
-  CHECK_DT(x, torch::kHalf);
-  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "x must be [B,H,W,C] with C % 8 == 0");
+  const bool f32 = x.scalar_type() == torch::kFloat;
+  TORCH_CHECK(f32 || x.scalar_type() == torch::kHalf, "x must be fp16 or fp32");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % (f32 ? 4 : 8) == 0, "x must be [B,H,W,C] with C % 8 (fp16) / 4 (fp32) == 0");
   const int B = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
   auto y = torch::empty({B, C}, x.options());
-  if (B) avgpool_launch(reinterpret_cast<const half_t*>(x.data_ptr()), reinterpret_cast<half_t*>(y.data_ptr()), B, HW, C,
-                        cur_stream()); check_launch("avgpool");
+  if (!B) return y;
+  if (f32) {
+    avgpool_f32_launch(x.data_ptr<float>(), y.data_ptr<float>(), B, HW, C, cur_stream());
+    check_launch("avgpool_f32");
+    return y;
+  }
+  avgpool_launch(reinterpret_cast<const half_t*>(x.data_ptr()), reinterpret_cast<half_t*>(y.data_ptr()), B, HW, C,
+                 cur_stream()); check_launch("avgpool");
   return y;
 }
 
@@ -414,9 +516,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("relu"), py::arg("out_f32") = false, py::arg("tile") = -1, py::arg("out") = py::none());
   m.def("linear_splitk", &linear_splitk, "FC layer with split-K partial GEMMs + combine", py::arg("x"),
         py::arg("w"), py::arg("bias"), py::arg("relu"), py::arg("out_f32"), py::arg("splits"), py::arg("tile") = -1);
-  m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 NHWC4", py::arg("img"),
+  m.def("conv2d_nhwc_f32", &conv2d_nhwc_f32, "fp32 implicit-GEMM conv on f32 MFMA + bias (+res) (+relu)",
+        py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
+        py::arg("pad"), py::arg("relu"), py::arg("tile") = -1, py::arg("out") = py::none());
+  m.def("pick_tile_f32", &pick_tile_f32, "tile id the f32 conv heuristic picks for (M, Cout, C)");
+  m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 (or fp32) NHWC4", py::arg("img"),
         py::arg("start") = py::none(), py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1,
-        py::arg("sub") = 0);
+        py::arg("sub") = 0, py::arg("f32") = false);
   m.def("stem_fused", &stem_fused, "fused normalise + conv7x7/2 + bias + relu + maxpool3x3/2 (ResNet stem)",
         py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("start") = py::none(), py::arg("batch") = -1,
         py::arg("start_offset") = 0, py::arg("window") = -1, py::arg("sub") = 0);

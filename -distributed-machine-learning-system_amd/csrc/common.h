@@ -68,6 +68,15 @@ __device__ __forceinline__ void lds_waitcnt() {
 
 __device__ __forceinline__ void lds_tie(half8v& r) { asm volatile("" : "+v"(r)); }
 
+// fp32 flavour (conv_f32.hip): 4 consecutive f32 of one LDS row per lane
+__device__ __forceinline__ float4v lds_read_f4(uint32_t addr) {
+  float4v v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+
+__device__ __forceinline__ void lds_tie(float4v& r) { asm volatile("" : "+v"(r)); }
+
 // 8-byte global load the wait-count pass does not track (same reason as above:
 // a tracked load beside an LDS-DMA prefetch gets a vmcnt(0) at its first use).
 // The caller retires it with an explicit counted `s_waitcnt vmcnt(N)`.
@@ -85,5 +94,6 @@ __device__ __forceinline__ float4v gload_f4_untracked(const void* p) {
 }
 
 __device__ __forceinline__ void reg_tie(half4v& r) { asm volatile("" : "+v"(r)); }
+__device__ __forceinline__ void reg_tie(float4v& r) { asm volatile("" : "+v"(r)); }
 
 }  // namespace idunno

@@ -27,6 +27,36 @@ struct ConvArgs {
   int ablate;        // profiling only (set_conv_ablation), conv_glds: 1 skip epilogue stores, 2 skip residual loads
 };
 
+// fp32 (reference-precision) conv: same geometry fields as ConvArgs, f32 tensors.
+struct ConvF32Args {
+  const float* x;      // NHWC [B][H][W][C]  (C == 4: RGB+0 stem input)
+  const float* w;      // [Cout][Kpad]: big (kh, kw, c); small (kh, tap(nsub*4), c4)
+  const float* bias;   // [Cout]
+  const float* res;    // NHWC [B][Ho][Wo][Cout] or nullptr
+  float* y;            // NHWC [B][Ho][Wo][ldy]
+  int B, H, W, C;
+  int Ho, Wo, Cout, ldy;
+  int KH, KW, stride, pad;
+  int M;               // B*Ho*Wo
+  int nK;              // K stages (set by the launcher)
+  int cblk;            // big: C / BK; small: tap blocks per kh row (set by the launcher)
+  int nsub;            // small: ceil(KW / 4)
+  int Kpad;
+  int relu;
+  int tiles_n, tiles_m;
+  const void* zero;    // >= 16 zero bytes
+  int ldx;             // input pixel stride in floats (0: C)
+};
+
+bool conv_f32_launch(ConvF32Args a, bool small, int tile, hipStream_t st);   // false: unknown tile id
+int conv_f32_pick(int M, int Cout, int C);
+void preprocess_f32_launch(const uint8_t* img, float* out, long npix, const long long* start_idx,
+                           long long start_off, long long max_start, long long sub, long pix_per_img,
+                           hipStream_t st);
+void maxpool_f32_launch(const float* x, float* y, int B, int H, int W, int C, int Ho, int Wo, int k, int s,
+                        int pad, hipStream_t st);
+void avgpool_f32_launch(const float* x, float* y, int B, int HW, int C, hipStream_t st);
+
 void conv_igemm_launch(ConvArgs a, bool small, bool out_f32, int tile, hipStream_t st);
 int conv_pick_tile(int M, int Cout);
 bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);

@@ -1,0 +1,133 @@
+// fp32 companions of conv_f32.hip (the reference-precision path):
+//   * preprocess_f32  uint8 HWC -> normalised fp32 NHWC4 (4th channel 0), the
+//                     reference's ToTensor + Normalize (alexnet_resnet.py:57-62)
+//   * maxpool_f32     NHWC max pool, 4 channels (16 B) per lane
+//   * avgpool_f32     NHWC global average pool -> [B][C] fp32
+// The arithmetic is the same as the fp16 kernels in elementwise.hip, kept in f32.
+#include "../kernels.h"
+
+namespace idunno {
+
+__constant__ float kMeanF[3] = {0.485f, 0.456f, 0.406f};
+__constant__ float kStdF[3] = {0.229f, 0.224f, 0.225f};
+
+__device__ __forceinline__ float4v norm_px_f32(uint32_t b0, uint32_t b1, uint32_t b2) {
+  // (x/255 - mean)/std with a true division, as torchvision's Normalize
+  float4v o;
+  o[0] = ((float)b0 / 255.f - kMeanF[0]) / kStdF[0];
+  o[1] = ((float)b1 / 255.f - kMeanF[1]) / kStdF[1];
+  o[2] = ((float)b2 / 255.f - kMeanF[2]) / kStdF[2];
+  o[3] = 0.f;
+  return o;
+}
+
+// Four pixels per thread: 12 bytes in, 64 bytes (four 16-byte stores) out.
+__global__ void preprocess_f32_kernel(const uint8_t* __restrict__ img, float* __restrict__ out, long npix,
+                                      const long long* __restrict__ start_idx, long long start_off,
+                                      long long max_start, long long sub, long pix_per_img) {
+  const long p = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (p >= npix) return;
+  if (start_idx != nullptr) {
+    long long s0 = *start_idx - start_off;
+    s0 = (s0 < 0 ? 0 : (s0 > max_start ? max_start : s0)) + sub;
+    img += (size_t)s0 * pix_per_img * 3;
+  }
+  const uint8_t* s = img + p * 3;
+  float4v* d = reinterpret_cast<float4v*>(out + p * 4);
+  if (p + 4 <= npix && (reinterpret_cast<uintptr_t>(s) & 3) == 0) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(s);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    d[0] = norm_px_f32(w0 & 255u, (w0 >> 8) & 255u, (w0 >> 16) & 255u);
+    d[1] = norm_px_f32(w0 >> 24, w1 & 255u, (w1 >> 8) & 255u);
+    d[2] = norm_px_f32((w1 >> 16) & 255u, w1 >> 24, w2 & 255u);
+    d[3] = norm_px_f32((w2 >> 8) & 255u, (w2 >> 16) & 255u, w2 >> 24);
+    return;
+  }
+  const int n = (int)(npix - p < 4 ? npix - p : 4);
+  for (int i = 0; i < n; ++i) d[i] = norm_px_f32(s[3 * i], s[3 * i + 1], s[3 * i + 2]);
+}
+
+void preprocess_f32_launch(const uint8_t* img, float* out, long npix, const long long* start_idx,
+                           long long start_off, long long max_start, long long sub, long pix_per_img,
+                           hipStream_t st) {
+  const int bs = 256;
+  const long grid = ((npix + 3) / 4 + bs - 1) / bs;
+  hipLaunchKernelGGL(preprocess_f32_kernel, dim3((unsigned)grid), dim3(bs), 0, st, img, out, npix, start_idx,
+                     start_off, max_start, sub, pix_per_img);
+}
+
+// NHWC max pool, C % 4 == 0: one thread = 4 channels of one output pixel.
+__global__ void maxpool_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int H, int W,
+                                   int C, int Ho, int Wo, int k, int s, int pad) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cv = C / 4;
+  const long total = (long)B * Ho * Wo * cv;
+  if (t >= total) return;
+  const int c4 = (int)(t % cv);
+  long pix = t / cv;
+  const int ow = (int)(pix % Wo);
+  pix /= Wo;
+  const int oh = (int)(pix % Ho);
+  const int b = (int)(pix / Ho);
+  float4v m = float4v{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  const int ih0 = oh * s - pad, iw0 = ow * s - pad;
+  for (int dy = 0; dy < k; ++dy) {
+    const int ih = ih0 + dy;
+    if ((unsigned)ih >= (unsigned)H) continue;
+    for (int dx = 0; dx < k; ++dx) {
+      const int iw = iw0 + dx;
+      if ((unsigned)iw >= (unsigned)W) continue;
+      const float4v v = *reinterpret_cast<const float4v*>(x + (((size_t)b * H + ih) * W + iw) * C + c4 * 4);
+      m[0] = fmaxf(m[0], v[0]);
+      m[1] = fmaxf(m[1], v[1]);
+      m[2] = fmaxf(m[2], v[2]);
+      m[3] = fmaxf(m[3], v[3]);
+    }
+  }
+  *reinterpret_cast<float4v*>(y + (size_t)t * 4) = m;
+}
+
+void maxpool_f32_launch(const float* x, float* y, int B, int H, int W, int C, int Ho, int Wo, int k, int s,
+                        int pad, hipStream_t st) {
+  const long total = (long)B * Ho * Wo * (C / 4);
+  const int bs = 256;
+  hipLaunchKernelGGL(maxpool_f32_kernel, dim3((unsigned)((total + bs - 1) / bs)), dim3(bs), 0, st, x, y, B, H, W,
+                     C, Ho, Wo, k, s, pad);
+}
+
+// NHWC global average pool -> [B][C] fp32.  One 256-thread workgroup per
+// image; thread (g, c4) sums pixels g, g+G, ... of 4-channel chunk c4, the G
+// partial sums meet in LDS (same decomposition as the fp16 avgpool_kernel).
+__global__ void __launch_bounds__(256) avgpool_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int B,
+                                                          int HW, int C) {
+  __shared__ float4v part[256];
+  const int b = blockIdx.x;
+  const int cv = C / 4;
+  const float* p = x + (size_t)b * HW * C;
+  const float inv = 1.f / (float)HW;
+  if (cv >= 256) {
+    for (int c4 = threadIdx.x; c4 < cv; c4 += 256) {
+      float4v acc = float4v{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < HW; ++i) acc += *reinterpret_cast<const float4v*>(p + (size_t)i * C + c4 * 4);
+      *reinterpret_cast<float4v*>(y + (size_t)b * C + c4 * 4) = acc * inv;
+    }
+    return;
+  }
+  const int G = 256 / cv;
+  const int c4 = threadIdx.x % cv, g = threadIdx.x / cv;
+  float4v acc = float4v{0.f, 0.f, 0.f, 0.f};
+  if (g < G)
+    for (int i = g; i < HW; i += G) acc += *reinterpret_cast<const float4v*>(p + (size_t)i * C + c4 * 4);
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  if (g == 0) {
+    for (int k = 1; k < G; ++k) acc += part[k * cv + c4];
+    *reinterpret_cast<float4v*>(y + (size_t)b * C + c4 * 4) = acc * inv;
+  }
+}
+
+void avgpool_f32_launch(const float* x, float* y, int B, int HW, int C, hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_f32_kernel, dim3((unsigned)B), dim3(256), 0, st, x, y, B, HW, C);
+}
+
+}  // namespace idunno

@@ -30,7 +30,7 @@ from . import reference as ref
 
 @dataclass
 class Conv:
-    w: torch.Tensor          # packed [Cout, Kpad] fp16
+    w: torch.Tensor          # packed [Cout, Kpad] fp16 (fp32 for dtype "fp32" programs)
     b: torch.Tensor          # [Cout] fp32
     cin: int
     cout: int
@@ -69,12 +69,13 @@ class Program:
     features: list = field(default_factory=list)  # alexnet: ("conv", Conv) | ("pool", (k, s, p))
     fcs: list = field(default_factory=list)       # list[Conv] as 1x1 convs (last -> fp32 logits)
     num_classes: int = 1000
+    dtype: str = "fp16"       # activation / weight precision: "fp16" | "fp32" (reference precision)
 
     def to(self, device):
         p = Program(self.name, self.kind, self.stem.to(device) if self.stem else None,
                     [b.to(device) for b in self.blocks],
                     [(k, v.to(device) if k == "conv" else v) for k, v in self.features],
-                    [f.to(device) for f in self.fcs], self.num_classes)
+                    [f.to(device) for f in self.fcs], self.num_classes, self.dtype)
         return p
 
     def param_bytes(self) -> int:
@@ -112,9 +113,28 @@ def fold_bn(w: torch.Tensor, b: torch.Tensor | None, bn: nn.BatchNorm2d | None):
     return w.float(), b.float()
 
 
-def pack_conv_weight(w: torch.Tensor) -> tuple[torch.Tensor, bool]:
-    """[Cout, Cin, KH, KW] fp32 -> packed fp16 [Cout, Kpad], small flag."""
+DTYPES = ("fp16", "fp32")
+
+
+def pack_conv_weight(w: torch.Tensor, dtype: str = "fp16") -> tuple[torch.Tensor, bool]:
+    """[Cout, Cin, KH, KW] fp32 -> packed [Cout, Kpad], small flag.
+
+    fp16: small (Cin <= 4) rows are 8 taps x 4 channels (K stage of the f16
+    kernels); big rows (kh, kw, c) with Cin % 64 == 0.
+    fp32: small rows are 4 taps x 4 channels (one BK=16 stage of conv_f32.hip);
+    big rows (kh, kw, c) with Cin % 16 == 0."""
     cout, cin, kh, kw = w.shape
+    if dtype == "fp32":
+        if cin <= 4:
+            nsub = (kw + 3) // 4
+            p = torch.zeros(cout, kh, nsub * 4, 4, dtype=torch.float32)
+            p[:, :, :kw, :cin] = w.permute(0, 2, 3, 1)
+            return p.reshape(cout, kh * nsub * 16).contiguous(), True
+        if cin % 16 != 0:
+            raise ValueError(f"Cin={cin} unsupported (need 3/4 or a multiple of 16)")
+        return w.permute(0, 2, 3, 1).reshape(cout, kh * kw * cin).float().contiguous(), False
+    if dtype != "fp16":
+        raise ValueError(f"dtype must be one of {DTYPES}, got {dtype!r}")
     if cin <= 4:
         nsub = (kw + 7) // 8
         p = torch.zeros(cout, kh, nsub * 8, 4, dtype=torch.float32)
@@ -129,54 +149,58 @@ def unpack_conv_weight(c: Conv) -> torch.Tensor:
     """Inverse of pack_conv_weight -> fp32 [Cout, Cin, KH, KW]."""
     w = c.w.float()
     if c.small:
-        nsub = (c.kw + 7) // 8
-        return w.view(c.cout, c.kh, nsub * 8, 4)[:, :, :c.kw, :c.cin].permute(0, 3, 1, 2).contiguous()
+        tpr = 4 if c.w.dtype == torch.float32 else 8        # taps per K row (see pack_conv_weight)
+        nsub = (c.kw + tpr - 1) // tpr
+        return w.view(c.cout, c.kh, nsub * tpr, 4)[:, :, :c.kw, :c.cin].permute(0, 3, 1, 2).contiguous()
     return w.view(c.cout, c.kh, c.kw, c.cin).permute(0, 3, 1, 2).contiguous()
 
 
-def make_conv(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, relu: bool) -> Conv:
+def make_conv(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, relu: bool, dtype: str = "fp16") -> Conv:
     w, b = fold_bn(conv.weight, conv.bias, bn)
-    pw, small = pack_conv_weight(w)
+    pw, small = pack_conv_weight(w, dtype)
     return Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, conv.kernel_size[0],
                 conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small)
 
 
-def make_fc(lin: nn.Linear, relu: bool, perm: torch.Tensor | None = None) -> Conv:
+def make_fc(lin: nn.Linear, relu: bool, perm: torch.Tensor | None = None, dtype: str = "fp16") -> Conv:
     w = lin.weight.detach().float()
     if perm is not None:
         w = w[:, perm]
     k = w.shape[1]
     if k % 64 != 0:
         raise ValueError(f"FC in_features={k} must be a multiple of 64")
-    return Conv(w.half().contiguous(), lin.bias.detach().float().contiguous(), k, w.shape[0], 1, 1, 1,
+    return Conv((w if dtype == "fp32" else w.half()).contiguous(), lin.bias.detach().float().contiguous(), k, w.shape[0], 1, 1, 1,
                 0, relu, False)
 
 
-def compile_model(m: nn.Module, name: str) -> Program:
+def compile_model(m: nn.Module, name: str, dtype: str = "fp16") -> Program:
+    if dtype not in DTYPES:
+        raise ValueError(f"dtype must be one of {DTYPES}, got {dtype!r}")
     m = m.eval()
+    dt = dtype
     if isinstance(m, ref.ResNet):
-        p = Program(name, "resnet", stem=make_conv(m.conv1, m.bn1, True))
+        p = Program(name, "resnet", stem=make_conv(m.conv1, m.bn1, True, dt), dtype=dt)
         for li in range(1, 5):
             for blk in getattr(m, f"layer{li}"):
-                down = make_conv(blk.downsample[0], blk.downsample[1], False) if blk.downsample else None
+                down = make_conv(blk.downsample[0], blk.downsample[1], False, dt) if blk.downsample else None
                 if isinstance(blk, ref.BasicBlock):
-                    convs = [make_conv(blk.conv1, blk.bn1, True), make_conv(blk.conv2, blk.bn2, True)]
+                    convs = [make_conv(blk.conv1, blk.bn1, True, dt), make_conv(blk.conv2, blk.bn2, True, dt)]
                 else:
-                    convs = [make_conv(blk.conv1, blk.bn1, True), make_conv(blk.conv2, blk.bn2, True),
-                             make_conv(blk.conv3, blk.bn3, True)]
+                    convs = [make_conv(blk.conv1, blk.bn1, True, dt), make_conv(blk.conv2, blk.bn2, True, dt),
+                             make_conv(blk.conv3, blk.bn3, True, dt)]
                 p.blocks.append(Block(convs, down))
-        p.fcs = [make_fc(m.fc, False)]
+        p.fcs = [make_fc(m.fc, False, dtype=dt)]
         p.num_classes = m.fc.out_features
         return p
     if isinstance(m, ref.AlexNet):
-        p = Program(name, "alexnet")
+        p = Program(name, "alexnet", dtype=dt)
         mods = list(m.features)
         i = 0
         while i < len(mods):
             mod = mods[i]
             if isinstance(mod, nn.Conv2d):
                 relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
-                p.features.append(("conv", make_conv(mod, None, relu)))
+                p.features.append(("conv", make_conv(mod, None, relu, dt)))
                 i += 2 if relu else 1
                 continue
             if isinstance(mod, nn.MaxPool2d):
@@ -186,15 +210,16 @@ def compile_model(m: nn.Module, name: str) -> Program:
         c, hw = 256, 36
         perm = torch.arange(c * hw).view(c, hw).t().reshape(-1)
         lins = [mm for mm in m.classifier if isinstance(mm, nn.Linear)]
-        p.fcs = [make_fc(lins[0], True, perm), make_fc(lins[1], True), make_fc(lins[2], False)]
+        p.fcs = [make_fc(lins[0], True, perm, dt), make_fc(lins[1], True, dtype=dt),
+                 make_fc(lins[2], False, dtype=dt)]
         p.num_classes = lins[2].out_features
         return p
     raise TypeError(f"cannot compile {type(m).__name__}")
 
 
-def build_program(name: str, seed: int = 0, randomize_bn: bool = False) -> Program:
+def build_program(name: str, seed: int = 0, randomize_bn: bool = False, dtype: str = "fp16") -> Program:
     name = ref.canonical(name)
-    return compile_model(ref.build(name, seed=seed, randomize_bn=randomize_bn), name)
+    return compile_model(ref.build(name, seed=seed, randomize_bn=randomize_bn), name, dtype)
 
 
 # ---------------------------------------------------------------------------
@@ -275,6 +300,8 @@ class HipRunner:
         native = tuple(img_u8.shape[1:3]) == (224, 224)
         if start is not None and not native:
             raise ValueError("device-side windows need 224x224 shards")
+        if p.dtype == "fp32":
+            return self._logits_f32(img_u8, start, batch, start_offset, native)
         s = p.stem
         fused = (self.fuse_stem and native and p.kind == "resnet" and s.small and s.kh == 7 and s.kw == 7
                  and s.stride == 2 and s.pad == 3 and s.cout == 64)
@@ -305,6 +332,31 @@ class HipRunner:
         for i, fc in enumerate(p.fcs):
             last = i == len(p.fcs) - 1
             x = o.linear(x, fc.w, fc.b, relu=fc.relu, out_f32=last)
+        return x
+
+    def _logits_f32(self, img_u8, start, batch, start_offset, native):
+        """Reference-precision forward: every activation, weight and product in
+        fp32 (conv_f32.hip on the f32-input MFMA, elementwise_f32.hip)."""
+        o, p = self.ops, self.p
+        if not native:
+            raise ValueError("the fp32 path takes 224x224 inputs (resize on host first)")
+        x = o.preprocess(img_u8, start, batch, start_offset, f32=True)
+        if p.kind == "resnet":
+            s = p.stem
+            x = o.conv2d(x, s.w, s.b, s.kh, s.kw, s.stride, s.pad, s.relu)
+            x = o.maxpool2d(x, 3, 2, 1)
+            for blk in p.blocks:
+                x = self._block(blk, x)
+            x = o.global_avgpool(x)
+        else:
+            for k, v in p.features:
+                if k == "conv":
+                    x = o.conv2d(x, v.w, v.b, v.kh, v.kw, v.stride, v.pad, v.relu)
+                else:
+                    x = o.maxpool2d(x, *v)
+            x = x.reshape(x.shape[0], -1)
+        for fc in p.fcs:
+            x = o.linear(x, fc.w, fc.b, relu=fc.relu)
         return x
 
     def _block(self, blk, x, out=None):

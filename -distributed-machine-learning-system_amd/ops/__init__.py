@@ -17,7 +17,14 @@ __all__ = [
 def conv2d(x, w, bias, kh: int, kw: int, stride: int, pad: int, relu: bool,
            residual=None, out_f32: bool = False, tile: int = -1, out=None):
     """Implicit-GEMM MFMA convolution with fused bias / residual / ReLU
-    (into ``out`` when given: a contiguous NHWC tensor, e.g. a batch slice)."""
+    (into ``out`` when given: a contiguous NHWC tensor, e.g. a batch slice).
+
+    fp16 activations -> f16 MFMA kernels (f32 accumulate); fp32 activations
+    -> the reference-precision kernel on the f32-input MFMA (conv_f32.hip)."""
+    import torch
+
+    if x.dtype == torch.float32:
+        return load().conv2d_nhwc_f32(x, w, bias, residual, kh, kw, stride, pad, relu, tile, out)
     return load().conv2d_nhwc(x, w, bias, residual, kh, kw, stride, pad, relu, out_f32, tile, out)
 
 
@@ -34,6 +41,9 @@ def linear(x, w, bias, relu: bool = False, out_f32: bool = False, splits: int | 
     with ``splits`` > 1 as split-K partial GEMMs + one combine kernel."""
     b, k = x.shape
     n = w.shape[0]
+    if x.dtype.is_floating_point and x.element_size() == 4:
+        y = load().conv2d_nhwc_f32(x.view(b, 1, 1, k), w, bias, None, 1, 1, 1, 0, relu, -1, None)
+        return y.view(b, n)
     if splits is None:
         splits = LINEAR_SPLITS
     if splits > 1:
@@ -42,14 +52,15 @@ def linear(x, w, bias, relu: bool = False, out_f32: bool = False, splits: int | 
     return y.view(b, n)
 
 
-def preprocess(img_u8, start=None, batch: int = -1, start_offset: int = 0, window: int = -1, sub: int = 0):
-    """uint8 [B,H,W,3] -> normalised fp16 [B,H,W,4] (4th channel zero).
+def preprocess(img_u8, start=None, batch: int = -1, start_offset: int = 0, window: int = -1, sub: int = 0,
+               f32: bool = False):
+    """uint8 [B,H,W,3] -> normalised fp16 (``f32``: fp32) [B,H,W,4] (4th channel zero).
     With ``start`` (int64 GPU scalar) and ``batch``, reads images
     [*start - start_offset, ... + batch) of the shard ``img_u8`` (device-side
     window; ``start`` may be a global image index and ``start_offset`` the
     shard's first global index).  A window of ``window`` images may be done
     in parts: this call covers images [sub, sub + batch) of it."""
-    return load().preprocess(img_u8, start, batch, start_offset, window, sub)
+    return load().preprocess(img_u8, start, batch, start_offset, window, sub, f32)
 
 
 def resize_crop(img_u8, resize: int = 256, crop: int = 224):
@@ -81,6 +92,10 @@ def softmax_top1(logits, packed=None):
 
 def pick_tile(m: int, cout: int) -> int:
     return int(load().pick_tile(m, cout))
+
+
+def pick_tile_f32(m: int, cout: int, cin: int) -> int:
+    return int(load().pick_tile_f32(m, cout, cin))
 
 
 def synth_images(seed: int, start: int, n: int, device, hw: int = 224):

@@ -44,12 +44,13 @@ class Env:
         return self.world > 1
 
 
-def init_from_env(backend: str | None = None, timeout_s: float = 300.0) -> Env:
-    """Initialise the default process group from torchrun-style env vars."""
+def init_from_env(backend: str | None = None, timeout_s: float = 300.0, cpu: bool = False) -> Env:
+    """Initialise the default process group from torchrun-style env vars
+    (``cpu``: stay off the GPU even where one exists -- gloo dry runs)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    gpu = torch.cuda.is_available()
+    gpu = not cpu and torch.cuda.is_available()
     if gpu:
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)

@@ -1,0 +1,58 @@
+"""bench.py contract on the CPU: self-launch of N rank processes (no torchrun),
+gloo collectives, weak + strong scaling keys, and non-zero exit when a rank
+dies (VERDICT r1 "Next round" item 1)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args, timeout=240):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", *args],
+                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def _line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out       # exactly one JSON line (rank 0)
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [1, 2, 8])
+def test_bench_self_launch_dry_run(n):
+    steps, warmup = 3, 1
+    r = _run("--gpus", str(n), "--steps", str(steps), "--warmup", str(warmup))
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == n
+    assert d["config"]["parallelism"] == f"dp{n}"
+    assert d["config"]["global_batch"] == 400 * n
+    assert d["steps"] == steps and d["warmup"] == warmup
+    assert d["scaling"] == "weak" and d["higher_is_better"] is True
+    # warmup + timed + >= 5 unloaded latency rounds, 400 images per GPU each
+    assert d["results_recorded"] == (warmup + steps + 5) * 400 * n
+    assert d["strong_chunk_per_gpu"] == -(-400 // n)
+    assert d["images_per_s_strong"] > 0 and d["p50_query_latency_strong_s"] > 0
+    for k in ("metric", "value", "unit", "ms_per_step", "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+
+
+def test_bench_rank_failure_exits_nonzero():
+    r = _run("--gpus", "2", "--steps", "3", "--warmup", "1", "--fail-rank", "1")
+    assert r.returncode != 0
+    assert "failing on purpose" in r.stderr
+
+
+def test_bench_world_mismatch_is_an_error():
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--gpus", "2"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+    assert "WORLD_SIZE" in r.stdout

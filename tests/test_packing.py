@@ -63,3 +63,36 @@ def test_concurrent_builds_give_identical_weights():
         t.join()
     for sd in out[1:]:
         assert all(torch.equal(sd[k], out[0][k]) for k in out[0])
+
+
+@pytest.mark.parametrize("name", ["resnet18", "alexnet"])
+def test_fp32_program_is_exact_fold_of_reference(name):
+    """dtype "fp32": weights stay fp32 (no rounding), so the emulated packed
+    program matches the module to fp32 folding error only."""
+    m = ref.build(name, seed=2, randomize_bn=True)
+    p = packed.compile_model(m, name, dtype="fp32")
+    assert p.dtype == "fp32"
+    assert all(c.w.dtype == torch.float32 for c in p.all_convs())
+    torch.manual_seed(1)
+    img = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        r = m(ref.preprocess_u8(img))
+    e = packed.emulate(p, img)
+    assert (r - e).abs().max().item() < 1e-4 * r.abs().max().item()
+
+
+def test_pack_unpack_roundtrip_fp32():
+    for shape in [(64, 3, 7, 7), (64, 3, 11, 11), (12, 3, 5, 5), (128, 64, 3, 3), (20, 48, 3, 3)]:
+        w = torch.randn(*shape)
+        pw, small = packed.pack_conv_weight(w, "fp32")
+        assert pw.dtype == torch.float32
+        c = packed.Conv(pw, torch.zeros(shape[0]), shape[1], shape[0], shape[2], shape[3], 1, 0, False, small)
+        assert small == (shape[1] == 3)
+        assert torch.equal(packed.unpack_conv_weight(c), w)
+    # small-C rows are 4 taps x 4 channels: kw 7 -> 8 taps, 11 -> 12 taps
+    assert packed.pack_conv_weight(torch.randn(64, 3, 7, 7), "fp32")[0].shape == (64, 7 * 2 * 16)
+    assert packed.pack_conv_weight(torch.randn(64, 3, 11, 11), "fp32")[0].shape == (64, 11 * 3 * 16)
+    with pytest.raises(ValueError):
+        packed.pack_conv_weight(torch.randn(8, 20, 3, 3), "fp32")
+    with pytest.raises(ValueError):
+        packed.pack_conv_weight(torch.randn(8, 64, 3, 3), "bf8")
