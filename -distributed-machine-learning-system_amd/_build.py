@@ -6,6 +6,11 @@ compiled to an object under ``build/`` and linked into ``_C.so`` next to this
 file, so the built library travels with the repository snapshot to the GPU box.
 
 Usage: ``python -m idunno._build [--force] [-j N]``.
+
+``IDUNNO_EXPERIMENTAL=1`` also builds the non-default experimental conv loops
+(``csrc/kernels/experimental/``: conv_big, conv_pers, conv3x3_patch; kept for
+A/B sweeps, never selected by the default tile heuristics) and defines
+``IDUNNO_EXPERIMENTAL`` for the bindings.
 """
 from __future__ import annotations
 
@@ -42,9 +47,16 @@ def _torch_paths():
     return incs, torch_lib, abi
 
 
+def experimental() -> bool:
+    return os.environ.get("IDUNNO_EXPERIMENTAL", "0") not in ("", "0")
+
+
 def sources() -> list[Path]:
-    # csrc/tests/ holds standalone host programs (sanitizer checks), not extension code
-    return sorted(p for p in [*CSRC.rglob("*.hip"), *CSRC.rglob("*.cpp")] if "tests" not in p.relative_to(CSRC).parts)
+    # csrc/tests/ holds standalone host programs (sanitizer checks), not extension code;
+    # csrc/kernels/experimental/ only with IDUNNO_EXPERIMENTAL=1
+    skip = {"tests"} if experimental() else {"tests", "experimental"}
+    return sorted(p for p in [*CSRC.rglob("*.hip"), *CSRC.rglob("*.cpp")]
+                  if not skip & set(p.relative_to(CSRC).parts))
 
 
 def headers() -> list[Path]:
@@ -59,13 +71,24 @@ def _compile_cmd(src: Path, obj: Path, incs, abi) -> list[str]:
         "-Wno-unused-result", "-Wno-deprecated-declarations",
         f"-I{sysconfig.get_paths()['include']}", f"-I{CSRC}",
     ]
+    if experimental():
+        cmd.append("-DIDUNNO_EXPERIMENTAL=1")
     cmd += [f"-I{i}" for i in incs]
     cmd += ["-c", str(src), "-o", str(obj)]
     return cmd
 
 
+FLAGS = BUILD / "flags.txt"
+
+
+def _flags() -> str:
+    return f"experimental={int(experimental())}"
+
+
 def needs_build(force: bool = False) -> bool:
     if force or not TARGET.exists():
+        return True
+    if not FLAGS.exists() or FLAGS.read_text() != _flags():
         return True
     t = TARGET.stat().st_mtime
     return any(p.stat().st_mtime > t for p in [*sources(), *headers(), Path(__file__)])
@@ -77,6 +100,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         return TARGET
     incs, torch_lib, abi = _torch_paths()
     BUILD.mkdir(parents=True, exist_ok=True)
+    if not FLAGS.exists() or FLAGS.read_text() != _flags():
+        force = True                       # a build-flag change recompiles everything
     hdr_mtime = max([p.stat().st_mtime for p in headers()] + [Path(__file__).stat().st_mtime])
     objs, todo = [], []
     for src in sources():
@@ -109,6 +134,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
     os.replace(str(TARGET) + ".tmp", TARGET)
+    FLAGS.write_text(_flags())
     return TARGET
 
 

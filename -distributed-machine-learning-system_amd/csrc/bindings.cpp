@@ -40,11 +40,21 @@ static torch::Tensor zero_buffer(const torch::Device& dev) {
   return b;
 }
 
+#ifdef IDUNNO_EXPERIMENTAL
 // Whether auto tile selection routes 3x3/s1 convs to the LDS-patch kernel
 // (set_conv3x3_patch_default from Python; off until the per-layer sweep says so).
 static bool g_patch_default = false;
 static bool conv3x3_patch_default() { return g_patch_default; }
 void set_conv3x3_patch_default(bool on) { g_patch_default = on; }
+#endif
+// Whether the experimental conv loops (conv_big / conv_pers / conv3x3_patch) are built in.
+bool has_experimental() {
+#ifdef IDUNNO_EXPERIMENTAL
+  return true;
+#else
+  return false;
+#endif
+}
 // Whether auto tile selection routes 3x3/s1 64->64 convs to the resident-weight
 // kernel (tile 50, conv3x3_c64.hip): on by default since sweep r1 #6 (ResNet18
 // layer1 at B=400: 112 / 153 us vs 178 / 207 us for the best im2col tile,
@@ -146,6 +156,7 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     return y;
   }
   a.zero = zero_buffer(x.device()).data_ptr();
+#ifdef IDUNNO_EXPERIMENTAL
   const bool patch_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 &&
                         conv3x3_patch_supported(H, W, C, Cout);
   if (tile == 40 || (tile < 0 && patch_ok && conv3x3_patch_default())) {
@@ -154,6 +165,7 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
                          a.relu, cur_stream()); check_launch("conv3x3_patch");
     return y;
   }
+#endif
   const bool c64_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 && conv3x3_c64_supported(C, Cout);
   if (tile == 50 || (tile < 0 && c64_ok && g_c64_default)) {
     TORCH_CHECK(c64_ok, "tile 50 (resident-weight 3x3 64->64 conv) does not support this shape");
@@ -162,6 +174,7 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     return y;
   }
   const int t = tile >= 10 ? (int)tile : conv_glds_pick(a.M, Cout);
+#ifdef IDUNNO_EXPERIMENTAL
   if (t >= 70 && t < 80) {             // persistent loop (conv_pers.hip); 1-stage convs fall back to tile 65
     if (conv_pers_launch(a, out_f32, t, cur_stream())) {
       check_launch("conv_pers");
@@ -176,6 +189,7 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     check_launch("conv_big");
     return y;
   }
+#endif
   TORCH_CHECK(conv_glds_launch(a, out_f32, t, cur_stream()), "unknown conv tile id ", t);
   check_launch("conv_glds");
   return y;
@@ -255,13 +269,15 @@ torch::Tensor conv2d_nhwc_f32(torch::Tensor x, torch::Tensor w, torch::Tensor bi
   a.relu = relu ? 1 : 0;
   if (M == 0) return y;
   a.zero = zero_buffer(x.device()).data_ptr();
-  const int t = tile >= 0 ? (int)tile : conv_f32_pick(a.M, Cout, C);
+  const int t = tile >= 0 ? (int)tile : conv_f32_pick(a.M, Cout, Kpad, small);
   TORCH_CHECK(conv_f32_launch(a, small, t, cur_stream()), "unknown / unsupported f32 conv tile id ", t);
   check_launch("conv_f32");
   return y;
 }
 
-int64_t pick_tile_f32(int64_t M, int64_t Cout, int64_t C) { return conv_f32_pick((int)M, (int)Cout, (int)C); }
+int64_t pick_tile_f32(int64_t M, int64_t Cout, int64_t K, bool small) {
+  return conv_f32_pick((int)M, (int)Cout, (int)K, small);
+}
 
 // Per-device fp32 zeros (the bias of split-K partial GEMMs), grown on demand,
 // never freed (same reasoning as zero_buffer).
@@ -519,7 +535,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_nhwc_f32", &conv2d_nhwc_f32, "fp32 implicit-GEMM conv on f32 MFMA + bias (+res) (+relu)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("tile") = -1, py::arg("out") = py::none());
-  m.def("pick_tile_f32", &pick_tile_f32, "tile id the f32 conv heuristic picks for (M, Cout, C)");
+  m.def("pick_tile_f32", &pick_tile_f32, "tile id the f32 conv heuristic picks for (M, Cout, K, small)");
   m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 (or fp32) NHWC4", py::arg("img"),
         py::arg("start") = py::none(), py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1,
         py::arg("sub") = 0, py::arg("f32") = false);
@@ -541,6 +557,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "profiling only: 1 skip pool, 2 skip conv MFMAs, 4 skip patch normalise (wrong outputs)");
   m.def("set_conv3x3_c64_default", &set_conv3x3_c64_default,
         "route auto-tiled 3x3/s1 64->64 convs to the resident-weight kernel (tile 50)");
+#ifdef IDUNNO_EXPERIMENTAL
   m.def("set_conv3x3_patch_default", &set_conv3x3_patch_default,
         "route auto-tiled 3x3/s1 convs to the LDS-patch kernel (tile 40)");
+#endif
+  m.def("has_experimental", &has_experimental, "experimental conv loops built in (IDUNNO_EXPERIMENTAL=1)");
 }

@@ -49,7 +49,7 @@ struct ConvF32Args {
 };
 
 bool conv_f32_launch(ConvF32Args a, bool small, int tile, hipStream_t st);   // false: unknown tile id
-int conv_f32_pick(int M, int Cout, int C);
+int conv_f32_pick(int M, int Cout, int K, bool small);
 void preprocess_f32_launch(const uint8_t* img, float* out, long npix, const long long* start_idx,
                            long long start_off, long long max_start, long long sub, long pix_per_img,
                            hipStream_t st);

@@ -29,6 +29,7 @@
 // run (register double buffer), so LDS latency hides behind MFMA issue.
 // LDS = 72 KiB weights + 2 x 43 KiB patch buffers = 158 KiB (1 workgroup/CU).
 #include "../kernels.h"
+#include "../launch_util.h"
 
 namespace idunno {
 
@@ -305,17 +306,10 @@ void conv3x3_c64_launch(const half_t* x, const half_t* w, const float* bias, con
   a.tiles_x = (W + TW - 1) / TW;
   a.tiles_y = (H + TH - 1) / TH;
   a.ntiles = B * a.tiles_x * a.tiles_y;
-  static int cus = 0;
-  if (!cus) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_c64_kernel<true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_c64_kernel<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
-  }
+  // LDS opt-in and CU count per (kernel, device), thread-safe (launch_util.h)
+  ensure_lds_attr(reinterpret_cast<const void*>(&conv3x3_c64_kernel<true>), LDS);
+  ensure_lds_attr(reinterpret_cast<const void*>(&conv3x3_c64_kernel<false>), LDS);
+  const int cus = device_cu_count();
   const int grid = a.ntiles < cus ? a.ntiles : cus;   // persistent, one workgroup per CU
   if (res)
     hipLaunchKernelGGL(conv3x3_c64_kernel<true>, dim3(grid), dim3(64 * NW), LDS, st, a);

@@ -323,14 +323,16 @@ bool conv_f32_launch(ConvF32Args a, bool small, int tile, hipStream_t st) {
   return res ? f32_dispatch<true, false>(a, tile, st) : f32_dispatch<false, false>(a, tile, st);
 }
 
-// Default tile per (M, Cout): enough blocks to cover 256 CUs at least twice,
-// else the next smaller tile (first guess; tools/bench_layers.py --dtype fp32
-// sweeps the table on hardware).
-int conv_f32_pick(int M, int Cout, int C) {
+// Default tile per (M, Cout, K = KH*KW*C), from the per-layer sweep on MI355X
+// (tools/bench_layers_f32.py, profiles/r2_v1_layers_f32.md): 64x128 for the RGB
+// stems (K <= 4*...: C == 4), 64x64 for short-K 1x1 convs (prologue-bound),
+// 64x256 for Cout 64, 128x128 where it fills >= 4 waves of 256 CUs, else 128x64.
+int conv_f32_pick(int M, int Cout, int K, bool small) {
   const long tiles128 = (long)((M + 127) / 128) * ((Cout + 127) / 128);
+  if (small) return 105;
+  if (K <= 256) return 107;
   if (Cout <= 64) return M >= 256 * 256 ? 102 : 105;
-  if (Cout % 256 == 0 && tiles128 >= 4 * 512) return 104;
-  if (tiles128 >= 512) return 100;
+  if (tiles128 >= 1024) return 100;
   return 103;
 }
 

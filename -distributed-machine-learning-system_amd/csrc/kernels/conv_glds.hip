@@ -17,6 +17,7 @@
 // fragment read uses the same XOR (rule 21).  Out-of-image taps (padding) and
 // rows past M / Cout load from a 16-byte zero buffer instead of branching.
 #include "../kernels.h"
+#include "../launch_util.h"
 
 namespace idunno {
 
@@ -269,12 +270,7 @@ static void glds_cfg(ConvArgs a, hipStream_t st) {
   const int grid = a.tiles_n * a.tiles_m;
   const size_t lds = (size_t)NS * (BN + BM) * BK * 2;
   auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    attr = true;
-  }
+  ensure_lds_attr(reinterpret_cast<const void*>(kern), (int)lds);   // per (kernel, device), launch_util.h
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WN * WM), lds, st, a);
 }
 

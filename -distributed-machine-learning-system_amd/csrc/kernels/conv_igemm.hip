@@ -30,6 +30,7 @@
 // ds_read_b128 fragment reads are bank-conflict free (derivation in
 // docs/KERNELS.md).
 #include "../kernels.h"
+#include "../launch_util.h"
 
 namespace idunno {
 
@@ -248,13 +249,9 @@ static void launch_cfg(ConvArgs a, hipStream_t st) {
   a.tiles_m = (a.M + BM - 1) / BM;
   const int grid = a.tiles_n * a.tiles_m;
   const size_t lds = 2 * (size_t)(BN + BM) * BK * 2;
-  static bool attr_set = false;   // >64 KiB dynamic LDS needs an explicit opt-in
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv_igemm_kernel<BN, BM, BK, WN, WM, SMALL, HAS_RES, OUT_F32>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
-  }
+  // >64 KiB dynamic LDS needs an explicit opt-in, per (kernel, device): launch_util.h
+  ensure_lds_attr(reinterpret_cast<const void*>(&conv_igemm_kernel<BN, BM, BK, WN, WM, SMALL, HAS_RES, OUT_F32>),
+                  (int)lds);
   hipLaunchKernelGGL((conv_igemm_kernel<BN, BM, BK, WN, WM, SMALL, HAS_RES, OUT_F32>), dim3(grid),
                      dim3(256), lds, st, a);
 }

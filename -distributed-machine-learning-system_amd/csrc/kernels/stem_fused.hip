@@ -25,6 +25,7 @@
 //     vertically (5 LDS rows per two pooled rows) with 16-byte stores.
 // Bias + ReLU are applied after the max (both commute with it).
 #include "../kernels.h"
+#include "../launch_util.h"
 
 namespace idunno {
 
@@ -330,12 +331,7 @@ void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, h
   g.tiles_y = (g.Hp + PTY - 1) / PTY;
   g.ntiles = B * g.tiles_x * g.tiles_y;
   g.ablate = g_stem_ablate;
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  }
+  const int ncu = device_cu_count();   // per device (launch_util.h)
   const int per = g_stem_wgs * ncu;   // persistent: g_stem_wgs workgroups per CU
   const int grid = g.ntiles < per ? g.ntiles : per;
   hipLaunchKernelGGL(stem_fused_kernel, dim3(grid), dim3(256), LDS, st, img, w, bias, y, g, start_idx, start_off,

@@ -1,6 +1,7 @@
 """Functional wrappers around the gfx950 HIP kernels (``idunno._C``).
 
-Tensors are NHWC fp16 activations on the current GPU.  Every function runs on
+Tensors are NHWC fp16 (or, for the reference-precision path, fp32) activations
+on the current GPU.  Every function runs on
 PyTorch's current HIP stream, so sequences of these ops can be captured into a
 hipGraph with ``torch.cuda.graph``.
 """
@@ -10,7 +11,7 @@ from ._ext import available, load, so_path
 
 __all__ = [
     "available", "load", "so_path", "conv2d", "linear", "preprocess", "resize_crop",
-    "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile", "synth_images",
+    "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile", "pick_tile_f32", "synth_images", "stem_fused",
 ]
 
 
@@ -38,10 +39,13 @@ LINEAR_SPLITS: int = 1
 
 def linear(x, w, bias, relu: bool = False, out_f32: bool = False, splits: int | None = None):
     """y = x @ w.T + bias: the conv kernel as a 1x1 conv on a 1x1 image, or
-    with ``splits`` > 1 as split-K partial GEMMs + one combine kernel."""
+    with ``splits`` > 1 as split-K partial GEMMs + one combine kernel
+    (fp32 ``x``: the f32 conv kernel, fp32 out)."""
+    import torch
+
     b, k = x.shape
     n = w.shape[0]
-    if x.dtype.is_floating_point and x.element_size() == 4:
+    if x.dtype == torch.float32:
         y = load().conv2d_nhwc_f32(x.view(b, 1, 1, k), w, bias, None, 1, 1, 1, 0, relu, -1, None)
         return y.view(b, n)
     if splits is None:
@@ -94,8 +98,9 @@ def pick_tile(m: int, cout: int) -> int:
     return int(load().pick_tile(m, cout))
 
 
-def pick_tile_f32(m: int, cout: int, cin: int) -> int:
-    return int(load().pick_tile_f32(m, cout, cin))
+def pick_tile_f32(m: int, cout: int, k: int, small: bool = False) -> int:
+    """Default fp32 tile for an implicit GEMM of M pixels x Cout x K (= KH*KW*C)."""
+    return int(load().pick_tile_f32(m, cout, k, small))
 
 
 def synth_images(seed: int, start: int, n: int, device, hw: int = 224):
