@@ -275,6 +275,54 @@ torch::Tensor conv2d_nhwc_f32(torch::Tensor x, torch::Tensor w, torch::Tensor bi
   return y;
 }
 
+// fp32 Winograd F(2x2,3x3) conv (3x3 / stride 1 / pad 1): x [B,H,W,C] f32 NHWC,
+// u [16, Cout, C] f32 (= G g G^T, models/packed.py wino_weight), y = act(conv + bias (+ res)).
+torch::Tensor conv2d_wino_f32(torch::Tensor x, torch::Tensor u, torch::Tensor bias, c10::optional<torch::Tensor> res,
+                              bool relu, int64_t variant) {
+  CHECK_DEV(x);
+  CHECK_DEV(u);
+  CHECK_DEV(bias);
+  CHECK_CONTIG(x);
+  CHECK_CONTIG(u);
+  CHECK_CONTIG(bias);
+  CHECK_DT(x, torch::kFloat);
+  CHECK_DT(u, torch::kFloat);
+  CHECK_DT(bias, torch::kFloat);
+  TORCH_CHECK(u.device() == x.device() && bias.device() == x.device(), "operands on different devices");
+  TORCH_CHECK(x.dim() == 4 && u.dim() == 3 && u.size(0) == 16 && bias.dim() == 1, "bad ranks / U must be [16, Cout, C]");
+  const int B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Cout = u.size(1);
+  TORCH_CHECK(u.size(2) == C && bias.size(0) == Cout, "U / bias shape mismatch");
+  TORCH_CHECK(C % 16 == 0 && Cout % 32 == 0, "winograd conv needs C % 16 == 0 and Cout % 32 == 0");
+  TORCH_CHECK(conv_wino_f32_supported(H, W, C, Cout), "winograd conv: unsupported image size");
+  TORCH_CHECK((long)B * H * W * std::max(C, Cout) < (1L << 31), "tensor too large for int32 indexing");
+  auto y = torch::empty({B, H, W, Cout}, x.options());
+  const float* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    auto& r = *res;
+    CHECK_DEV(r);
+    CHECK_CONTIG(r);
+    CHECK_DT(r, torch::kFloat);
+    TORCH_CHECK(r.device() == x.device(), "residual on a different device");
+    TORCH_CHECK(r.dim() == 4 && r.size(0) == B && r.size(1) == H && r.size(2) == W && r.size(3) == Cout,
+                "residual shape mismatch");
+    rp = r.data_ptr<float>();
+  }
+  if (B == 0) return y;
+  WinoArgs a{};
+  a.x = x.data_ptr<float>();
+  a.u = u.data_ptr<float>();
+  a.bias = bias.data_ptr<float>();
+  a.res = rp;
+  a.y = y.data_ptr<float>();
+  a.zero = zero_buffer(x.device()).data_ptr();
+  a.B = B; a.H = H; a.W = W; a.C = C; a.Cout = Cout;
+  a.relu = relu ? 1 : 0;
+  TORCH_CHECK(conv_wino_f32_launch(a, (int)variant, cur_stream()), "winograd conv launch rejected the shape");
+  check_launch("conv_wino_f32");
+  return y;
+}
+
 int64_t pick_tile_f32(int64_t M, int64_t Cout, int64_t K, bool small) {
   return conv_f32_pick((int)M, (int)Cout, (int)K, small);
 }
@@ -535,6 +583,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_nhwc_f32", &conv2d_nhwc_f32, "fp32 implicit-GEMM conv on f32 MFMA + bias (+res) (+relu)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("tile") = -1, py::arg("out") = py::none());
+  m.def("conv2d_wino_f32", &conv2d_wino_f32, "fp32 Winograd F(2x2,3x3) conv (3x3/s1/p1) + bias (+res) (+relu)",
+        py::arg("x"), py::arg("u"), py::arg("bias"), py::arg("res"), py::arg("relu"), py::arg("variant") = 0);
+  m.def("wino_supported", &conv_wino_f32_supported, "winograd conv geometry fits (H, W, C, Cout)");
   m.def("pick_tile_f32", &pick_tile_f32, "tile id the f32 conv heuristic picks for (M, Cout, K, small)");
   m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 (or fp32) NHWC4", py::arg("img"),
         py::arg("start") = py::none(), py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1,

@@ -49,6 +49,26 @@ struct ConvF32Args {
 };
 
 bool conv_f32_launch(ConvF32Args a, bool small, int tile, hipStream_t st);   // false: unknown tile id
+
+// fp32 Winograd F(2x2,3x3) conv (3x3, stride 1, pad 1), conv_wino_f32.hip.
+struct WinoArgs {
+  const float* x;      // NHWC [B][H][W][C]
+  const float* u;      // [16][Cout][C]: U = G g G^T per (e, cout, cin)
+  const float* bias;   // [Cout]
+  const float* res;    // NHWC [B][H][W][Cout] or nullptr
+  float* y;            // NHWC [B][H][W][Cout]
+  const void* zero;    // >= 16 zero bytes
+  int B, H, W, C, Cout;
+  int relu;
+  // block geometry (set by the launcher)
+  int TX, TY;          // 2x2 tiles per row / column
+  int IMG, R, bpi;     // images per block, tile rows per block, blocks per image
+  int RIN, NP;         // staged input rows per image, pixels per column-parity half row
+  int raw_ins;         // 1 KiB DMA instructions of the staged input region
+  int nblk_t, nblk_n;  // tile blocks, 32-channel output blocks
+};
+bool conv_wino_f32_launch(WinoArgs a, int variant, hipStream_t st);   // false: shape unsupported
+bool conv_wino_f32_supported(int H, int W, int C, int Cout);
 int conv_f32_pick(int M, int Cout, int K, bool small);
 void preprocess_f32_launch(const uint8_t* img, float* out, long npix, const long long* start_idx,
                            long long start_off, long long max_start, long long sub, long pix_per_img,

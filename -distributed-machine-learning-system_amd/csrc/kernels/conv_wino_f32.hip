@@ -1,0 +1,327 @@
+// fp32 3x3 / stride-1 / pad-1 convolution by Winograd F(2x2, 3x3), fully fused
+// (input transform -> 16 GEMMs on the f32-input MFMA -> output transform ->
+// bias / residual / ReLU) in ONE kernel.  All arithmetic is fp32: this is the
+// algorithm cuDNN / MIOpen use for fp32 3x3 convs, here written for gfx950.
+//
+// Why: the fp32 direct conv (conv_f32.hip) already runs at ~120 TF/s, i.e. at
+// the f32-MFMA roofline (157 TF peak, 1/16 of f16), on every ResNet 3x3 layer
+// (profiles/r2_v1_layers_f32.md).  The only way past that roofline at fp32 is
+// fewer multiplications: F(2x2,3x3) computes a 2x2 output tile from a 4x4 input
+// patch with 16 instead of 36 products per (cin, cout), 2.25x less MFMA work.
+//
+//   V = B^T d B  (4x4 input patch d, per channel)      B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]
+//   U = G g G^T  (3x3 filter g, precomputed on host)  G   = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1]
+//   M_e = sum_c U_e[cout][c] V_e[c][tile]   for the 16 elements e = (i, j)
+//   Y = A^T M A  (2x2 output tile)                     A^T = [1 1 1 0; 0 1 -1 -1]
+//
+// Structure (one workgroup = 32 output channels x T = 16*NW tiles, all 16 e):
+//   * the raw input region of the block's tiles (whole tile rows of one image,
+//     or whole images when an image has few tiles) is staged once per
+//     16-channel chunk by LDS-DMA (global_load_lds_dwordx4), deduplicated (a
+//     4x4 patch per tile would be 4x the bytes);
+//   * U for the 32 channels, 16 e and the chunk's 16 input channels (32 KiB)
+//     is staged next to it; two stages, so chunk k+1 lands while k computes;
+//   * every wave owns 16 tiles (the MFMA's 16 columns) x all 32 output
+//     channels x all 16 e: 32 accumulators of 4 f32.  A lane reads the 4x4
+//     patch of ITS tile for ITS 4 channels (16 ds_read_b128), transforms it in
+//     registers, and the 16 results ARE its B operands of the 16 e-GEMMs (lane
+//     l: tile l&15, channels 4(l>>4)..+3, the conv_f32.hip k-permutation), so V
+//     never touches LDS or HBM;
+//   * because a wave holds all 16 e of its (tile, channel) accumulators, the
+//     output transform, bias, residual and ReLU run in registers and each lane
+//     stores whole 16-byte channel quads of NHWC output.
+// LDS raw layout: [image row][column parity][pixel][4 chunks of 4 channels],
+// chunk XOR ((pixel >> 2) & 1) << 1: a wave's 16 lanes of one channel group
+// read 16 consecutive even (or odd) pixels of one row -> 16 distinct 16-byte
+// bank slots per ds_read_b128 lane group (conflict-free, checked offline).
+#include "../kernels.h"
+#include "../launch_util.h"
+
+namespace idunno {
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+constexpr int kRawMax = 40 * 1024;      // staged input region per stage (bytes)
+constexpr int kUBytes = 16 * 32 * 64;   // 16 e x 32 couts x 16 channels x 4 B = 32 KiB
+constexpr int kStage = kRawMax + kUBytes;
+
+__device__ __forceinline__ int raw_swz(int p) { return ((p >> 2) & 1) << 1; }
+
+}  // namespace
+
+template <int NW, bool HAS_RES>
+__global__ void __launch_bounds__(64 * NW, 1) conv_wino_f32_kernel(const WinoArgs a) {
+  constexpr int T = 16 * NW;
+  constexpr int RAW_INS = kRawMax / 1024;             // DMA instructions (max) for the raw region
+  constexpr int RAW_PER_WAVE = (RAW_INS + NW - 1) / NW;
+  constexpr int U_PER_WAVE = (kUBytes / 1024) / NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;                            // channel group of this lane (4 channels)
+
+  // ---- block -> (tile block, output-channel block) ----------------------------
+  const int nwg = a.nblk_t * a.nblk_n;
+  const int lid = xcd_remap(blockIdx.x, nwg);
+  const int tb = lid / a.nblk_n, nb = lid - tb * a.nblk_n;
+  const int n0 = nb * 32;
+  int b0, ty0, imgs, rows;
+  if (a.IMG > 1) {
+    b0 = tb * a.IMG;
+    ty0 = 0;
+    imgs = min(a.IMG, a.B - b0);
+    rows = a.TY;
+  } else {
+    b0 = tb / a.bpi;
+    ty0 = (tb - b0 * a.bpi) * a.R;
+    imgs = 1;
+    rows = min(a.R, a.TY - ty0);
+  }
+  const int per_img = a.R * a.TX;                     // tile slots per image in the block
+
+  // ---- DMA sources (per lane, per instruction; + channel offset per stage) -----
+  const float* zero = reinterpret_cast<const float*>(a.zero);
+  const int raw_chunks = a.raw_ins * 64;
+  int raw_off[RAW_PER_WAVE];
+#pragma unroll
+  for (int j = 0; j < RAW_PER_WAVE; ++j) {
+    const int ins = wave + NW * j;
+    const int L = ins * 64 + lane;
+    raw_off[j] = -1;
+    if (ins < a.raw_ins && L < raw_chunks) {
+      const int qs = L & 3;
+      int rest = L >> 2;
+      const int p = rest % a.NP;
+      rest /= a.NP;
+      const int half = rest & 1;
+      const int lr = rest >> 1;
+      const int img = lr / a.RIN, rin = lr - img * a.RIN;
+      const int iy = 2 * ty0 + rin - 1, ix = 2 * p + half - 1;
+      const int q = qs ^ raw_swz(p);
+      if (img < imgs && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+        raw_off[j] = (((b0 + img) * a.H + iy) * a.W + ix) * a.C + 4 * q;
+    }
+  }
+  int u_off[U_PER_WAVE];
+#pragma unroll
+  for (int j = 0; j < U_PER_WAVE; ++j) {
+    const int ins = wave + NW * j;
+    const int row = ins * 16 + (lane >> 2);            // (e, n) row of 64 B
+    const int e = row >> 5, n = row & 31;
+    const int q = (lane & 3) ^ swz_r(n, 4);
+    u_off[j] = (e * a.Cout + n0 + n) * a.C + 4 * q;
+  }
+  const int nk = a.C / 16;
+  auto issue = [&](int k, int buf) {
+    char* base = smem + buf * kStage;
+    const int c0 = k * 16;
+#pragma unroll
+    for (int j = 0; j < RAW_PER_WAVE; ++j) {
+      const int ins = wave + NW * j;
+      if (ins < a.raw_ins) {
+        const float* src = raw_off[j] >= 0 ? a.x + raw_off[j] + c0 : zero;
+        __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(base + ins * 1024), 16, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < U_PER_WAVE; ++j) {
+      const int ins = wave + NW * j;
+      __builtin_amdgcn_global_load_lds((glb_void_t*)(a.u + u_off[j] + c0),
+                                       (lds_void_t*)(base + kRawMax + ins * 1024), 16, 0, 0);
+    }
+  };
+
+  // ---- this lane's tile and its patch addresses in the raw image --------------
+  const int slot = wave * 16 + (lane & 15);
+  const int s_img = slot / per_img, s_rem = slot - s_img * per_img;
+  const int s_tyl = s_rem / a.TX, s_tx = s_rem - s_tyl * a.TX;
+  const bool s_ok = slot < T && s_img < imgs && s_tyl < rows;
+  // byte offset of patch element (py, px): row (img*RIN + 2*tyl + py), parity px&1,
+  // pixel tx + (px>>1), chunk g ^ swz(pixel)
+  const int rowb = 2 * a.NP * 64;                     // bytes per staged image row
+  const int pbase = s_ok ? ((s_img * a.RIN + 2 * s_tyl) * rowb) : 0;
+  int colb[4];
+#pragma unroll
+  for (int px = 0; px < 4; ++px) {
+    const int p = s_ok ? s_tx + (px >> 1) : 0;
+    colb[px] = (px & 1) * a.NP * 64 + p * 64 + ((g ^ raw_swz(p)) << 4);
+  }
+
+  float4v acc[16][2];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    acc[e][0] = float4v{0.f, 0.f, 0.f, 0.f};
+    acc[e][1] = float4v{0.f, 0.f, 0.f, 0.f};
+  }
+
+  issue(0, 0);
+  for (int k = 0; k < nk; ++k) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of chunk k landed
+    __builtin_amdgcn_s_barrier();                       // everyone's landed; buffer k+1 free
+    if (k + 1 < nk) issue(k + 1, (k + 1) & 1);
+    const uint32_t sb = lds_addr(smem) + (k & 1) * kStage;
+
+    // raw 4x4 patch of this lane's tile, its 4 channels -> V = B^T d B
+    float4v d[4][4];
+#pragma unroll
+    for (int py = 0; py < 4; ++py)
+#pragma unroll
+      for (int px = 0; px < 4; ++px) d[py][px] = lds_read_f4(sb + pbase + py * rowb + colb[px]);
+    lds_waitcnt<0>();
+#pragma unroll
+    for (int py = 0; py < 4; ++py)
+#pragma unroll
+      for (int px = 0; px < 4; ++px) lds_tie(d[py][px]);
+    float4v v[16];
+#pragma unroll
+    for (int px = 0; px < 4; ++px) {                    // rows: tmp = B^T d
+      const float4v t0 = d[0][px] - d[2][px], t1 = d[1][px] + d[2][px];
+      const float4v t2 = d[2][px] - d[1][px], t3 = d[1][px] - d[3][px];
+      d[0][px] = t0;
+      d[1][px] = t1;
+      d[2][px] = t2;
+      d[3][px] = t3;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {                       // columns: V = tmp B
+      v[i * 4 + 0] = d[i][0] - d[i][2];
+      v[i * 4 + 1] = d[i][1] + d[i][2];
+      v[i * 4 + 2] = d[i][2] - d[i][1];
+      v[i * 4 + 3] = d[i][1] - d[i][3];
+    }
+
+    // 16 GEMM updates: M_e[32 couts][16 tiles] += U_e[32][16 ch] * V_e[16 ch][16 tiles]
+    const uint32_t ub = sb + kRawMax;
+    auto uaddr = [&](int e, int i) {
+      const int n = i * 16 + (lane & 15);
+      return ub + (e * 32 + n) * 64 + ((g ^ swz_r(n, 4)) << 4);
+    };
+    float4v ua[2][2];
+    ua[0][0] = lds_read_f4(uaddr(0, 0));
+    ua[0][1] = lds_read_f4(uaddr(0, 1));
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int cb = e & 1, nbf = cb ^ 1;
+      if (e + 1 < 16) {
+        ua[nbf][0] = lds_read_f4(uaddr(e + 1, 0));
+        ua[nbf][1] = lds_read_f4(uaddr(e + 1, 1));
+        lds_waitcnt<2>();
+      } else {
+        lds_waitcnt<0>();
+      }
+      lds_tie(ua[cb][0]);
+      lds_tie(ua[cb][1]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[e][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][0][t], v[e][t], acc[e][0], 0, 0, 0);
+        acc[e][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][1][t], v[e][t], acc[e][1], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- output transform Y = A^T M A, bias, residual, ReLU, NHWC store -----------
+  if (!s_ok) return;
+  const int b = b0 + s_img;
+  const int oy0 = 2 * (ty0 + s_tyl), ox0 = 2 * s_tx;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int n = n0 + i * 16 + 4 * g;
+    const float4v bv = *reinterpret_cast<const float4v*>(a.bias + n);
+    // per output channel r (vector lane of the float4 accumulators)
+    float4v y00, y01, y10, y11;
+    {
+      float4v m[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) m[e] = acc[e][i];
+      float4v t0[4], t1[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        t0[j] = m[0 * 4 + j] + m[1 * 4 + j] + m[2 * 4 + j];
+        t1[j] = m[1 * 4 + j] - m[2 * 4 + j] - m[3 * 4 + j];
+      }
+      y00 = t0[0] + t0[1] + t0[2];
+      y01 = t0[1] - t0[2] - t0[3];
+      y10 = t1[0] + t1[1] + t1[2];
+      y11 = t1[1] - t1[2] - t1[3];
+    }
+    float4v yy[4] = {y00, y01, y10, y11};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int oy = oy0 + (q >> 1), ox = ox0 + (q & 1);
+      if (oy >= a.H || ox >= a.W) continue;
+      const size_t off = (((size_t)b * a.H + oy) * a.W + ox) * a.Cout + n;
+      float4v o = yy[q] + bv;
+      if constexpr (HAS_RES) o += *reinterpret_cast<const float4v*>(a.res + off);
+      if (a.relu) {
+        o[0] = fmaxf(o[0], 0.f);
+        o[1] = fmaxf(o[1], 0.f);
+        o[2] = fmaxf(o[2], 0.f);
+        o[3] = fmaxf(o[3], 0.f);
+      }
+      *reinterpret_cast<float4v*>(a.y + off) = o;
+    }
+  }
+}
+
+// Host-side block geometry for T = 16*nw tiles per block; false if the shape
+// does not fit (caller falls back to the direct conv).
+static bool wino_geometry(WinoArgs& a, int nw) {
+  const int T = 16 * nw;
+  a.TX = (a.W + 1) / 2;
+  a.TY = (a.H + 1) / 2;
+  if (a.TX > T) return false;
+  const int per = a.TX * a.TY;
+  auto raw_bytes = [&](int imgs, int R) { return imgs * (2 * R + 2) * 2 * (a.TX + 1) * 64; };
+  if (per <= T) {
+    a.R = a.TY;
+    a.IMG = T / per;
+    while (a.IMG > 1 && raw_bytes(a.IMG, a.R) > kRawMax) --a.IMG;
+    if (a.IMG == 1) a.bpi = 1;
+  } else {
+    a.IMG = 1;
+    a.R = T / a.TX;
+    while (a.R > 1 && raw_bytes(1, a.R) > kRawMax) --a.R;
+    a.bpi = (a.TY + a.R - 1) / a.R;
+  }
+  if (raw_bytes(a.IMG, a.R) > kRawMax) return false;
+  a.RIN = 2 * a.R + 2;
+  a.NP = a.TX + 1;
+  a.raw_ins = (raw_bytes(a.IMG, a.R) + 1023) / 1024;
+  a.nblk_t = a.IMG > 1 ? (a.B + a.IMG - 1) / a.IMG : a.B * a.bpi;
+  a.nblk_n = a.Cout / 32;
+  return true;
+}
+
+bool conv_wino_f32_supported(int H, int W, int C, int Cout) {
+  WinoArgs a{};
+  a.B = 1; a.H = H; a.W = W; a.C = C; a.Cout = Cout;
+  return C % 16 == 0 && Cout % 32 == 0 && wino_geometry(a, 4);
+}
+
+template <int NW, bool R>
+static void wino_cfg(WinoArgs a, hipStream_t st) {
+  const int lds = 2 * kStage;
+  auto kern = conv_wino_f32_kernel<NW, R>;
+  ensure_lds_attr(reinterpret_cast<const void*>(kern), lds);
+  hipLaunchKernelGGL(kern, dim3(a.nblk_t * a.nblk_n), dim3(64 * NW), lds, st, a);
+}
+
+// variant: 0 = 4 waves (64 tiles per block), 1 = 8 waves (128 tiles per block)
+bool conv_wino_f32_launch(WinoArgs a, int variant, hipStream_t st) {
+  const int nw = variant == 1 ? 8 : 4;
+  if (a.C % 16 || a.Cout % 32 || !wino_geometry(a, nw)) return false;
+  const bool res = a.res != nullptr;
+  if (nw == 8) {
+    if (res) wino_cfg<8, true>(a, st);
+    else wino_cfg<8, false>(a, st);
+  } else {
+    if (res) wino_cfg<4, true>(a, st);
+    else wino_cfg<4, false>(a, st);
+  }
+  return true;
+}
+
+}  // namespace idunno

@@ -7,12 +7,17 @@ of ops whose weights are laid out for the gfx950 implicit-GEMM kernel:
     b' = beta - mean * g/sqrt(v+eps)  ("BN folded into conv
     weights/bias at load time")
   * conv weights [Cout, Cin, KH, KW] -> [Cout, KH, KW, Cin] fp16 (K contiguous)
-  * RGB stems (Cin = 3) -> [Cout, KH, ceil(KW/8)*8, 4] (one K-stage per kh row)
+  * RGB stems (Cin = 3) -> [Cout, KH, ceil(KW/8)*8, 4] (one K-stage per kh row;
+    fp32 programs: ceil(KW/4)*4 taps)
+  * fp32 programs (dtype "fp32", the reference's precision) keep fp32 weights;
+    their 3x3/stride-1 convs also carry the Winograd F(2x2,3x3) filter
+    transform U = G g G^T [16, Cout, Cin] (conv_wino_f32.hip)
   * AlexNet fc6 columns permuted from NCHW-flatten to NHWC-flatten order
   * dropout elided (identity in eval), AdaptiveAvgPool(6,6) elided at 224 input
 
 The same program runs on two executors: ``HipRunner`` (the real path, HIP
-kernels, fp16 activations / fp32 accumulation) and ``emulate`` (fp32 torch
+kernels, fp16 activations / fp32 accumulation, or all-fp32 for dtype
+"fp32") and ``emulate`` (fp32 torch
 re-execution of the *packed* weights — used on CPU to test folding/packing
 without a GPU).
 """
@@ -40,10 +45,12 @@ class Conv:
     pad: int
     relu: bool
     small: bool = False      # RGB stem packing
+    wino: torch.Tensor | None = None   # fp32 3x3/s1: Winograd U = G g G^T [16, Cout, Cin]
 
     def to(self, device):
         return Conv(self.w.to(device), self.b.to(device), self.cin, self.cout, self.kh, self.kw,
-                    self.stride, self.pad, self.relu, self.small)
+                    self.stride, self.pad, self.relu, self.small,
+                    None if self.wino is None else self.wino.to(device))
 
     @property
     def flops_per_out_pixel(self) -> int:
@@ -155,9 +162,29 @@ def unpack_conv_weight(c: Conv) -> torch.Tensor:
     return w.view(c.cout, c.kh, c.kw, c.cin).permute(0, 3, 1, 2).contiguous()
 
 
+# Winograd F(2x2, 3x3) filter transform (Lavin & Gray): U = G g G^T
+WINO_G = torch.tensor([[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]], dtype=torch.float64)
+
+
+def wino_weight(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, 3, 3] -> U [16, Cout, Cin] fp32, U[4i+j] = (G g G^T)[i][j],
+    computed in fp64 and rounded once (conv_wino_f32.hip's A operand)."""
+    assert w.shape[2:] == (3, 3)
+    u = torch.einsum("ia,ocab,jb->ijoc", WINO_G, w.double(), WINO_G)
+    return u.reshape(16, w.shape[0], w.shape[1]).float().contiguous()
+
+
+def wino_eligible(cin: int, cout: int, kh: int, kw: int, stride: int, pad: int) -> bool:
+    return kh == 3 and kw == 3 and stride == 1 and pad == 1 and cin % 16 == 0 and cout % 32 == 0
+
+
 def make_conv(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, relu: bool, dtype: str = "fp16") -> Conv:
     w, b = fold_bn(conv.weight, conv.bias, bn)
     pw, small = pack_conv_weight(w, dtype)
+    if dtype == "fp32" and wino_eligible(conv.in_channels, conv.out_channels, *conv.kernel_size, conv.stride[0],
+                                         conv.padding[0]):
+        return Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, 3, 3, 1, 1, relu, small,
+                    wino_weight(w))
     return Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, conv.kernel_size[0],
                 conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small)
 
@@ -273,12 +300,20 @@ class HipRunner:
     static input buffer, removing per-kernel launch overhead.
     """
 
-    def __init__(self, program: Program, device=None, fuse_stem: bool = True, front_split: int | None = None):
+    def __init__(self, program: Program, device=None, fuse_stem: bool = True, front_split: int | None = None,
+                 winograd: bool = True, wino_variant: int | None = None):
         from .. import ops
 
         ops.load()
         self.ops = ops
         self.fuse_stem = fuse_stem
+        # fp32 3x3/s1 convs through the fused Winograd F(2x2,3x3) kernel (2.25x
+        # fewer f32-MFMA products than the direct conv; conv_wino_f32.hip)
+        self.winograd = winograd
+        # None = measured default per layer (tools/bench_layers_f32.py,
+        # profiles/r2_v2_layers_wino.md): 8-wave blocks (128 tiles) where the image
+        # has >= 14 rows, 4-wave blocks (64 tiles) for the 7x7 layer4
+        self.wino_variant = wino_variant
         # >1: stem + the full-resolution blocks (ResNet layer1) run on this many
         # batch parts, each part's activations small enough to stay in the
         # 256 MiB Infinity Cache between the stem and the end of layer1.
@@ -350,27 +385,28 @@ class HipRunner:
             x = o.global_avgpool(x)
         else:
             for k, v in p.features:
-                if k == "conv":
-                    x = o.conv2d(x, v.w, v.b, v.kh, v.kw, v.stride, v.pad, v.relu)
-                else:
-                    x = o.maxpool2d(x, *v)
+                x = self._conv(v, x) if k == "conv" else o.maxpool2d(x, *v)
             x = x.reshape(x.shape[0], -1)
         for fc in p.fcs:
             x = o.linear(x, fc.w, fc.b, relu=fc.relu)
         return x
 
+    def _conv(self, c, x, residual=None, out=None):
+        if c.wino is not None and self.winograd and out is None and x.dtype == torch.float32 \
+                and self.ops.wino_supported(x.shape[1], x.shape[2], c.cin, c.cout):
+            var = self.wino_variant if self.wino_variant is not None else (1 if x.shape[1] >= 14 else 0)
+            return self.ops.conv2d_wino(x, c.wino, c.b, c.relu, residual, var)
+        return self.ops.conv2d(x, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu, residual=residual, out=out)
+
     def _block(self, blk, x, out=None):
         """One residual block; the last conv fuses +identity and ReLU (into ``out``)."""
-        o = self.ops
         idt = x
         if blk.down is not None:
-            d = blk.down
-            idt = o.conv2d(x, d.w, d.b, d.kh, d.kw, d.stride, d.pad, False)
+            idt = self._conv(blk.down, x)
         y = x
         for c in blk.convs[:-1]:
-            y = o.conv2d(y, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu)
-        c = blk.convs[-1]
-        return o.conv2d(y, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu, residual=idt, out=out)
+            y = self._conv(c, y)
+        return self._conv(blk.convs[-1], y, residual=idt, out=out)
 
     def _front_blocks(self) -> int:
         """Leading blocks that keep the stem's resolution (ResNet layer1)."""

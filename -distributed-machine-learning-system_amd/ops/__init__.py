@@ -12,6 +12,7 @@ from ._ext import available, load, so_path
 __all__ = [
     "available", "load", "so_path", "conv2d", "linear", "preprocess", "resize_crop",
     "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile", "pick_tile_f32", "synth_images", "stem_fused",
+    "conv2d_wino", "wino_supported",
 ]
 
 
@@ -27,6 +28,16 @@ def conv2d(x, w, bias, kh: int, kw: int, stride: int, pad: int, relu: bool,
     if x.dtype == torch.float32:
         return load().conv2d_nhwc_f32(x, w, bias, residual, kh, kw, stride, pad, relu, tile, out)
     return load().conv2d_nhwc(x, w, bias, residual, kh, kw, stride, pad, relu, out_f32, tile, out)
+
+
+def conv2d_wino(x, u, bias, relu: bool, residual=None, variant: int = 0):
+    """fp32 3x3/stride-1/pad-1 conv by fused Winograd F(2x2,3x3) (conv_wino_f32.hip);
+    ``u`` = models.packed.wino_weight(w) [16, Cout, Cin]."""
+    return load().conv2d_wino_f32(x, u, bias, residual, relu, variant)
+
+
+def wino_supported(h: int, w: int, cin: int, cout: int) -> bool:
+    return cin % 16 == 0 and cout % 32 == 0 and bool(load().wino_supported(h, w, cin, cout))
 
 
 # Default K split of FC layers.  Measured (tools/ab_linear_split.py,

@@ -211,3 +211,41 @@ def test_f32_window_graph_matches_eager(ops):
         torch.cuda.synchronize()
         assert torch.equal(c0, c1) and torch.equal(p0, p1)
         assert torch.equal(packed[:, 0], c0)
+
+
+WINO_CASES = [
+    # (B, H, W, Cin, Cout)
+    (2, 56, 56, 64, 64),      # resnet layer1: 2 tile rows per block, 14 blocks per image
+    (2, 28, 28, 128, 128),    # layer2: partial last block (4, 4, 4, 2 tile rows)
+    (2, 14, 14, 256, 256),    # layer3: one image per block (49 of 64 tile slots)
+    (5, 7, 7, 512, 512),      # layer4: 4 images per block, odd size (padded 2x2 tiles), partial last block
+    (2, 13, 13, 192, 384),    # alexnet conv3
+    (1, 9, 5, 48, 32),        # odd everything
+]
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("B,H,W,Cin,Cout", WINO_CASES)
+def test_conv_wino_f32(ops, B, H, W, Cin, Cout, res, variant):
+    """Fused Winograd F(2x2,3x3) fp32 conv vs the fp64 direct conv."""
+    from idunno.models.packed import wino_weight
+
+    torch.manual_seed(B + H * 7 + W + Cin + Cout + res)
+    x = torch.randn(B, H, W, Cin, device=DEV)
+    w = torch.randn(Cout, Cin, 3, 3) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    r = torch.randn(B, H, W, Cout, device=DEV) if res else None
+    assert ops.wino_supported(H, W, Cin, Cout)
+    y = ops.conv2d_wino(x, wino_weight(w).to(DEV), b.to(DEV), True, r, variant)
+    _check(y, _ref_conv64(x, w, b, 1, 1, True, r), rel=5e-5)
+
+
+def test_runner_winograd_matches_direct(ops):
+    from idunno.models import HipRunner, build_program
+
+    p = build_program("resnet18", seed=2, randomize_bn=True, dtype="fp32")
+    img = ops.synth_images(5, 0, 6, DEV)
+    a = HipRunner(p, winograd=True).logits(img)
+    b = HipRunner(p, winograd=False).logits(img)
+    assert (a - b).abs().max().item() <= 2e-5 * b.abs().max().item()
