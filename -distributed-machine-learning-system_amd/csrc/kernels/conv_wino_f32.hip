@@ -266,9 +266,257 @@ __global__ void __launch_bounds__(64 * NW, 1) conv_wino_f32_kernel(const WinoArg
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// v2: software-pipelined, 4 waves (one per SIMD, up to 512 registers each).
+// v1's waves all hit the barrier together, so every SIMD idles its matrix pipe
+// while the raw patch is read and transformed (and one wave per SIMD has no
+// partner to cover it).  v2 keeps the raw input one chunk AHEAD of U in two
+// separate rings: at chunk k the wave multiplies V(k) (registers) by U(k)
+// while it reads raw(k+1) and transforms it into V(k+1) between the MFMAs.
+//   LDS: raw ring 2 x 26 KiB + U ring 2 x 32 KiB = 116 KiB (one block per CU).
+//   Before barrier k: raw(k+1) and U(k) landed (issued one chunk earlier);
+//   after it: issue raw(k+2) into raw(k)'s slot and U(k+1) into U(k-1)'s slot.
+// ---------------------------------------------------------------------------
+constexpr int kRaw2 = 26 * 1024;
+
+template <bool HAS_RES>
+__global__ void __launch_bounds__(256, 1) conv_wino2_f32_kernel(const WinoArgs a) {
+  constexpr int NW = 4, T = 64;
+  constexpr int RAW_PER_WAVE = (kRaw2 / 1024 + NW - 1) / NW;
+  constexpr int U_PER_WAVE = (kUBytes / 1024) / NW;
+  constexpr int RAW0 = 0, U0 = 2 * kRaw2;                 // ring bases
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+
+  const int nwg = a.nblk_t * a.nblk_n;
+  const int lid = xcd_remap(blockIdx.x, nwg);
+  const int tb = lid / a.nblk_n, nb = lid - tb * a.nblk_n;
+  const int n0 = nb * 32;
+  int b0, ty0, imgs, rows;
+  if (a.IMG > 1) {
+    b0 = tb * a.IMG;
+    ty0 = 0;
+    imgs = min(a.IMG, a.B - b0);
+    rows = a.TY;
+  } else {
+    b0 = tb / a.bpi;
+    ty0 = (tb - b0 * a.bpi) * a.R;
+    imgs = 1;
+    rows = min(a.R, a.TY - ty0);
+  }
+  const int per_img = a.R * a.TX;
+
+  const float* zero = reinterpret_cast<const float*>(a.zero);
+  int raw_off[RAW_PER_WAVE];
+#pragma unroll
+  for (int j = 0; j < RAW_PER_WAVE; ++j) {
+    const int ins = wave + NW * j;
+    const int L = ins * 64 + lane;
+    raw_off[j] = -1;
+    if (ins < a.raw_ins) {
+      const int qs = L & 3;
+      int rest = L >> 2;
+      const int p = rest % a.NP;
+      rest /= a.NP;
+      const int half = rest & 1;
+      const int lr = rest >> 1;
+      const int img = lr / a.RIN, rin = lr - img * a.RIN;
+      const int iy = 2 * ty0 + rin - 1, ix = 2 * p + half - 1;
+      const int q = qs ^ raw_swz(p);
+      if (img < imgs && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+        raw_off[j] = (((b0 + img) * a.H + iy) * a.W + ix) * a.C + 4 * q;
+    }
+  }
+  int u_off[U_PER_WAVE];
+#pragma unroll
+  for (int j = 0; j < U_PER_WAVE; ++j) {
+    const int ins = wave + NW * j;
+    const int row = ins * 16 + (lane >> 2);
+    const int e = row >> 5, n = row & 31;
+    const int q = (lane & 3) ^ swz_r(n, 4);
+    u_off[j] = (e * a.Cout + n0 + n) * a.C + 4 * q;
+  }
+  const int nk = a.C / 16;
+  auto issue_raw = [&](int k) {
+    char* base = smem + RAW0 + (k & 1) * kRaw2;
+    const int c0 = k * 16;
+#pragma unroll
+    for (int j = 0; j < RAW_PER_WAVE; ++j) {
+      const int ins = wave + NW * j;
+      if (ins < a.raw_ins) {
+        const float* src = raw_off[j] >= 0 ? a.x + raw_off[j] + c0 : zero;
+        __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(base + ins * 1024), 16, 0, 0);
+      }
+    }
+  };
+  auto issue_u = [&](int k) {
+    char* base = smem + U0 + (k & 1) * kUBytes;
+    const int c0 = k * 16;
+#pragma unroll
+    for (int j = 0; j < U_PER_WAVE; ++j) {
+      const int ins = wave + NW * j;
+      __builtin_amdgcn_global_load_lds((glb_void_t*)(a.u + u_off[j] + c0), (lds_void_t*)(base + ins * 1024), 16, 0,
+                                       0);
+    }
+  };
+
+  const int slot = wave * 16 + (lane & 15);
+  const int s_img = slot / per_img, s_rem = slot - s_img * per_img;
+  const int s_tyl = s_rem / a.TX, s_tx = s_rem - s_tyl * a.TX;
+  const bool s_ok = slot < T && s_img < imgs && s_tyl < rows;
+  const int rowb = 2 * a.NP * 64;
+  const int pbase = s_ok ? ((s_img * a.RIN + 2 * s_tyl) * rowb) : 0;
+  int colb[4];
+#pragma unroll
+  for (int px = 0; px < 4; ++px) {
+    const int p = s_ok ? s_tx + (px >> 1) : 0;
+    colb[px] = (px & 1) * a.NP * 64 + p * 64 + ((g ^ raw_swz(p)) << 4);
+  }
+  const uint32_t sbase = lds_addr(smem);
+  auto read_raw = [&](int k, float4v (&d)[4][4]) {
+    const uint32_t rb = sbase + RAW0 + (k & 1) * kRaw2 + pbase;
+#pragma unroll
+    for (int py = 0; py < 4; ++py)
+#pragma unroll
+      for (int px = 0; px < 4; ++px) d[py][px] = lds_read_f4(rb + py * rowb + colb[px]);
+  };
+  // V = B^T d B in two halves: rows (d -> B^T d, in place) then columns
+  auto transform_rows = [&](float4v (&d)[4][4], int px) {
+    const float4v t0 = d[0][px] - d[2][px], t1 = d[1][px] + d[2][px];
+    const float4v t2 = d[2][px] - d[1][px], t3 = d[1][px] - d[3][px];
+    d[0][px] = t0;
+    d[1][px] = t1;
+    d[2][px] = t2;
+    d[3][px] = t3;
+  };
+  auto transform_cols = [&](float4v (&d)[4][4], float4v (&v)[16], int i) {
+    v[i * 4 + 0] = d[i][0] - d[i][2];
+    v[i * 4 + 1] = d[i][1] + d[i][2];
+    v[i * 4 + 2] = d[i][2] - d[i][1];
+    v[i * 4 + 3] = d[i][1] - d[i][3];
+  };
+  auto uaddr = [&](int k, int e, int i) {
+    const int n = i * 16 + (lane & 15);
+    return sbase + U0 + (k & 1) * kUBytes + (e * 32 + n) * 64 + ((g ^ swz_r(n, 4)) << 4);
+  };
+
+  float4v acc[16][2];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    acc[e][0] = float4v{0.f, 0.f, 0.f, 0.f};
+    acc[e][1] = float4v{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // prologue: raw(0), U(0), raw(1) in flight; V(0) transformed up front
+  float4v va[16], vb[16];
+  {
+    issue_raw(0);
+    issue_u(0);
+    if (nk > 1) issue_raw(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    float4v d[4][4];
+    read_raw(0, d);
+    lds_waitcnt<0>();
+#pragma unroll
+    for (int py = 0; py < 4; ++py)
+#pragma unroll
+      for (int px = 0; px < 4; ++px) lds_tie(d[py][px]);
+#pragma unroll
+    for (int px = 0; px < 4; ++px) transform_rows(d, px);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) transform_cols(d, va, i);
+  }
+
+  // one chunk: MFMAs of V(k) x U(k); raw(k+1) -> V(k+1) between them
+  auto chunk = [&](int k, float4v (&vc)[16], float4v (&vn)[16]) {
+    __builtin_amdgcn_s_barrier();          // all waves done with chunk k-1 (raw(k) and U(k-1) slots free)
+    if (k + 2 < nk) issue_raw(k + 2);
+    if (k + 1 < nk) issue_u(k + 1);
+    const bool more = k + 1 < nk;
+    float4v d[4][4];
+    if (more) read_raw(k + 1, d);
+    float4v ua[2][2];
+    ua[0][0] = lds_read_f4(uaddr(k, 0, 0));
+    ua[0][1] = lds_read_f4(uaddr(k, 0, 1));
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int cb = e & 1, nbf = cb ^ 1;
+      if (e + 1 < 16) {
+        ua[nbf][0] = lds_read_f4(uaddr(k, e + 1, 0));
+        ua[nbf][1] = lds_read_f4(uaddr(k, e + 1, 1));
+        lds_waitcnt<2>();                  // in-order: raw(k+1) reads and U(e) retired
+      } else {
+        lds_waitcnt<0>();
+      }
+      lds_tie(ua[cb][0]);
+      lds_tie(ua[cb][1]);
+      if (e == 0 && more) {
+#pragma unroll
+        for (int py = 0; py < 4; ++py)
+#pragma unroll
+          for (int px = 0; px < 4; ++px) lds_tie(d[py][px]);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[e][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][0][t], vc[e][t], acc[e][0], 0, 0, 0);
+        acc[e][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][1][t], vc[e][t], acc[e][1], 0, 0, 0);
+      }
+      // spread the next chunk's transform over the MFMA stream (8 MFMAs per e)
+      if (more) {
+        if (e >= 1 && e <= 4) transform_rows(d, e - 1);
+        if (e >= 5 && e <= 8) transform_cols(d, vn, e - 5);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // raw(k+2), U(k+1) of this wave landed
+  };
+  int k = 0;
+  for (; k + 1 < nk; k += 2) {
+    chunk(k, va, vb);
+    chunk(k + 1, vb, va);
+  }
+  if (k < nk) chunk(k, va, vb);
+
+  // ---- output transform Y = A^T M A, bias, residual, ReLU, NHWC store -----------
+  if (!s_ok) return;
+  const int b = b0 + s_img;
+  const int oy0 = 2 * (ty0 + s_tyl), ox0 = 2 * s_tx;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int n = n0 + i * 16 + 4 * g;
+    const float4v bv = *reinterpret_cast<const float4v*>(a.bias + n);
+    float4v t0[4], t1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      t0[j] = acc[0 * 4 + j][i] + acc[1 * 4 + j][i] + acc[2 * 4 + j][i];
+      t1[j] = acc[1 * 4 + j][i] - acc[2 * 4 + j][i] - acc[3 * 4 + j][i];
+    }
+    const float4v yy[4] = {t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3], t1[0] + t1[1] + t1[2],
+                           t1[1] - t1[2] - t1[3]};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int oy = oy0 + (q >> 1), ox = ox0 + (q & 1);
+      if (oy >= a.H || ox >= a.W) continue;
+      const size_t off = (((size_t)b * a.H + oy) * a.W + ox) * a.Cout + n;
+      float4v o = yy[q] + bv;
+      if constexpr (HAS_RES) o += *reinterpret_cast<const float4v*>(a.res + off);
+      if (a.relu) {
+        o[0] = fmaxf(o[0], 0.f);
+        o[1] = fmaxf(o[1], 0.f);
+        o[2] = fmaxf(o[2], 0.f);
+        o[3] = fmaxf(o[3], 0.f);
+      }
+      *reinterpret_cast<float4v*>(a.y + off) = o;
+    }
+  }
+}
+
 // Host-side block geometry for T = 16*nw tiles per block; false if the shape
 // does not fit (caller falls back to the direct conv).
-static bool wino_geometry(WinoArgs& a, int nw) {
+static bool wino_geometry(WinoArgs& a, int nw, int raw_max = kRawMax) {
   const int T = 16 * nw;
   a.TX = (a.W + 1) / 2;
   a.TY = (a.H + 1) / 2;
@@ -278,15 +526,15 @@ static bool wino_geometry(WinoArgs& a, int nw) {
   if (per <= T) {
     a.R = a.TY;
     a.IMG = T / per;
-    while (a.IMG > 1 && raw_bytes(a.IMG, a.R) > kRawMax) --a.IMG;
+    while (a.IMG > 1 && raw_bytes(a.IMG, a.R) > raw_max) --a.IMG;
     if (a.IMG == 1) a.bpi = 1;
   } else {
     a.IMG = 1;
     a.R = T / a.TX;
-    while (a.R > 1 && raw_bytes(1, a.R) > kRawMax) --a.R;
+    while (a.R > 1 && raw_bytes(1, a.R) > raw_max) --a.R;
     a.bpi = (a.TY + a.R - 1) / a.R;
   }
-  if (raw_bytes(a.IMG, a.R) > kRawMax) return false;
+  if (raw_bytes(a.IMG, a.R) > raw_max) return false;
   a.RIN = 2 * a.R + 2;
   a.NP = a.TX + 1;
   a.raw_ins = (raw_bytes(a.IMG, a.R) + 1023) / 1024;
@@ -298,7 +546,7 @@ static bool wino_geometry(WinoArgs& a, int nw) {
 bool conv_wino_f32_supported(int H, int W, int C, int Cout) {
   WinoArgs a{};
   a.B = 1; a.H = H; a.W = W; a.C = C; a.Cout = Cout;
-  return C % 16 == 0 && Cout % 32 == 0 && wino_geometry(a, 4);
+  return C % 16 == 0 && Cout % 32 == 0 && wino_geometry(a, 4, kRaw2);
 }
 
 template <int NW, bool R>
@@ -309,8 +557,17 @@ static void wino_cfg(WinoArgs a, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3(a.nblk_t * a.nblk_n), dim3(64 * NW), lds, st, a);
 }
 
-// variant: 0 = 4 waves (64 tiles per block), 1 = 8 waves (128 tiles per block)
+// variant: 0 = 4 waves (64 tiles per block), 1 = 8 waves (128 tiles per block),
+//          2 = software-pipelined 4 waves (64 tiles per block)
 bool conv_wino_f32_launch(WinoArgs a, int variant, hipStream_t st) {
+  if (variant == 2) {
+    if (a.C % 16 || a.Cout % 32 || !wino_geometry(a, 4, kRaw2)) return false;
+    const int lds = 2 * kRaw2 + 2 * kUBytes;
+    auto kern = a.res != nullptr ? conv_wino2_f32_kernel<true> : conv_wino2_f32_kernel<false>;
+    ensure_lds_attr(reinterpret_cast<const void*>(kern), lds);
+    hipLaunchKernelGGL(kern, dim3(a.nblk_t * a.nblk_n), dim3(256), lds, st, a);
+    return true;
+  }
   const int nw = variant == 1 ? 8 : 4;
   if (a.C % 16 || a.Cout % 32 || !wino_geometry(a, nw)) return false;
   const bool res = a.res != nullptr;

@@ -72,9 +72,9 @@ def main():
             from idunno.models.packed import wino_weight
 
             u = wino_weight(w).to(dev)
-            for var in (0, 1):
+            for var in (0, 1, 2):
                 r[f"wino{var}_us"] = timeit(lambda: ops.conv2d_wino(x, u, c.b, True, res, var))
-            r["wino_tf"] = flops / min(r["wino0_us"], r["wino1_us"]) / 1e6
+            r["wino_tf"] = flops / min(r["wino0_us"], r["wino1_us"], r["wino2_us"]) / 1e6
         us_def = timeit(lambda: ops.conv2d(x, c.w, c.b, c.kh, c.kw, c.stride, c.pad, True, residual=res))
         r["def_us"] = us_def
         if a.torch and not c.small:
@@ -90,13 +90,14 @@ def main():
         rows.append(r)
         print(json.dumps(r), flush=True)
     print(f"\n| layer | H | cin | cout | k/s | default | def us | def TF/s | best tile | best us | best TF/s |"
-          " wino4 us | wino8 us | wino eff. TF/s |" + (" torch us |" if a.torch else ""))
-    print("|---|---:|---:|---:|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|" + ("---:|" if a.torch else ""))
+          " wino4 us | wino8 us | wino4p us | wino eff. TF/s |" + (" torch us |" if a.torch else ""))
+    print("|---|---:|---:|---:|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|" + ("---:|" if a.torch else ""))
     for r in rows:
         best = min(v for k, v in r.items() if isinstance(k, int))
         print(f"| {r['layer']} | {r['H']} | {r['cin']} | {r['cout']} | {r['k']}/{r['s']} | {r['default']} | "
               f"{r['def_us']:.0f} | {r['tf_def']:.1f} | {r['best_tile']} | {best:.0f} | {r['tf_best']:.1f} |"
               f" {r.get('wino0_us', float('nan')):.0f} | {r.get('wino1_us', float('nan')):.0f} |"
+              f" {r.get('wino2_us', float('nan')):.0f} |"
               f" {r.get('wino_tf', float('nan')):.1f} |"
               + (f" {r.get('torch_us', float('nan')):.0f} |" if a.torch else ""))
     print(f"\nunique layers: default sum {tot_def:.0f} us, best-tile sum {tot_best:.0f} us")

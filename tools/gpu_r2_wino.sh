@@ -10,6 +10,6 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -u tools/bench_layers_f32.py --batch 400 --json $OUT/layers_f32w.json > $OUT/layers_f32w.log 2>&1
 rc=$?; echo "[layers] rc=$rc"; sed -n '/^| layer/,$p' $OUT/layers_f32w.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > $OUT/bench_f32w.log 2>&1
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-extras > $OUT/bench_f32w.log 2>&1
 rc=$?; echo "[bench] rc=$rc"; tail -1 $OUT/bench_f32w.log
 exit $rc
