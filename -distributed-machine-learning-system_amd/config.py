@@ -31,7 +31,7 @@ class ClusterConfig:
     worker_budget: int = 8                   # reference RATE_FACTOR (:44) -> GPUs shared by jobs
     max_chunk: int = 1024                    # largest per-worker batch (HBM is not the limit)
     dataset_size: int = 10000                # reference dataset: 10,000 images (report p.1)
-    dtype: str = "fp16"
+    dtype: str = "fp32"                      # executor precision: "fp32" (the reference's) | "fp16"
     model_seed: int = 0
     data_seed: int = 1234
 
@@ -51,9 +51,11 @@ class ClusterConfig:
     store_root: str = "/tmp/idunno"
 
     # -- collective data plane (one node per process only) ----------------------
-    collective_rounds: bool = False          # run queries as RCCL/gloo rounds when the group is healthy
+    # run queries as RCCL/gloo rounds when the group is healthy; None = auto:
+    # on for GPU nodes started one per process by idunno.launch
+    collective_rounds: bool | None = None
     collective_port_offset: int = 500        # TCPStore port = base_port + offset + epoch % 100
-    collective_timeout_s: float = 30.0
+    collective_timeout_s: float = 30.0       # rendezvous timeout; a round's liveness comes from membership
 
     # -- checkpoint / resume ----------------------------------------------------
     checkpoint_period_s: float = 0.0         # coordinator writes state to disk (0 = off)
@@ -115,7 +117,7 @@ class ClusterConfig:
             if ev is None:
                 continue
             cur = getattr(cfg, k)
-            if isinstance(cur, bool):
+            if isinstance(cur, bool) or (cur is None and k == "collective_rounds"):
                 val = ev.lower() in ("1", "true", "yes")
             elif isinstance(cur, int):
                 val = int(ev)

@@ -50,7 +50,10 @@ def run_node(a) -> int:
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
-    ex = make_executor(a.executor, dev if dev.type == "cuda" else None, seed=cfg.model_seed)
+    ex = make_executor(a.executor, dev if dev.type == "cuda" else None, seed=cfg.model_seed, dtype=cfg.dtype)
+    if cfg.collective_rounds is None:
+        # one node per process: queries run as RCCL rounds on GPU nodes by default
+        cfg.collective_rounds = dev.type == "cuda" and a.executor in ("auto", "hip")
     tr = TcpTransport(name, cfg.address, cfg.address(name))
     node = Node(cfg, name, tr, ex)
     node.source = (SdfsSource(node.sdfs, dev) if a.source == "sdfs" else SyntheticSource(cfg.data_seed, dev))

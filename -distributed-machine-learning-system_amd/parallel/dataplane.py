@@ -105,6 +105,30 @@ class QueryPlane:
         row = self._desc[self.env.rank].tolist()
         return tuple(int(v) for v in row)
 
+    def dispatch_async(self, table: list[tuple[int, int, int, int]] | None):
+        """Start the descriptor broadcast; returns the collective's Work (None
+        on a single rank).  The row is in ``self._desc`` once it completed."""
+        if self.env.rank == self.coord:
+            assert table is not None and len(table) == self.env.world
+            for row in table:
+                if row[3] != NO_WORK and row[3] - row[2] + 1 > self.max_chunk:
+                    raise ValueError(f"chunk {row} larger than max_chunk={self.max_chunk}")
+            self._desc.copy_(torch.tensor(table, dtype=torch.int64), non_blocking=True)
+        if not self.env.distributed:
+            return None
+        return dist.broadcast(self._desc, src=self.coord, group=self.group, async_op=True)
+
+    def my_row(self) -> tuple[int, int, int, int]:
+        return tuple(int(v) for v in self._desc[self.env.rank].tolist())
+
+    def gather_async(self):
+        """Start the gather of the send buffer to the coordinator (Work or None)."""
+        if not self.env.distributed:
+            return None
+        if self.env.rank == self.coord:
+            return dist.gather(self._pack, self._gathered, dst=self.coord, group=self.group, async_op=True)
+        return dist.gather(self._pack, None, dst=self.coord, group=self.group, async_op=True)
+
     def dispatch_device(self, table: list[tuple[int, int, int, int]] | None, slot: int = 0) -> torch.Tensor:
         """Asynchronous dispatch: no host synchronisation anywhere.
 

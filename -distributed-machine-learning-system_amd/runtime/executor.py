@@ -74,21 +74,32 @@ class TorchExecutor(Executor):
 
 
 class HipExecutor(Executor):
-    """gfx950 kernels; per-(model, batch) hipGraphs, weights resident in HBM."""
+    """gfx950 kernels; per-(model, batch) hipGraphs, weights resident in HBM.
 
-    def __init__(self, device="cuda", seed: int = 0, use_graphs: bool = True, max_graphs: int = 16):
+    ``dtype`` "fp32" runs the reference-precision path (f32-input MFMA), "fp16"
+    the f16-MFMA path.  Thread-safe: the TCP worker loop and the collective
+    round driver of a node may call ``run`` / ``run_packed`` at the same time
+    (a TCP re-dispatch next to a round chunk of the same model and size); the
+    static graph input, the replay and the result read-back of one call are
+    one critical section (results of two chunks must never mix)."""
+
+    def __init__(self, device="cuda", seed: int = 0, use_graphs: bool = True, max_graphs: int = 16,
+                 dtype: str = "fp32"):
         from .. import ops
         from ..models import HipRunner, build_program
 
         ops.load()  # loud failure if the extension is missing on a GPU host
         self.device = torch.device(device)
         self.seed = seed
+        self.dtype = dtype
         self.use_graphs = use_graphs
         self.max_graphs = max_graphs
         self._HipRunner, self._build = HipRunner, build_program
         self.runners: dict[str, object] = {}
         self.lock = threading.Lock()
+        self.run_lock = threading.Lock()      # one forward (copy-in, replay, read-back) at a time
         self.stream = None      # private HIP stream: nodes sharing a GPU overlap
+        self._host_out = None   # pinned [max_graph_batch, 2] int32 result buffer
         self.closed = False
 
     def runner(self, name):
@@ -97,33 +108,63 @@ class HipExecutor(Executor):
             r = self.runners.get(name)
             if r is None:
                 with torch.cuda.device(self.device):
-                    r = self._HipRunner(self._build(name, seed=self.seed), self.device)
+                    r = self._HipRunner(self._build(name, seed=self.seed, dtype=self.dtype), self.device)
                 self.runners[name] = r
         return r
 
     def warmup(self, model, batch):
         if self.use_graphs:
-            with torch.cuda.device(self.device):
+            with torch.cuda.device(self.device), self.run_lock:
                 self.runner(model).capture(batch)
+
+    def _forward(self, r, images, packed):
+        """cls, prob of ``images`` on the private stream (caller holds run_lock);
+        with ``packed`` the (class, prob bits) pairs are also written there."""
+        n = images.shape[0]
+        s = self.stream
+        if not self.closed and packed is None and \
+                ((self.use_graphs and len(r._graphs) < self.max_graphs) or n in r._graphs):
+            sin, replay = r.capture(n)
+            sin.copy_(images)
+            return replay()
+        return r.forward(images.contiguous(), packed=packed)
+
+    def _enter(self, images):
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(device=self.device)
+        s = self.stream
+        s.wait_stream(torch.cuda.current_stream(self.device))   # images were produced there
+        images.record_stream(s)
+        return s
 
     def run(self, model, images, start, end):
         r = self.runner(model)
         n = images.shape[0]
-        with torch.cuda.device(self.device):
-            if self.stream is None:
-                self.stream = torch.cuda.Stream(device=self.device)
-            s = self.stream
-            s.wait_stream(torch.cuda.current_stream(self.device))   # images were produced there
-            images.record_stream(s)
+        with torch.cuda.device(self.device), self.run_lock:
+            s = self._enter(images)
             with torch.cuda.stream(s):
-                if not self.closed and ((self.use_graphs and len(r._graphs) < self.max_graphs) or n in r._graphs):
-                    sin, replay = r.capture(n)
-                    sin.copy_(images)
-                    cls, prob = replay()
-                else:
-                    cls, prob = r.forward(images.contiguous())
-                out = torch.stack([cls, prob.view(torch.int32)], dim=1).cpu()
-        return out[:, 0].numpy().copy(), out[:, 1].contiguous().view(torch.float32).numpy().copy()
+                cls, prob = self._forward(r, images, None)
+                if self._host_out is None or self._host_out.shape[0] < n:
+                    self._host_out = torch.empty(max(n, 1024), 2, dtype=torch.int32, pin_memory=True)
+                out = self._host_out[:n]
+                out[:, 0].copy_(cls, non_blocking=True)          # pinned D2H, no pageable bounce
+                out[:, 1].copy_(prob.view(torch.int32), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(s)
+            ev.synchronize()
+            return out[:, 0].numpy().copy(), out[:, 1].contiguous().view(torch.float32).numpy().copy()
+
+    def run_packed(self, model, images, packed) -> None:
+        """Device-resident result path (collective rounds): write (class, prob
+        bits) pairs of ``images`` into the int32 [>= n, 2] device tensor
+        ``packed`` (the RCCL gather's send buffer) on the current stream's
+        order; nothing comes back to the host."""
+        r = self.runner(model)
+        with torch.cuda.device(self.device), self.run_lock:
+            s = self._enter(images)
+            with torch.cuda.stream(s):
+                r.forward(images.contiguous(), packed=packed)
+            torch.cuda.current_stream(self.device).wait_stream(s)
 
 
     def close(self) -> None:
@@ -136,12 +177,12 @@ class HipExecutor(Executor):
             r.close()
 
 
-def make_executor(kind: str, device=None, seed: int = 0) -> Executor:
+def make_executor(kind: str, device=None, seed: int = 0, dtype: str = "fp32") -> Executor:
     kind = kind.lower()
     if kind == "auto":
         kind = "hip" if torch.cuda.is_available() else "torch"
     if kind == "hip":
-        return HipExecutor(device or "cuda", seed=seed)
+        return HipExecutor(device or "cuda", seed=seed, dtype=dtype)
     if kind == "torch":
         return TorchExecutor(device or "cpu", seed=seed)
     if kind == "fake":

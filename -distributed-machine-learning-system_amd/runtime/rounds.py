@@ -16,6 +16,18 @@ mp4_machinelearning.py:560-613); the TCP path stays as the fallback:
 Each node runs ONE driver thread that owns the process group, so forming,
 rounds and teardown never race: as coordinator it forms epochs and serves the
 round queue, as a member it follows the latest GROUP_FORM it was sent.
+
+Liveness: collectives are polled against the failure
+detector, never waited on blindly.  The coordinator abandons a round as soon
+as membership marks one of its members dead (``failure_timeout_s``), falls
+back to TCP for the live members' chunks and aborts the epoch in the
+background; a member abandons its wait when a newer epoch is announced or
+the coordinator is dead.  Idle gaps are free (the process-group timeout is
+long), so no keepalive rounds are needed.
+
+Results stay on the device: a member's forward writes its packed top-1 pairs
+straight into the gather's send buffer (``HipExecutor.run_packed``), and the
+coordinator copies the whole round to the host once.
 """
 from __future__ import annotations
 
@@ -27,7 +39,7 @@ import time
 import numpy as np
 
 from ..parallel.dataplane import NO_WORK
-from ..parallel.elastic import MODEL_IDS, STOP, ElasticGroup
+from ..parallel.elastic import MODEL_IDS, STOP, ElasticGroup, RoundAbandoned
 from .messages import Type
 
 log = logging.getLogger("idunno.rounds")
@@ -97,8 +109,38 @@ class RoundPlane:
         self._wake.set()
         return True
 
+    # -- liveness checks (polled while a collective is pending) ---------------------------
+    def _check_coordinator(self, members: list[str]):
+        n = self.node
+        alive = set(n.membership.alive())
+
+        def check():
+            if not n.alive_flag:
+                raise RoundAbandoned("node stopping")
+            if not n.is_coordinator:
+                raise RoundAbandoned("no longer coordinator")
+            dead = [m for m in members if m not in alive and not n.membership.is_alive(m)]
+            if dead:
+                raise RoundAbandoned(f"member(s) {dead} failed")
+        return check
+
+    def _check_member(self, coordinator: str):
+        n = self.node
+
+        def check():
+            if not n.alive_flag:
+                raise RoundAbandoned("node stopping")
+            if self._pending_form is not None:
+                raise RoundAbandoned("newer epoch announced")
+            if coordinator != n.name and not n.membership.is_alive(coordinator):
+                raise RoundAbandoned(f"coordinator {coordinator} failed")
+        return check
+
     # -- driver thread ---------------------------------------------------------------------
-    def _run_chunk(self, model: str, s: int, e: int):
+    def _run_chunk(self, model: str, s: int, e: int, packed=None):
+        """This member's chunk of a round.  On a GPU executor the packed top-1
+        pairs go straight into ``packed`` (the gather's send buffer) and None
+        is returned; otherwise (cls, prob) host arrays."""
         n = self.node
         delay = self.cfg.worker_start_delay_s + n.extra_delay_s
         if delay:
@@ -108,10 +150,17 @@ class RoundPlane:
         with n.tracer.span("round.stage", **tags):
             imgs = n.source.get(s, e) if n.source is not None else None
         with n.tracer.span("round.compute", **tags):
-            cls, prob = n.executor.run(model, imgs, s, e)
+            run_packed = getattr(n.executor, "run_packed", None)
+            if run_packed is not None and packed is not None and imgs is not None and \
+                    imgs.device.type == "cuda" and packed.device == imgs.device:
+                run_packed(model, imgs, packed[:e - s + 1])
+                out = None
+            else:
+                cls, prob = n.executor.run(model, imgs, s, e)
+                out = np.ascontiguousarray(cls, np.int32), np.ascontiguousarray(prob, np.float32)
         n.chunks_done += 1
         self._last_compute = time.perf_counter() - t0
-        return np.ascontiguousarray(cls, np.int32), np.ascontiguousarray(prob, np.float32)
+        return out
 
     def _driver(self) -> None:
         n = self.node
@@ -130,10 +179,13 @@ class RoundPlane:
                 self._drop_group()
         self._drop_group()
 
-    def _drop_group(self) -> None:
+    def _drop_group(self, abandoned: bool = False) -> None:
         with self.lock:
             self.healthy = False
-        self.group.teardown()
+        if abandoned:
+            self.group.abort_async()          # collectives may still be pending on dead peers
+        else:
+            self.group.teardown()
 
     # coordinator -------------------------------------------------------------------------
     def _coordinator_step(self) -> None:
@@ -158,24 +210,29 @@ class RoundPlane:
             if members != self.group.members:
                 self._fallback(model, qnum, table, members)
                 continue
+            t0 = time.perf_counter()
             try:
-                out = self.group.round(table, self._run_chunk)
+                out = self.group.round(table, self._run_chunk, check=self._check_coordinator(members))
             except Exception as e:  # noqa: BLE001
                 self.rounds_failed += 1
                 log.warning("%s: round failed in epoch %d (%s); falling back to TCP", n.name, self.group.epoch, e)
                 n.tracer.instant("round.failed", epoch=self.group.epoch, q=qnum)
-                self._drop_group()
+                self._drop_group(abandoned=True)
                 self._fallback(model, qnum, table, members)
                 self._flush_queue_to_tcp()
-                # the failure detector re-forms on a death; re-form anyway in case it was transient
-                self.schedule_reform("round failure", delay=self.cfg.failure_timeout_s * 1.5)
+                # the failure detector re-forms on a death; re-form anyway in case it was
+                # transient -- after the detector had time to drop a dead member
+                self.schedule_reform("round failure", delay=self.cfg.failure_timeout_s * 1.2)
                 return
+            round_s = time.perf_counter() - t0
             self.rounds_done += 1
             now = time.time()
             for row, cls, prob in out:
                 w = members[table.index(row)]
+                # the members run in parallel: the round's wall time is each chunk's
+                # (stage + compute) time as the fair-time scheduler measures it
                 res = {"t": Type.RESULT, "model": model, "qnum": qnum, "start": row[2], "end": row[3],
-                       "worker": w, "cls": cls.tobytes(), "prob": prob.tobytes(), "compute_s": 0.0,
+                       "worker": w, "cls": cls.tobytes(), "prob": prob.tobytes(), "compute_s": round_s,
                        "epoch": n.membership.epoch, "t_done": now}
                 n._ingest_result(dict(res, src=n.name))
                 if n.standby != n.name and n.membership.is_alive(n.standby):
@@ -183,12 +240,14 @@ class RoundPlane:
 
     def _reform(self) -> None:
         n = self.node
+        abandoned = False
         if self.group.formed:
             try:                                   # let members leave the old epoch cleanly
-                self.group.round([(0, 0, STOP, NO_WORK)] * len(self.group.members), self._run_chunk)
+                self.group.round([(0, 0, STOP, NO_WORK)] * len(self.group.members), self._run_chunk,
+                                 check=self._check_coordinator(self.group.members))
             except Exception:  # noqa: BLE001
-                pass
-        self._drop_group()
+                abandoned = True
+        self._drop_group(abandoned=abandoned)
         self._flush_queue_to_tcp()
         members = [n.name] + [m for m in n.membership.alive() if m != n.name]
         with self.lock:
@@ -240,15 +299,18 @@ class RoundPlane:
             self.epoch, self.members = epoch, members
         if not self.group.form(n.name, members, epoch, self.cfg.host, port):
             return
+        check = self._check_member(members[0])
+        abandoned = False
         while n.alive_flag:
             try:
-                r = self.group.round(None, self._run_chunk)
+                r = self.group.round(None, self._run_chunk, check=check)
             except Exception as e:  # noqa: BLE001
                 log.info("%s: left epoch %d (%s)", n.name, epoch, e)
+                abandoned = True
                 break
             if r == "stop":
                 break
             self.rounds_done += 1
-        self._drop_group()
+        self._drop_group(abandoned=abandoned)
         if self._pending_form is not None:
             self._wake.set()
