@@ -16,6 +16,16 @@ Deliberate fixes:
   A11 query numbers are coordinator-assigned
   A13 single writer: every mutation goes through this object under one lock,
       and result ingestion is idempotent by chunk key (model, qnum, start, end)
+
+Standby replication (reference send_metadata pushes str() dumps
+of every table every second, mp4_machinelearning.py:971-1011): every mutation
+bumps ``seq`` and appends ``(seq, op, args)`` to a bounded log.  The
+coordinator pushes only the entries after the standby's acknowledged sequence
+number (``deltas_since``); the standby applies them in order
+(``apply_deltas``) and asks for a full snapshot only when it sees a gap or the
+log has been truncated past its position.  Queries whose chunks are all
+finished leave the open-query index, so ``pending()`` and the scheduler's
+per-submit scans are O(open work), not O(history).
 """
 from __future__ import annotations
 
@@ -113,7 +123,105 @@ class JobState:
         self.query_submit_time: dict = {}
         self.query_latency: dict = defaultdict(list)    # model -> [end-to-end seconds]
         self.jobs: dict = {}                            # job id -> {model, start, end, next}
+        # compaction indexes: (model, qnum) -> number of 'w' entries (only open queries),
+        # and the (model, first start, last end) span of every submitted query
+        self._open: dict = {}
+        self._spans: set = set()
+        # replication log: (seq, op, args) for every mutation since log_base
+        self._log: list = []
+        self._log_base = 0                              # seq of the entry before _log[0]
+        self.log_cap = 100_000
+        self.mirror_seq = 0                             # standby: last coordinator seq applied
         racecheck.instrument(self, self._TABLES)
+
+    # -- replication log ------------------------------------------------------------
+    def _bump(self, op: str, *args) -> None:
+        """One mutation: seq + 1 and its log entry (caller holds the lock)."""
+        self.seq += 1
+        self._log.append((self.seq, op, args))
+        if len(self._log) > self.log_cap:              # truncate: a standby that far behind re-syncs
+            drop = len(self._log) - self.log_cap // 2
+            self._log_base = self._log[drop - 1][0]
+            del self._log[:drop]
+
+    def deltas_since(self, seq: int) -> list | None:
+        """Log entries after ``seq`` (oldest first), or None when the log no
+        longer reaches back that far (the caller sends a full snapshot)."""
+        with self.lock:
+            if seq >= self.seq:
+                return []
+            if seq < self._log_base or not self._log:
+                return None
+            i = seq - self._log_base                    # entries are consecutive seqs
+            if i < 0 or i >= len(self._log) or self._log[i][0] != seq + 1:
+                return None
+            return [list(e) for e in self._log[i:]]
+
+    def _open_add(self, key, n: int) -> None:
+        v = self._open.get(key, 0) + n
+        if v > 0:
+            self._open[key] = v
+        else:
+            self._open.pop(key, None)
+
+    def _mark_finished(self, key, start: int, end: int, now: float):
+        """'w' -> 'f' for the chunk [start, end] of query ``key``; returns the
+        (worker, t_start) of the entry it closed, or None."""
+        entries = self.worker_set.get(key, [])
+        for i, ent in enumerate(entries):
+            if ent[1] == start and ent[2] == end and ent[3] == "w":
+                w, s, e, _, t_start, _ = ent
+                entries[i] = (w, s, e, "f", t_start, now)
+                try:
+                    self.working_vm_set[w].remove((key[0], key[1], s, e))
+                except ValueError:
+                    pass
+                if not self.working_vm_set[w]:
+                    self.working_vm_set.pop(w, None)
+                self._open_add(key, -1)
+                return w, t_start
+        return None
+
+    def apply_deltas(self, entries: list) -> bool:
+        """Standby: apply coordinator log entries in order (entries at or below
+        ``mirror_seq`` are skipped, so re-sends are harmless).  Returns False on
+        a gap (the coordinator then sends a full snapshot)."""
+        with self.lock:
+            for seq, op, args in entries:
+                if seq <= self.mirror_seq:
+                    continue
+                if seq != self.mirror_seq + 1:
+                    return False
+                self._apply_one(op, args)
+                self.mirror_seq = seq
+            return True
+
+    def _apply_one(self, op: str, args) -> None:
+        if op == "qnum":
+            m, v = args
+            self.next_qnum[m] = max(self.next_qnum.get(m, 0), int(v))
+        elif op == "job":
+            jid, job, (m, v) = args
+            cur = self.jobs.get(jid)
+            if cur is None or job["next"] > cur["next"]:
+                self.jobs[jid] = dict(job)
+            self.next_qnum[m] = max(self.next_qnum.get(m, 0), int(v))
+        elif op == "advance":
+            jid, nxt = args
+            if jid in self.jobs:
+                self.jobs[jid]["next"] = max(self.jobs[jid]["next"], int(nxt))
+        elif op == "assign":
+            model, qnum, chunks, now = args
+            self._assign_locked(model, qnum, chunks, now, emit=False)
+        elif op == "result":
+            model, qnum, start, end, now = args
+            self._mark_finished((model, qnum), int(start), int(end), now)
+        elif op == "reassign":
+            failed, new_worker, chunk, now = args
+            self._reassign_locked(failed, new_worker, tuple(chunk), now, emit=False)
+        elif op == "reopen":
+            self._reopen_locked(emit=False)
+        # "noop" (a duplicate result) changes nothing
 
     # -- coordinator-side jobs (C28 variant), replicated to the standby ----------
     def add_job(self, model: str, start: int, end: int, bs: int | None = None) -> int:
@@ -131,7 +239,7 @@ class JobState:
             self.next_qnum[model] += nq
             self.jobs[jid] = {"model": model, "start": int(start), "end": int(end), "next": int(start),
                               "bs": bs, "qbase": qbase}
-            self.seq += 1
+            self._bump("job", jid, dict(self.jobs[jid]), (model, self.next_qnum[model]))
             return jid
 
     def images_held(self, model: str, qnum, s: int, e: int) -> bool:
@@ -147,7 +255,7 @@ class JobState:
     def advance_job(self, jid: int, nxt: int) -> None:
         with self.lock:
             self.jobs[jid]["next"] = int(nxt)
-            self.seq += 1
+            self._bump("advance", jid, int(nxt))
 
     def unfinished_jobs(self) -> list[int]:
         with self.lock:
@@ -157,16 +265,14 @@ class JobState:
         """True if some query of ``model`` already covers exactly [s, e] chunks
         (used when a promoted standby resumes a job from a lagging snapshot)."""
         with self.lock:
-            for (m, _q), ents in self.worker_set.items():
-                if m == model and ents and min(x[1] for x in ents) == s and max(x[2] for x in ents) == e:
-                    return True
-            return False
+            return (model, int(s), int(e)) in self._spans
 
     # -- ids --------------------------------------------------------------------
     def new_query_number(self, model: str) -> int:
         """Coordinator-assigned query number (fix A11; the reference counted on the client)."""
         with self.lock:
             self.next_qnum[model] += 1
+            self._bump("qnum", model, self.next_qnum[model])
             return self.next_qnum[model]
 
     # -- mutations --------------------------------------------------------------
@@ -174,12 +280,24 @@ class JobState:
         """Record a dispatched query: chunks = [(worker, start, end), ...]."""
         now = self.clock() if now is None else now
         with self.lock:
-            key = (model, qnum)
-            self.query_submit_time.setdefault(key, now)
-            for w, s, e in chunks:
-                self.worker_set[key].append((w, int(s), int(e), "w", now, now))
-                self.working_vm_set[w].append((model, qnum, int(s), int(e)))
-            self.seq += 1
+            self._assign_locked(model, qnum, chunks, now, emit=True)
+
+    def _assign_locked(self, model, qnum, chunks, now, emit: bool) -> None:
+        key = (model, qnum)
+        chunks = [(w, int(s), int(e)) for w, s, e in chunks]
+        self.query_submit_time.setdefault(key, now)
+        ents = self.worker_set[key]
+        for w, s, e in chunks:
+            if (model, qnum, s, e) in self._done_keys:      # mirror: result already held
+                ents.append((w, s, e, "f", now, now))
+                continue
+            ents.append((w, s, e, "w", now, now))
+            self.working_vm_set[w].append((model, qnum, s, e))
+            self._open_add(key, 1)
+        if ents:
+            self._spans.add((model, min(x[1] for x in ents), max(x[2] for x in ents)))
+        if emit:
+            self._bump("assign", model, qnum, [list(c) for c in chunks], now)
 
     def record_result(self, model: str, qnum, worker: str, start: int, end: int, cls, prob,
                       now: float | None = None) -> bool:
@@ -191,27 +309,14 @@ class JobState:
             ck = (model, qnum, start, end)
             key = (model, qnum)
             entries = self.worker_set.get(key, [])
-            was_done = bool(entries) and all(ent[3] == "f" for ent in entries)
-            hit = None
-            for i, ent in enumerate(entries):
-                if ent[1] == start and ent[2] == end and ent[3] == "w":
-                    hit = i
-                    break
-            t_start = now
-            if hit is not None:
-                w, s, e, _, t_start, _ = entries[hit]
-                entries[hit] = (w, s, e, "f", t_start, now)
-                try:
-                    self.working_vm_set[w].remove((model, qnum, s, e))
-                except ValueError:
-                    pass
-                if not self.working_vm_set[w]:
-                    self.working_vm_set.pop(w, None)
+            was_done = bool(entries) and key not in self._open
             # a duplicate still closes a matching 'w' entry (a re-dispatch with the
             # same chunk boundaries as the answered original) before it is dropped
+            hit = self._mark_finished(key, start, end, now)
+            t_start = hit[1] if hit is not None else now
             dup = ck in self._done_keys
             self._done_keys.add(ck)
-            if entries and not was_done and all(ent[3] == "f" for ent in entries):
+            if entries and not was_done and key not in self._open:
                 self.finished_queries[model] += 1
                 t0 = self.query_submit_time.get(key)
                 if t0 is not None:
@@ -220,7 +325,7 @@ class JobState:
             # (re-dispatch after a failure / a resumed job) are not counted again
             n = 0 if dup else _add_interval(self._done_imgs[key], start, end)   # fix A3: end-start+1 when new
             if n == 0:
-                self.seq += 1
+                self._bump("result" if hit is not None else "noop", model, qnum, start, end, now)
                 return False
             self.finished_images[model] += n
             self._rate_win[model].append((now, n))
@@ -231,7 +336,7 @@ class JobState:
             self.results[f"{model} {qnum}"].append(
                 ChunkResult(start, end, np.asarray(cls, dtype=np.int32), np.asarray(prob, dtype=np.float32),
                             worker))
-            self.seq += 1
+            self._bump("result", model, qnum, start, end, now)
             return True
 
     def reopen_unheld(self) -> int:
@@ -240,17 +345,21 @@ class JobState:
         go back to 'w', so a promoted standby recomputes them instead of
         reporting a query done whose results it cannot show (c4)."""
         with self.lock:
-            n = 0
-            for (m, q), ents in self.worker_set.items():
-                ivs = self._done_imgs.get((m, q), [])
-                for i, (w, s, e, st, t0, t1) in enumerate(ents):
-                    if st == "f" and not any(a <= s and e <= b for a, b in ivs):
-                        ents[i] = (w, s, e, "w", t0, t1)
-                        self.working_vm_set[w].append((m, q, s, e))
-                        n += 1
-            if n:
-                self.seq += 1
-            return n
+            return self._reopen_locked(emit=True)
+
+    def _reopen_locked(self, emit: bool) -> int:
+        n = 0
+        for (m, q), ents in self.worker_set.items():
+            ivs = self._done_imgs.get((m, q), [])
+            for i, (w, s, e, st, t0, t1) in enumerate(ents):
+                if st == "f" and not any(a <= s and e <= b for a, b in ivs):
+                    ents[i] = (w, s, e, "w", t0, t1)
+                    self.working_vm_set[w].append((m, q, s, e))
+                    self._open_add((m, q), 1)
+                    n += 1
+        if n and emit:
+            self._bump("reopen")
+        return n
 
     def chunks_of(self, worker: str) -> list[tuple]:
         with self.lock:
@@ -260,33 +369,43 @@ class JobState:
         """Move one in-flight chunk of a failed worker to ``new_worker``
         (reference transfer_failed_inference_work, mp4_machinelearning.py:706-760)."""
         now = self.clock() if now is None else now
-        model, qnum, s, e = chunk
         with self.lock:
-            key = (model, qnum)
-            ents = self.worker_set.get(key, [])
-            for i, ent in enumerate(ents):
-                if ent[0] == failed and ent[1] == s and ent[2] == e and ent[3] == "w":
-                    ents.pop(i)
-                    break
-            ents.append((new_worker, s, e, "w", now, now))
-            try:
-                self.working_vm_set[failed].remove(chunk)
-            except (ValueError, KeyError):
-                pass
-            if not self.working_vm_set.get(failed):
-                self.working_vm_set.pop(failed, None)
-            self.working_vm_set[new_worker].append(chunk)
-            self.seq += 1
+            self._reassign_locked(failed, new_worker, tuple(chunk), now, emit=True)
+
+    def _reassign_locked(self, failed, new_worker, chunk, now, emit: bool) -> None:
+        model, qnum, s, e = chunk
+        key = (model, qnum)
+        ents = self.worker_set[key]
+        for i, ent in enumerate(ents):
+            if ent[0] == failed and ent[1] == s and ent[2] == e and ent[3] == "w":
+                ents.pop(i)
+                self._open_add(key, -1)
+                break
+        ents.append((new_worker, s, e, "w", now, now))
+        self._open_add(key, 1)
+        try:
+            self.working_vm_set[failed].remove(chunk)
+        except (ValueError, KeyError):
+            pass
+        if not self.working_vm_set.get(failed):
+            self.working_vm_set.pop(failed, None)
+        self.working_vm_set[new_worker].append(chunk)
+        if emit:
+            self._bump("reassign", failed, new_worker, list(chunk), now)
 
     def pending(self) -> list[tuple]:
         """All chunks still marked 'w': [(model, qnum, worker, s, e, t_start)]."""
         with self.lock:
             out = []
-            for (model, q), ents in self.worker_set.items():
-                for w, s, e, st, t0, _ in ents:
+            for (model, q) in self._open:
+                for w, s, e, st, t0, _ in self.worker_set.get((model, q), []):
                     if st == "w":
                         out.append((model, q, w, s, e, t0))
             return out
+
+    def pending_count(self) -> int:
+        with self.lock:
+            return sum(self._open.values())
 
     # -- metrics ------------------------------------------------------------------
     def _expire(self, model: str, now: float) -> None:
@@ -321,7 +440,7 @@ class JobState:
         tables are appended to by the result-ingest threads meanwhile)."""
         with self.lock:
             return {"ok": True, "done": {m: self.images_done(m) for m in self.models()},
-                    "pending": len(self.pending()),
+                    "pending": self.pending_count(),
                     "latency": {m: list(v) for m, v in self.query_latency.items()},
                     "finished_queries": dict(self.finished_queries)}
 
@@ -417,6 +536,7 @@ class JobState:
             if snap["seq"] < self.seq and not keep_results:
                 return
             self.seq = max(self.seq, snap["seq"])
+            self._log, self._log_base = [], self.seq      # history before the snapshot is not in the log
             self.worker_set = defaultdict(list)
             for k, v in snap["worker_set"]:
                 self.worker_set[(k[0], k[1])] = [tuple(e) for e in v]
@@ -448,6 +568,16 @@ class JobState:
                             pass
             for w in [w for w, v in self.working_vm_set.items() if not v]:
                 self.working_vm_set.pop(w)
+            self._open = {}
+            self._spans = set()
+            for key, ents in self.worker_set.items():
+                nw = sum(1 for ent in ents if ent[3] == "w")
+                if nw:
+                    self._open[key] = nw
+                if ents:
+                    self._spans.add((key[0], min(x[1] for x in ents), max(x[2] for x in ents)))
+            if keep_results:
+                self.mirror_seq = int(snap["seq"])        # deltas continue from the snapshot
             for m, n in snap["next_qnum"].items():
                 self.next_qnum[m] = max(self.next_qnum.get(m, 0), n)
             self.query_processing_time_meta.update(snap["meta"])

@@ -63,6 +63,8 @@ class Node:
         self.standby = cfg.standby_name
         self.alive_flag = True
         self.meta_seq = -1
+        self._standby_ack: tuple | None = None     # (epoch, seq) the standby has applied; None = re-sync
+        self.meta_bytes = 0                        # bytes of the last METADATA push (delta size check)
         self.chunks_done = 0
         self.logger = self._make_logger()
         self._stop = threading.Event()
@@ -179,8 +181,7 @@ class Node:
             self._ingest_result(msg)
             return None
         if t == Type.METADATA:
-            self._apply_metadata(msg)
-            return None
+            return self._apply_metadata(msg)
         if t == Type.STATS:
             return self._stats(msg.get("view", "c1"))
         if t == Type.GREP:
@@ -457,20 +458,54 @@ class Node:
                 last_ckpt = time.monotonic()
 
     def push_metadata(self) -> bool:
-        snap = {"t": Type.METADATA, "seq": self.state.seq, "epoch": self.membership.epoch,
-                "jobs": self.state.snapshot(include_results=False), "sdfs": self.sdfs.snapshot(),
-                "avg_time": dict(self.sched.avg_time)}
-        return self.transport.send(self.standby, snap)
+        """Replicate the job state to the hot standby: the job-table mutations
+        since the standby's last acknowledged sequence number (a full snapshot
+        only on first contact, after a gap, or when the log was truncated),
+        plus the small SDFS / scheduler tables.  Request/reply, so the ack
+        drives the next push (reference: a full str() dump every second,
+        mp4_machinelearning.py:971-987)."""
+        import msgpack
 
-    def _apply_metadata(self, msg: dict) -> None:
+        epoch = self.membership.epoch
+        ack = self._standby_ack
+        deltas = None
+        if ack is not None and ack[0] == epoch:
+            deltas = self.state.deltas_since(ack[1])
+        msg = {"t": Type.METADATA, "seq": self.state.seq, "epoch": epoch, "sdfs": self.sdfs.snapshot(),
+               "avg_time": dict(self.sched.avg_time)}
+        if deltas is None:
+            msg.update(kind="snapshot", jobs=self.state.snapshot(include_results=False))
+        else:
+            msg.update(kind="delta", base=ack[1], deltas=deltas)
+        self.meta_bytes = len(msgpack.packb(msg, use_bin_type=True))
+        try:
+            r = self.transport.request(self.standby, msg, self.cfg.rpc_timeout_s)
+        except TransportError:
+            return False
+        if r and r.get("ok"):
+            self._standby_ack = (epoch, int(r["seq"]))
+            return True
+        self._standby_ack = None if not r or r.get("resync") else (epoch, int(r.get("seq", 0)))
+        return False
+
+    def _apply_metadata(self, msg: dict) -> dict:
         if self.is_coordinator:
-            return
-        if msg.get("epoch", 0) < self.membership.epoch:
-            return
-        self.state.restore(msg["jobs"], keep_results=True)
+            return {"ok": False, "resync": True, "error": "coordinator does not mirror"}
+        epoch = int(msg.get("epoch", 0))
+        if epoch < self.membership.epoch:
+            return {"ok": False, "resync": True, "error": "stale epoch"}
+        if msg.get("kind", "snapshot") == "snapshot":
+            self.state.restore(msg["jobs"], keep_results=True)
+            self._mirror_epoch = epoch
+        else:
+            if getattr(self, "_mirror_epoch", None) != epoch or int(msg["base"]) > self.state.mirror_seq:
+                return {"ok": False, "resync": True, "seq": self.state.mirror_seq}
+            if not self.state.apply_deltas(msg["deltas"]):
+                return {"ok": False, "resync": True, "seq": self.state.mirror_seq}
         self.sdfs.restore(msg["sdfs"])
         self.sched.avg_time.update(msg.get("avg_time", {}))
-        self.meta_seq = msg.get("seq", 0)
+        self.meta_seq = self.state.mirror_seq
+        return {"ok": True, "seq": self.state.mirror_seq}
 
     def _on_master_failure(self, old: str) -> None:
         if self.name == self.standby:
@@ -485,6 +520,7 @@ class Node:
         self.logger.warning("%s promoting to coordinator (epoch %d): %s", self.name, epoch, why)
         self.membership.become_master(epoch)
         self.promotions += 1
+        self._standby_ack = None
         for n in self.membership.alive():
             if n not in (self.name, old):
                 self.transport.send(n, {"t": Type.PROMOTE, "epoch": epoch})

@@ -214,3 +214,23 @@ def test_executor_failure_retried_elsewhere():
         check_results(cl, "resnet18", 0, 399)
     finally:
         c.stop()
+
+
+def test_standby_mirrors_by_deltas(cluster):
+    """After the first full snapshot the coordinator pushes only the job-table
+    mutations since the standby's ack; the standby's mirror catches up."""
+    coord = cluster.coordinator()
+    sb = cluster.nodes[coord.standby]
+    cl = cluster.client()
+    cl.inference(0, 3999, "resnet18")
+    cl.wait_idle(10, {"resnet18": 4000})
+    synced = lambda: sb.state.mirror_seq == coord.state.seq and coord._standby_ack == (0, coord.state.seq)  # noqa: E731
+    assert wait_for(synced, 5), (sb.state.mirror_seq, coord.state.seq, coord._standby_ack)
+    big = coord.meta_bytes
+    cl.inference(4000, 4399, "resnet18")
+    cl.wait_idle(10, {"resnet18": 4400})
+    assert wait_for(synced, 5)
+    # one query = a few log entries; the push no longer carries the 11 earlier queries
+    assert coord.meta_bytes < 8000, coord.meta_bytes
+    assert sorted(q for q in sb.state.worker_set) == sorted(q for q in coord.state.worker_set)
+    assert big >= 0
