@@ -60,39 +60,54 @@ class SyntheticSource:
         if self.device.type == "cuda":
             from .. import ops
 
-            return ops.synth_images(self.seed, start, n, self.device)
+            with torch.cuda.device(self.device):       # the kernel runs on this device's current stream
+                return ops.synth_images(self.seed, start, n, self.device)
         return torch.from_numpy(synth_images_cpu(self.seed, start, n))
 
 
 class HbmStager:
-    """Host -> HBM staging through pinned memory on a side stream."""
+    """Host -> HBM staging through pinned memory on a side stream.
 
-    def __init__(self, device: torch.device, pinned_bytes: int = 64 << 20):
+    Two pinned buffers in ping-pong: while the DMA engine copies piece k out of
+    one buffer (hipMemcpyAsync on the side stream), the host fills piece k+1
+    into the other; a buffer is reused only after the event of ITS last copy,
+    so the host memcpy and the DMA overlap instead of alternating."""
+
+    def __init__(self, device: torch.device, pinned_bytes: int = 64 << 20, nbuf: int = 2):
         self.device = torch.device(device)
         self.gpu = self.device.type == "cuda"
         self.stream = torch.cuda.Stream(device=self.device) if self.gpu else None
-        self.pinned = torch.empty(pinned_bytes, dtype=torch.uint8, pin_memory=self.gpu)
+        per = max(1 << 20, pinned_bytes // nbuf)
+        self.pinned = [torch.empty(per, dtype=torch.uint8, pin_memory=self.gpu) for _ in range(nbuf)]
+        self._done = [None] * nbuf        # event of the last copy out of each buffer
         self.lock = threading.Lock()
 
     def stage(self, data: bytes | np.ndarray, shape: tuple) -> torch.Tensor:
-        """Copy host bytes to a new device tensor of ``shape`` (uint8)."""
+        """Copy host bytes to a new device tensor of ``shape`` (uint8).  The
+        current stream is made to wait for the copy; nothing blocks the host
+        beyond the ping-pong buffer reuse."""
         src = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) \
             else np.ascontiguousarray(data).reshape(-1).view(np.uint8)
         if not self.gpu:
             return torch.from_numpy(src.copy()).view(*shape)
         out = torch.empty(src.size, dtype=torch.uint8, device=self.device)
-        step = self.pinned.numel()
+        step = self.pinned[0].numel()
+        nb = len(self.pinned)
         with self.lock:
-            for off in range(0, src.size, step):
+            ev = None
+            for i, off in enumerate(range(0, src.size, step)):
+                b = i % nb
                 n = min(step, src.size - off)
-                # wait until the previous async copy out of `pinned` has drained
-                self.stream.synchronize()
-                self.pinned[:n].numpy()[:] = src[off:off + n]
+                if self._done[b] is not None:
+                    self._done[b].synchronize()     # the DMA that last read buffer b has finished
+                self.pinned[b][:n].numpy()[:] = src[off:off + n]
                 with torch.cuda.stream(self.stream):
-                    out[off:off + n].copy_(self.pinned[:n], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(self.stream)
-        torch.cuda.current_stream(self.device).wait_event(ev)
+                    out[off:off + n].copy_(self.pinned[b][:n], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.stream)
+                self._done[b] = ev
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
         return out.view(*shape)
 
 

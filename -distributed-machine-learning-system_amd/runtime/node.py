@@ -71,6 +71,9 @@ class Node:
         self._threads: list[threading.Thread] = []
         self.promotions = 0
         self._retries: dict = {}
+        self._pf: dict = {}                         # (start, end) -> Future of staged images
+        self._pf_lock = threading.Lock()
+        self._pf_pool = None
         self.tracer = Tracer(name)
         self.device = getattr(executor, "device", None)  # GPU of this node (None = CPU)
         self.rounds = None                          # collective round plane (cfg.collective_rounds)
@@ -553,6 +556,54 @@ class Node:
             self.rounds.schedule_reform(f"promoted (epoch {epoch})", delay=0.5)
 
     # -- worker ---------------------------------------------------------------------------
+    def _prefetch_next(self) -> None:
+        """Stage the images of the next queued JOB on a helper thread while the
+        current chunk computes (SURVEY.md §2.7 "double-buffered staging"): the
+        SDFS shard fetch + host->HBM copy of chunk k+1 overlaps the forward of
+        chunk k.  At most one chunk ahead."""
+        if self.source is None or not self.cfg.prefetch:
+            return
+        with self.jobs.mutex:
+            nxt = next((m for m in self.jobs.queue if m is not None), None)
+        if nxt is None:
+            return
+        key = (int(nxt["start"]), int(nxt["end"]))
+        with self._pf_lock:
+            if key in self._pf or len(self._pf) >= 2:
+                return
+            if self._pf_pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+
+                self._pf_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"{self.name}-prefetch")
+            tags = dict(model=nxt["model"], q=nxt["qnum"], start=key[0], end=key[1], prefetch=True)
+
+            dev = self.device
+
+            def stage():
+                import contextlib
+
+                import torch
+
+                ctx = torch.cuda.device(dev) if dev is not None and torch.device(dev).type == "cuda" \
+                    else contextlib.nullcontext()
+                with ctx, self.tracer.span("chunk.stage", **tags):
+                    imgs = self.source.get(*key)
+                    if imgs is not None and imgs.device.type == "cuda":
+                        torch.cuda.current_stream(imgs.device).synchronize()   # staged before handing over
+                    return imgs
+            self._pf[key] = self._pf_pool.submit(stage)
+
+    def _staged(self, s: int, e: int):
+        """Images of [s, e]: the prefetched tensor if one is ready or in flight."""
+        with self._pf_lock:
+            fut = self._pf.pop((s, e), None)
+        if fut is not None:
+            try:
+                return fut.result()
+            except Exception:  # noqa: BLE001  (fall through to a direct fetch)
+                self.logger.exception("prefetch of [%d,%d] failed", s, e)
+        return self.source.get(s, e) if self.source is not None else None
+
     def _worker_loop(self) -> None:
         while not self._stop.is_set():
             msg = self.jobs.get()
@@ -577,7 +628,8 @@ class Node:
         t0 = time.perf_counter()
         tags = dict(model=model, q=msg["qnum"], start=s, end=e)
         with self.tracer.span("chunk.stage", **tags):
-            imgs = self.source.get(s, e) if self.source is not None else None
+            imgs = self._staged(s, e)
+        self._prefetch_next()                 # next JOB's images stage while this one computes
         with self.tracer.span("chunk.compute", **tags):
             cls, prob = self.executor.run(model, imgs, s, e)
         dt = time.perf_counter() - t0
