@@ -508,24 +508,27 @@ class HipRunner:
             gc.collect()
 
     # -- hipGraph -------------------------------------------------------------
-    def capture(self, batch: int, hw: int = 224):
-        """Capture forward for a fixed batch; returns (static_in, replay_fn)."""
-        if batch in self._graphs:
-            g, sin, sout = self._graphs[batch]
-            return sin, self._replayer(g, sout)
+    def capture(self, batch: int, hw: int = 224, packed: torch.Tensor | None = None):
+        """Capture forward for a fixed batch; returns (static_in, replay_fn).
+        With ``packed`` the graph also writes (class, prob bits) pairs into
+        that caller-owned buffer (e.g. a collective round's send buffer)."""
+        key = batch if packed is None else ("pk", batch, packed.data_ptr())
+        if key in self._graphs:
+            g, sin, sout = self._graphs[key]
+            return sin, self._replayer(g, sout, packed)
         sin = torch.zeros(batch, hw, hw, 3, dtype=torch.uint8, device=self.device)
         with _CAPTURE_LOCK:  # one capture at a time per process; other threads keep launching
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):
                 for _ in range(2):
-                    self.forward(sin)
+                    self.forward(sin, packed=packed)
             torch.cuda.current_stream(self.device).wait_stream(s)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                sout = self.forward(sin)
-        self._graphs[batch] = (g, sin, sout)
-        return sin, self._replayer(g, sout)
+                sout = self.forward(sin, packed=packed)
+        self._graphs[key] = (g, sin, sout)
+        return sin, self._replayer(g, sout, packed)
 
     def flops_per_image(self) -> float:
         """Useful (unpadded) FLOPs for one 224x224 image."""

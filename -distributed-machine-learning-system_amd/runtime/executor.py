@@ -160,10 +160,17 @@ class HipExecutor(Executor):
         ``packed`` (the RCCL gather's send buffer) on the current stream's
         order; nothing comes back to the host."""
         r = self.runner(model)
+        n = images.shape[0]
         with torch.cuda.device(self.device), self.run_lock:
             s = self._enter(images)
             with torch.cuda.stream(s):
-                r.forward(images.contiguous(), packed=packed)
+                key = ("pk", n, packed.data_ptr())
+                if not self.closed and ((self.use_graphs and len(r._graphs) < self.max_graphs) or key in r._graphs):
+                    sin, replay = r.capture(n, packed=packed)
+                    sin.copy_(images)
+                    replay()
+                else:
+                    r.forward(images.contiguous(), packed=packed)
             torch.cuda.current_stream(self.device).wait_stream(s)
 
 

@@ -156,6 +156,7 @@ class Node:
         self.membership.stop()
         if self.rounds is not None:
             self.rounds.stop()
+            self.rounds.join(timeout=5.0)
         self.jobs.put(None)
         self.transport.close()
         close = getattr(self.executor, "close", None)

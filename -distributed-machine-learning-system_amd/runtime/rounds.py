@@ -59,6 +59,7 @@ class RoundPlane:
         self.rounds_failed = 0
         self._reform_at: float | None = None
         self._pending_form: dict | None = None
+        self._released = False
         self._wake = threading.Event()
         self._thread: threading.Thread | None = None
 
@@ -68,6 +69,26 @@ class RoundPlane:
 
     def stop(self) -> None:
         self._wake.set()
+
+    def join(self, timeout: float = 5.0) -> None:
+        """Wait for the driver thread and any background epoch abort to end
+        (a process must not exit while a communicator is being torn down)."""
+        th = self._thread
+        if th is not None and th is not threading.current_thread():
+            th.join(timeout)
+        self.group._join_aborter(timeout)
+
+    def release(self, timeout: float = 10.0) -> bool:
+        """Coordinator: end the epoch cleanly (a STOP round lets every member
+        leave its round loop and destroy the group) and form no new one.
+        Used before a planned shutdown of the whole cluster."""
+        done = threading.Event()
+        with self.lock:
+            self.healthy = False
+            self._released = True
+        self.q.put(("__release__", done))
+        self._wake.set()
+        return done.wait(timeout)
 
     # -- triggers (any thread) ----------------------------------------------------------
     def schedule_reform(self, reason: str, delay: float = 0.2) -> None:
@@ -191,7 +212,7 @@ class RoundPlane:
     def _coordinator_step(self) -> None:
         n = self.node
         with self.lock:
-            due = self._reform_at is not None and time.monotonic() >= self._reform_at
+            due = self._reform_at is not None and time.monotonic() >= self._reform_at and not self._released
             if due:
                 self._reform_at = None
         if due:
@@ -204,9 +225,14 @@ class RoundPlane:
             return
         while n.alive_flag and self._reform_at is None:
             try:
-                model, qnum, table, members = self.q.get(timeout=0.05)
+                item = self.q.get(timeout=0.05)
             except queue.Empty:
                 return
+            if item[0] == "__release__":
+                self._stop_epoch()
+                item[1].set()
+                return
+            model, qnum, table, members = item
             if members != self.group.members:
                 self._fallback(model, qnum, table, members)
                 continue
@@ -238,16 +264,20 @@ class RoundPlane:
                 if n.standby != n.name and n.membership.is_alive(n.standby):
                     n.transport.send(n.standby, res)
 
-    def _reform(self) -> None:
-        n = self.node
+    def _stop_epoch(self) -> None:
+        """Let members leave the current epoch cleanly (STOP round), then drop it."""
         abandoned = False
         if self.group.formed:
-            try:                                   # let members leave the old epoch cleanly
+            try:
                 self.group.round([(0, 0, STOP, NO_WORK)] * len(self.group.members), self._run_chunk,
                                  check=self._check_coordinator(self.group.members))
             except Exception:  # noqa: BLE001
                 abandoned = True
         self._drop_group(abandoned=abandoned)
+
+    def _reform(self) -> None:
+        n = self.node
+        self._stop_epoch()
         self._flush_queue_to_tcp()
         members = [n.name] + [m for m in n.membership.alive() if m != n.name]
         with self.lock:
@@ -271,9 +301,14 @@ class RoundPlane:
     def _flush_queue_to_tcp(self) -> None:
         while True:
             try:
-                model, qnum, table, members = self.q.get_nowait()
+                item = self.q.get_nowait()
             except queue.Empty:
                 return
+            if item[0] == "__release__":
+                self._stop_epoch()
+                item[1].set()
+                continue
+            model, qnum, table, members = item
             self._fallback(model, qnum, table, members)
 
     def _fallback(self, model, qnum, table, members) -> None:

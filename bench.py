@@ -30,6 +30,12 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
   any rank fails.  Under torchrun (RANK set) it is one rank of the job.
   --dry-run: gloo on the CPU with a fake forward (tests the launcher, the
   collectives and the JSON contract without a GPU).
+  --system: the same metric through the fault-tolerant cluster runtime: every
+  rank runs a Node (membership + failure detector, coordinator on rank 0, hot
+  standby on the last rank), rank 0's client submits the queries to the
+  coordinator, which schedules them (fair-time split) as RCCL rounds over the
+  ranks (N > 1; TCP control plane for N = 1) and ingests the results into the
+  job-state tables.  Prints one JSON line with "mode": "system".
 """
 from __future__ import annotations
 
@@ -66,6 +72,7 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true", help="CPU + gloo + fake forward (launcher/contract test)")
     ap.add_argument("--fail-rank", type=int, default=-1, help="testing: this rank exits 3 after warmup")
     ap.add_argument("--launch-timeout", type=float, default=1500.0, help="self-launch: seconds before ranks are killed")
+    ap.add_argument("--system", action="store_true", help="measure through the node runtime (see docstring)")
     return ap.parse_args(argv)
 
 
@@ -146,6 +153,9 @@ def main(argv=None) -> int:
     a = parse(argv)
     if "RANK" not in os.environ and a.gpus > 1:
         return launch_local(a, argv)
+
+    if a.system:
+        return run_system(a)
 
     import numpy as np
     import torch
@@ -342,6 +352,125 @@ def main(argv=None) -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def run_system(a) -> int:
+    """One rank of the --system measurement (see the module docstring)."""
+    import tempfile
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from idunno.config import ClusterConfig
+    from idunno.runtime.client import Client
+    from idunno.runtime.data import SyntheticSource
+    from idunno.runtime.executor import FakeExecutor, HipExecutor
+    from idunno.runtime.messages import Type
+    from idunno.runtime.node import Node
+    from idunno.runtime.transport import TcpTransport, wait_for
+
+    rank = int(os.environ.get("RANK", "0"))
+    W = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if W != a.gpus:
+        print(json.dumps({"error": f"--gpus {a.gpus} but WORLD_SIZE={W}"}), flush=True)
+        return 2
+    gpu = not a.dry_run and torch.cuda.is_available()
+    if not a.dry_run and not gpu:
+        print(json.dumps({"error": "bench.py --system needs a GPU (MI355X); use --dry-run on CPU"}), flush=True)
+        return 2
+    dev = torch.device("cuda", local) if gpu else torch.device("cpu")
+    if gpu:
+        torch.cuda.set_device(dev)
+    B = a.batch
+    base = int(os.environ.get("MASTER_PORT", "29500")) + 200
+    tmp = tempfile.mkdtemp(prefix=f"idunno_bench_r{rank}_")
+    cfg = ClusterConfig(num_nodes=W, base_port=base, store_root=tmp, collective_rounds=W > 1, dtype=a.dtype,
+                        max_chunk=B, rpc_timeout_s=60.0, worker_budget=W, dataset_size=10 ** 9,
+                        batch_size={a.model: W * B}, collective_port_offset=100)
+    name = cfg.node_name(rank)
+    ex = FakeExecutor() if a.dry_run else HipExecutor(dev, seed=a.seed, dtype=a.dtype)
+    node = Node(cfg, name, TcpTransport(name, cfg.address, cfg.address(name)), ex)
+    node.source = None if a.dry_run else SyntheticSource(cfg.data_seed, dev)
+    if not a.dry_run:
+        ex.warmup(a.model, B)                       # capture before the clock starts
+    if rank != 0:
+        time.sleep(1.0)                             # the coordinator listens first
+    node.start(join=True)
+    if rank != 0:
+        t_end = time.time() + a.launch_timeout
+        while node.alive_flag and time.time() < t_end:
+            time.sleep(0.2)
+        node.stop()
+        return 0
+    cl = Client(node)
+    try:
+        assert wait_for(lambda: len(node.membership.alive()) == W, 60), node.membership.table()
+        if W > 1:
+            assert wait_for(lambda: node.rounds.group.formed and len(node.rounds.group.members) == W, 60)
+        per_q = W * B
+        nxt = [0]
+
+        def submit(k):
+            for _ in range(k):
+                s0 = nxt[0]
+                nxt[0] += per_q
+                cl.submit(a.model, s0, s0 + per_q - 1)
+
+        def done():
+            return node.state.images_done(a.model)
+
+        def wait_done(target, timeout=600):
+            return wait_for(lambda: done() >= target and node.state.pending_count() == 0, timeout, 0.001)
+
+        submit(a.warmup)
+        assert wait_done(nxt[0]), node.state.summary()
+        lat0 = len(node.state.query_latency[a.model])
+        t0 = time.perf_counter()
+        submit(a.steps)
+        assert wait_done(nxt[0]), node.state.summary()
+        elapsed = time.perf_counter() - t0
+        loaded = sorted(node.state.query_latency[a.model][lat0:])
+        lat1 = len(node.state.query_latency[a.model])
+        for _ in range(max(5, min(a.steps, 20))):   # unloaded: one query at a time
+            submit(1)
+            assert wait_done(nxt[0])
+        unloaded = sorted(node.state.query_latency[a.model][lat1:])
+        rounds = node.rounds.rounds_done if node.rounds is not None else 0
+        ips = per_q * a.steps / elapsed
+        p50 = unloaded[len(unloaded) // 2]
+        out = {
+            "metric": METRIC if (a.model == "resnet18" and B == QUERY) else
+            f"images/sec (whole node) + p50 query latency, {a.model} bs={B} at {W} GPU",
+            "value": round(ips, 2), "unit": "images/sec", "n_gpus": W, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(1000 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(ips / BASELINE_IMG_PER_S, 2) if a.model == "resnet18" and B == QUERY else None,
+            "dtype": "fp32" if a.dry_run else a.dtype, "mode": "system",
+            "data": "synthetic uint8 224x224x3 images (SyntheticSource on each GPU), random-init weights",
+            "config": {"model": a.model, "global_batch": per_q, "seq_len": None, "image_hw": 224,
+                       "batch_per_gpu": B, "parallelism": f"dp{W}",
+                       "path": ("client -> coordinator Node (membership, standby) -> fair-time split -> "
+                                + ("RCCL rounds" if W > 1 else "local JOB queue") + " -> job-state ingest"),
+                       "dry_run": a.dry_run},
+            "p50_query_latency_s": round(p50, 6),
+            "p50_query_latency_loaded_s": round(loaded[len(loaded) // 2], 6) if loaded else None,
+            "p50_vs_baseline_speedup": round(BASELINE_P50_S / p50, 1),
+            "results_recorded": done(), "collective_rounds": rounds,
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+        return 0
+    finally:
+        if node.rounds is not None:
+            node.rounds.release()                   # members leave the epoch cleanly
+        for m in node.membership.alive():
+            if m != node.name:
+                node.transport.send(m, {"t": Type.KILL})
+        time.sleep(0.2)
+        node.stop()
 
 
 def numerics_check(runner, a, device, n: int = 8) -> dict:

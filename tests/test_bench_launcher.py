@@ -56,3 +56,17 @@ def test_bench_world_mismatch_is_an_error():
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 2
     assert "WORLD_SIZE" in r.stdout
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_bench_system_mode_dry_run(n):
+    """--system: queries go client -> coordinator Node -> fair-time split ->
+    collective rounds (n > 1) / local JOB queue (n = 1) -> job-state ingest."""
+    r = _run("--system", "--gpus", str(n), "--steps", "4", "--warmup", "1", timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["mode"] == "system" and d["n_gpus"] == n
+    assert d["results_recorded"] == (1 + 4 + 5) * 400 * n
+    if n > 1:
+        assert d["collective_rounds"] >= 10          # every query ran as a round
+    assert d["p50_query_latency_s"] > 0
