@@ -52,8 +52,10 @@ def run_node(a) -> int:
         dev = torch.device("cpu")
     ex = make_executor(a.executor, dev if dev.type == "cuda" else None, seed=cfg.model_seed, dtype=cfg.dtype)
     if cfg.collective_rounds is None:
-        # one node per process: queries run as RCCL rounds on GPU nodes by default
-        cfg.collective_rounds = dev.type == "cuda" and a.executor in ("auto", "hip")
+        # one node per process and per GPU: queries run as RCCL rounds by default
+        # (RCCL needs a distinct GPU per rank; nodes sharing a GPU use the TCP path)
+        cfg.collective_rounds = dev.type == "cuda" and a.executor in ("auto", "hip") and \
+            torch.cuda.device_count() >= cfg.num_nodes
     tr = TcpTransport(name, cfg.address, cfg.address(name))
     node = Node(cfg, name, tr, ex)
     node.source = (SdfsSource(node.sdfs, dev) if a.source == "sdfs" else SyntheticSource(cfg.data_seed, dev))
