@@ -275,6 +275,12 @@ torch::Tensor conv2d_nhwc_f32(torch::Tensor x, torch::Tensor w, torch::Tensor bi
   return y;
 }
 
+static int g_wino_ablate_host = 0;
+static void set_wino_ablation_host(int64_t mode) {
+  g_wino_ablate_host = (int)mode;
+  set_wino_ablation((int)mode);
+}
+
 // fp32 Winograd F(2x2,3x3) conv (3x3 / stride 1 / pad 1): x [B,H,W,C] f32 NHWC,
 // u [16, Cout, C] f32 (= G g G^T, models/packed.py wino_weight), y = act(conv + bias (+ res)).
 torch::Tensor conv2d_wino_f32(torch::Tensor x, torch::Tensor u, torch::Tensor bias, c10::optional<torch::Tensor> res,
@@ -318,6 +324,7 @@ torch::Tensor conv2d_wino_f32(torch::Tensor x, torch::Tensor u, torch::Tensor bi
   a.zero = zero_buffer(x.device()).data_ptr();
   a.B = B; a.H = H; a.W = W; a.C = C; a.Cout = Cout;
   a.relu = relu ? 1 : 0;
+  a.ablate = g_wino_ablate_host;
   TORCH_CHECK(conv_wino_f32_launch(a, (int)variant, cur_stream()), "winograd conv launch rejected the shape");
   check_launch("conv_wino_f32");
   return y;
@@ -585,6 +592,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pad"), py::arg("relu"), py::arg("tile") = -1, py::arg("out") = py::none());
   m.def("conv2d_wino_f32", &conv2d_wino_f32, "fp32 Winograd F(2x2,3x3) conv (3x3/s1/p1) + bias (+res) (+relu)",
         py::arg("x"), py::arg("u"), py::arg("bias"), py::arg("res"), py::arg("relu"), py::arg("variant") = 0);
+  m.def("set_wino_ablation", &set_wino_ablation_host,
+        "profiling only: winograd conv ablation (1 no DMA, 2 no raw/transform, 4 no U reads, 8 no stores)");
+  m.def("set_wino_pairing", &set_wino_pairing, "A/B: winograd e-GEMMs in pairs or one at a time (default)");
   m.def("wino_supported", &conv_wino_f32_supported, "winograd conv geometry fits (H, W, C, Cout)");
   m.def("pick_tile_f32", &pick_tile_f32, "tile id the f32 conv heuristic picks for (M, Cout, K, small)");
   m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 (or fp32) NHWC4", py::arg("img"),

@@ -66,7 +66,11 @@ struct WinoArgs {
   int RIN, NP;         // staged input rows per image, pixels per column-parity half row
   int raw_ins;         // 1 KiB DMA instructions of the staged input region
   int nblk_t, nblk_n;  // tile blocks, 32-channel output blocks
+  int ablate;          // profiling only (set_wino_ablation): 1 no DMA, 2 no raw read/transform,
+                       // 4 no U reads, 8 no epilogue stores -- outputs are wrong
 };
+void set_wino_ablation(int mode);
+void set_wino_pairing(bool on);
 bool conv_wino_f32_launch(WinoArgs a, int variant, hipStream_t st);   // false: shape unsupported
 bool conv_wino_f32_supported(int H, int W, int C, int Cout);
 int conv_f32_pick(int M, int Cout, int K, bool small);

@@ -48,14 +48,45 @@ constexpr int kRawMax = 40 * 1024;      // staged input region per stage (bytes)
 constexpr int kUBytes = 16 * 32 * 64;   // 16 e x 32 couts x 16 channels x 4 B = 32 KiB
 constexpr int kStage = kRawMax + kUBytes;
 
-__device__ __forceinline__ int raw_swz(int p) { return ((p >> 2) & 1) << 1; }
+__device__ __forceinline__ int raw_swz(int p) { return wino_raw_swz(p); }   // tile_math.h
+
+int g_wino_ablate = 0;
+
+template <bool ASM>
+__device__ __forceinline__ float4v ldsr(uint32_t addr) {
+  if constexpr (ASM) return lds_read_f4(addr);
+  else return *reinterpret_cast<const __attribute__((address_space(3))) float4v*>((size_t)addr);
+}
+template <bool ASM, int N>
+__device__ __forceinline__ void lds_wait() {
+  if constexpr (ASM) lds_waitcnt<N>();
+}
+template <bool ASM>
+__device__ __forceinline__ void ldst(float4v& r) {
+  if constexpr (ASM) lds_tie(r);
+}
 
 }  // namespace
 
-template <int NW, bool HAS_RES>
-__global__ void __launch_bounds__(64 * NW, 1) conv_wino_f32_kernel(const WinoArgs a) {
+void set_wino_ablation(int mode) { g_wino_ablate = mode; }
+extern bool g_wino_pair;
+void set_wino_pairing(bool on) { g_wino_pair = on; }
+
+// SINGLE: one LDS stage of 26 KiB raw + 32 KiB U (58 KiB) instead of two of
+// 40 + 32 KiB, so TWO 4-wave blocks share a CU: each block's DMA wait,
+// transform and epilogue (its output stores are 64 KiB) then overlap the other
+// block's MFMAs -- with one 144-KiB block per CU they cannot (ablation:
+// setup + epilogue alone took 16 % of the layer1 conv).
+template <int NW, bool HAS_RES, bool PAIR, bool SINGLE = false, bool ABL = false>
+__global__ void __launch_bounds__(64 * NW, SINGLE ? 2 : 1) conv_wino_f32_kernel(const WinoArgs a) {
   constexpr int T = 16 * NW;
-  constexpr int RAW_INS = kRawMax / 1024;             // DMA instructions (max) for the raw region
+  // single stage: no LDS-DMA is in flight while the chunk's LDS reads run, so
+  // they are ordinary (compiler-scheduled, counted-wait) loads; with the
+  // double-buffered ring they go through inline asm (common.h)
+  constexpr bool ASMRD = !SINGLE;
+  constexpr int RAWB = SINGLE ? 26 * 1024 : kRawMax;  // raw region bytes per stage
+  constexpr int STG = RAWB + kUBytes;
+  constexpr int RAW_INS = RAWB / 1024;                // DMA instructions (max) for the raw region
   constexpr int RAW_PER_WAVE = (RAW_INS + NW - 1) / NW;
   constexpr int U_PER_WAVE = (kUBytes / 1024) / NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -116,7 +147,7 @@ __global__ void __launch_bounds__(64 * NW, 1) conv_wino_f32_kernel(const WinoArg
   }
   const int nk = a.C / 16;
   auto issue = [&](int k, int buf) {
-    char* base = smem + buf * kStage;
+    char* base = smem + buf * STG;
     const int c0 = k * 16;
 #pragma unroll
     for (int j = 0; j < RAW_PER_WAVE; ++j) {
@@ -130,7 +161,7 @@ __global__ void __launch_bounds__(64 * NW, 1) conv_wino_f32_kernel(const WinoArg
     for (int j = 0; j < U_PER_WAVE; ++j) {
       const int ins = wave + NW * j;
       __builtin_amdgcn_global_load_lds((glb_void_t*)(a.u + u_off[j] + c0),
-                                       (lds_void_t*)(base + kRawMax + ins * 1024), 16, 0, 0);
+                                       (lds_void_t*)(base + RAWB + ins * 1024), 16, 0, 0);
     }
   };
 
@@ -157,68 +188,167 @@ __global__ void __launch_bounds__(64 * NW, 1) conv_wino_f32_kernel(const WinoArg
     acc[e][1] = float4v{0.f, 0.f, 0.f, 0.f};
   }
 
-  issue(0, 0);
-  for (int k = 0; k < nk; ++k) {
+  const int abl = ABL ? a.ablate : 0;   // compiled out in production instances
+  if (!(ABL && (abl & 1))) issue(0, 0);
+  const int nk_run = (ABL && (abl & 16)) ? 0 : nk;            // 16: setup + epilogue only
+  for (int k = 0; k < nk_run; ++k) {
+    if constexpr (SINGLE) {
+      if (k > 0) {
+        __syncthreads();                                // every wave done reading chunk k-1
+        if (!(ABL && (abl & 1))) issue(k, 0);
+      }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of chunk k landed
-    __builtin_amdgcn_s_barrier();                       // everyone's landed; buffer k+1 free
-    if (k + 1 < nk) issue(k + 1, (k + 1) & 1);
-    const uint32_t sb = lds_addr(smem) + (k & 1) * kStage;
+    // everyone's landed; (double) buffer k+1 free.  Single stage: a full
+    // __syncthreads (memory fence) -- its LDS reads are compiler-visible loads
+    // that must not move above it; the ring keeps the raw s_barrier
+    if constexpr (SINGLE) __syncthreads();
+    else __builtin_amdgcn_s_barrier();
+    if constexpr (!SINGLE) {
+      if (k + 1 < nk && !(ABL && (abl & 1))) issue(k + 1, (k + 1) & 1);
+    }
+    const uint32_t sb = lds_addr(smem) + (SINGLE ? 0 : (k & 1)) * STG;
 
     // raw 4x4 patch of this lane's tile, its 4 channels -> V = B^T d B
     float4v d[4][4];
+    if (ABL && (abl & 2)) {
+#pragma unroll
+      for (int py = 0; py < 4; ++py)
+#pragma unroll
+        for (int px = 0; px < 4; ++px) d[py][px] = float4v{1.f, 2.f, 3.f, (float)(py * 4 + px + k)};
+    } else {
+#pragma unroll
+      for (int py = 0; py < 4; ++py)
+#pragma unroll
+        for (int px = 0; px < 4; ++px) d[py][px] = ldsr<ASMRD>(sb + pbase + py * rowb + colb[px]);
+    }
+    lds_wait<ASMRD, 0>();
 #pragma unroll
     for (int py = 0; py < 4; ++py)
 #pragma unroll
-      for (int px = 0; px < 4; ++px) d[py][px] = lds_read_f4(sb + pbase + py * rowb + colb[px]);
-    lds_waitcnt<0>();
+      for (int px = 0; px < 4; ++px) ldst<ASMRD>(d[py][px]);
+    // V = B^T d B one row i at a time, just ahead of that row's 4 e-GEMMs: the
+    // transform of row i+1 runs while row i's MFMAs are in flight, and only 4
+    // V registers (not 16) are live next to the raw patch
+    auto vrow = [&](int i, float4v (&v)[4]) {
+      float4v t[4];
 #pragma unroll
-    for (int py = 0; py < 4; ++py)
-#pragma unroll
-      for (int px = 0; px < 4; ++px) lds_tie(d[py][px]);
-    float4v v[16];
-#pragma unroll
-    for (int px = 0; px < 4; ++px) {                    // rows: tmp = B^T d
-      const float4v t0 = d[0][px] - d[2][px], t1 = d[1][px] + d[2][px];
-      const float4v t2 = d[2][px] - d[1][px], t3 = d[1][px] - d[3][px];
-      d[0][px] = t0;
-      d[1][px] = t1;
-      d[2][px] = t2;
-      d[3][px] = t3;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {                       // columns: V = tmp B
-      v[i * 4 + 0] = d[i][0] - d[i][2];
-      v[i * 4 + 1] = d[i][1] + d[i][2];
-      v[i * 4 + 2] = d[i][2] - d[i][1];
-      v[i * 4 + 3] = d[i][1] - d[i][3];
-    }
+      for (int px = 0; px < 4; ++px) {
+        if (i == 0) t[px] = d[0][px] - d[2][px];
+        else if (i == 1) t[px] = d[1][px] + d[2][px];
+        else if (i == 2) t[px] = d[2][px] - d[1][px];
+        else t[px] = d[1][px] - d[3][px];
+      }
+      v[0] = t[0] - t[2];
+      v[1] = t[1] + t[2];
+      v[2] = t[2] - t[1];
+      v[3] = t[1] - t[3];
+    };
 
     // 16 GEMM updates: M_e[32 couts][16 tiles] += U_e[32][16 ch] * V_e[16 ch][16 tiles]
-    const uint32_t ub = sb + kRawMax;
+    const uint32_t ub = sb + RAWB;
     auto uaddr = [&](int e, int i) {
       const int n = i * 16 + (lane & 15);
       return ub + (e * 32 + n) * 64 + ((g ^ swz_r(n, 4)) << 4);
     };
-    float4v ua[2][2];
-    ua[0][0] = lds_read_f4(uaddr(0, 0));
-    ua[0][1] = lds_read_f4(uaddr(0, 1));
+    if constexpr (PAIR) {
+    // e is processed in PAIRS: the 4 MFMAs of one k-step t then cycle over 4
+    // independent accumulators (e, e+1) x (cout half 0, 1), so a dependent
+    // v_mfma_f32_16x16x4_f32 (40-cycle result latency, 32-cycle issue) never
+    // waits on its predecessor (one e at a time alternated between only 2
+    // accumulators: "MFMA-only" ablation ran at ~60 % of the issue rate).
+    // U fragments of a pair: double-buffered (read pair p+1 while p multiplies)
+    // at one wave per SIMD; single-buffered at two (the partner wave covers the
+    // LDS latency, and the 8-wave kernel stays inside 256 registers).
+    constexpr bool UDB = NW <= 4 && !SINGLE;
+    float4v ua[UDB ? 2 : 1][2][2];                      // [buffer][e of pair][cout half]
+    auto read_pair = [&](int p, int buf) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        ua[buf][q][0] = ldsr<ASMRD>(uaddr(2 * p + q, 0));
+        ua[buf][q][1] = ldsr<ASMRD>(uaddr(2 * p + q, 1));
+      }
+    };
+    if constexpr (UDB) {
+      if (!(ABL && (abl & 4))) read_pair(0, 0);
+    }
+    float4v vr[4];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int cb = UDB ? (p & 1) : 0;
+      if ((p & 1) == 0) vrow(p >> 1, vr);
+      if (ABL && (abl & 4)) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          ua[cb][q][0] = float4v{1.f, 2.f, (float)p, (float)k};
+          ua[cb][q][1] = float4v{2.f, 1.f, (float)k, (float)q};
+        }
+      } else if constexpr (UDB) {
+        if (p + 1 < 8) {
+          read_pair(p + 1, cb ^ 1);
+          lds_wait<ASMRD, 4>();
+        } else {
+          lds_wait<ASMRD, 0>();
+        }
+      } else {
+        read_pair(p, 0);
+        lds_wait<ASMRD, 0>();
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        ldst<ASMRD>(ua[cb][q][0]);
+        ldst<ASMRD>(ua[cb][q][1]);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int e = 2 * p + q;
+          acc[e][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][q][0][t], vr[e & 3][t], acc[e][0], 0, 0, 0);
+          acc[e][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][q][1][t], vr[e & 3][t], acc[e][1], 0, 0, 0);
+        }
+    }
+    } else {
+    // read -> wait -> use (no register double buffer: a value an inline-asm
+    // ds_read defines before its wait may be copied by the register allocator
+    // ahead of the wait; with a read-ahead buffer variant 0 returned garbage)
+    constexpr bool UDB = false;
+    float4v ua[UDB ? 2 : 1][2];
+    if constexpr (UDB) {
+      if (!(ABL && (abl & 4))) {
+        ua[0][0] = ldsr<ASMRD>(uaddr(0, 0));
+        ua[0][1] = ldsr<ASMRD>(uaddr(0, 1));
+      }
+    }
+    float4v vr[4];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int cb = e & 1, nbf = cb ^ 1;
-      if (e + 1 < 16) {
-        ua[nbf][0] = lds_read_f4(uaddr(e + 1, 0));
-        ua[nbf][1] = lds_read_f4(uaddr(e + 1, 1));
-        lds_waitcnt<2>();
+      const int cb = UDB ? (e & 1) : 0, nbf = UDB ? (cb ^ 1) : 0;
+      if ((e & 3) == 0) vrow(e >> 2, vr);
+      if (ABL && (abl & 4)) {
+        ua[cb][0] = float4v{1.f, 2.f, (float)e, (float)k};
+        ua[cb][1] = float4v{2.f, 1.f, (float)k, (float)e};
+      } else if constexpr (UDB) {
+        if (e + 1 < 16) {
+          ua[nbf][0] = ldsr<ASMRD>(uaddr(e + 1, 0));
+          ua[nbf][1] = ldsr<ASMRD>(uaddr(e + 1, 1));
+          lds_wait<ASMRD, 2>();
+        } else {
+          lds_wait<ASMRD, 0>();
+        }
       } else {
-        lds_waitcnt<0>();
+        ua[0][0] = ldsr<ASMRD>(uaddr(e, 0));
+        ua[0][1] = ldsr<ASMRD>(uaddr(e, 1));
+        lds_wait<ASMRD, 0>();
       }
-      lds_tie(ua[cb][0]);
-      lds_tie(ua[cb][1]);
+      ldst<ASMRD>(ua[cb][0]);
+      ldst<ASMRD>(ua[cb][1]);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        acc[e][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][0][t], v[e][t], acc[e][0], 0, 0, 0);
-        acc[e][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][1][t], v[e][t], acc[e][1], 0, 0, 0);
+        acc[e][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][0][t], vr[e & 3][t], acc[e][0], 0, 0, 0);
+        acc[e][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][1][t], vr[e & 3][t], acc[e][1], 0, 0, 0);
       }
+    }
     }
   }
 
@@ -260,6 +390,10 @@ __global__ void __launch_bounds__(64 * NW, 1) conv_wino_f32_kernel(const WinoArg
         o[1] = fmaxf(o[1], 0.f);
         o[2] = fmaxf(o[2], 0.f);
         o[3] = fmaxf(o[3], 0.f);
+      }
+      if (ABL && (a.ablate & 8)) {
+        if (o[0] == 12345.f) a.y[0] = o[1];
+        continue;
       }
       *reinterpret_cast<float4v*>(a.y + off) = o;
     }
@@ -439,36 +573,48 @@ __global__ void __launch_bounds__(256, 1) conv_wino2_f32_kernel(const WinoArgs a
     const bool more = k + 1 < nk;
     float4v d[4][4];
     if (more) read_raw(k + 1, d);
-    float4v ua[2][2];
-    ua[0][0] = lds_read_f4(uaddr(k, 0, 0));
-    ua[0][1] = lds_read_f4(uaddr(k, 0, 1));
+    // e in pairs: 4 independent accumulators per k-step (see the v1 kernel)
+    float4v ua[2][2][2];                                // [buffer][e of pair][cout half]
+    auto read_pair = [&](int p, int buf) {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int cb = e & 1, nbf = cb ^ 1;
-      if (e + 1 < 16) {
-        ua[nbf][0] = lds_read_f4(uaddr(k, e + 1, 0));
-        ua[nbf][1] = lds_read_f4(uaddr(k, e + 1, 1));
-        lds_waitcnt<2>();                  // in-order: raw(k+1) reads and U(e) retired
+      for (int q = 0; q < 2; ++q) {
+        ua[buf][q][0] = lds_read_f4(uaddr(k, 2 * p + q, 0));
+        ua[buf][q][1] = lds_read_f4(uaddr(k, 2 * p + q, 1));
+      }
+    };
+    read_pair(0, 0);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int cb = p & 1;
+      if (p + 1 < 8) {
+        read_pair(p + 1, cb ^ 1);
+        lds_waitcnt<4>();                  // in-order: raw(k+1) reads and pair p retired
       } else {
         lds_waitcnt<0>();
       }
-      lds_tie(ua[cb][0]);
-      lds_tie(ua[cb][1]);
-      if (e == 0 && more) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        lds_tie(ua[cb][q][0]);
+        lds_tie(ua[cb][q][1]);
+      }
+      if (p == 0 && more) {
 #pragma unroll
         for (int py = 0; py < 4; ++py)
 #pragma unroll
           for (int px = 0; px < 4; ++px) lds_tie(d[py][px]);
       }
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        acc[e][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][0][t], vc[e][t], acc[e][0], 0, 0, 0);
-        acc[e][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][1][t], vc[e][t], acc[e][1], 0, 0, 0);
-      }
-      // spread the next chunk's transform over the MFMA stream (8 MFMAs per e)
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int e = 2 * p + q;
+          acc[e][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][q][0][t], vc[e][t], acc[e][0], 0, 0, 0);
+          acc[e][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[cb][q][1][t], vc[e][t], acc[e][1], 0, 0, 0);
+        }
+      // spread the next chunk's transform over the MFMA stream (16 MFMAs per pair)
       if (more) {
-        if (e >= 1 && e <= 4) transform_rows(d, e - 1);
-        if (e >= 5 && e <= 8) transform_cols(d, vn, e - 5);
+        if (p >= 1 && p <= 4) transform_rows(d, p - 1);
+        if (p >= 4 && p <= 7) transform_cols(d, vn, p - 4);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // raw(k+2), U(k+1) of this wave landed
@@ -549,17 +695,33 @@ bool conv_wino_f32_supported(int H, int W, int C, int Cout) {
   return C % 16 == 0 && Cout % 32 == 0 && wino_geometry(a, 4, kRaw2);
 }
 
+bool g_wino_pair = false;  // A/B switch (set_wino_pairing): e-GEMMs in pairs (4w: -4 %, 8w: +13 % time, same box)
+
 template <int NW, bool R>
 static void wino_cfg(WinoArgs a, hipStream_t st) {
   const int lds = 2 * kStage;
-  auto kern = conv_wino_f32_kernel<NW, R>;
+  auto kern = a.ablate ? conv_wino_f32_kernel<NW, R, false, false, true>
+              : g_wino_pair ? conv_wino_f32_kernel<NW, R, true> : conv_wino_f32_kernel<NW, R, false>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), lds);
   hipLaunchKernelGGL(kern, dim3(a.nblk_t * a.nblk_n), dim3(64 * NW), lds, st, a);
 }
 
 // variant: 0 = 4 waves (64 tiles per block), 1 = 8 waves (128 tiles per block),
-//          2 = software-pipelined 4 waves (64 tiles per block)
+//          2 = software-pipelined 4 waves (64 tiles per block),
+//          3 = 4 waves, one 58-KiB stage, two blocks per CU
 bool conv_wino_f32_launch(WinoArgs a, int variant, hipStream_t st) {
+  if (variant == 3) {
+    if (a.C % 16 || a.Cout % 32 || !wino_geometry(a, 4, kRaw2)) return false;
+    const int lds = kRaw2 + kUBytes;
+    const bool r = a.res != nullptr;
+    auto kern = a.ablate ? (r ? conv_wino_f32_kernel<4, true, false, true, true>
+                              : conv_wino_f32_kernel<4, false, false, true, true>)
+                : g_wino_pair ? (r ? conv_wino_f32_kernel<4, true, true, true> : conv_wino_f32_kernel<4, false, true, true>)
+                              : (r ? conv_wino_f32_kernel<4, true, false, true> : conv_wino_f32_kernel<4, false, false, true>);
+    ensure_lds_attr(reinterpret_cast<const void*>(kern), lds);
+    hipLaunchKernelGGL(kern, dim3(a.nblk_t * a.nblk_n), dim3(256), lds, st, a);
+    return true;
+  }
   if (variant == 2) {
     if (a.C % 16 || a.Cout % 32 || !wino_geometry(a, 4, kRaw2)) return false;
     const int lds = 2 * kRaw2 + 2 * kUBytes;

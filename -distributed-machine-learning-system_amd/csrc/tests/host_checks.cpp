@@ -91,6 +91,29 @@ static void check_swizzle(const char* name, int cpr, F swz) {
       }
 }
 
+// conv_wino_f32 raw patch read: lane l (tile l & 15 of a row segment starting at
+// pixel p0, channel group g = l >> 4) reads pixel p0 + (l & 15) (+1 for the odd
+// patch columns), chunk g ^ wino_raw_swz(pixel) of a 64-byte pixel slot
+static void check_wino_raw() {
+  for (int p0 = 0; p0 < 64; ++p0)
+    for (int shift = 0; shift < 2; ++shift)
+      for (auto& grp : kGroups) {
+        int used[16] = {0};
+        for (int l : grp) {
+          const int p = p0 + (l & 15) + shift, g = l >> 4;
+          const int addr = p * 64 + ((g ^ wino_raw_swz(p)) << 4);
+          used[(addr / 16) % 16]++;
+        }
+        for (int s = 0; s < 16; ++s)
+          CHECK(used[s] == 1, "wino raw p0 %d shift %d: bank slot %d used %d times\n", p0, shift, s, used[s]);
+      }
+  for (int p = 0; p < 256; ++p) {   // a permutation of the pixel's 4 chunks
+    int hit[4] = {0};
+    for (int g = 0; g < 4; ++g) hit[g ^ wino_raw_swz(p)]++;
+    for (int c = 0; c < 4; ++c) CHECK(hit[c] == 1, "wino raw pixel %d: chunk %d hit %d times\n", p, c, hit[c]);
+  }
+}
+
 int main() {
   check_groups_partition();
   check_xcd_remap();
@@ -98,6 +121,7 @@ int main() {
   check_swizzle("conv_glds swz_r", 4, [](int r) { return swz_r(r, 4); });
   check_swizzle("conv3x3_patch/conv_big swz8", 8, [](int r) { return swz8(r); });
   check_swizzle("conv3x3_c64 c64_swz", 8, [](int r) { return c64_swz(r); });
+  check_wino_raw();
   std::printf("host_checks: %d failure(s)\n", g_fail);
   return g_fail ? 1 : 0;
 }

@@ -26,6 +26,11 @@ __host__ __device__ __forceinline__ int swz_r(int row, int cpr) {
   return (0x78 >> (2 * q)) & 3;
 }
 
+// conv_wino_f32: staged raw-input pixel p (64 bytes = 4 chunks of 4 channels) of
+// one column-parity half row; a wave's 16 lanes of one channel group read 16
+// consecutive pixels -> 16 distinct bank slots per ds_read_b128 lane group.
+__host__ __device__ __forceinline__ int wino_raw_swz(int p) { return ((p >> 2) & 1) << 1; }
+
 // conv3x3_c64: 128-byte rows (64 channels)
 __host__ __device__ __forceinline__ int c64_swz(int row) { return row & 6; }
 

@@ -310,9 +310,10 @@ class HipRunner:
         # fp32 3x3/s1 convs through the fused Winograd F(2x2,3x3) kernel (2.25x
         # fewer f32-MFMA products than the direct conv; conv_wino_f32.hip)
         self.winograd = winograd
-        # None = measured default per layer (tools/bench_layers_f32.py,
-        # profiles/r2_v3_layers_wino.md): 8-wave blocks (128 tiles) where the image
-        # has >= 14 rows, the pipelined 4-wave kernel (64 tiles) for the 7x7 layer4
+        # None = measured default (tools/wino_ablate.py, profiles/r2_v6_wino_variants.md):
+        # variant 3 -- 4-wave blocks of 64 tiles, one 58-KiB LDS stage, two blocks
+        # per CU -- is the fastest on every ResNet layer shape (same-box A/B:
+        # 0.86-0.88x the 8-wave variant's time at 56/28/14, 0.67x at 7x7)
         self.wino_variant = wino_variant
         # >1: stem + the full-resolution blocks (ResNet layer1) run on this many
         # batch parts, each part's activations small enough to stay in the
@@ -394,7 +395,7 @@ class HipRunner:
     def _conv(self, c, x, residual=None, out=None):
         if c.wino is not None and self.winograd and out is None and x.dtype == torch.float32 \
                 and self.ops.wino_supported(x.shape[1], x.shape[2], c.cin, c.cout):
-            var = self.wino_variant if self.wino_variant is not None else (1 if x.shape[1] >= 14 else 2)
+            var = self.wino_variant if self.wino_variant is not None else 3
             return self.ops.conv2d_wino(x, c.wino, c.b, c.relu, residual, var)
         return self.ops.conv2d(x, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu, residual=residual, out=out)
 

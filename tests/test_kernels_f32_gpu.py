@@ -224,7 +224,7 @@ WINO_CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("res", [False, True])
 @pytest.mark.parametrize("B,H,W,Cin,Cout", WINO_CASES)
 def test_conv_wino_f32(ops, B, H, W, Cin, Cout, res, variant):
