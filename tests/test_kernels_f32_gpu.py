@@ -241,6 +241,31 @@ def test_conv_wino_f32(ops, B, H, W, Cin, Cout, res, variant):
     _check(y, _ref_conv64(x, w, b, 1, 1, True, r), rel=5e-5)
 
 
+@pytest.mark.parametrize("lin", [True, False])
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [
+    (7, 14, 14, 32, 64),      # 49 tiles per image: blocks span up to 3 images
+    (3, 28, 28, 32, 32),      # 196 tiles per image: blocks cross one image boundary
+    (4, 13, 11, 16, 32),      # odd sizes: padded tiles inside consecutive-tile blocks
+    (9, 7, 7, 16, 32),        # 16 tiles per image: the images-per-block mode
+])
+def test_conv_wino_f32_linear(ops, B, H, W, Cin, Cout, lin):
+    """Variant 3 with the consecutive-tile (LIN) blocking on and off."""
+    from idunno.models.packed import wino_weight
+
+    torch.manual_seed(B * H + W + Cin)
+    x = torch.randn(B, H, W, Cin, device=DEV)
+    w = torch.randn(Cout, Cin, 3, 3) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    r = torch.randn(B, H, W, Cout, device=DEV)
+    ops.load().set_wino_linear(lin)
+    try:
+        y = ops.conv2d_wino(x, wino_weight(w).to(DEV), b.to(DEV), True, r, 3)
+        torch.cuda.synchronize()
+    finally:
+        ops.load().set_wino_linear(True)
+    _check(y, _ref_conv64(x, w, b, 1, 1, True, r), rel=5e-5)
+
+
 def test_runner_winograd_matches_direct(ops):
     from idunno.models import HipRunner, build_program
 
