@@ -47,6 +47,9 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 constexpr int kRawMax = 40 * 1024;      // staged input region per stage (bytes)
 constexpr int kUBytes = 16 * 32 * 64;   // 16 e x 32 couts x 16 channels x 4 B = 32 KiB
 constexpr int kStage = kRawMax + kUBytes;
+// variant 3 (one stage, two blocks per CU): 64 KiB per block.  40 KiB (LIN also
+// at 56x56) measured neutral there (559 vs 559 us, profiles/r2_v8_wino_linear.md)
+constexpr int kRaw3 = 32 * 1024;
 
 __device__ __forceinline__ int raw_swz(int p) { return wino_raw_swz(p); }   // tile_math.h
 
@@ -72,7 +75,7 @@ void set_wino_ablation(int mode) { g_wino_ablate = mode; }
 extern bool g_wino_pair;
 void set_wino_pairing(bool on) { g_wino_pair = on; }
 
-// SINGLE: one LDS stage of 26 KiB raw + 32 KiB U (58 KiB) instead of two of
+// SINGLE: one LDS stage of 32 KiB raw + 32 KiB U (64 KiB) instead of two of
 // 40 + 32 KiB, so TWO 4-wave blocks share a CU: each block's DMA wait,
 // transform and epilogue (its output stores are 64 KiB) then overlap the other
 // block's MFMAs -- with one 144-KiB block per CU they cannot (ablation:
@@ -84,7 +87,7 @@ __global__ void __launch_bounds__(64 * NW, SINGLE ? 2 : 1) conv_wino_f32_kernel(
   // they are ordinary (compiler-scheduled, counted-wait) loads; with the
   // double-buffered ring they go through inline asm (common.h)
   constexpr bool ASMRD = !SINGLE;
-  constexpr int RAWB = SINGLE ? 26 * 1024 : kRawMax;  // raw region bytes per stage
+  constexpr int RAWB = SINGLE ? kRaw3 : kRawMax;      // raw region bytes per stage
   constexpr int STG = RAWB + kUBytes;
   constexpr int RAW_INS = RAWB / 1024;                // DMA instructions (max) for the raw region
   constexpr int RAW_PER_WAVE = (RAW_INS + NW - 1) / NW;
@@ -99,8 +102,23 @@ __global__ void __launch_bounds__(64 * NW, SINGLE ? 2 : 1) conv_wino_f32_kernel(
   const int lid = xcd_remap(blockIdx.x, nwg);
   const int tb = lid / a.nblk_n, nb = lid - tb * a.nblk_n;
   const int n0 = nb * 32;
+  const int rowb = 2 * a.NP * 64;                     // bytes per staged image row
   int b0, ty0, imgs, rows;
-  if (a.IMG > 1) {
+  int t0 = 0, vr0 = 0, n_ins = a.raw_ins;             // LIN: first tile, first virtual row, DMA count
+  const int per = a.TX * a.TY;
+  if (a.LIN) {
+    // virtual input rows: image b owns rows [b*RIN, (b+1)*RIN), row r = input row
+    // r-1 (rows -1 and >= H are the zero padding), so the block's consecutive
+    // tiles -- even across an image boundary -- read one contiguous row range
+    t0 = tb * T;
+    const int tl = min(t0 + T, a.B * per) - 1;
+    const int bf = t0 / per, bl = tl / per;
+    vr0 = bf * a.RIN + 2 * ((t0 - bf * per) / a.TX);
+    const int vr_end = bl * a.RIN + 2 * ((tl - bl * per) / a.TX) + 4;
+    n_ins = ((vr_end - vr0) * rowb + 1023) >> 10;
+    b0 = ty0 = 0;
+    imgs = rows = 0;
+  } else if (a.IMG > 1) {
     b0 = tb * a.IMG;
     ty0 = 0;
     imgs = min(a.IMG, a.B - b0);
@@ -115,25 +133,33 @@ __global__ void __launch_bounds__(64 * NW, SINGLE ? 2 : 1) conv_wino_f32_kernel(
 
   // ---- DMA sources (per lane, per instruction; + channel offset per stage) -----
   const float* zero = reinterpret_cast<const float*>(a.zero);
-  const int raw_chunks = a.raw_ins * 64;
   int raw_off[RAW_PER_WAVE];
 #pragma unroll
   for (int j = 0; j < RAW_PER_WAVE; ++j) {
     const int ins = wave + NW * j;
     const int L = ins * 64 + lane;
     raw_off[j] = -1;
-    if (ins < a.raw_ins && L < raw_chunks) {
+    if (ins < n_ins) {
       const int qs = L & 3;
       int rest = L >> 2;
       const int p = rest % a.NP;
       rest /= a.NP;
       const int half = rest & 1;
       const int lr = rest >> 1;
-      const int img = lr / a.RIN, rin = lr - img * a.RIN;
-      const int iy = 2 * ty0 + rin - 1, ix = 2 * p + half - 1;
+      const int ix = 2 * p + half - 1;
       const int q = qs ^ raw_swz(p);
-      if (img < imgs && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
-        raw_off[j] = (((b0 + img) * a.H + iy) * a.W + ix) * a.C + 4 * q;
+      int img, iy;
+      if (a.LIN) {
+        const int vr = vr0 + lr;
+        img = vr / a.RIN;
+        iy = vr - img * a.RIN - 1;
+      } else {
+        img = lr / a.RIN;
+        iy = 2 * ty0 + (lr - img * a.RIN) - 1;
+        img = img < imgs ? b0 + img : a.B;
+      }
+      if (img < a.B && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+        raw_off[j] = ((img * a.H + iy) * a.W + ix) * a.C + 4 * q;
     }
   }
   int u_off[U_PER_WAVE];
@@ -152,7 +178,7 @@ __global__ void __launch_bounds__(64 * NW, SINGLE ? 2 : 1) conv_wino_f32_kernel(
 #pragma unroll
     for (int j = 0; j < RAW_PER_WAVE; ++j) {
       const int ins = wave + NW * j;
-      if (ins < a.raw_ins) {
+      if (ins < n_ins) {
         const float* src = raw_off[j] >= 0 ? a.x + raw_off[j] + c0 : zero;
         __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(base + ins * 1024), 16, 0, 0);
       }
@@ -166,14 +192,29 @@ __global__ void __launch_bounds__(64 * NW, SINGLE ? 2 : 1) conv_wino_f32_kernel(
   };
 
   // ---- this lane's tile and its patch addresses in the raw image --------------
+  // (s_b, s_ty, s_tx): image, tile row, tile column; byte offset of patch element
+  // (py, px): staged row (s_row + py), parity px&1, pixel tx + (px>>1), chunk g ^ swz(pixel)
   const int slot = wave * 16 + (lane & 15);
-  const int s_img = slot / per_img, s_rem = slot - s_img * per_img;
-  const int s_tyl = s_rem / a.TX, s_tx = s_rem - s_tyl * a.TX;
-  const bool s_ok = slot < T && s_img < imgs && s_tyl < rows;
-  // byte offset of patch element (py, px): row (img*RIN + 2*tyl + py), parity px&1,
-  // pixel tx + (px>>1), chunk g ^ swz(pixel)
-  const int rowb = 2 * a.NP * 64;                     // bytes per staged image row
-  const int pbase = s_ok ? ((s_img * a.RIN + 2 * s_tyl) * rowb) : 0;
+  int s_b, s_ty, s_tx, s_row;
+  bool s_ok;
+  if (a.LIN) {
+    const int t = t0 + slot;
+    s_ok = t < a.B * per;
+    s_b = t / per;
+    const int rem = t - s_b * per;
+    s_ty = rem / a.TX;
+    s_tx = rem - s_ty * a.TX;
+    s_row = s_b * a.RIN + 2 * s_ty - vr0;
+  } else {
+    const int s_img = slot / per_img, s_rem = slot - s_img * per_img;
+    const int s_tyl = s_rem / a.TX;
+    s_tx = s_rem - s_tyl * a.TX;
+    s_ok = slot < T && s_img < imgs && s_tyl < rows;
+    s_b = b0 + s_img;
+    s_ty = ty0 + s_tyl;
+    s_row = s_img * a.RIN + 2 * s_tyl;
+  }
+  const int pbase = s_ok ? s_row * rowb : 0;
   int colb[4];
 #pragma unroll
   for (int px = 0; px < 4; ++px) {
@@ -354,8 +395,8 @@ __global__ void __launch_bounds__(64 * NW, SINGLE ? 2 : 1) conv_wino_f32_kernel(
 
   // ---- output transform Y = A^T M A, bias, residual, ReLU, NHWC store -----------
   if (!s_ok) return;
-  const int b = b0 + s_img;
-  const int oy0 = 2 * (ty0 + s_tyl), ox0 = 2 * s_tx;
+  const int b = s_b;
+  const int oy0 = 2 * s_ty, ox0 = 2 * s_tx;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int n = n0 + i * 16 + 4 * g;
@@ -661,11 +702,14 @@ __global__ void __launch_bounds__(256, 1) conv_wino2_f32_kernel(const WinoArgs a
 }
 
 // Host-side block geometry for T = 16*nw tiles per block; false if the shape
-// does not fit (caller falls back to the direct conv).
-static bool wino_geometry(WinoArgs& a, int nw, int raw_max = kRawMax) {
+// does not fit (caller falls back to the direct conv).  ``lin``: use the
+// consecutive-tile (LIN) blocking when the rectangular one leaves tile slots
+// idle and every block's virtual-row range fits ``raw_max``.
+static bool wino_geometry(WinoArgs& a, int nw, int raw_max = kRawMax, bool lin = false) {
   const int T = 16 * nw;
   a.TX = (a.W + 1) / 2;
   a.TY = (a.H + 1) / 2;
+  a.LIN = 0;
   if (a.TX > T) return false;
   const int per = a.TX * a.TY;
   auto raw_bytes = [&](int imgs, int R) { return imgs * (2 * R + 2) * 2 * (a.TX + 1) * 64; };
@@ -686,6 +730,27 @@ static bool wino_geometry(WinoArgs& a, int nw, int raw_max = kRawMax) {
   a.raw_ins = (raw_bytes(a.IMG, a.R) + 1023) / 1024;
   a.nblk_t = a.IMG > 1 ? (a.B + a.IMG - 1) / a.IMG : a.B * a.bpi;
   a.nblk_n = a.Cout / 32;
+  const long used = (long)a.B * per;
+  if (lin && used * 100 < (long)a.nblk_t * T * 95) {
+    // every block's staged rows (the kernel's own formula); periodic in the
+    // block index with period lcm(T, per) / T <= per blocks
+    const int rin = 2 * a.TY + 2, rowb = 2 * a.NP * 64;
+    const long nblk = (used + T - 1) / T;
+    int worst = 0;
+    for (long tb = 0; tb < nblk && tb <= per; ++tb) {
+      const long t0 = tb * T, tl = std::min(t0 + T, used) - 1;
+      const long bf = t0 / per, bl = tl / per;
+      const long v0 = bf * rin + 2 * ((t0 - bf * per) / a.TX);
+      const long v1 = bl * rin + 2 * ((tl - bl * per) / a.TX) + 4;
+      worst = std::max(worst, (int)(v1 - v0) * rowb);
+    }
+    if (worst <= raw_max) {
+      a.LIN = 1;
+      a.RIN = rin;
+      a.raw_ins = (worst + 1023) / 1024;
+      a.nblk_t = (int)nblk;
+    }
+  }
   return true;
 }
 
@@ -695,6 +760,8 @@ bool conv_wino_f32_supported(int H, int W, int C, int Cout) {
   return C % 16 == 0 && Cout % 32 == 0 && wino_geometry(a, 4, kRaw2);
 }
 
+bool g_wino_lin = true;    // A/B switch (set_wino_linear): LIN blocking in variant 3
+void set_wino_linear(bool on) { g_wino_lin = on; }
 bool g_wino_pair = false;  // A/B switch (set_wino_pairing): e-GEMMs in pairs (4w: -4 %, 8w: +13 % time, same box)
 
 template <int NW, bool R>
@@ -711,8 +778,8 @@ static void wino_cfg(WinoArgs a, hipStream_t st) {
 //          3 = 4 waves, one 58-KiB stage, two blocks per CU
 bool conv_wino_f32_launch(WinoArgs a, int variant, hipStream_t st) {
   if (variant == 3) {
-    if (a.C % 16 || a.Cout % 32 || !wino_geometry(a, 4, kRaw2)) return false;
-    const int lds = kRaw2 + kUBytes;
+    if (a.C % 16 || a.Cout % 32 || !wino_geometry(a, 4, kRaw3, g_wino_lin)) return false;
+    const int lds = kRaw3 + kUBytes;
     const bool r = a.res != nullptr;
     auto kern = a.ablate ? (r ? conv_wino_f32_kernel<4, true, false, true, true>
                               : conv_wino_f32_kernel<4, false, false, true, true>)
