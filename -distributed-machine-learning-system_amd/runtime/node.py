@@ -74,6 +74,9 @@ class Node:
         self._pf: dict = {}                         # (start, end) -> Future of staged images
         self._pf_lock = threading.Lock()
         self._pf_pool = None
+        self._rerep_lock = threading.Lock()     # SDFS re-replication after a failure (own thread)
+        self._rerep_pool = None
+        self._rerep_pending: list = []
         self.tracer = Tracer(name)
         self.device = getattr(executor, "device", None)  # GPU of this node (None = CPU)
         self.rounds = None                          # collective round plane (cfg.collective_rounds)
@@ -158,6 +161,9 @@ class Node:
             self.rounds.stop()
             self.rounds.join(timeout=5.0)
         self.jobs.put(None)
+        for pool in (self._rerep_pool, self._pf_pool):
+            if pool is not None:
+                pool.shutdown(wait=False, cancel_futures=True)
         self.transport.close()
         close = getattr(self.executor, "close", None)
         if close is not None:
@@ -413,12 +419,10 @@ class Node:
             return
         if self.rounds is not None:
             self.rounds.schedule_reform(f"{node} failed")
+        # chunks first: the dead node's work is re-dispatched at once; SDFS
+        # re-replication (seconds of file copies for a node holding shards)
+        # follows on its own thread instead of delaying the recovery
         t0 = time.monotonic()
-        try:
-            moves = self.sdfs.rereplicate(node)
-        except Exception:  # noqa: BLE001
-            self.logger.exception("re-replication failed")
-            moves = []
         chunks = self.state.chunks_of(node)
         alive = self.membership.alive()
         for ch in chunks:
@@ -429,8 +433,34 @@ class Node:
                 continue
             self.state.reassign(node, w, ch)
             self._send_job(w, model, qnum, s, e)
-        self.logger.warning("failure of %s: re-dispatched %d chunks, re-replicated %d files in %.3fs",
-                            node, len(chunks), len(moves), time.monotonic() - t0)
+        self.logger.warning("failure of %s: re-dispatched %d chunks in %.3fs", node, len(chunks),
+                            time.monotonic() - t0)
+        with self._rerep_lock:
+            if self._rerep_pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+
+                self._rerep_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"{self.name}-rerep")
+            self._rerep_pending.append(self._rerep_pool.submit(self._rereplicate, node))
+
+    def _rereplicate(self, node: str) -> int:
+        t0 = time.monotonic()
+        try:
+            moves = self.sdfs.rereplicate(node)
+        except Exception:  # noqa: BLE001
+            self.logger.exception("re-replication failed")
+            return 0
+        self.logger.warning("failure of %s: re-replicated %d files in %.3fs", node, len(moves),
+                            time.monotonic() - t0)
+        return len(moves)
+
+    def wait_rereplication(self, timeout: float | None = None) -> bool:
+        """Block until every re-replication started so far has finished."""
+        from concurrent.futures import wait
+
+        with self._rerep_lock:
+            futs = list(self._rerep_pending)
+            self._rerep_pending = [f for f in futs if not f.done()]
+        return not wait(futs, timeout=timeout).not_done
 
     def _straggler_loop(self) -> None:
         """Resend chunks running longer than straggler_timeout_s (A7 fixed; off by default)."""

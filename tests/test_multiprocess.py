@@ -2,6 +2,7 @@
 an MI355X host), fake executor on the CPU.  Nodes are SIGKILLed mid-query to
 exercise failure detection, chunk re-dispatch and standby promotion across
 process boundaries (SURVEY.md §4 "multi-process single node")."""
+import ast
 import os
 import signal
 import socket
@@ -85,7 +86,7 @@ def test_multiprocess_cluster_failures():
         idx = set()
         for k, chunks in res.items():
             for ch in chunks:
-                idx |= {int(t[0][5:-5]) for t in eval(ch)}
+                idx |= {int(t[0][5:-5]) for t in ast.literal_eval(ch)}
         assert idx == set(range(1600))
     finally:
         me.stop()
