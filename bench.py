@@ -8,7 +8,10 @@ random-init weights (no datasets or checkpoints are reachable).
 Precision: the reference classifies in fp32 (torchvision eager,
 /root/reference/alexnet_resnet.py:17-22, 74-75), so the headline runs the
 framework's fp32 path: fp32 activations and weights, every conv / FC on the
-f32-input MFMA (v_mfma_f32_16x16x4_f32, exact f32 products, f32 accumulate).
+f32-input MFMA (v_mfma_f32_16x16x4_f32, exact f32 products, f32 accumulate);
+3x3 stride-1 convs by fused fp32 Winograd F(2x2,3x3) (the fp32 algorithm
+cuDNN / MIOpen pick for these layers; logits agree with torch fp32 to ~1e-6
+relative, reported as ``max_rel_logit_err_vs_torch_fp32``).
 The fp16 path (f16 MFMA, f32 accumulate) is reported as extra keys.
 
 One *step* is one round of the cluster's query path, end to end:
@@ -332,7 +335,7 @@ def main(argv=None) -> int:
             "config": {"model": a.model, "global_batch": W * B, "seq_len": None, "image_hw": 224,
                        "batch_per_gpu": B, "parallelism": f"dp{W}", "graph": not a.no_graph,
                        "compute": ("f32-input MFMA (v_mfma_f32_16x16x4_f32), fp32 activations/weights, "
-                                   "fp32 accumulate") if a.dtype == "fp32" else
+                                   "fp32 accumulate; 3x3/s1 convs by fused fp32 Winograd F(2x2,3x3)") if a.dtype == "fp32" else
                        "f16 MFMA, fp16 activations, fp32 accumulate",
                        "dry_run": a.dry_run},
             "p50_query_latency_s": round(p50, 6) if p50 else None,
