@@ -596,6 +596,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "profiling only: winograd conv ablation (1 no DMA, 2 no raw/transform, 4 no U reads, 8 no stores)");
   m.def("set_wino_pairing", &set_wino_pairing, "A/B: winograd e-GEMMs in pairs or one at a time (default)");
   m.def("set_wino_linear", &set_wino_linear, "A/B: variant-3 consecutive-tile (LIN) blocking (default on)");
+  m.def("set_wino_rotation", &set_wino_rotation, "A/B: variant-3 rotated raw rows (default off)");
   m.def("wino_supported", &conv_wino_f32_supported, "winograd conv geometry fits (H, W, C, Cout)");
   m.def("pick_tile_f32", &pick_tile_f32, "tile id the f32 conv heuristic picks for (M, Cout, K, small)");
   m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 (or fp32) NHWC4", py::arg("img"),

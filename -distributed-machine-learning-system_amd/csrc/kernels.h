@@ -64,6 +64,8 @@ struct WinoArgs {
   int TX, TY;          // 2x2 tiles per row / column
   int IMG, R, bpi;     // images per block, tile rows per block, blocks per image
   int RIN, NP;         // staged input rows per image, pixels per column-parity half row
+  int NPP, RMUL;       // pixel positions per staged half row (>= NP) and the row rotation
+                       // multiplier: row r holds pixel p at ((r/2)*RMUL + p) mod NPP
   int raw_ins;         // 1 KiB DMA instructions of the staged input region (max over blocks)
   int LIN;             // 1: a block takes 16*NW CONSECUTIVE tiles of the flattened (image,
                        // tile row, tile column) order, staging virtual rows (RIN = 2*TY+2 per
@@ -75,6 +77,7 @@ struct WinoArgs {
 void set_wino_ablation(int mode);
 void set_wino_pairing(bool on);
 void set_wino_linear(bool on);
+void set_wino_rotation(bool on);
 bool conv_wino_f32_launch(WinoArgs a, int variant, hipStream_t st);   // false: shape unsupported
 bool conv_wino_f32_supported(int H, int W, int C, int Cout);
 int conv_f32_pick(int M, int Cout, int K, bool small);

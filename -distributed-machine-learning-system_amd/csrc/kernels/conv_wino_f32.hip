@@ -47,9 +47,9 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 constexpr int kRawMax = 40 * 1024;      // staged input region per stage (bytes)
 constexpr int kUBytes = 16 * 32 * 64;   // 16 e x 32 couts x 16 channels x 4 B = 32 KiB
 constexpr int kStage = kRawMax + kUBytes;
-// variant 3 (one stage, two blocks per CU): 64 KiB per block.  40 KiB (LIN also
-// at 56x56) measured neutral there (559 vs 559 us, profiles/r2_v8_wino_linear.md)
-constexpr int kRaw3 = 32 * 1024;
+// variant 3 (one stage, two blocks per CU): 72 KiB per block (the rotated 7x7
+// layout holds 4 images x 10 rows x 2 x 8 pixels x 64 B = 40 KiB)
+constexpr int kRaw3 = 40 * 1024;
 
 __device__ __forceinline__ int raw_swz(int p) { return wino_raw_swz(p); }   // tile_math.h
 
@@ -75,7 +75,7 @@ void set_wino_ablation(int mode) { g_wino_ablate = mode; }
 extern bool g_wino_pair;
 void set_wino_pairing(bool on) { g_wino_pair = on; }
 
-// SINGLE: one LDS stage of 32 KiB raw + 32 KiB U (64 KiB) instead of two of
+// SINGLE: one LDS stage of 40 KiB raw + 32 KiB U (72 KiB) instead of two of
 // 40 + 32 KiB, so TWO 4-wave blocks share a CU: each block's DMA wait,
 // transform and epilogue (its output stores are 64 KiB) then overlap the other
 // block's MFMAs -- with one 144-KiB block per CU they cannot (ablation:
@@ -102,7 +102,7 @@ __global__ void __launch_bounds__(64 * NW, SINGLE ? 2 : 1) conv_wino_f32_kernel(
   const int lid = xcd_remap(blockIdx.x, nwg);
   const int tb = lid / a.nblk_n, nb = lid - tb * a.nblk_n;
   const int n0 = nb * 32;
-  const int rowb = 2 * a.NP * 64;                     // bytes per staged image row
+  const int rowb = 2 * a.NPP * 64;                    // bytes per staged image row
   int b0, ty0, imgs, rows;
   int t0 = 0, vr0 = 0, n_ins = a.raw_ins;             // LIN: first tile, first virtual row, DMA count
   const int per = a.TX * a.TY;
@@ -142,14 +142,19 @@ __global__ void __launch_bounds__(64 * NW, SINGLE ? 2 : 1) conv_wino_f32_kernel(
     if (ins < n_ins) {
       const int qs = L & 3;
       int rest = L >> 2;
-      const int p = rest % a.NP;
-      rest /= a.NP;
+      const int pos = rest % a.NPP;                  // LDS pixel position in the half row
+      rest /= a.NPP;
       const int half = rest & 1;
       const int lr = rest >> 1;
+      // row rotation: staged row lr holds pixel p at position (p + f(lr)) mod NPP
+      const int p = (pos + a.NPP - ((lr >> 1) * a.RMUL) % a.NPP) % a.NPP;
       const int ix = 2 * p + half - 1;
-      const int q = qs ^ raw_swz(p);
+      const int q = qs ^ raw_swz(pos);
       int img, iy;
-      if (a.LIN) {
+      if (p >= a.NP) {
+        img = a.B;                                   // padding position of a rotated row
+        iy = 0;
+      } else if (a.LIN) {
         const int vr = vr0 + lr;
         img = vr / a.RIN;
         iy = vr - img * a.RIN - 1;
@@ -215,11 +220,19 @@ __global__ void __launch_bounds__(64 * NW, SINGLE ? 2 : 1) conv_wino_f32_kernel(
     s_row = s_img * a.RIN + 2 * s_tyl;
   }
   const int pbase = s_ok ? s_row * rowb : 0;
-  int colb[4];
+  // patch rows 0-1 and 2-3 sit in staged row pairs s_row/2 and s_row/2 + 1,
+  // each rotated by its own f = (pair * RMUL) mod NPP: with RMUL = TX, the
+  // lanes of one ds_read_b128 group (consecutive tiles, possibly across tile
+  // rows) read pixels at consecutive positions mod 8 -> distinct bank slots
+  int colb[2][4];
 #pragma unroll
-  for (int px = 0; px < 4; ++px) {
-    const int p = s_ok ? s_tx + (px >> 1) : 0;
-    colb[px] = (px & 1) * a.NP * 64 + p * 64 + ((g ^ raw_swz(p)) << 4);
+  for (int h = 0; h < 2; ++h) {
+    const int f = (((s_row >> 1) + h) * a.RMUL) % a.NPP;
+#pragma unroll
+    for (int px = 0; px < 4; ++px) {
+      const int pos = s_ok ? (s_tx + (px >> 1) + f) % a.NPP : 0;
+      colb[h][px] = (px & 1) * a.NPP * 64 + pos * 64 + ((g ^ raw_swz(pos)) << 4);
+    }
   }
 
   float4v acc[16][2];
@@ -261,7 +274,7 @@ __global__ void __launch_bounds__(64 * NW, SINGLE ? 2 : 1) conv_wino_f32_kernel(
 #pragma unroll
       for (int py = 0; py < 4; ++py)
 #pragma unroll
-        for (int px = 0; px < 4; ++px) d[py][px] = ldsr<ASMRD>(sb + pbase + py * rowb + colb[px]);
+        for (int px = 0; px < 4; ++px) d[py][px] = ldsr<ASMRD>(sb + pbase + py * rowb + colb[py >> 1][px]);
     }
     lds_wait<ASMRD, 0>();
 #pragma unroll
@@ -704,15 +717,21 @@ __global__ void __launch_bounds__(256, 1) conv_wino2_f32_kernel(const WinoArgs a
 // Host-side block geometry for T = 16*nw tiles per block; false if the shape
 // does not fit (caller falls back to the direct conv).  ``lin``: use the
 // consecutive-tile (LIN) blocking when the rectangular one leaves tile slots
-// idle and every block's virtual-row range fits ``raw_max``.
-static bool wino_geometry(WinoArgs& a, int nw, int raw_max = kRawMax, bool lin = false) {
+// idle and every block's virtual-row range fits ``raw_max``.  ``rot``: rotate
+// the staged rows (pixel positions padded to a multiple of 8 per half row) so
+// the patch reads of lanes whose tiles lie in different tile rows hit distinct
+// LDS banks; dropped when the padded rows do not fit.
+static bool wino_geometry_np(WinoArgs& a, int nw, int raw_max, bool lin, int npp) {
   const int T = 16 * nw;
   a.TX = (a.W + 1) / 2;
   a.TY = (a.H + 1) / 2;
   a.LIN = 0;
+  a.NP = a.TX + 1;
+  a.NPP = npp;
   if (a.TX > T) return false;
   const int per = a.TX * a.TY;
-  auto raw_bytes = [&](int imgs, int R) { return imgs * (2 * R + 2) * 2 * (a.TX + 1) * 64; };
+  const int rowb = 2 * a.NPP * 64;
+  auto raw_bytes = [&](int imgs, int R) { return imgs * (2 * R + 2) * rowb; };
   if (per <= T) {
     a.R = a.TY;
     a.IMG = T / per;
@@ -726,7 +745,6 @@ static bool wino_geometry(WinoArgs& a, int nw, int raw_max = kRawMax, bool lin =
   }
   if (raw_bytes(a.IMG, a.R) > raw_max) return false;
   a.RIN = 2 * a.R + 2;
-  a.NP = a.TX + 1;
   a.raw_ins = (raw_bytes(a.IMG, a.R) + 1023) / 1024;
   a.nblk_t = a.IMG > 1 ? (a.B + a.IMG - 1) / a.IMG : a.B * a.bpi;
   a.nblk_n = a.Cout / 32;
@@ -734,7 +752,7 @@ static bool wino_geometry(WinoArgs& a, int nw, int raw_max = kRawMax, bool lin =
   if (lin && used * 100 < (long)a.nblk_t * T * 95) {
     // every block's staged rows (the kernel's own formula); periodic in the
     // block index with period lcm(T, per) / T <= per blocks
-    const int rin = 2 * a.TY + 2, rowb = 2 * a.NP * 64;
+    const int rin = 2 * a.TY + 2;
     const long nblk = (used + T - 1) / T;
     int worst = 0;
     for (long tb = 0; tb < nblk && tb <= per; ++tb) {
@@ -754,6 +772,25 @@ static bool wino_geometry(WinoArgs& a, int nw, int raw_max = kRawMax, bool lin =
   return true;
 }
 
+static bool wino_geometry(WinoArgs& a, int nw, int raw_max = kRawMax, bool lin = false, bool rot = false) {
+  a.RMUL = 0;
+  if (rot) {
+    WinoArgs r = a;
+    const int npp = (a.W + 1) / 2 + 1;
+    if (wino_geometry_np(r, nw, raw_max, lin, (npp + 7) / 8 * 8)) {
+      // keep the rotation only if it costs no tile slots
+      WinoArgs p = a;
+      wino_geometry_np(p, nw, raw_max, lin, npp);
+      if (r.nblk_t <= p.nblk_t) {
+        a = r;
+        a.RMUL = a.TX;
+        return true;
+      }
+    }
+  }
+  return wino_geometry_np(a, nw, raw_max, lin, (a.W + 1) / 2 + 1);
+}
+
 bool conv_wino_f32_supported(int H, int W, int C, int Cout) {
   WinoArgs a{};
   a.B = 1; a.H = H; a.W = W; a.C = C; a.Cout = Cout;
@@ -762,6 +799,12 @@ bool conv_wino_f32_supported(int H, int W, int C, int Cout) {
 
 bool g_wino_lin = true;    // A/B switch (set_wino_linear): LIN blocking in variant 3
 void set_wino_linear(bool on) { g_wino_lin = on; }
+// A/B switch (set_wino_rotation): rotated raw rows in variant 3.  Off: the
+// rotation removes the simulated 2-way raw-read bank conflicts (PMC lds_conf
+// 0.21-0.23) but measured 0.99-1.00x at 56/28/14 and 1.02x (slower) at 7x7
+// (profiles/r2_v11_wino_rotation.md) -- the conflicts are not on the critical path
+bool g_wino_rot = false;
+void set_wino_rotation(bool on) { g_wino_rot = on; }
 bool g_wino_pair = false;  // A/B switch (set_wino_pairing): e-GEMMs in pairs (4w: -4 %, 8w: +13 % time, same box)
 
 template <int NW, bool R>
@@ -778,7 +821,7 @@ static void wino_cfg(WinoArgs a, hipStream_t st) {
 //          3 = 4 waves, one 58-KiB stage, two blocks per CU
 bool conv_wino_f32_launch(WinoArgs a, int variant, hipStream_t st) {
   if (variant == 3) {
-    if (a.C % 16 || a.Cout % 32 || !wino_geometry(a, 4, kRaw3, g_wino_lin)) return false;
+    if (a.C % 16 || a.Cout % 32 || !wino_geometry(a, 4, kRaw3, g_wino_lin, g_wino_rot)) return false;
     const int lds = kRaw3 + kUBytes;
     const bool r = a.res != nullptr;
     auto kern = a.ablate ? (r ? conv_wino_f32_kernel<4, true, false, true, true>
