@@ -46,9 +46,12 @@ struct ConvF32Args {
   int tiles_n, tiles_m;
   const void* zero;    // >= 16 zero bytes
   int ldx;             // input pixel stride in floats (0: C)
+  // packed-row stem input (mode 2, preprocess_pack3_f32): x = [B][H][nc][wp]
+  int nc, wp, cpk;     // row copies, floats per copy row, 16-byte chunks per kh row (ceil(3*KW/4))
 };
 
-bool conv_f32_launch(ConvF32Args a, bool small, int tile, hipStream_t st);   // false: unknown tile id
+// mode: 0 big-C (kh, kw, c), 1 small-C NHWC4 stems, 2 packed-row RGB stems
+bool conv_f32_launch(ConvF32Args a, int mode, int tile, hipStream_t st);   // false: unknown tile id
 
 // fp32 Winograd F(2x2,3x3) conv (3x3, stride 1, pad 1), conv_wino_f32.hip.
 struct WinoArgs {
@@ -81,6 +84,12 @@ void set_wino_rotation(bool on);
 bool conv_wino_f32_launch(WinoArgs a, int variant, hipStream_t st);   // false: shape unsupported
 bool conv_wino_f32_supported(int H, int W, int C, int Cout);
 int conv_f32_pick(int M, int Cout, int K, bool small);
+// uint8 HWC -> packed-row fp32 stem input [B][H][nc][wp] (conv mode 2): copy c of
+// row y is the normalised row (3 floats per pixel, `pad` zero pixels first) shifted
+// left by c * (4 / nc) floats
+void preprocess_pack3_f32_launch(const uint8_t* img, float* out, int B, int H, int W, int pad, int nc, int wp,
+                                 const long long* start_idx, long long start_off, long long max_start,
+                                 long long sub, hipStream_t st);
 void preprocess_f32_launch(const uint8_t* img, float* out, long npix, const long long* start_idx,
                            long long start_off, long long max_start, long long sub, long pix_per_img,
                            hipStream_t st);

@@ -33,6 +33,11 @@
 //         chunk c = all 4 channels of tap kw = blk*BK/4 + c (one pixel), so a
 //         7x7/11x11 stem streams whole pixels; padding taps read the zero
 //         buffer and have zero weights.
+//   pack3 (mode 2, RGB stems from preprocess_pack3_f32): the 3*KW floats of one
+//         kernel row are contiguous in a packed row copy in which they start
+//         16-byte aligned; K = (kh, chunk of 4 floats), ceil(3*KW/4) chunks per
+//         kh, 4 chunks per stage.  The 7x7/2 ResNet stem: K 168 (+8 pad) vs 224
+//         for NHWC4, the 11x11/4 AlexNet conv1: 400 vs 528.
 #include "../kernels.h"
 #include "../launch_util.h"
 
@@ -63,8 +68,9 @@ __device__ __forceinline__ void wait_ring(int pending) {
 
 }  // namespace
 
-template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool SMALL>
+template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, int KM>
 __global__ void __launch_bounds__(64 * WN * WM) conv_f32_kernel(const ConvF32Args a) {
+  constexpr bool SMALL = KM == 1, P3 = KM == 2;
   constexpr int NW = WN * WM;
   constexpr int TN = BN / WN, TM = BM / WM;
   constexpr int FN = TN / 16, FM = TM / 16;
@@ -78,7 +84,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_f32_kernel(const ConvF32Arg
   constexpr int A_BYTES = BN * RB, STAGE = (BN + BM) * RB;
   static_assert(NS >= 2 && NS <= 4, "ring depth");
   static_assert(G * (NS - 2) < 64, "vmcnt immediate");
-  static_assert(!SMALL || BK == 16, "small-C packing is 4 taps x 4 channels per 16 floats");
+  static_assert(KM == 0 || BK == 16, "small-C / pack3 stages are 16 floats");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -104,16 +110,30 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_f32_kernel(const ConvF32Arg
   // B (pixels): image base, top-left input coordinate and the lane's chunk
   const int ldx = a.ldx ? a.ldx : a.C;
   int b_base[GB], b_ih0[GB], b_iw0[GB];
+  // pack3: this lane's (kh, chunk) of the stage being issued (advanced by 4
+  // chunks per stage; cpk >= 4 is checked on the host)
+  int p_kh[P3 ? GB : 1], p_q[P3 ? GB : 1];
+  const int prow = a.nc * a.wp;                        // pack3: floats per image row (all copies)
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int row = (wave + NW * j) * RPI + lrow;
     const int m = m0 + row;
     const int ch = lslot ^ swz_r(row, CPR);
+    if constexpr (P3) {
+      p_kh[j] = 0;
+      p_q[j] = ch;
+    }
     if (m < a.M) {
       const int hw = a.Ho * a.Wo;
       const int b = m / hw, r = m - b * hw;
       const int oh = r / a.Wo, ow = r - oh * a.Wo;
-      b_base[j] = b * a.H * a.W * ldx + (SMALL ? 0 : ch * 4);
+      if constexpr (P3) {
+        const int r0 = 3 * a.stride * ow;               // first float of the pixel's kernel row in R
+        const int sh = r0 & 3, g = 4 / a.nc;            // copy sh/g starts it 16-byte aligned
+        b_base[j] = b * a.H * prow + (sh / g) * a.wp + r0 - sh;
+      } else {
+        b_base[j] = b * a.H * a.W * ldx + (SMALL ? 0 : ch * 4);
+      }
       b_ih0[j] = oh * a.stride - a.pad;
       b_iw0[j] = ow * a.stride - a.pad + (SMALL ? ch : 0);   // small: chunk = tap offset
     } else {
@@ -137,6 +157,19 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_f32_kernel(const ConvF32Arg
     }
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
+      if constexpr (P3) {
+        const int ih = b_ih0[j] + p_kh[j];
+        const bool ok = p_kh[j] < a.KH && (unsigned)ih < (unsigned)a.H;
+        const float* src = ok ? a.x + b_base[j] + ih * prow + 4 * p_q[j] : zero;
+        __builtin_amdgcn_global_load_lds((glb_void_t*)src,
+                                         (lds_void_t*)(base + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
+        p_q[j] += CPR;
+        if (p_q[j] >= a.cpk) {
+          p_q[j] -= a.cpk;
+          ++p_kh[j];
+        }
+        continue;
+      }
       int ih, iw, coff;
       if constexpr (SMALL) {
         ih = b_ih0[j] + i_kh;
@@ -268,11 +301,14 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_f32_kernel(const ConvF32Arg
   }
 }
 
-template <int BN, int BM, int BK, int WN, int WM, int NS, bool R, bool S>
+template <int BN, int BM, int BK, int WN, int WM, int NS, bool R, int S>
 static void f32_cfg(ConvF32Args a, hipStream_t st) {
   a.tiles_n = (a.Cout + BN - 1) / BN;
   a.tiles_m = (a.M + BM - 1) / BM;
-  if constexpr (S) {
+  if constexpr (S == 2) {
+    a.cblk = 1;
+    a.nK = (a.KH * a.cpk + BK / 4 - 1) / (BK / 4);
+  } else if constexpr (S == 1) {
     a.cblk = a.nsub;                 // tap blocks per kh row
     a.nK = a.KH * a.nsub;
   } else {
@@ -297,8 +333,8 @@ static void f32_cfg(ConvF32Args a, hipStream_t st) {
 //   107:  64x64,  BK 16, 4 waves (2x2, 32x32 per wave), 3 stages   24 KiB
 //   108: 128x128, BK 16, 4 waves (2x2),                 4 stages   64 KiB
 //   109:  64x256, BK 16, 4 waves (1x4, 64x64 per wave), 4 stages   80 KiB
-// The small-C (stem) path supports every id (all are BK 16) except 101.
-template <bool R, bool S>
+// The small-C and pack3 (stem) paths support every id (all are BK 16) except 101.
+template <bool R, int S>
 static bool f32_dispatch(ConvF32Args a, int tile, hipStream_t st) {
   switch (tile) {
     case 100: f32_cfg<128, 128, 16, 2, 2, 3, R, S>(a, st); return true;
@@ -317,10 +353,11 @@ static bool f32_dispatch(ConvF32Args a, int tile, hipStream_t st) {
   }
 }
 
-bool conv_f32_launch(ConvF32Args a, bool small, int tile, hipStream_t st) {
+bool conv_f32_launch(ConvF32Args a, int mode, int tile, hipStream_t st) {
   const bool res = a.res != nullptr;
-  if (small) return res ? f32_dispatch<true, true>(a, tile, st) : f32_dispatch<false, true>(a, tile, st);
-  return res ? f32_dispatch<true, false>(a, tile, st) : f32_dispatch<false, false>(a, tile, st);
+  if (mode == 2) return res ? f32_dispatch<true, 2>(a, tile, st) : f32_dispatch<false, 2>(a, tile, st);
+  if (mode == 1) return res ? f32_dispatch<true, 1>(a, tile, st) : f32_dispatch<false, 1>(a, tile, st);
+  return res ? f32_dispatch<true, 0>(a, tile, st) : f32_dispatch<false, 0>(a, tile, st);
 }
 
 // Default tile per (M, Cout, K = KH*KW*C), from the per-layer sweep on MI355X

@@ -46,11 +46,13 @@ class Conv:
     relu: bool
     small: bool = False      # RGB stem packing
     wino: torch.Tensor | None = None   # fp32 3x3/s1: Winograd U = G g G^T [16, Cout, Cin]
+    p3: torch.Tensor | None = None     # fp32 RGB stem on packed rows (pack_conv_weight_p3)
 
     def to(self, device):
         return Conv(self.w.to(device), self.b.to(device), self.cin, self.cout, self.kh, self.kw,
                     self.stride, self.pad, self.relu, self.small,
-                    None if self.wino is None else self.wino.to(device))
+                    None if self.wino is None else self.wino.to(device),
+                    None if self.p3 is None else self.p3.to(device))
 
     @property
     def flops_per_out_pixel(self) -> int:
@@ -152,6 +154,27 @@ def pack_conv_weight(w: torch.Tensor, dtype: str = "fp16") -> tuple[torch.Tensor
     return w.permute(0, 2, 3, 1).reshape(cout, kh * kw * cin).half().contiguous(), False
 
 
+def pack_conv_weight_p3(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, 3, KH, KW] -> [Cout, ceil(KH*cpk/4)*16] fp32 for the packed-row
+    stem (conv_f32.hip mode 2): K = (kh, f) with f = 3*kw + c over
+    cpk = ceil(3*KW/4) 16-byte chunks per kernel row (f >= 3*KW: zero), the
+    order in which preprocess_pack3_f32 lays a kernel row's pixels out."""
+    cout, cin, kh, kw = w.shape
+    if cin != 3 or kw < 5:
+        raise ValueError("packed-row stems take 3 input channels and KW >= 5")
+    cpk = (3 * kw + 3) // 4
+    nk = (kh * cpk + 3) // 4
+    rows = torch.zeros(cout, kh, 4 * cpk, dtype=torch.float32)
+    rows[:, :, :3 * kw] = w.float().permute(0, 2, 3, 1).reshape(cout, kh, 3 * kw)
+    p = torch.zeros(cout, nk * 16, dtype=torch.float32)
+    p[:, :kh * 4 * cpk] = rows.reshape(cout, -1)
+    return p.contiguous()
+
+
+def pack3_eligible(cin: int, kw: int) -> bool:
+    return cin == 3 and kw >= 5
+
+
 def unpack_conv_weight(c: Conv) -> torch.Tensor:
     """Inverse of pack_conv_weight -> fp32 [Cout, Cin, KH, KW]."""
     w = c.w.float()
@@ -185,8 +208,10 @@ def make_conv(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, relu: bool, dtype: str
                                          conv.padding[0]):
         return Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, 3, 3, 1, 1, relu, small,
                     wino_weight(w))
+    p3 = pack_conv_weight_p3(w) if dtype == "fp32" and pack3_eligible(conv.in_channels, conv.kernel_size[1]) \
+        else None
     return Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, conv.kernel_size[0],
-                conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small)
+                conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small, None, p3)
 
 
 def make_fc(lin: nn.Linear, relu: bool, perm: torch.Tensor | None = None, dtype: str = "fp16") -> Conv:
@@ -301,7 +326,7 @@ class HipRunner:
     """
 
     def __init__(self, program: Program, device=None, fuse_stem: bool = True, front_split: int | None = None,
-                 winograd: bool = True, wino_variant: int | None = None):
+                 winograd: bool = True, wino_variant: int | None = None, pack3: bool = True):
         from .. import ops
 
         ops.load()
@@ -310,6 +335,7 @@ class HipRunner:
         # fp32 3x3/s1 convs through the fused Winograd F(2x2,3x3) kernel (2.25x
         # fewer f32-MFMA products than the direct conv; conv_wino_f32.hip)
         self.winograd = winograd
+        self.pack3 = pack3           # fp32 RGB stems on packed rows (conv_f32.hip mode 2)
         # None = measured default (tools/wino_ablate.py, profiles/r2_v6_wino_variants.md):
         # variant 3 -- 4-wave blocks of 64 tiles, one 58-KiB LDS stage, two blocks
         # per CU -- is the fastest on every ResNet layer shape (same-box A/B:
@@ -376,16 +402,22 @@ class HipRunner:
         o, p = self.ops, self.p
         if not native:
             raise ValueError("the fp32 path takes 224x224 inputs (resize on host first)")
-        x = o.preprocess(img_u8, start, batch, start_offset, f32=True)
+        first = p.stem if p.kind == "resnet" else p.features[0][1]
+        if self.pack3 and first.p3 is not None:
+            # RGB stem on packed rows (K 168 vs 224 for the 7x7/2, 400 vs 528 for the 11x11/4)
+            x3 = o.preprocess_pack3(img_u8, first.kw, first.stride, first.pad, start, batch, start_offset)
+            x = o.conv2d_pack3(x3, first.p3, first.b, img_u8.shape[2], first.kh, first.kw, first.stride,
+                               first.pad, first.relu)
+        else:
+            x = o.preprocess(img_u8, start, batch, start_offset, f32=True)
+            x = o.conv2d(x, first.w, first.b, first.kh, first.kw, first.stride, first.pad, first.relu)
         if p.kind == "resnet":
-            s = p.stem
-            x = o.conv2d(x, s.w, s.b, s.kh, s.kw, s.stride, s.pad, s.relu)
             x = o.maxpool2d(x, 3, 2, 1)
             for blk in p.blocks:
                 x = self._block(blk, x)
             x = o.global_avgpool(x)
         else:
-            for k, v in p.features:
+            for k, v in p.features[1:]:
                 x = self._conv(v, x) if k == "conv" else o.maxpool2d(x, *v)
             x = x.reshape(x.shape[0], -1)
         for fc in p.fcs:

@@ -12,7 +12,7 @@ from ._ext import available, load, so_path
 __all__ = [
     "available", "load", "so_path", "conv2d", "linear", "preprocess", "resize_crop",
     "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile", "pick_tile_f32", "synth_images", "stem_fused",
-    "conv2d_wino", "wino_supported",
+    "conv2d_wino", "wino_supported", "preprocess_pack3", "conv2d_pack3",
 ]
 
 
@@ -34,6 +34,17 @@ def conv2d_wino(x, u, bias, relu: bool, residual=None, variant: int = 0):
     """fp32 3x3/stride-1/pad-1 conv by fused Winograd F(2x2,3x3) (conv_wino_f32.hip);
     ``u`` = models.packed.wino_weight(w) [16, Cout, Cin]."""
     return load().conv2d_wino_f32(x, u, bias, residual, relu, variant)
+
+
+def preprocess_pack3(img_u8, kw: int, stride: int, pad: int, start=None, batch: int = -1, start_offset: int = 0,
+                     window: int = -1, sub: int = 0):
+    """uint8 [B,H,W,3] -> packed-row fp32 stem input [B, H, nc, wp] (window args as ``preprocess``)."""
+    return load().preprocess_pack3(img_u8, kw, stride, pad, start, batch, start_offset, window, sub)
+
+
+def conv2d_pack3(x3, w, bias, width: int, kh: int, kw: int, stride: int, pad: int, relu: bool, tile: int = -1):
+    """fp32 RGB stem conv on packed rows; ``w`` = models.packed.pack_conv_weight_p3(w)."""
+    return load().conv2d_pack3_f32(x3, w, bias, width, kh, kw, stride, pad, relu, tile)
 
 
 def wino_supported(h: int, w: int, cin: int, cout: int) -> bool:

@@ -278,3 +278,49 @@ def test_runner_winograd_matches_direct(ops):
     a = HipRunner(p, winograd=True).logits(img)
     b = HipRunner(p, winograd=False).logits(img)
     assert (a - b).abs().max().item() <= 2e-5 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("tile", [-1] + [t for t in F32_TILES if t != 101])
+@pytest.mark.parametrize("B,H,W,k,s,p,Cout", [
+    (2, 224, 224, 7, 2, 3, 64),     # ResNet stem
+    (2, 224, 224, 11, 4, 2, 64),    # AlexNet conv1
+    (1, 37, 29, 7, 2, 3, 64),       # ragged image, odd width: both row copies, padding on every border
+    (3, 20, 20, 5, 1, 2, 12),       # stride 1: four row copies
+])
+def test_conv_f32_pack3_stems(ops, tile, B, H, W, k, s, p, Cout):
+    """RGB stems on packed rows (preprocess_pack3 + conv_f32 mode 2) vs fp64."""
+    from idunno.models.packed import pack_conv_weight_p3
+    from idunno.models.reference import preprocess_u8
+
+    torch.manual_seed(H + k + tile)
+    img = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=DEV)
+    w = torch.randn(Cout, 3, k, k) / (3 * k * k) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    x3 = ops.preprocess_pack3(img, k, s, p)
+    y = ops.conv2d_pack3(x3, pack_conv_weight_p3(w).to(DEV), b.to(DEV), W, k, k, s, p, True, tile)
+    ref = _ref_conv64(preprocess_u8(img).permute(0, 2, 3, 1), w, b, s, p, True)
+    assert y.shape == ref.shape
+    _check(y, ref)
+
+
+def test_preprocess_pack3_window(ops):
+    """Device-side window start (graph capture) reads the same images as slicing."""
+    torch.manual_seed(11)
+    shard = torch.randint(0, 256, (10, 32, 30, 3), dtype=torch.uint8, device=DEV)
+    start = torch.tensor([103], dtype=torch.int64, device=DEV)        # global index, shard starts at 100
+    a = ops.preprocess_pack3(shard, 7, 2, 3, start, 4, 100)
+    b = ops.preprocess_pack3(shard[3:7].contiguous(), 7, 2, 3)
+    assert torch.equal(a, b)
+    part = ops.preprocess_pack3(shard, 7, 2, 3, start, 2, 100, 4, 2)
+    assert torch.equal(part, b[2:])
+
+
+@pytest.mark.parametrize("name", ["resnet18", "alexnet"])
+def test_runner_pack3_matches_nhwc4_stem(ops, name):
+    from idunno.models import HipRunner, build_program
+
+    p = build_program(name, seed=3, randomize_bn=True, dtype="fp32")
+    img = ops.synth_images(9, 0, 5, DEV)
+    a = HipRunner(p, pack3=True).logits(img)
+    b = HipRunner(p, pack3=False).logits(img)
+    assert (a - b).abs().max().item() <= 2e-5 * b.abs().max().item()
