@@ -336,6 +336,8 @@ class HipRunner:
         # fewer f32-MFMA products than the direct conv; conv_wino_f32.hip)
         self.winograd = winograd
         self.pack3 = pack3           # fp32 RGB stems on packed rows (conv_f32.hip mode 2)
+        self.side_down = False       # downsample conv on a second stream (A/B: tools/ab_flag.py --attr)
+        self._side: dict = {}
         # None = measured default (tools/wino_ablate.py, profiles/r2_v6_wino_variants.md):
         # variant 3 -- 4-wave blocks of 64 tiles, one 58-KiB LDS stage, two blocks
         # per CU -- is the fastest on every ResNet layer shape (same-box A/B:
@@ -432,14 +434,36 @@ class HipRunner:
         return self.ops.conv2d(x, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu, residual=residual, out=out)
 
     def _block(self, blk, x, out=None):
-        """One residual block; the last conv fuses +identity and ReLU (into ``out``)."""
+        """One residual block; the last conv fuses +identity and ReLU (into ``out``).
+        With ``side_down`` the 1x1 downsample conv runs on a second stream,
+        concurrently with the block's first conv (a fork/join that hipGraph
+        capture keeps as two parallel branches)."""
         idt = x
+        join = None
         if blk.down is not None:
-            idt = self._conv(blk.down, x)
+            if self.side_down and x.is_cuda:
+                cur = torch.cuda.current_stream(x.device)
+                side = self._side_stream(x.device)
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    idt = self._conv(blk.down, x)
+                x.record_stream(side)          # x / idt cross streams: keep the allocator honest
+                idt.record_stream(cur)
+                join = side
+            else:
+                idt = self._conv(blk.down, x)
         y = x
         for c in blk.convs[:-1]:
             y = self._conv(c, y)
+        if join is not None:
+            torch.cuda.current_stream(x.device).wait_stream(join)
         return self._conv(blk.convs[-1], y, residual=idt, out=out)
+
+    def _side_stream(self, device):
+        st = self._side.get(device)
+        if st is None:
+            st = self._side[device] = torch.cuda.Stream(device=device)
+        return st
 
     def _front_blocks(self) -> int:
         """Leading blocks that keep the stem's resolution (ResNet layer1)."""

@@ -324,3 +324,23 @@ def test_runner_pack3_matches_nhwc4_stem(ops, name):
     a = HipRunner(p, pack3=True).logits(img)
     b = HipRunner(p, pack3=False).logits(img)
     assert (a - b).abs().max().item() <= 2e-5 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp16"])
+def test_runner_side_stream_downsample(ops, dtype):
+    """Downsample convs on a second stream (eager and captured) give the same logits."""
+    from idunno.models import HipRunner, build_program
+
+    p = build_program("resnet18", seed=5, randomize_bn=True, dtype=dtype)
+    img = ops.synth_images(3, 0, 16, DEV)
+    a = HipRunner(p)
+    b = HipRunner(p)
+    b.side_down = True
+    la, lb = a.logits(img), b.logits(img)
+    assert torch.equal(la, lb)
+    sin, run = b.capture(16)
+    sin.copy_(img)
+    cls, prob = run()
+    c0, p0 = a.forward(img)
+    torch.cuda.synchronize()
+    assert torch.equal(cls, c0) and torch.equal(prob, p0)
