@@ -589,7 +589,7 @@ torch::Tensor resize_crop(torch::Tensor img, int64_t resize, int64_t crop) {
   return out;
 }
 
-torch::Tensor maxpool2d_nhwc(torch::Tensor x, int64_t k, int64_t s, int64_t pad) {
+torch::Tensor maxpool2d_nhwc(torch::Tensor x, int64_t k, int64_t s, int64_t pad, c10::optional<torch::Tensor> out) {
   CHECK_DEV(x);
   CHECK_CONTIG(x);
   const bool f32 = x.scalar_type() == torch::kFloat;
@@ -599,7 +599,17 @@ torch::Tensor maxpool2d_nhwc(torch::Tensor x, int64_t k, int64_t s, int64_t pad)
   const int B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int Ho = (H + 2 * pad - k) / s + 1, Wo = (W + 2 * pad - k) / s + 1;
   TORCH_CHECK(Ho > 0 && Wo > 0, "empty output");
-  auto y = torch::empty({B, Ho, Wo, C}, x.options());
+  torch::Tensor y;
+  if (out.has_value() && out->defined()) {        // e.g. a batch slice of a larger tensor
+    y = *out;
+    CHECK_DEV(y);
+    CHECK_CONTIG(y);
+    TORCH_CHECK(y.scalar_type() == x.scalar_type() && y.device() == x.device(), "out dtype/device mismatch");
+    TORCH_CHECK(y.dim() == 4 && y.size(0) == B && y.size(1) == Ho && y.size(2) == Wo && y.size(3) == C,
+                "out shape mismatch");
+  } else {
+    y = torch::empty({B, Ho, Wo, C}, x.options());
+  }
   if (!B) return y;
   if (f32) {
     maxpool_f32_launch(x.data_ptr<float>(), y.data_ptr<float>(), B, H, W, C, Ho, Wo, k, s, pad, cur_stream());
@@ -696,7 +706,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("start") = py::none(), py::arg("batch") = -1,
         py::arg("start_offset") = 0, py::arg("window") = -1, py::arg("sub") = 0);
   m.def("resize_crop", &resize_crop, "bilinear resize + centre crop + normalise");
-  m.def("maxpool2d_nhwc", &maxpool2d_nhwc, "NHWC max pool");
+  m.def("maxpool2d_nhwc", &maxpool2d_nhwc, "NHWC max pool (into ``out`` when given)", py::arg("x"), py::arg("k"),
+        py::arg("s"), py::arg("pad"), py::arg("out") = py::none());
   m.def("global_avgpool_nhwc", &global_avgpool_nhwc, "NHWC global average pool");
   m.def("softmax_top1", &softmax_top1, "fused row softmax + argmax", py::arg("logits"),
         py::arg("packed") = py::none());

@@ -337,6 +337,7 @@ class HipRunner:
         self.winograd = winograd
         self.pack3 = pack3           # fp32 RGB stems on packed rows (conv_f32.hip mode 2)
         self.side_down = False       # downsample conv on a second stream (A/B: tools/ab_flag.py --attr)
+        self.stem_parts: int | None = None   # fp32 ResNet: stem + maxpool on batch parts (None = 1)
         self._side: dict = {}
         # None = measured default (tools/wino_ablate.py, profiles/r2_v6_wino_variants.md):
         # variant 3 -- 4-wave blocks of 64 tiles, one 58-KiB LDS stage, two blocks
@@ -405,14 +406,31 @@ class HipRunner:
         if not native:
             raise ValueError("the fp32 path takes 224x224 inputs (resize on host first)")
         first = p.stem if p.kind == "resnet" else p.features[0][1]
-        if self.pack3 and first.p3 is not None:
-            # RGB stem on packed rows (K 168 vs 224 for the 7x7/2, 400 vs 528 for the 11x11/4)
-            x3 = o.preprocess_pack3(img_u8, first.kw, first.stride, first.pad, start, batch, start_offset)
-            x = o.conv2d_pack3(x3, first.p3, first.b, img_u8.shape[2], first.kh, first.kw, first.stride,
-                               first.pad, first.relu)
-        else:
-            x = o.preprocess(img_u8, start, batch, start_offset, f32=True)
-            x = o.conv2d(x, first.w, first.b, first.kh, first.kw, first.stride, first.pad, first.relu)
+        nb = batch if start is not None else img_u8.shape[0]
+        parts = self.stem_parts if self.stem_parts is not None else 1
+        if p.kind == "resnet" and parts > 1 and nb >= 2 * parts:
+            # stem + maxpool on batch parts: a part's 112x112x64 stem output
+            # (nb/parts x 3.2 MB) stays in the 256-MB Infinity Cache between the
+            # conv's stores and the pool's reads instead of round-tripping HBM
+            n = -(-nb // parts)
+            x = None
+            for sub in range(0, nb, n):
+                m = min(n, nb - sub)
+                if start is not None:
+                    y = self._stem_f32(first, img_u8, start, m, start_offset, window=nb, sub=sub)
+                else:
+                    y = self._stem_f32(first, img_u8[sub:sub + m], None, -1, 0)
+                if x is None:
+                    x = torch.empty((nb, (y.shape[1] + 1) // 2, (y.shape[2] + 1) // 2, y.shape[3]),
+                                    dtype=y.dtype, device=y.device)
+                o.maxpool2d(y, 3, 2, 1, out=x[sub:sub + m])
+            for blk in p.blocks:
+                x = self._block(blk, x)
+            x = o.global_avgpool(x)
+            for fc in p.fcs:
+                x = o.linear(x, fc.w, fc.b, relu=fc.relu)
+            return x
+        x = self._stem_f32(first, img_u8, start, batch, start_offset)
         if p.kind == "resnet":
             x = o.maxpool2d(x, 3, 2, 1)
             for blk in p.blocks:
@@ -425,6 +443,18 @@ class HipRunner:
         for fc in p.fcs:
             x = o.linear(x, fc.w, fc.b, relu=fc.relu)
         return x
+
+    def _stem_f32(self, first, img_u8, start, batch, start_offset, window: int = -1, sub: int = 0):
+        """fp32 RGB stem conv (+ReLU) of a window / part of the images."""
+        o = self.ops
+        if self.pack3 and first.p3 is not None:
+            # packed rows: K 176 vs 224 for the 7x7/2, 400 vs 528 for the 11x11/4
+            x3 = o.preprocess_pack3(img_u8, first.kw, first.stride, first.pad, start, batch, start_offset, window,
+                                    sub)
+            return o.conv2d_pack3(x3, first.p3, first.b, img_u8.shape[2], first.kh, first.kw, first.stride,
+                                  first.pad, first.relu)
+        x = o.preprocess(img_u8, start, batch, start_offset, window, sub, f32=True)
+        return o.conv2d(x, first.w, first.b, first.kh, first.kw, first.stride, first.pad, first.relu)
 
     def _conv(self, c, x, residual=None, out=None):
         if c.wino is not None and self.winograd and out is None and x.dtype == torch.float32 \

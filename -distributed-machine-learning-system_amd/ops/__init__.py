@@ -101,8 +101,8 @@ def stem_fused(img_u8, w, bias, start=None, batch: int = -1, start_offset: int =
     return load().stem_fused(img_u8, w, bias, start, batch, start_offset, window, sub)
 
 
-def maxpool2d(x, k: int = 3, s: int = 2, pad: int = 1):
-    return load().maxpool2d_nhwc(x, k, s, pad)
+def maxpool2d(x, k: int = 3, s: int = 2, pad: int = 1, out=None):
+    return load().maxpool2d_nhwc(x, k, s, pad, out)
 
 
 def global_avgpool(x):

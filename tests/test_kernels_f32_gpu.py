@@ -344,3 +344,21 @@ def test_runner_side_stream_downsample(ops, dtype):
     c0, p0 = a.forward(img)
     torch.cuda.synchronize()
     assert torch.equal(cls, c0) and torch.equal(prob, p0)
+
+
+def test_runner_stem_parts_bitwise(ops):
+    """fp32 stem + maxpool on batch parts (eager and device-window graph) = one pass."""
+    from idunno.models import HipRunner, build_program
+
+    p = build_program("resnet18", seed=6, randomize_bn=True, dtype="fp32")
+    shard = ops.synth_images(4, 0, 24, DEV)
+    a = HipRunner(p)
+    b = HipRunner(p)
+    b.stem_parts = 3
+    assert torch.equal(a.logits(shard[:10]), b.logits(shard[:10]))
+    _s, run_a = a.capture_window(shard, 12)
+    _s2, run_b = b.capture_window(shard, 12)
+    ca, pa = run_a()
+    cb, pb = run_b()
+    torch.cuda.synchronize()
+    assert torch.equal(ca, cb) and torch.equal(pa, pb)

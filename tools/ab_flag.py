@@ -23,6 +23,7 @@ def main():
     ap.add_argument("setter", nargs="?", default=None)
     ap.add_argument("--attr", default=None, help="HipRunner attribute to switch instead of an extension setter")
     ap.add_argument("--dtype", default="fp32")
+    ap.add_argument("--values", default=None, help="with --attr: 'a,b' integer values instead of False,True")
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--batch", type=int, default=400)
     ap.add_argument("--iters", type=int, default=30)
@@ -37,7 +38,8 @@ def main():
     prog = build_program(a.model, dtype=a.dtype)
     shard = ops.synth_images(1234, 0, a.batch, dev)
     runs, outs, keep = {}, {}, []
-    for flag in (False, True):
+    vals = (False, True) if not a.values else tuple(int(v) for v in a.values.split(","))
+    for flag in vals:
         setter(flag)
         r = HipRunner(prog, dev)
         if a.attr:
@@ -49,8 +51,9 @@ def main():
         torch.cuda.synchronize()
         outs[flag] = (cls.clone(), prob.clone())
     setter(False)
-    agree = (outs[False][0] == outs[True][0]).float().mean().item()
-    dprob = (outs[False][1] - outs[True][1]).abs().max().item()
+    v0, v1 = vals
+    agree = (outs[v0][0] == outs[v1][0]).float().mean().item()
+    dprob = (outs[v0][1] - outs[v1][1]).abs().max().item()
     print(f"{a.setter or a.attr}: top-1 agreement off vs on {agree:.4f}, max |dprob| {dprob:.2e}", flush=True)
     res = {k: [] for k in runs}
     for _ in range(a.rounds):
@@ -67,7 +70,7 @@ def main():
     for flag, v in res.items():
         print(f"{a.setter or a.attr}({flag!s:5s}) {a.model} b{a.batch}: median {statistics.median(v):.4f} ms  "
               f"min {min(v):.4f} ms  rounds {[round(x, 4) for x in v]}", flush=True)
-    off, on = statistics.median(res[False]), statistics.median(res[True])
+    off, on = statistics.median(res[v0]), statistics.median(res[v1])
     print(f"on vs off: {100 * (off / on - 1):+.2f}% throughput", flush=True)
 
 
