@@ -49,6 +49,7 @@ class ClusterConfig:
 
     # -- SDFS ---------------------------------------------------------------------
     replication: int = 4                     # reference places 4-5 replicas (utils.py:48-55)
+    sdfs_peer_copy: bool = True              # shards another node holds in HBM: GPU-to-GPU copy (IPC)
     store_root: str = "/tmp/idunno"
 
     # -- collective data plane (one node per process only) ----------------------

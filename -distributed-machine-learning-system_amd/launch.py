@@ -58,7 +58,8 @@ def run_node(a) -> int:
             torch.cuda.device_count() >= cfg.num_nodes
     tr = TcpTransport(name, cfg.address, cfg.address(name))
     node = Node(cfg, name, tr, ex)
-    node.source = (SdfsSource(node.sdfs, dev) if a.source == "sdfs" else SyntheticSource(cfg.data_seed, dev))
+    node.source = (SdfsSource(node.sdfs, dev, peer_copy=cfg.sdfs_peer_copy) if a.source == "sdfs"
+                   else SyntheticSource(cfg.data_seed, dev))
     if a.index != cfg.coordinator:
         time.sleep(a.join_delay)
     node.start(join=True)

@@ -116,9 +116,14 @@ def shard_name(k: int) -> str:
 
 
 class SdfsSource:
-    """Images from SDFS shards, cached in HBM (LRU by bytes)."""
+    """Images from SDFS shards, cached in HBM (LRU by bytes).
 
-    def __init__(self, sdfs, device, shard_images: int = 500, cache_bytes: int = 32 << 30):
+    A shard another node already holds in HBM is copied GPU-to-GPU from that
+    node (SDFS FETCH_HBM + runtime/ipc.py) instead of being read from a
+    replica over TCP and staged host->HBM; every shard this node caches is
+    announced to the SDFS master so peers can do the same (``peer_copy``)."""
+
+    def __init__(self, sdfs, device, shard_images: int = 500, cache_bytes: int = 32 << 30, peer_copy: bool = True):
         self.sdfs = sdfs
         self.device = torch.device(device)
         self.S = int(shard_images)
@@ -127,6 +132,21 @@ class SdfsSource:
         self.cache_bytes = cache_bytes
         self.lock = threading.Lock()
         self.fetches = 0
+        self.peer_fetches = 0
+        self.peer_copy = peer_copy and self.device.type == "cuda"
+        if self.device.type == "cuda":
+            sdfs.hbm_provider = self.export_shard
+
+    def export_shard(self, name: str, consumer_pid: int | None = None):
+        """IPC export of a cached shard (SDFS FETCH_HBM), or None."""
+        from .ipc import export_tensor
+
+        with self.lock:
+            t = next((v for k, v in self.cache.items() if shard_name(k) == name), None)
+        if t is None:
+            return None
+        torch.cuda.current_stream(self.device).synchronize()     # staged bytes have landed
+        return export_tensor(t, consumer_pid)
 
     def _shard(self, k: int) -> torch.Tensor:
         with self.lock:
@@ -134,18 +154,29 @@ class SdfsSource:
             if t is not None:
                 self.cache.move_to_end(k)
                 return t
-        data = self.sdfs.get_bytes(shard_name(k))
-        if data is None:
-            raise KeyError(f"missing SDFS shard {shard_name(k)}")
-        n = len(data) // IMG_BYTES
-        t = self.stager.stage(data, (n, HW, HW, 3))
+        name = shard_name(k)
+        t = self.sdfs.fetch_hbm(name, self.device) if self.peer_copy else None
+        if t is not None:
+            self.peer_fetches += 1
+        else:
+            data = self.sdfs.get_bytes(name)
+            if data is None:
+                raise KeyError(f"missing SDFS shard {name}")
+            n = len(data) // IMG_BYTES
+            t = self.stager.stage(data, (n, HW, HW, 3))
+        dropped = []
         with self.lock:
             self.fetches += 1
             self.cache[k] = t
             tot = sum(v.numel() for v in self.cache.values())
             while tot > self.cache_bytes and len(self.cache) > 1:
-                _, old = self.cache.popitem(last=False)
+                ko, old = self.cache.popitem(last=False)
                 tot -= old.numel()
+                dropped.append(ko)
+        if self.device.type == "cuda":
+            self.sdfs.announce_hbm(name)
+            for ko in dropped:
+                self.sdfs.announce_hbm(shard_name(ko), held=False)
         return t
 
     def get(self, start: int, end: int) -> torch.Tensor:

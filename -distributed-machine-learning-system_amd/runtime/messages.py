@@ -28,6 +28,8 @@ class Type:
     REPLICATE = "REPLICATE"          # master -> replica: store (name, version, bytes)
     UNLINK = "UNLINK"                # master -> replica: remove all versions
     FETCH = "FETCH"                  # master -> replica: read (name, version)
+    HBM_HAS = "HBM_HAS"              # node -> SDFS master: I hold / dropped this file in HBM
+    FETCH_HBM = "FETCH_HBM"          # node -> node: IPC handle of your HBM copy (GPU-to-GPU copy)
     INFERENCE = "INFERENCE"          # client -> coordinator: a query
     JOB = "JOB"                      # coordinator -> worker: one chunk
     RESULT = "RESULT"                # worker -> coordinator (+ standby): top-1 of a chunk

@@ -177,7 +177,7 @@ class Node:
         if t in (Type.PING, Type.PONG, Type.JOIN, Type.LEAVE, Type.PROMOTE):
             return self.membership.handle(msg)
         if t in (Type.REPLICATE, Type.FETCH, Type.UNLINK, Type.PUT, Type.GET, Type.LS, Type.DELETE,
-                 Type.GET_VERSIONS):
+                 Type.GET_VERSIONS, Type.HBM_HAS, Type.FETCH_HBM):
             return self.sdfs.handle(msg)
         if t == Type.INFERENCE:
             if msg.get("job"):

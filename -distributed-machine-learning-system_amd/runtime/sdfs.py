@@ -11,6 +11,12 @@ Semantics kept from the reference (mp4_machinelearning.py:305-481, 886-945,
   * when a node fails, every file it held is re-replicated to the next live
     ring node that does not already hold it.
 
+Cross-GPU replica copies: nodes that stage a file into
+HBM announce it to the master (HBM_HAS); a node about to stage the same file
+first asks one of those holders for a HIP IPC handle (FETCH_HBM) and copies
+the bytes GPU-to-GPU (runtime/ipc.py, over xGMI between GPUs) instead of
+reading a replica over TCP and copying host->HBM.
+
 Deliberate fixes: a *stable* hash (crc32) instead of the per-process salted
 ``hash()`` (A8); delete really unlinks every version on every replica (A9);
 transfers are single length-prefixed frames, not 4 KB recv loops with fixed
@@ -131,7 +137,10 @@ class Sdfs:
         # master metadata (reference sdfs_file_version / sdfs_file_process / sdfs_store_dict)
         self.file_version: dict[str, int] = {}
         self.file_replicas: dict[str, list[str]] = {}
-        racecheck.instrument(self, ("file_version", "file_replicas"), f"Sdfs[{node.name}]")
+        self.hbm_holders: dict[str, list[str]] = {}   # master: nodes holding a file in HBM
+        self.hbm_provider = None                      # this node: name -> IPC export dict or None
+        self.peer_copies = 0
+        racecheck.instrument(self, ("file_version", "file_replicas", "hbm_holders"), f"Sdfs[{node.name}]")
 
     # -- metadata (master) --------------------------------------------------------
     def store_dict(self) -> dict[str, list[str]]:
@@ -169,6 +178,7 @@ class Sdfs:
             if not reps or not all(r in alive for r in reps):
                 reps = ring_placement(name, self._ring(), self.node.cfg.replication)
             self.file_version[name] = ver
+            self.hbm_holders.pop(name, None)          # HBM copies of older versions are stale
         ok = []
         for r in reps:
             try:
@@ -187,12 +197,14 @@ class Sdfs:
                 return {"ok": False, "exists": False}
             alive = set(self._ring())
             reps = [r for r in self.file_replicas.get(name, []) if r in alive]
-            return {"ok": True, "exists": True, "ver": self.file_version[name], "replicas": reps}
+            hbm = [h for h in self.hbm_holders.get(name, []) if h in alive]
+            return {"ok": True, "exists": True, "ver": self.file_version[name], "replicas": reps, "hbm": hbm}
 
     def _master_delete(self, name: str) -> dict:
         with self.lock:
             reps = self.file_replicas.pop(name, [])
             existed = self.file_version.pop(name, None) is not None
+            self.hbm_holders.pop(name, None)
         for r in reps:
             try:
                 self._req(r, {"t": Type.UNLINK, "name": name})
@@ -258,6 +270,15 @@ class Sdfs:
             return self._master_locate(msg["name"])
         if t == Type.DELETE:
             return self._master_delete(msg["name"])
+        if t == Type.HBM_HAS:
+            with self.lock:
+                if msg["name"] in self.file_version:
+                    hs = [h for h in self.hbm_holders.get(msg["name"], []) if h != msg["node"]]
+                    self.hbm_holders[msg["name"]] = hs + [msg["node"]] if msg.get("held", True) else hs
+            return {"ok": True}
+        if t == Type.FETCH_HBM:
+            meta = self.hbm_provider(msg["name"], msg.get("pid")) if self.hbm_provider is not None else None
+            return {"ok": meta is not None, "meta": meta}
         return None
 
     # -- client API (any node) -------------------------------------------------------
@@ -290,6 +311,39 @@ class Sdfs:
 
     def get_bytes(self, name: str, ver: int | None = None) -> bytes | None:
         return self._fetch(name, ver)
+
+    def announce_hbm(self, name: str, held: bool = True) -> None:
+        """Tell the master this node holds (or dropped) ``name`` in HBM."""
+        msg = {"t": Type.HBM_HAS, "name": name, "node": self.node.name, "held": held}
+        master = self._master()
+        try:
+            if master == self.node.name:
+                self.handle(dict(msg, src=self.node.name))
+            else:
+                self.node.transport.send(master, msg)
+        except Exception:  # noqa: BLE001  (best effort: peers fall back to replicas)
+            pass
+
+    def fetch_hbm(self, name: str, device):
+        """GPU-to-GPU copy of ``name`` from a node holding it in HBM, or None."""
+        from .ipc import import_copy
+
+        try:
+            loc = self._req(self._master(), {"t": Type.GET, "name": name})
+        except Exception:  # noqa: BLE001
+            return None
+        for h in loc.get("hbm", []):
+            if h == self.node.name:
+                continue
+            try:
+                rep = self._req(h, {"t": Type.FETCH_HBM, "name": name, "pid": os.getpid()})
+                if rep.get("ok") and rep.get("meta"):
+                    t = import_copy(rep["meta"], device)
+                    self.peer_copies += 1
+                    return t
+            except Exception as e:  # noqa: BLE001
+                log.warning("hbm copy of %s from %s failed: %s", name, h, e)
+        return None
 
     def get(self, name: str, local: str) -> bool:
         data = self._fetch(name, None)

@@ -1,5 +1,7 @@
 """Cluster path on the GPU: HIP executor + synthetic / SDFS-staged image
 sources, several nodes sharing cuda:0 (one MI355X box)."""
+import ast
+
 import numpy as np
 import pytest
 import torch
@@ -47,7 +49,7 @@ def _collect(cl, model, n):
     for k, chunks in res.items():
         if k.startswith(model + " "):
             for ch in chunks:
-                for name, cat, p in eval(ch):
+                for name, cat, p in ast.literal_eval(ch):
                     got[int(name[5:-5])] = (int(cat.split("_")[1]), p)
     assert sorted(got) == list(range(n))
     return got
@@ -92,3 +94,24 @@ def test_cluster_hip_vs_fp32_oracle_and_sdfs_path():
         c2.stop()
     # same images, same kernels: bit-identical answers whichever path fed them
     assert all(got2[i][0] == got[i][0] for i in range(200))
+
+
+def test_sdfs_shard_peer_copy_between_nodes():
+    """A shard one node holds in HBM reaches another node as a GPU-to-GPU copy
+    (SDFS FETCH_HBM), not through a replica read + host staging."""
+    from idunno.runtime.data import put_synthetic_dataset, synth_images_cpu
+
+    c = _cluster("sdfs")
+    try:
+        put_synthetic_dataset(c.nodes["node00"].sdfs, 100, c.cfg.data_seed, shard_images=50)
+        a, b = c.nodes["node01"], c.nodes["node02"]
+        ta = a.source.get(0, 49)
+        torch.cuda.synchronize()
+        assert a.source.peer_fetches == 0
+        tb = b.source.get(10, 59)                 # shard 0 from node01's HBM, shard 1 from a replica
+        torch.cuda.synchronize()
+        assert b.source.peer_fetches == 1 and b.sdfs.peer_copies == 1
+        want = torch.from_numpy(synth_images_cpu(c.cfg.data_seed, 0, 60)).cuda()
+        assert torch.equal(ta, want[:50]) and torch.equal(tb, want[10:60])
+    finally:
+        c.stop()

@@ -92,6 +92,7 @@ def main():
     ap.add_argument("--scenarios", default="overlap,worker:1,worker:4,coord:1")
     ap.add_argument("--images", type=int, default=4000, help="SDFS dataset size (500-image shards)")
     ap.add_argument("--prefetch", type=int, default=1)
+    ap.add_argument("--peer-copy", type=int, default=1, help="SDFS shards GPU-to-GPU from HBM holders (IPC)")
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("--json", default=None)
     ap.add_argument("--trace", default=None)
@@ -116,6 +117,7 @@ def main():
     tmp = tempfile.mkdtemp(prefix="idunno_mpc_")
     log_dir = a.log_dir or tmp
     env = dict(os.environ, PYTHONPATH=ROOT, IDUNNO_PREFETCH=str(a.prefetch), IDUNNO_DTYPE=a.dtype,
+               IDUNNO_SDFS_PEER_COPY=str(a.peer_copy),
                IDUNNO_METADATA_PERIOD_S="0.2", IDUNNO_RPC_TIMEOUT_S="10", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cfg = ClusterConfig.load(env=env, num_nodes=n, base_port=base, store_root=tmp)
     procs = {}
@@ -135,9 +137,9 @@ def main():
     me_name = cfg.node_name(n - 1)
     me = Node(cfg, me_name, TcpTransport(me_name, cfg.address, cfg.address(me_name)),
               make_executor(a.executor, dev if a.executor == "hip" else None, seed=cfg.model_seed, dtype=cfg.dtype))
-    me.source = SdfsSource(me.sdfs, dev)
+    me.source = SdfsSource(me.sdfs, dev, peer_copy=bool(a.peer_copy))
     out = {"nodes": n, "processes": n, "executor": f"{a.executor} {cfg.dtype}", "gpus": torch.cuda.device_count(),
-           "detector": f"{cfg.heartbeat_period_s}s/{cfg.failure_timeout_s}s", "prefetch": bool(a.prefetch),
+           "detector": f"{cfg.heartbeat_period_s}s/{cfg.failure_timeout_s}s", "prefetch": bool(a.prefetch), "sdfs_peer_copy": bool(a.peer_copy),
            "kill": "SIGKILL of the node's OS process", "data": f"synthetic uint8 224x224 in SDFS ({a.images} images)"}
     victims = iter(range(2, n - 1))
     cl = Client(me)
