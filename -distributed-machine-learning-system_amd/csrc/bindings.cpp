@@ -275,6 +275,59 @@ torch::Tensor conv2d_nhwc_f32(torch::Tensor x, torch::Tensor w, torch::Tensor bi
   return y;
 }
 
+static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
+
+// fp32 FC layer y = act(x @ w.T + bias) with K split over `splits` slices in ONE
+// conv_f32 launch (grid = tiles x splits, fp32 partials) + the split-K combine.
+torch::Tensor linear_f32_splitk(torch::Tensor x, torch::Tensor w, torch::Tensor bias, bool relu, int64_t splits,
+                                int64_t tile) {
+  CHECK_DEV(x);
+  CHECK_DEV(w);
+  CHECK_DEV(bias);
+  CHECK_CONTIG(x);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(bias);
+  CHECK_DT(x, torch::kFloat);
+  CHECK_DT(w, torch::kFloat);
+  CHECK_DT(bias, torch::kFloat);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && bias.dim() == 1, "bad ranks");
+  TORCH_CHECK(w.device() == x.device() && bias.device() == x.device(), "operands on different devices");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && bias.size(0) == N, "shape mismatch");
+  TORCH_CHECK(N % 4 == 0, "N must be a multiple of 4");
+  TORCH_CHECK(splits >= 1 && splits <= 16 && K % (16 * splits) == 0, "K must split into multiples of 16");
+  TORCH_CHECK(splits * M * N < (1L << 31) && M * K < (1L << 31), "too large for int32 indexing");
+  auto y = torch::empty({M, N}, x.options());
+  if (M == 0) return y;
+  auto part = torch::empty({splits, M, N}, x.options());
+  const int64_t Ks = K / splits;
+  auto zb = zero_f32(x.device(), N);
+  ConvF32Args a{};
+  a.x = x.data_ptr<float>();
+  a.w = w.data_ptr<float>();
+  a.bias = zb.data_ptr<float>();
+  a.res = nullptr;
+  a.y = part.data_ptr<float>();
+  a.B = (int)M; a.H = 1; a.W = 1; a.C = (int)Ks; a.ldx = (int)K;
+  a.Ho = 1; a.Wo = 1; a.Cout = (int)N; a.ldy = (int)N;
+  a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0;
+  a.M = (int)M;
+  a.Kpad = (int)K;
+  a.relu = 0;
+  a.zero = zero_buffer(x.device()).data_ptr();
+  a.ksplit = (int)splits;
+  a.kslice = (int)Ks;
+  a.ysplit = (long)(M * N);
+  const int t = tile >= 0 ? (int)tile : conv_f32_pick((int)M, (int)N, (int)Ks, false);
+  TORCH_CHECK(t != 101 || Ks % 32 == 0, "tile 101 needs K slices of 32");
+  TORCH_CHECK(conv_f32_launch(a, 0, t, cur_stream()), "unknown / unsupported f32 conv tile id ", t);
+  check_launch("linear_f32_splitk");
+  splitk_reduce_launch(part.data_ptr<float>(), (int)splits, (long)(M * N), (int)N, bias.data_ptr<float>(),
+                       relu ? 1 : 0, y.data_ptr(), true, cur_stream());
+  check_launch("splitk_reduce");
+  return y;
+}
+
 // Packed-row geometry of an RGB stem (conv_f32 mode 2 / preprocess_pack3_f32):
 // nc row copies (the distinct 16-byte phases of 3*stride*ox), wp floats each.
 static void pack3_geometry(int W, int KW, int stride, int pad, int& nc, int& wp, int& cpk) {
@@ -684,6 +737,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_nhwc_f32", &conv2d_nhwc_f32, "fp32 implicit-GEMM conv on f32 MFMA + bias (+res) (+relu)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("tile") = -1, py::arg("out") = py::none());
+  m.def("linear_f32_splitk", &linear_f32_splitk, "fp32 FC with split-K in one launch + combine", py::arg("x"),
+        py::arg("w"), py::arg("bias"), py::arg("relu"), py::arg("splits"), py::arg("tile") = -1);
   m.def("conv2d_pack3_f32", &conv2d_pack3_f32, "fp32 RGB stem conv on packed rows (preprocess_pack3) + bias (+relu)",
         py::arg("x3"), py::arg("w"), py::arg("bias"), py::arg("W"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("tile") = -1);

@@ -48,6 +48,11 @@ struct ConvF32Args {
   int ldx;             // input pixel stride in floats (0: C)
   // packed-row stem input (mode 2, preprocess_pack3_f32): x = [B][H][nc][wp]
   int nc, wp, cpk;     // row copies, floats per copy row, 16-byte chunks per kh row (ceil(3*KW/4))
+  // split-K in ONE launch (big-C 1x1 only, FC layers): block s / (tiles) takes
+  // K slice s: x and w advance by s*kslice floats, y by s*ysplit (fp32 partials)
+  int ksplit;          // 0/1: off
+  int kslice;
+  long ysplit;
 };
 
 // mode: 0 big-C (kh, kw, c), 1 small-C NHWC4 stems, 2 packed-row RGB stems

@@ -92,9 +92,14 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_f32_kernel(const ConvF32Arg
   const int wn = wave / WM, wm = wave % WM;
 
   const int nwg = a.tiles_n * a.tiles_m;
-  const int lid = xcd_remap(blockIdx.x, nwg);
+  const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
+  const int lid_all = xcd_remap(blockIdx.x, nwg * nsplit);
+  const int split = lid_all / nwg, lid = lid_all - split * nwg;
   const int tm = lid / a.tiles_n, tn = lid % a.tiles_n;
   const int n0 = tn * BN, m0 = tm * BM;
+  const float* const xin = a.x + (size_t)split * a.kslice;         // split-K: this block's K slice
+  const float* const win = a.w + (size_t)split * a.kslice;
+  float* const yout = a.y + (size_t)split * a.ysplit;
 
   const float* zero = reinterpret_cast<const float*>(a.zero);
   const int lrow = lane / CPR, lslot = lane % CPR;
@@ -105,7 +110,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_f32_kernel(const ConvF32Arg
   for (int j = 0; j < GA; ++j) {
     const int row = (wave + NW * j) * RPI + lrow;
     const int n = n0 + row;
-    a_src[j] = n < a.Cout ? a.w + (size_t)n * a.Kpad + (lslot ^ swz_r(row, CPR)) * 4 : nullptr;
+    a_src[j] = n < a.Cout ? win + (size_t)n * a.Kpad + (lslot ^ swz_r(row, CPR)) * 4 : nullptr;
   }
   // B (pixels): image base, top-left input coordinate and the lane's chunk
   const int ldx = a.ldx ? a.ldx : a.C;
@@ -160,7 +165,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_f32_kernel(const ConvF32Arg
       if constexpr (P3) {
         const int ih = b_ih0[j] + p_kh[j];
         const bool ok = p_kh[j] < a.KH && (unsigned)ih < (unsigned)a.H;
-        const float* src = ok ? a.x + b_base[j] + ih * prow + 4 * p_q[j] : zero;
+        const float* src = ok ? xin + b_base[j] + ih * prow + 4 * p_q[j] : zero;
         __builtin_amdgcn_global_load_lds((glb_void_t*)src,
                                          (lds_void_t*)(base + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
         p_q[j] += CPR;
@@ -181,7 +186,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_f32_kernel(const ConvF32Arg
         coff = i_c * BK;
       }
       const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const float* src = ok ? a.x + b_base[j] + (ih * a.W + iw) * ldx + coff : zero;
+      const float* src = ok ? xin + b_base[j] + (ih * a.W + iw) * ldx + coff : zero;
       __builtin_amdgcn_global_load_lds((glb_void_t*)src,
                                        (lds_void_t*)(base + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
     }
@@ -296,7 +301,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_f32_kernel(const ConvF32Arg
         v[2] = fmaxf(v[2], 0.f);
         v[3] = fmaxf(v[3], 0.f);
       }
-      *reinterpret_cast<float4v*>(a.y + (size_t)m * a.ldy + n) = v;
+      *reinterpret_cast<float4v*>(yout + (size_t)m * a.ldy + n) = v;
     }
   }
 }
@@ -315,7 +320,7 @@ static void f32_cfg(ConvF32Args a, hipStream_t st) {
     a.cblk = a.C / BK;
     a.nK = a.KH * a.KW * a.cblk;
   }
-  const int grid = a.tiles_n * a.tiles_m;
+  const int grid = a.tiles_n * a.tiles_m * (a.ksplit > 1 ? a.ksplit : 1);
   const int lds = NS * (BN + BM) * BK * 4;
   auto kern = conv_f32_kernel<BN, BM, BK, WN, WM, NS, R, S>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), lds);

@@ -59,6 +59,19 @@ def wino_supported(h: int, w: int, cin: int, cout: int) -> bool:
 LINEAR_SPLITS: int = 1
 
 
+def f32_linear_splits(m: int, k: int, n: int) -> int:
+    """Split-K factor for an fp32 FC layer: enough K slices (one launch, fp32
+    partials + combine) for ~1024 blocks of 128x64 tiles, K slices >= 256.
+    Measured (tools/fc_f32_sweep.py, profiles/r2_v16_fc_f32_sweep.md): AlexNet
+    fc6 430 -> 339 us, fc8 178 -> 50 us; ResNet18 fc 26 -> 14 us; ResNet50 fc
+    94 -> 54 us."""
+    tiles = -(-n // 128) * -(-m // 64)
+    s = 1
+    while s < 8 and tiles * s < 1024 and k % (16 * 2 * s) == 0 and k // (2 * s) >= 256:
+        s *= 2
+    return s
+
+
 def linear(x, w, bias, relu: bool = False, out_f32: bool = False, splits: int | None = None):
     """y = x @ w.T + bias: the conv kernel as a 1x1 conv on a 1x1 image, or
     with ``splits`` > 1 as split-K partial GEMMs + one combine kernel
@@ -68,6 +81,9 @@ def linear(x, w, bias, relu: bool = False, out_f32: bool = False, splits: int | 
     b, k = x.shape
     n = w.shape[0]
     if x.dtype == torch.float32:
+        s = f32_linear_splits(b, k, n) if splits is None else splits
+        if s > 1:
+            return load().linear_f32_splitk(x, w, bias, relu, s, -1)
         y = load().conv2d_nhwc_f32(x.view(b, 1, 1, k), w, bias, None, 1, 1, 1, 0, relu, -1, None)
         return y.view(b, n)
     if splits is None:

@@ -362,3 +362,15 @@ def test_runner_stem_parts_bitwise(ops):
     cb, pb = run_b()
     torch.cuda.synchronize()
     assert torch.equal(ca, cb) and torch.equal(pa, pb)
+
+
+@pytest.mark.parametrize("splits", [1, 2, 4, 8])
+@pytest.mark.parametrize("M,K,N", [(500, 9216, 4096), (37, 512, 1000), (130, 2048, 36)])
+def test_linear_f32_splitk_one_launch(ops, M, K, N, splits):
+    """fp32 FC with split-K slices in one conv_f32 launch + combine, vs fp64."""
+    torch.manual_seed(M + K + N + splits)
+    x = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV) / K ** 0.5
+    b = torch.randn(N, device=DEV) * 0.1
+    y = ops.load().linear_f32_splitk(x, w, b, True, splits, -1)
+    _check(y, torch.relu(x.double() @ w.double().t() + b.double()))
