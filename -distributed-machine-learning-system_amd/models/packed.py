@@ -595,11 +595,13 @@ class HipRunner:
             gc.collect()
 
     # -- hipGraph -------------------------------------------------------------
-    def capture(self, batch: int, hw: int = 224, packed: torch.Tensor | None = None):
+    def capture(self, batch: int, hw: int = 224, packed: torch.Tensor | None = None, slot: int = 0):
         """Capture forward for a fixed batch; returns (static_in, replay_fn).
         With ``packed`` the graph also writes (class, prob bits) pairs into
-        that caller-owned buffer (e.g. a collective round's send buffer)."""
-        key = batch if packed is None else ("pk", batch, packed.data_ptr())
+        that caller-owned buffer (e.g. a collective round's send buffer).
+        ``slot`` > 0 captures an independent copy (own static buffers), so two
+        forwards of the same batch size can be in flight."""
+        key = (batch if slot == 0 else (batch, slot)) if packed is None else ("pk", batch, packed.data_ptr())
         if key in self._graphs:
             g, sin, sout = self._graphs[key]
             return sin, self._replayer(g, sout, packed)

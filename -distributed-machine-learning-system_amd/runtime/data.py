@@ -137,6 +137,11 @@ class SdfsSource:
         if self.device.type == "cuda":
             sdfs.hbm_provider = self.export_shard
 
+    def cached(self, start: int, end: int) -> bool:
+        """All shards of [start, end] already in HBM (get() will not fetch)."""
+        with self.lock:
+            return all(k in self.cache for k in range(start // self.S, end // self.S + 1))
+
     def export_shard(self, name: str, consumer_pid: int | None = None):
         """IPC export of a cached shard (SDFS FETCH_HBM), or None."""
         from .ipc import export_tensor
@@ -250,6 +255,9 @@ class JpegSource:
             self.missing.append(i)
             return np.zeros((HW, HW, 3), np.uint8)
         return load_image_u8(data)
+
+    def cached(self, start: int, end: int) -> bool:
+        return False                      # every chunk decodes on host threads
 
     def get(self, start: int, end: int) -> torch.Tensor:
         arr = np.stack(list(self.pool.map(self._one, range(start, end + 1))))

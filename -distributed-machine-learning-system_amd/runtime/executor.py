@@ -23,11 +23,27 @@ import torch
 from ..models import reference as ref
 
 
+class Done:
+    """An already finished ``Executor.submit`` (synchronous executors)."""
+
+    def __init__(self, res):
+        self._res = res
+
+    def result(self):
+        return self._res
+
+
 class Executor:
     device = torch.device("cpu")
 
     def run(self, model: str, images: torch.Tensor | None, start: int, end: int):
         raise NotImplementedError
+
+    def submit(self, model: str, images: torch.Tensor | None, start: int, end: int):
+        """Start a chunk; ``.result()`` of the returned handle gives what
+        ``run`` returns.  Asynchronous executors let the node's worker launch
+        chunk k+1 before it post-processes chunk k."""
+        return Done(self.run(model, images, start, end))
 
     def warmup(self, model: str, batch: int) -> None:
         pass
@@ -73,6 +89,22 @@ class TorchExecutor(Executor):
         return cls.to(torch.int32).cpu().numpy(), prob.float().cpu().numpy()
 
 
+class _HipPending:
+    def __init__(self, ex, slot, ev, out):
+        self.ex, self.slot, self.ev, self.out = ex, slot, ev, out
+        self._res = None
+
+    def result(self):
+        if self._res is None:
+            try:
+                self.ev.synchronize()
+                out = self.out
+                self._res = (out[:, 0].numpy().copy(), out[:, 1].contiguous().view(torch.float32).numpy().copy())
+            finally:
+                self.ex._release(self.slot)
+        return self._res
+
+
 class HipExecutor(Executor):
     """gfx950 kernels; per-(model, batch) hipGraphs, weights resident in HBM.
 
@@ -99,7 +131,12 @@ class HipExecutor(Executor):
         self.lock = threading.Lock()
         self.run_lock = threading.Lock()      # one forward (copy-in, replay, read-back) at a time
         self.stream = None      # private HIP stream: nodes sharing a GPU overlap
-        self._host_out = None   # pinned [max_graph_batch, 2] int32 result buffer
+        # two launch slots (graph set + pinned result buffer each): a chunk can
+        # run while the previous one's results are read back and ingested
+        self._slots = [None, None]                      # pinned [>= n, 2] int32 per slot
+        self._slot_busy = [False, False]
+        self._slot_cv = threading.Condition()
+        self._next_slot = 0
         self.closed = False
 
     def runner(self, name):
@@ -117,14 +154,15 @@ class HipExecutor(Executor):
             with torch.cuda.device(self.device), self.run_lock:
                 self.runner(model).capture(batch)
 
-    def _forward(self, r, images, packed):
+    def _forward(self, r, images, packed, slot: int = 0):
         """cls, prob of ``images`` on the private stream (caller holds run_lock);
-        with ``packed`` the (class, prob bits) pairs are also written there."""
+        with ``packed`` the (class, prob bits) pairs are also written there.
+        Launch slot ``slot`` replays its own graph (own static buffers)."""
         n = images.shape[0]
-        s = self.stream
+        key = n if slot == 0 else (n, slot)
         if not self.closed and packed is None and \
-                ((self.use_graphs and len(r._graphs) < self.max_graphs) or n in r._graphs):
-            sin, replay = r.capture(n)
+                ((self.use_graphs and len(r._graphs) < self.max_graphs) or key in r._graphs):
+            sin, replay = r.capture(n, slot=slot)
             sin.copy_(images)
             return replay()
         return r.forward(images.contiguous(), packed=packed)
@@ -137,22 +175,43 @@ class HipExecutor(Executor):
         images.record_stream(s)
         return s
 
-    def run(self, model, images, start, end):
+    def submit(self, model, images, start, end):
+        """Launch one chunk (copy-in, graph replay, pinned D2H) on a free slot
+        and return at once; ``.result()`` waits for it and frees the slot.
+        At most two chunks are in flight per executor."""
         r = self.runner(model)
         n = images.shape[0]
-        with torch.cuda.device(self.device), self.run_lock:
-            s = self._enter(images)
-            with torch.cuda.stream(s):
-                cls, prob = self._forward(r, images, None)
-                if self._host_out is None or self._host_out.shape[0] < n:
-                    self._host_out = torch.empty(max(n, 1024), 2, dtype=torch.int32, pin_memory=True)
-                out = self._host_out[:n]
-                out[:, 0].copy_(cls, non_blocking=True)          # pinned D2H, no pageable bounce
-                out[:, 1].copy_(prob.view(torch.int32), non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(s)
-            ev.synchronize()
-            return out[:, 0].numpy().copy(), out[:, 1].contiguous().view(torch.float32).numpy().copy()
+        with self._slot_cv:
+            while all(self._slot_busy):
+                self._slot_cv.wait()
+            slot = self._next_slot if not self._slot_busy[self._next_slot] else self._next_slot ^ 1
+            self._slot_busy[slot] = True
+            self._next_slot = slot ^ 1
+        try:
+            with torch.cuda.device(self.device), self.run_lock:
+                s = self._enter(images)
+                with torch.cuda.stream(s):
+                    cls, prob = self._forward(r, images, None, slot)
+                    host = self._slots[slot]
+                    if host is None or host.shape[0] < n:
+                        host = self._slots[slot] = torch.empty(max(n, 1024), 2, dtype=torch.int32, pin_memory=True)
+                    out = host[:n]
+                    out[:, 0].copy_(cls, non_blocking=True)          # pinned D2H, no pageable bounce
+                    out[:, 1].copy_(prob.view(torch.int32), non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(s)
+        except BaseException:
+            self._release(slot)
+            raise
+        return _HipPending(self, slot, ev, out)
+
+    def _release(self, slot: int) -> None:
+        with self._slot_cv:
+            self._slot_busy[slot] = False
+            self._slot_cv.notify_all()
+
+    def run(self, model, images, start, end):
+        return self.submit(model, images, start, end).result()
 
     def run_packed(self, model, images, packed) -> None:
         """Device-resident result path (collective rounds): write (class, prob

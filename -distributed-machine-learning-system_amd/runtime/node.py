@@ -77,6 +77,7 @@ class Node:
         self._rerep_lock = threading.Lock()     # SDFS re-replication after a failure (own thread)
         self._rerep_pool = None
         self._rerep_pending: list = []
+        self._last_chunk_done: float | None = None   # worker: completion time of the previous chunk
         self.tracer = Tracer(name)
         self.device = getattr(executor, "device", None)  # GPU of this node (None = CPU)
         self.rounds = None                          # collective round plane (cfg.collective_rounds)
@@ -636,22 +637,72 @@ class Node:
         return self.source.get(s, e) if self.source is not None else None
 
     def _worker_loop(self) -> None:
+        """JOB queue -> executor, two chunks deep: chunk k+1 is launched before
+        chunk k's results are read back and sent, so the host-side result path
+        (read-back, RESULT messages, ingest) overlaps the next forward."""
+        pending = None
         while not self._stop.is_set():
-            msg = self.jobs.get()
+            if pending is None:
+                msg = self.jobs.get()
+            else:
+                try:
+                    msg = self.jobs.get_nowait()
+                except queue.Empty:
+                    self._finish_safe(pending)
+                    pending = None
+                    continue
             if msg is None or self._stop.is_set():
+                if pending is not None:
+                    self._finish_safe(pending)
                 return
+            if pending is not None and not self._quick_start(msg):
+                # a pause (fault-injection delay) or a slow staging (cold SDFS
+                # shard) ahead: answer the finished chunk first
+                self._finish_safe(pending)
+                pending = None
             try:
-                self.run_chunk(msg)
+                ctx = self.start_chunk(msg)
             except Exception as e:  # noqa: BLE001
-                self.logger.exception("chunk failed: %s", msg)
-                err = {"t": Type.RESULT, "model": msg["model"], "qnum": msg["qnum"], "start": msg["start"],
-                       "end": msg["end"], "worker": self.name, "error": f"{type(e).__name__}: {e}"}
-                if self.membership.master == self.name:
-                    self._ingest_result(dict(err, src=self.name))
-                else:
-                    self.transport.send(self.membership.master, err)
+                self._chunk_failed(msg, e)
+                ctx = None
+            if pending is not None:
+                self._finish_safe(pending)
+            pending = ctx
+
+    def _quick_start(self, msg: dict) -> bool:
+        """Whether start_chunk(msg) launches without a pause: no configured
+        delay, and its images are prefetched, cached or synthesised."""
+        if self.cfg.worker_start_delay_s + self.extra_delay_s > 0:
+            return False
+        key = (int(msg["start"]), int(msg["end"]))
+        with self._pf_lock:
+            fut = self._pf.get(key)
+        if fut is not None:
+            return fut.done()
+        cached = getattr(self.source, "cached", None)
+        return cached is None or cached(*key)
+
+    def _chunk_failed(self, msg: dict, e: Exception) -> None:
+        self.logger.exception("chunk failed: %s", msg)
+        err = {"t": Type.RESULT, "model": msg["model"], "qnum": msg["qnum"], "start": msg["start"],
+               "end": msg["end"], "worker": self.name, "error": f"{type(e).__name__}: {e}"}
+        if self.membership.master == self.name:
+            self._ingest_result(dict(err, src=self.name))
+        else:
+            self.transport.send(self.membership.master, err)
+
+    def _finish_safe(self, ctx) -> None:
+        try:
+            self.finish_chunk(ctx)
+        except Exception as e:  # noqa: BLE001
+            self._chunk_failed(ctx[0], e)
 
     def run_chunk(self, msg: dict) -> None:
+        self.finish_chunk(self.start_chunk(msg))
+
+    def start_chunk(self, msg: dict):
+        """Stage the chunk's images and launch its forward (returns at once on
+        an asynchronous executor)."""
         delay = self.cfg.worker_start_delay_s + self.extra_delay_s
         if delay:
             time.sleep(delay)
@@ -661,11 +712,24 @@ class Node:
         with self.tracer.span("chunk.stage", **tags):
             imgs = self._staged(s, e)
         self._prefetch_next()                 # next JOB's images stage while this one computes
-        with self.tracer.span("chunk.compute", **tags):
-            cls, prob = self.executor.run(model, imgs, s, e)
-        dt = time.perf_counter() - t0
+        t_launch = time.time()
+        handle = self.executor.submit(model, imgs, s, e)
+        return (msg, t0, tags, t_launch, handle)
+
+    def finish_chunk(self, ctx) -> None:
+        """Wait for a launched chunk, send / ingest its RESULT."""
+        msg, t0, tags, t_launch, handle = ctx
+        cls, prob = handle.result()
+        t_done = time.time()
+        self.tracer.complete("chunk.compute", t_launch, t_done, **tags)
+        # its own time: from launch, or from the previous chunk's completion if
+        # it had to queue behind that one on the GPU (fair-time averages)
+        prev = self._last_chunk_done
+        self._last_chunk_done = t_done
+        dt = (time.perf_counter() - t0) if prev is None or prev <= t_launch else (t_done - prev)
         if not self.alive_flag:
             return
+        model, s, e = msg["model"], int(msg["start"]), int(msg["end"])
         res = {"t": Type.RESULT, "model": model, "qnum": msg["qnum"], "start": s, "end": e,
                "worker": self.name, "cls": np.ascontiguousarray(cls, np.int32).tobytes(),
                "prob": np.ascontiguousarray(prob, np.float32).tobytes(), "compute_s": dt,

@@ -115,3 +115,71 @@ def test_sdfs_shard_peer_copy_between_nodes():
         assert torch.equal(ta, want[:50]) and torch.equal(tb, want[10:60])
     finally:
         c.stop()
+
+
+def _eager(ex, model, imgs):
+    r = ex.runner(model)
+    cls, prob = r.forward(imgs.contiguous())
+    torch.cuda.synchronize()
+    return cls.cpu().numpy(), prob.cpu().numpy()
+
+
+def test_hip_executor_two_threads_same_batch():
+    """chunks of two threads (TCP worker + round driver) through one
+    executor, same chunk size, different images: results never mix."""
+    import threading
+
+    from idunno import ops
+    from idunno.runtime.executor import HipExecutor
+
+    ex = HipExecutor("cuda", seed=0)
+    imgs = [ops.synth_images(100 + i, 0, 48, "cuda") for i in range(6)]
+    want = [_eager(ex, "resnet18", im) for im in imgs]
+    got = {}
+    errs = []
+
+    def worker(ids):
+        try:
+            for _ in range(3):
+                for i in ids:
+                    got.setdefault(i, []).append(ex.run("resnet18", imgs[i], 0, 47))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker, args=(ids,)) for ids in ((0, 1, 2), (3, 4, 5))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not errs, errs
+    for i in range(6):
+        for cls, prob in got[i]:
+            assert np.array_equal(cls, want[i][0]) and np.allclose(prob, want[i][1], rtol=0, atol=0)
+    ex.close()
+
+
+def test_hip_executor_submit_two_in_flight():
+    """submit() launches up to two chunks before their read-back; a third
+    waits for a free slot; every result matches the eager forward."""
+    import threading
+
+    from idunno import ops
+    from idunno.runtime.executor import HipExecutor
+
+    ex = HipExecutor("cuda", seed=0)
+    imgs = [ops.synth_images(200 + i, 0, 40, "cuda") for i in range(3)]
+    want = [_eager(ex, "resnet18", im) for im in imgs]
+    a = ex.submit("resnet18", imgs[0], 0, 39)
+    b = ex.submit("resnet18", imgs[1], 0, 39)
+    third = {}
+    t = threading.Thread(target=lambda: third.setdefault("h", ex.submit("resnet18", imgs[2], 0, 39)))
+    t.start()
+    t.join(0.5)
+    assert t.is_alive()                    # both slots busy
+    ra = a.result()
+    t.join(60)
+    assert not t.is_alive()
+    rb, rc = b.result(), third["h"].result()
+    for (cls, prob), (wc, wp) in zip((ra, rb, rc), want):
+        assert np.array_equal(cls, wc) and np.array_equal(prob, wp)
+    ex.close()
