@@ -330,7 +330,11 @@ class JobState:
             self.finished_images[model] += n
             self._rate_win[model].append((now, n))
             bs = self.batchsize.get(model, n)
-            self._ptime_win[model].append((now, (now - t_start) / n * bs))
+            if hit is not None:
+                # c2 needs the chunk's dispatch time: a result that reaches the
+                # standby before the replicated assignment has none (it would
+                # enter the window as a 0-second chunk)
+                self._ptime_win[model].append((now, (now - t_start) / n * bs))
             self._expire(model, now)
             self._c2_dirty.add(model)   # stats recomputed when read (c2 / snapshot), not per chunk
             self.results[f"{model} {qnum}"].append(
