@@ -328,38 +328,46 @@ torch::Tensor linear_f32_splitk(torch::Tensor x, torch::Tensor w, torch::Tensor 
   return y;
 }
 
-// Packed-row geometry of an RGB stem (conv_f32 mode 2 / preprocess_pack3_f32):
-// nc row copies (the distinct 16-byte phases of 3*stride*ox), wp floats each.
-static void pack3_geometry(int W, int KW, int stride, int pad, int& nc, int& wp, int& cpk) {
-  const int g = stride % 4 == 0 ? 4 : (stride % 2 == 0 ? 2 : 1);   // gcd(stride, 4)
-  nc = 4 / g;
-  wp = (3 * (W + 2 * pad) + 3 + 3) / 4 * 4;
-  cpk = (3 * KW + 3) / 4;
+// Packed-row geometry of an RGB stem (conv_f32 mode 2 / conv_glds pack3,
+// preprocess_pack3): nc row copies (the distinct 16-byte phases of 3*stride*ox
+// for E = 16 / elem_bytes elements per chunk), wp elements each, cpk 16-byte
+// chunks per kernel row.
+static void pack3_geometry(int W, int KW, int stride, int pad, int elem_bytes, int& nc, int& wp, int& cpk) {
+  const int E = 16 / elem_bytes;
+  int g = 1;                                   // gcd(3 * stride, E), E a power of two
+  while (g < E && (3 * stride) % (2 * g) == 0) g *= 2;
+  nc = E / g;
+  wp = (3 * (W + 2 * pad) + E - 1 + E - 1) / E * E;
+  cpk = (3 * KW + E - 1) / E;
 }
 
-// fp32 RGB stem conv on packed rows: x3 [B, H, nc, wp] from preprocess_pack3,
-// w [Cout, ceil(KH*cpk/4)*16] (models/packed.py pack_conv_weight_p3), W = image width.
-torch::Tensor conv2d_pack3_f32(torch::Tensor x3, torch::Tensor w, torch::Tensor bias, int64_t W, int64_t KH,
-                               int64_t KW, int64_t stride, int64_t pad, bool relu, int64_t tile) {
+// RGB stem conv on packed rows: x3 [B, H, nc, wp] from preprocess_pack3 (fp32:
+// conv_f32 mode 2 on the f32 MFMA; fp16: conv_glds pack3 on the f16 MFMA),
+// w [Cout, nK * stage elements] (models/packed.py pack_conv_weight_p3), W = image width.
+torch::Tensor conv2d_pack3(torch::Tensor x3, torch::Tensor w, torch::Tensor bias, int64_t W, int64_t KH,
+                           int64_t KW, int64_t stride, int64_t pad, bool relu, int64_t tile) {
   CHECK_DEV(x3);
   CHECK_DEV(w);
   CHECK_DEV(bias);
   CHECK_CONTIG(x3);
   CHECK_CONTIG(w);
   CHECK_CONTIG(bias);
-  CHECK_DT(x3, torch::kFloat);
-  CHECK_DT(w, torch::kFloat);
+  const bool f16 = x3.scalar_type() == torch::kHalf;
+  TORCH_CHECK(f16 || x3.scalar_type() == torch::kFloat, "x3 must be fp32 or fp16");
+  TORCH_CHECK(w.scalar_type() == x3.scalar_type(), "w must have x3's dtype");
   CHECK_DT(bias, torch::kFloat);
   TORCH_CHECK(x3.dim() == 4 && w.dim() == 2 && bias.dim() == 1, "bad ranks");
   TORCH_CHECK(w.device() == x3.device() && bias.device() == x3.device(), "operands on different devices");
   TORCH_CHECK(KH >= 1 && KW >= 5 && stride >= 1 && pad >= 0 && W >= 1, "pack3 stem geometry: KW >= 5");
   int nc, wp, cpk;
-  pack3_geometry((int)W, (int)KW, (int)stride, (int)pad, nc, wp, cpk);
+  pack3_geometry((int)W, (int)KW, (int)stride, (int)pad, f16 ? 2 : 4, nc, wp, cpk);
+  TORCH_CHECK(nc <= 4, "pack3 stem: stride needs at most 4 row copies");
   const int B = x3.size(0), H = x3.size(1);
   TORCH_CHECK(x3.size(2) == nc && x3.size(3) == wp, "x3 must be [B, H, ", nc, ", ", wp, "] (preprocess_pack3)");
   const int Cout = w.size(0), Kpad = w.size(1);
-  const int nK = (KH * cpk + 3) / 4;
-  TORCH_CHECK(Kpad == nK * 16, "pack3 weight must be [Cout, ", nK * 16, "]");
+  // K stage = 16 fp32 / 64 fp16 elements = 4 / 8 chunks
+  const int cps = f16 ? 8 : 4, nK = (KH * cpk + cps - 1) / cps;
+  TORCH_CHECK(Kpad == nK * cps * (f16 ? 8 : 4), "pack3 weight must be [Cout, ", nK * cps * (f16 ? 8 : 4), "]");
   TORCH_CHECK(bias.size(0) == Cout && Cout % 4 == 0, "bias/Cout mismatch or Cout % 4");
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = ((int)W + 2 * pad - KW) / stride + 1;
   TORCH_CHECK(Ho > 0 && Wo > 0, "empty output");
@@ -367,6 +375,26 @@ torch::Tensor conv2d_pack3_f32(torch::Tensor x3, torch::Tensor w, torch::Tensor 
   TORCH_CHECK(M < (1L << 31) && (long)B * H * nc * wp < (1L << 31), "tensor too large for int32 indexing");
   auto y = torch::empty({B, Ho, Wo, Cout}, x3.options());
   if (M == 0) return y;
+  if (f16) {
+    ConvArgs a{};
+    a.x = reinterpret_cast<const half_t*>(x3.data_ptr());
+    a.w = reinterpret_cast<const half_t*>(w.data_ptr());
+    a.bias = bias.data_ptr<float>();
+    a.res = nullptr;
+    a.y = y.data_ptr();
+    a.B = B; a.H = H; a.W = (int)W; a.C = 3;
+    a.Ho = Ho; a.Wo = Wo; a.Cout = Cout; a.ldy = Cout;
+    a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
+    a.M = (int)M;
+    a.Kpad = Kpad;
+    a.relu = relu ? 1 : 0;
+    a.nc = nc; a.wp = wp; a.cpk = cpk;
+    a.zero = zero_buffer(x3.device()).data_ptr();
+    const int t = tile >= 0 ? (int)tile : 27;
+    TORCH_CHECK(conv_glds_launch(a, false, t, cur_stream()), "unsupported fp16 pack3 tile id ", t);
+    check_launch("conv_glds_pack3");
+    return y;
+  }
   ConvF32Args a{};
   a.x = x3.data_ptr<float>();
   a.w = w.data_ptr<float>();
@@ -600,7 +628,7 @@ torch::Tensor preprocess(torch::Tensor img, c10::optional<torch::Tensor> start, 
 // stride-`stride`, pad-`pad` stem (conv2d_pack3_f32); same window arguments as preprocess.
 torch::Tensor preprocess_pack3(torch::Tensor img, int64_t KW, int64_t stride, int64_t pad,
                                c10::optional<torch::Tensor> start, int64_t batch, int64_t start_offset,
-                               int64_t window, int64_t sub) {
+                               int64_t window, int64_t sub, bool f16) {
   CHECK_DEV(img);
   CHECK_CONTIG(img);
   CHECK_DT(img, torch::kUInt8);
@@ -611,12 +639,17 @@ torch::Tensor preprocess_pack3(torch::Tensor img, int64_t KW, int64_t stride, in
   const long long* sp = window_args(img, start, batch, window, sub, B, max_start);
   const int H = img.size(1), W = img.size(2);
   int nc, wp, cpk;
-  pack3_geometry(W, (int)KW, (int)stride, (int)pad, nc, wp, cpk);
+  pack3_geometry(W, (int)KW, (int)stride, (int)pad, f16 ? 2 : 4, nc, wp, cpk);
+  TORCH_CHECK(nc <= 4, "pack3 stem: stride needs at most 4 row copies");
   TORCH_CHECK((long)B * H * nc * wp < (1L << 31), "tensor too large for int32 indexing");
-  auto out = torch::empty({B, H, nc, wp}, img.options().dtype(torch::kFloat));
+  auto out = torch::empty({B, H, nc, wp}, img.options().dtype(f16 ? torch::kHalf : torch::kFloat));
   if (B == 0) return out;
-  preprocess_pack3_f32_launch(img.data_ptr<uint8_t>(), out.data_ptr<float>(), B, H, W, (int)pad, nc, wp, sp,
-                              start_offset, max_start, sp ? sub : 0, cur_stream());
+  if (f16)
+    preprocess_pack3_f16_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), B, H, W,
+                                (int)pad, nc, wp, sp, start_offset, max_start, sp ? sub : 0, cur_stream());
+  else
+    preprocess_pack3_f32_launch(img.data_ptr<uint8_t>(), out.data_ptr<float>(), B, H, W, (int)pad, nc, wp, sp,
+                                start_offset, max_start, sp ? sub : 0, cur_stream());
   check_launch("preprocess_pack3_f32");
   return out;
 }
@@ -739,12 +772,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pad"), py::arg("relu"), py::arg("tile") = -1, py::arg("out") = py::none());
   m.def("linear_f32_splitk", &linear_f32_splitk, "fp32 FC with split-K in one launch + combine", py::arg("x"),
         py::arg("w"), py::arg("bias"), py::arg("relu"), py::arg("splits"), py::arg("tile") = -1);
-  m.def("conv2d_pack3_f32", &conv2d_pack3_f32, "fp32 RGB stem conv on packed rows (preprocess_pack3) + bias (+relu)",
+  m.def("conv2d_pack3", &conv2d_pack3, "RGB stem conv on packed rows (preprocess_pack3), fp32 or fp16 + bias (+relu)",
         py::arg("x3"), py::arg("w"), py::arg("bias"), py::arg("W"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("tile") = -1);
   m.def("preprocess_pack3", &preprocess_pack3, "uint8 HWC -> packed-row fp32 stem input [B, H, nc, wp]",
         py::arg("img"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("start") = py::none(),
-        py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1, py::arg("sub") = 0);
+        py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1, py::arg("sub") = 0,
+        py::arg("f16") = false);
   m.def("conv2d_wino_f32", &conv2d_wino_f32, "fp32 Winograd F(2x2,3x3) conv (3x3/s1/p1) + bias (+res) (+relu)",
         py::arg("x"), py::arg("u"), py::arg("bias"), py::arg("res"), py::arg("relu"), py::arg("variant") = 0);
   m.def("set_wino_ablation", &set_wino_ablation_host,

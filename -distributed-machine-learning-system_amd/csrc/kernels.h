@@ -25,6 +25,8 @@ struct ConvArgs {
   const void* zero;  // >= 16 zero bytes (DMA source for padding taps)
   int ldx;           // conv_glds: input pixel stride in halfs (0: C); a K-slice of a wider row
   int ablate;        // profiling only (set_conv_ablation), conv_glds: 1 skip epilogue stores, 2 skip residual loads
+  int nc, wp, cpk;   // conv_glds pack3 (RGB stems on packed rows, preprocess_pack3_f16): row copies,
+                     // halfs per copy row, 16-byte chunks per kernel row (ceil(3*KW/8)); cpk = 0: off
 };
 
 // fp32 (reference-precision) conv: same geometry fields as ConvArgs, f32 tensors.
@@ -95,6 +97,9 @@ int conv_f32_pick(int M, int Cout, int K, bool small);
 void preprocess_pack3_f32_launch(const uint8_t* img, float* out, int B, int H, int W, int pad, int nc, int wp,
                                  const long long* start_idx, long long start_off, long long max_start,
                                  long long sub, hipStream_t st);
+void preprocess_pack3_f16_launch(const uint8_t* img, half_t* out, int B, int H, int W, int pad, int nc, int wp,
+                                 const long long* start_idx, long long start_off, long long max_start,
+                                 long long sub, hipStream_t st);
 void preprocess_f32_launch(const uint8_t* img, float* out, long npix, const long long* start_idx,
                            long long start_off, long long max_start, long long sub, long pix_per_img,
                            hipStream_t st);
@@ -104,7 +109,7 @@ void avgpool_f32_launch(const float* x, float* y, int B, int HW, int C, hipStrea
 
 void conv_igemm_launch(ConvArgs a, bool small, bool out_f32, int tile, hipStream_t st);
 int conv_pick_tile(int M, int Cout);
-bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
+bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);   // a.cpk > 0: pack3 stem
 bool conv_big_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 bool conv_pers_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);   // false: shape unsupported
 bool conv3x3_patch_supported(int H, int W, int C, int Cout);

@@ -43,7 +43,11 @@ __device__ __forceinline__ void wait_stages(int pending_stages) {
   wait_vmcnt<0>();
 }
 
-template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32>
+// P3: RGB stem on packed rows (preprocess_pack3_f16, x = [B][H][nc][wp] halfs):
+// the 3*KW halfs of one kernel row are contiguous in the row copy in which
+// they start 16-byte aligned; K = (kh, 16-byte chunk), ceil(3*KW/8) chunks per
+// kh (AlexNet 11x11/4: K 448 instead of 704 for NHWC4 on conv_igemm).
+template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false>
 __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs a) {
   constexpr int NW = WN * WM;
   constexpr int NT = 64 * NW;
@@ -86,6 +90,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
   // of wider rows when the caller splits K, e.g. linear_splitk)
   const int ldx = a.ldx ? a.ldx : a.C;
   int b_base[GB], b_ih0[GB], b_iw0[GB], b_ch[GB];
+  const int prow = a.nc * a.wp;                       // P3: halfs per image row (all copies)
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int row = (wave + NW * j) * RPI + lrow;
@@ -95,7 +100,13 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
       const int hw = a.Ho * a.Wo;
       const int b = m / hw, r = m - b * hw;
       const int oh = r / a.Wo, ow = r - oh * a.Wo;
-      b_base[j] = b * a.H * a.W * ldx + b_ch[j];
+      if constexpr (P3) {
+        const int r0 = 3 * a.stride * ow;              // first half of the pixel's kernel row in R
+        const int sh = r0 & 7, g = 8 / a.nc;           // copy sh/g starts it 16-byte aligned
+        b_base[j] = b * a.H * prow + (sh / g) * a.wp + r0 - sh;
+      } else {
+        b_base[j] = b * a.H * a.W * ldx + b_ch[j];
+      }
       b_ih0[j] = oh * a.stride - a.pad;
       b_iw0[j] = ow * a.stride - a.pad;
     } else {
@@ -118,6 +129,17 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
     const int coff = i_cb * BK;
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
+      if constexpr (P3) {
+        // this lane's chunk of stage i_s: flat chunk q = i_s*CPR + ch over (kh, chunk)
+        const int q = i_s * CPR + b_ch[j] / 8;
+        const int kh = q / a.cpk, jj = q - kh * a.cpk;
+        const int ih = b_ih0[j] + kh;
+        const bool ok = kh < a.KH && (unsigned)ih < (unsigned)a.H;
+        const half_t* src = ok ? a.x + b_base[j] + ih * prow + 8 * jj : zero;
+        __builtin_amdgcn_global_load_lds((glb_void_t*)src,
+                                         (lds_void_t*)(base + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
+        continue;
+      }
       const int ih = b_ih0[j] + i_kh, iw = b_iw0[j] + i_kw;
       const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
       const half_t* src = ok ? a.x + b_base[j] + (ih * a.W + iw) * ldx + coff : zero;
@@ -261,15 +283,20 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
   }
 }
 
-template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32>
+template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false>
 static void glds_cfg(ConvArgs a, hipStream_t st) {
   a.tiles_n = (a.Cout + BN - 1) / BN;
   a.tiles_m = (a.M + BM - 1) / BM;
-  a.cblk = a.C / BK;
-  a.nK = a.KH * a.KW * a.cblk;
+  if (P3) {
+    a.cblk = 1;
+    a.nK = (a.KH * a.cpk + BK / 8 - 1) / (BK / 8);
+  } else {
+    a.cblk = a.C / BK;
+    a.nK = a.KH * a.KW * a.cblk;
+  }
   const int grid = a.tiles_n * a.tiles_m;
   const size_t lds = (size_t)NS * (BN + BM) * BK * 2;
-  auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32>;
+  auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32, P3>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), (int)lds);   // per (kernel, device), launch_util.h
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WN * WM), lds, st, a);
 }
@@ -323,8 +350,25 @@ static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
   }
 }
 
+// pack3 stems: a few tile shapes (Cout 64: 64-row weight tiles)
+template <bool F>
+static bool glds_dispatch_p3(ConvArgs a, int tile, hipStream_t st) {
+  switch (tile) {
+    case 23: glds_cfg<64, 64, 64, 2, 2, 3, false, F, true>(a, st); return true;
+    case 27: glds_cfg<64, 128, 64, 1, 4, 2, false, F, true>(a, st); return true;
+    case 31: glds_cfg<64, 128, 32, 1, 4, 3, false, F, true>(a, st); return true;
+    case 33: glds_cfg<64, 256, 64, 1, 4, 2, false, F, true>(a, st); return true;
+    case 35: glds_cfg<64, 64, 64, 2, 2, 2, false, F, true>(a, st); return true;
+    default: return false;
+  }
+}
+
 bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
   const bool res = a.res != nullptr;
+  if (a.cpk > 0) {
+    if (res) return false;
+    return out_f32 ? glds_dispatch_p3<true>(a, tile, st) : glds_dispatch_p3<false>(a, tile, st);
+  }
   if (res) return out_f32 ? glds_dispatch<true, true>(a, tile, st) : glds_dispatch<true, false>(a, tile, st);
   return out_f32 ? glds_dispatch<false, true>(a, tile, st) : glds_dispatch<false, false>(a, tile, st);
 }

@@ -47,29 +47,35 @@ __global__ void preprocess_f32_kernel(const uint8_t* __restrict__ img, float* __
   for (int i = 0; i < n; ++i) d[i] = norm_px_f32(s[3 * i], s[3 * i + 1], s[3 * i + 2]);
 }
 
-// Packed-row stem input for conv_f32 mode 2: out[b][y][c][wp].  Copy c holds
-// the row R shifted left by c*g floats (g = 4 / nc), where R[f] = channel f%3
-// of pixel f/3 - pad, normalised, and zero outside the image -- so the 3*KW
-// contiguous floats a stride-s output pixel ox reads for one kernel row start
-// 16-byte aligned in copy (3*s*ox mod 4) / g, and the conv stages them with
-// whole 16-byte DMA chunks (K = KH * ceil(3*KW/4) * 4 instead of
-// KH * ceil(KW/4) * 16 for NHWC4).
-// One thread = the 12-float group k of EVERY copy of one row: copy c's group
-// is R[12k + c*g .. +12), all inside the 6 pixels 4k-pad .. 4k-pad+5, which are
-// loaded once (five aligned dwords realigned with v_alignbyte away from the row
-// ends) and normalised through an LDS table of the 256 x 3 byte values (same
-// arithmetic as preprocess_f32, one division per table entry).
-template <int NC>
-__global__ void __launch_bounds__(256) preprocess_pack3_f32_kernel(
-    const uint8_t* __restrict__ img, float* __restrict__ out, int B, int H, int W, int pad, int wp,
+// Packed-row stem input for conv_f32 mode 2 / conv_glds pack3 (T = float or
+// half): out[b][y][c][wp].  Copy c holds the row R shifted left by c*g
+// elements (g = E / nc, E = elements per 16-byte chunk: 4 floats / 8 halfs),
+// where R[f] = channel f%3 of pixel f/3 - pad, normalised, and zero outside
+// the image -- so the 3*KW contiguous elements a stride-s output pixel ox
+// reads for one kernel row start 16-byte aligned in copy (3*s*ox mod E) / g,
+// and the conv stages them with whole 16-byte DMA chunks (ResNet 7x7/2 fp32:
+// K 176 instead of 224 for NHWC4).
+// One thread = the 3-chunk group k (3E elements = E pixels) of EVERY copy of
+// one row: copy c's group is R[3Ek + c*g ..], all inside the E+2 pixels
+// Ek-pad .., loaded once (aligned dwords realigned with v_alignbyte away from
+// the row ends) and normalised through an LDS table of the 256 x 3 byte values
+// (same arithmetic as preprocess_f32, one division per table entry).
+template <typename T, int NC>
+__global__ void __launch_bounds__(256) preprocess_pack3_kernel(
+    const uint8_t* __restrict__ img, T* __restrict__ out, int B, int H, int W, int pad, int wp,
     const long long* __restrict__ start_idx, long long start_off, long long max_start, long long sub) {
-  constexpr int G = 4 / NC;
+  constexpr int E = 16 / (int)sizeof(T);               // elements per 16-byte chunk
+  constexpr int G = E / NC;                            // copy shift (elements)
+  constexpr int NPX = E + 2;                           // pixels loaded per group
+  constexpr int NV = 3 * NPX;                          // their normalised values
+  constexpr int NB = (NV + 3) / 4;                     // realigned dwords of their bytes
+  constexpr int ND = NB + 1;                           // aligned dword loads
   __shared__ float lut[3][256];
   const int tid = threadIdx.x;
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) lut[ch][tid] = ((float)tid / 255.f - kMeanF[ch]) / kStdF[ch];
   __syncthreads();
-  const int ng = (wp + 11) / 12;                       // 12-float groups per copy row
+  const int ng = (wp + 3 * E - 1) / (3 * E);           // groups per copy row
   const long t = (long)blockIdx.x * blockDim.x + tid;
   const long total = (long)B * H * ng;
   if (t >= total) return;
@@ -81,55 +87,76 @@ __global__ void __launch_bounds__(256) preprocess_pack3_f32_kernel(
   const int k = (int)(t % ng);
   const long r = t / ng;                               // b * H + y
   const uint8_t* row = img + (size_t)r * W * 3;
-  const int px0 = 4 * k - pad;                         // first of the 6 pixels
-  uint32_t bytes[5];                                   // 18 bytes of the 6 pixels (+2)
-  if (px0 >= 0 && px0 + 8 <= W) {                     // the 24 aligned bytes stay inside the row
+  const int px0 = E * k - pad;                         // first of the NPX pixels
+  uint32_t bytes[NB];
+  if (px0 >= 0 && 3 * px0 + 4 * ND <= 3 * W) {         // the aligned dwords stay inside the row
     const uint8_t* p = row + px0 * 3;
     const uint32_t* a = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(3));
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
-    uint32_t d[6];
+    uint32_t d[ND];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) d[i] = a[i];
+    for (int i = 0; i < ND; ++i) d[i] = a[i];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) bytes[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+    for (int i = 0; i < NB; ++i) bytes[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
   } else {
 #pragma unroll
-    for (int i = 0; i < 5; ++i) bytes[i] = 0;
+    for (int i = 0; i < NB; ++i) bytes[i] = 0;
 #pragma unroll
-    for (int i = 0; i < 18; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int px = px0 + i / 3;
       if (px >= 0 && px < W) bytes[i >> 2] |= (uint32_t)row[px * 3 + i % 3] << (8 * (i & 3));
     }
   }
-  float v[18];
+  float v[NV];
 #pragma unroll
-  for (int i = 0; i < 18; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int px = px0 + i / 3;
     v[i] = (px >= 0 && px < W) ? lut[i % 3][(bytes[i >> 2] >> (8 * (i & 3))) & 255u] : 0.f;
   }
-  const int n4 = min(3, (wp - 12 * k) / 4);           // float4s of this group inside the row
+  const int nch = min(3, (wp - 3 * E * k) / E);        // chunks of this group inside the row
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    float* dst = out + (r * NC + c) * wp + 12 * k;
+    T* dst = out + (r * NC + c) * wp + 3 * E * k;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      if (j >= n4) break;
-      *reinterpret_cast<float4v*>(dst + 4 * j) = float4v{v[c * G + 4 * j], v[c * G + 4 * j + 1],
-                                                         v[c * G + 4 * j + 2], v[c * G + 4 * j + 3]};
+      if (j >= nch) break;
+      if constexpr (E == 4) {
+        *reinterpret_cast<float4v*>(dst + 4 * j) = float4v{v[c * G + 4 * j], v[c * G + 4 * j + 1],
+                                                           v[c * G + 4 * j + 2], v[c * G + 4 * j + 3]};
+      } else {
+        half8v o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (half_t)v[c * G + 8 * j + e];
+        *reinterpret_cast<half8v*>(dst + 8 * j) = o;
+      }
     }
   }
+}
+
+template <typename T>
+static void pack3_launch(const uint8_t* img, T* out, int B, int H, int W, int pad, int nc, int wp,
+                         const long long* start_idx, long long start_off, long long max_start, long long sub,
+                         hipStream_t st) {
+  constexpr int E = 16 / (int)sizeof(T);
+  const int bs = 256;
+  const long total = (long)B * H * ((wp + 3 * E - 1) / (3 * E));
+  const long grid = (total + bs - 1) / bs;
+  auto kern = nc == 4 ? preprocess_pack3_kernel<T, 4>
+              : nc == 2 ? preprocess_pack3_kernel<T, 2> : preprocess_pack3_kernel<T, 1>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(bs), 0, st, img, out, B, H, W, pad, wp, start_idx, start_off,
+                     max_start, sub);
 }
 
 void preprocess_pack3_f32_launch(const uint8_t* img, float* out, int B, int H, int W, int pad, int nc, int wp,
                                  const long long* start_idx, long long start_off, long long max_start,
                                  long long sub, hipStream_t st) {
-  const int bs = 256;
-  const long total = (long)B * H * ((wp + 11) / 12);
-  const long grid = (total + bs - 1) / bs;
-  auto kern = nc == 4 ? preprocess_pack3_f32_kernel<4>
-              : nc == 2 ? preprocess_pack3_f32_kernel<2> : preprocess_pack3_f32_kernel<1>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(bs), 0, st, img, out, B, H, W, pad, wp, start_idx, start_off,
-                     max_start, sub);
+  pack3_launch<float>(img, out, B, H, W, pad, nc, wp, start_idx, start_off, max_start, sub, st);
+}
+
+void preprocess_pack3_f16_launch(const uint8_t* img, half_t* out, int B, int H, int W, int pad, int nc, int wp,
+                                 const long long* start_idx, long long start_off, long long max_start,
+                                 long long sub, hipStream_t st) {
+  pack3_launch<half_t>(img, out, B, H, W, pad, nc, wp, start_idx, start_off, max_start, sub, st);
 }
 
 void preprocess_f32_launch(const uint8_t* img, float* out, long npix, const long long* start_idx,

@@ -46,7 +46,7 @@ class Conv:
     relu: bool
     small: bool = False      # RGB stem packing
     wino: torch.Tensor | None = None   # fp32 3x3/s1: Winograd U = G g G^T [16, Cout, Cin]
-    p3: torch.Tensor | None = None     # fp32 RGB stem on packed rows (pack_conv_weight_p3)
+    p3: torch.Tensor | None = None     # RGB stem on packed rows (pack_conv_weight_p3)
 
     def to(self, device):
         return Conv(self.w.to(device), self.b.to(device), self.cin, self.cout, self.kh, self.kw,
@@ -154,25 +154,29 @@ def pack_conv_weight(w: torch.Tensor, dtype: str = "fp16") -> tuple[torch.Tensor
     return w.permute(0, 2, 3, 1).reshape(cout, kh * kw * cin).half().contiguous(), False
 
 
-def pack_conv_weight_p3(w: torch.Tensor) -> torch.Tensor:
-    """[Cout, 3, KH, KW] -> [Cout, ceil(KH*cpk/4)*16] fp32 for the packed-row
-    stem (conv_f32.hip mode 2): K = (kh, f) with f = 3*kw + c over
-    cpk = ceil(3*KW/4) 16-byte chunks per kernel row (f >= 3*KW: zero), the
-    order in which preprocess_pack3_f32 lays a kernel row's pixels out."""
+def pack_conv_weight_p3(w: torch.Tensor, dtype: str = "fp32") -> torch.Tensor:
+    """[Cout, 3, KH, KW] -> packed-row stem weights: K = (kh, f) with
+    f = 3*kw + c over cpk = ceil(3*KW/E) 16-byte chunks per kernel row
+    (E = 4 fp32 / 8 fp16 elements; f >= 3*KW: zero), the order in which
+    preprocess_pack3 lays a kernel row's pixels out; padded to whole K stages
+    (16 fp32 = conv_f32.hip mode 2, 64 fp16 = conv_glds pack3)."""
     cout, cin, kh, kw = w.shape
     if cin != 3 or kw < 5:
         raise ValueError("packed-row stems take 3 input channels and KW >= 5")
-    cpk = (3 * kw + 3) // 4
-    nk = (kh * cpk + 3) // 4
-    rows = torch.zeros(cout, kh, 4 * cpk, dtype=torch.float32)
+    e, stage = (4, 16) if dtype == "fp32" else (8, 64)
+    cpk = (3 * kw + e - 1) // e
+    nk = (kh * cpk * e + stage - 1) // stage
+    rows = torch.zeros(cout, kh, e * cpk, dtype=torch.float32)
     rows[:, :, :3 * kw] = w.float().permute(0, 2, 3, 1).reshape(cout, kh, 3 * kw)
-    p = torch.zeros(cout, nk * 16, dtype=torch.float32)
-    p[:, :kh * 4 * cpk] = rows.reshape(cout, -1)
-    return p.contiguous()
+    p = torch.zeros(cout, nk * stage, dtype=torch.float32)
+    p[:, :kh * e * cpk] = rows.reshape(cout, -1)
+    return p.contiguous() if dtype == "fp32" else p.half().contiguous()
 
 
-def pack3_eligible(cin: int, kw: int) -> bool:
-    return cin == 3 and kw >= 5
+def pack3_eligible(cin: int, kw: int, stride: int = 2, dtype: str = "fp32") -> bool:
+    """fp32: any stride (<= 4 row copies); fp16 (8 halfs per chunk): stride
+    even (2 or 4 row copies)."""
+    return cin == 3 and kw >= 5 and (dtype == "fp32" or stride % 2 == 0)
 
 
 def unpack_conv_weight(c: Conv) -> torch.Tensor:
@@ -208,7 +212,7 @@ def make_conv(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, relu: bool, dtype: str
                                          conv.padding[0]):
         return Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, 3, 3, 1, 1, relu, small,
                     wino_weight(w))
-    p3 = pack_conv_weight_p3(w) if dtype == "fp32" and pack3_eligible(conv.in_channels, conv.kernel_size[1]) \
+    p3 = pack_conv_weight_p3(w, dtype) if pack3_eligible(conv.in_channels, conv.kernel_size[1], conv.stride[0], dtype) \
         else None
     return Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, conv.kernel_size[0],
                 conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small, None, p3)
@@ -336,6 +340,7 @@ class HipRunner:
         # fewer f32-MFMA products than the direct conv; conv_wino_f32.hip)
         self.winograd = winograd
         self.pack3 = pack3           # fp32 RGB stems on packed rows (conv_f32.hip mode 2)
+        self.pack3_f16 = False       # fp16 AlexNet conv1 on packed rows (measured net-neutral, see _logits)
         self.side_down = False       # downsample conv on a second stream (A/B: tools/ab_flag.py --attr)
         self.stem_parts: int | None = None   # fp32 ResNet: stem + maxpool on batch parts (None = 1)
         self._side: dict = {}
@@ -370,7 +375,17 @@ class HipRunner:
         s = p.stem
         fused = (self.fuse_stem and native and p.kind == "resnet" and s.small and s.kh == 7 and s.kw == 7
                  and s.stride == 2 and s.pad == 3 and s.cout == 64)
-        if not fused:
+        first = p.features[0][1] if p.kind != "resnet" else None
+        p3 = (first is not None and native and self.pack3_f16 and first.p3 is not None)
+        if p3:
+            # AlexNet conv1 (11x11/4) on packed fp16 rows through conv_glds (K 448
+            # vs 704 for NHWC4 on the register-staged conv_igemm): conv 290 -> 220
+            # us at B=500, but the packed-row preprocess costs 133 vs 46 us, so it
+            # is off by default (profiles/r2_v21_alexnet_f16_pack3.md)
+            x3 = o.preprocess_pack3(img_u8, first.kw, first.stride, first.pad, start, batch, start_offset, f16=True)
+            x = o.conv2d_pack3(x3, first.p3, first.b, img_u8.shape[2], first.kh, first.kw, first.stride, first.pad,
+                               first.relu)
+        elif not fused:
             x = o.preprocess(img_u8, start, batch, start_offset) if native else o.resize_crop(img_u8, 256, 224)
         if p.kind == "resnet":
             nb = batch if start is not None else img_u8.shape[0]
@@ -388,7 +403,7 @@ class HipRunner:
                 x = self._block(blk, x)
             x = o.global_avgpool(x)
         else:
-            for k, v in p.features:
+            for k, v in p.features[1:] if p3 else p.features:
                 if k == "conv":
                     x = o.conv2d(x, v.w, v.b, v.kh, v.kw, v.stride, v.pad, v.relu)
                 else:

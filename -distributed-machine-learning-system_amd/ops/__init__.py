@@ -37,14 +37,16 @@ def conv2d_wino(x, u, bias, relu: bool, residual=None, variant: int = 0):
 
 
 def preprocess_pack3(img_u8, kw: int, stride: int, pad: int, start=None, batch: int = -1, start_offset: int = 0,
-                     window: int = -1, sub: int = 0):
-    """uint8 [B,H,W,3] -> packed-row fp32 stem input [B, H, nc, wp] (window args as ``preprocess``)."""
-    return load().preprocess_pack3(img_u8, kw, stride, pad, start, batch, start_offset, window, sub)
+                     window: int = -1, sub: int = 0, f16: bool = False):
+    """uint8 [B,H,W,3] -> packed-row stem input [B, H, nc, wp], fp32 (``f16``:
+    fp16) (window args as ``preprocess``)."""
+    return load().preprocess_pack3(img_u8, kw, stride, pad, start, batch, start_offset, window, sub, f16)
 
 
 def conv2d_pack3(x3, w, bias, width: int, kh: int, kw: int, stride: int, pad: int, relu: bool, tile: int = -1):
-    """fp32 RGB stem conv on packed rows; ``w`` = models.packed.pack_conv_weight_p3(w)."""
-    return load().conv2d_pack3_f32(x3, w, bias, width, kh, kw, stride, pad, relu, tile)
+    """RGB stem conv on packed rows (fp32: conv_f32 mode 2; fp16: conv_glds
+    pack3); ``w`` = models.packed.pack_conv_weight_p3(w, dtype)."""
+    return load().conv2d_pack3(x3, w, bias, width, kh, kw, stride, pad, relu, tile)
 
 
 def wino_supported(h: int, w: int, cin: int, cout: int) -> bool:

@@ -98,46 +98,56 @@ def test_pack_unpack_roundtrip_fp32():
         packed.pack_conv_weight(torch.randn(8, 64, 3, 3), "bf8")
 
 
-def _pack3_geometry(W, KW, stride, pad):
-    g = 4 if stride % 4 == 0 else (2 if stride % 2 == 0 else 1)
-    return 4 // g, (3 * (W + 2 * pad) + 3 + 3) // 4 * 4, (3 * KW + 3) // 4, g
+def _pack3_geometry(W, KW, stride, pad, E=4):
+    g = 1
+    while g < E and (3 * stride) % (2 * g) == 0:
+        g *= 2
+    return E // g, (3 * (W + 2 * pad) + 2 * E - 2) // E * E, (3 * KW + E - 1) // E, g
 
 
-def _emulate_pack3(img, w, b, stride, pad):
-    """The packed-row stem (preprocess_pack3_f32 + conv_f32 mode 2) index math in
-    torch: row copies, aligned chunk starts, (kh, chunk) K order."""
+def _emulate_pack3(img, w, b, stride, pad, dtype="fp32"):
+    """The packed-row stem (preprocess_pack3 + conv_f32 mode 2 / conv_glds
+    pack3) index math in torch: row copies, aligned chunk starts, (kh, chunk)
+    K order."""
+    E = 4 if dtype == "fp32" else 8
     B, H, W, _ = img.shape
     cout, _, KH, KW = w.shape
-    nc, wp, cpk, g = _pack3_geometry(W, KW, stride, pad)
+    nc, wp, cpk, g = _pack3_geometry(W, KW, stride, pad, E)
     x = ref.preprocess_u8(img).permute(0, 2, 3, 1).reshape(B, H, 3 * W)
-    R = torch.zeros(B, H, 3 * (W + 2 * pad) + 16)
+    R = torch.zeros(B, H, 3 * (W + 2 * pad) + 4 * E)
     R[:, :, 3 * pad:3 * pad + 3 * W] = x
     x3 = torch.stack([R[:, :, c * g:c * g + wp] for c in range(nc)], 2)       # [B, H, nc, wp]
     assert x3.shape == (B, H, nc, wp)
-    wpk = packed.pack_conv_weight_p3(w)
-    nk = (KH * cpk + 3) // 4
-    assert wpk.shape == (cout, nk * 16)
+    wpk = packed.pack_conv_weight_p3(w, dtype).float()
+    stage = 16 if dtype == "fp32" else 64
+    nk = (KH * cpk * E + stage - 1) // stage
+    assert wpk.shape == (cout, nk * stage)
     Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
     out = torch.zeros(B, Ho, Wo, cout)
     for oh in range(Ho):
         for ow in range(Wo):
             r0 = 3 * stride * ow
-            sh = r0 & 3
-            vec = torch.zeros(B, nk * 16)
+            sh = r0 % E
+            assert (r0 - sh) % E == 0 and sh % g == 0
+            vec = torch.zeros(B, nk * stage)
             for kh in range(KH):
                 ih = oh * stride - pad + kh
                 if 0 <= ih < H:
-                    vec[:, kh * 4 * cpk:(kh + 1) * 4 * cpk] = x3[:, ih, sh // g, r0 - sh:r0 - sh + 4 * cpk]
+                    vec[:, kh * E * cpk:(kh + 1) * E * cpk] = x3[:, ih, sh // g, r0 - sh:r0 - sh + E * cpk]
             out[:, oh, ow] = vec @ wpk.t() + b
     return out
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "fp16"])
 @pytest.mark.parametrize("H,W,KH,KW,stride,pad", [(23, 21, 7, 7, 2, 3), (31, 27, 11, 11, 4, 2), (9, 12, 5, 5, 1, 2)])
-def test_pack3_stem_layout_matches_conv(H, W, KH, KW, stride, pad):
+def test_pack3_stem_layout_matches_conv(H, W, KH, KW, stride, pad, dtype):
+    if dtype == "fp16" and not packed.pack3_eligible(3, KW, stride, dtype):
+        pytest.skip("fp16 packed rows need an even stride")
     torch.manual_seed(H + W)
     img = torch.randint(0, 256, (2, H, W, 3), dtype=torch.uint8)
     w = torch.randn(8, 3, KH, KW)
     b = torch.randn(8)
     ref_out = torch.nn.functional.conv2d(ref.preprocess_u8(img), w, b, stride, pad).permute(0, 2, 3, 1)
-    e = _emulate_pack3(img, w, b, stride, pad)
-    assert (e - ref_out).abs().max().item() < 1e-4 * ref_out.abs().max().item()
+    e = _emulate_pack3(img, w, b, stride, pad, dtype)
+    tol = 1e-4 if dtype == "fp32" else 2e-3          # fp16: rounded weights
+    assert (e - ref_out).abs().max().item() < tol * ref_out.abs().max().item()
