@@ -482,8 +482,13 @@ static torch::Tensor zero_f32(const torch::Device& dev, int64_t n) {
   const int i = dev.index() < 0 ? 0 : dev.index();
   TORCH_CHECK(i < 64, "device index out of range");
   std::lock_guard<std::mutex> lk(mu);
+  static std::vector<torch::Tensor>* retired = new std::vector<torch::Tensor>();
   auto& b = (*bufs)[i];
   if (!b.defined() || b.numel() < n) {
+    // a smaller buffer may still be read by queued kernels (other threads'
+    // streams, captured graphs): keep it alive instead of returning it to the
+    // caching allocator, where it could be reused while "zero"
+    if (b.defined()) retired->push_back(b);
     b = torch::zeros({std::max<int64_t>(n, 4096)}, torch::TensorOptions().dtype(torch::kFloat).device(dev));
     (void)hipStreamSynchronize(cur_stream());
   }
@@ -491,8 +496,8 @@ static torch::Tensor zero_f32(const torch::Device& dev, int64_t n) {
 }
 
 // y = act(x @ w.T + bias) with K split over `splits` partial GEMMs (the conv
-// kernel as a 1x1 conv on a K-slice of each row: ldx = K) into fp32 partials,
-// then one combine kernel.  For FC layers with few output tiles and a long K
+// kernel as a 1x1 conv on a K-slice of each row: ldx = K, all slices in one
+// launch) into fp32 partials, then one combine kernel.  For FC layers with few output tiles and a long K
 // (AlexNet fc6-fc8 at batch 500: 64-256 tiles, K = 4096-9216) one tile per CU
 // with 64-144 serial K stages cannot hide the DMA latency.
 torch::Tensor linear_splitk(torch::Tensor x, torch::Tensor w, torch::Tensor bias, bool relu, bool out_f32,
@@ -521,13 +526,15 @@ torch::Tensor linear_splitk(torch::Tensor x, torch::Tensor w, torch::Tensor bias
   const half_t* xp = reinterpret_cast<const half_t*>(x.data_ptr());
   const half_t* wp = reinterpret_cast<const half_t*>(w.data_ptr());
   const int t = tile >= 10 ? (int)tile : conv_glds_pick((int)M, (int)N);
-  for (int64_t s = 0; s < splits; ++s) {
+  {
+    // all slices in ONE launch (grid = tiles x splits): one launch per slice kept
+    // each slice at the unsplit block count and never paid (r1 A/B)
     ConvArgs a{};
-    a.x = xp + s * Ks;
-    a.w = wp + s * Ks;
+    a.x = xp;
+    a.w = wp;
     a.bias = zb.data_ptr<float>();
     a.res = nullptr;
-    a.y = part.data_ptr<float>() + s * M * N;
+    a.y = part.data_ptr<float>();
     a.B = (int)M; a.H = 1; a.W = 1; a.C = (int)Ks; a.ldx = (int)K;
     a.Ho = 1; a.Wo = 1; a.Cout = (int)N; a.ldy = (int)N;
     a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0;
@@ -535,6 +542,9 @@ torch::Tensor linear_splitk(torch::Tensor x, torch::Tensor w, torch::Tensor bias
     a.Kpad = (int)K;
     a.relu = 0;
     a.zero = zero;
+    a.ksplit = (int)splits;
+    a.kslice = (int)Ks;
+    a.ysplit = (long)(M * N);
     TORCH_CHECK(conv_glds_launch(a, true, t, cur_stream()), "unknown conv tile id ", t);
     check_launch("linear_splitk");
   }

@@ -27,6 +27,9 @@ struct ConvArgs {
   int ablate;        // profiling only (set_conv_ablation), conv_glds: 1 skip epilogue stores, 2 skip residual loads
   int nc, wp, cpk;   // conv_glds pack3 (RGB stems on packed rows, preprocess_pack3_f16): row copies,
                      // halfs per copy row, 16-byte chunks per kernel row (ceil(3*KW/8)); cpk = 0: off
+  int ksplit;        // conv_glds split-K in ONE launch (FC layers, fp32 partials): block s / tiles takes
+  int kslice;        // K slice s: x and w advance by s*kslice halfs, y by s*ysplit floats; 0/1: off
+  long ysplit;
 };
 
 // fp32 (reference-precision) conv: same geometry fields as ConvArgs, f32 tensors.

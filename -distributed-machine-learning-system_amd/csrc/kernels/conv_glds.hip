@@ -69,9 +69,13 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
   const int wn = wave / WM, wm = wave % WM;
 
   const int nwg = a.tiles_n * a.tiles_m;
-  const int lid = xcd_remap(blockIdx.x, nwg);
+  const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
+  const int lid_all = xcd_remap(blockIdx.x, nwg * nsplit);
+  const int split = lid_all / nwg, lid = lid_all - split * nwg;
   const int tm = lid / a.tiles_n, tn = lid % a.tiles_n;
   const int n0 = tn * BN, m0 = tm * BM;
+  const half_t* const xin = a.x + (size_t)split * a.kslice;        // split-K: this block's K slice
+  const half_t* const win = a.w + (size_t)split * a.kslice;
 
   const half_t* zero = reinterpret_cast<const half_t*>(a.zero);
   const int lrow = lane / CPR, lslot = lane % CPR;
@@ -84,7 +88,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
     const int row = (wave + NW * j) * RPI + lrow;
     const int n = n0 + row;
     a_ch[j] = (lslot ^ swz_r(row, CPR)) * 8;
-    a_src[j] = n < a.Cout ? a.w + (size_t)n * a.Kpad + a_ch[j] : nullptr;
+    a_src[j] = n < a.Cout ? win + (size_t)n * a.Kpad + a_ch[j] : nullptr;
   }
   // B sources: pixel decomposition per instruction (pixel stride ldx: a K-slice
   // of wider rows when the caller splits K, e.g. linear_splitk)
@@ -135,14 +139,14 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
         const int kh = q / a.cpk, jj = q - kh * a.cpk;
         const int ih = b_ih0[j] + kh;
         const bool ok = kh < a.KH && (unsigned)ih < (unsigned)a.H;
-        const half_t* src = ok ? a.x + b_base[j] + ih * prow + 8 * jj : zero;
+        const half_t* src = ok ? xin + b_base[j] + ih * prow + 8 * jj : zero;
         __builtin_amdgcn_global_load_lds((glb_void_t*)src,
                                          (lds_void_t*)(base + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
         continue;
       }
       const int ih = b_ih0[j] + i_kh, iw = b_iw0[j] + i_kw;
       const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const half_t* src = ok ? a.x + b_base[j] + (ih * a.W + iw) * ldx + coff : zero;
+      const half_t* src = ok ? xin + b_base[j] + (ih * a.W + iw) * ldx + coff : zero;
       __builtin_amdgcn_global_load_lds((glb_void_t*)src,
                                        (lds_void_t*)(base + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
     }
@@ -270,7 +274,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
       if (a.ablate & 1) {
         if (v[0] == 12345.f) *reinterpret_cast<float*>(a.y) = v[1] + v[2] + v[3];   // keep the math alive
       } else if constexpr (OUT_F32) {
-        *reinterpret_cast<float4v*>(static_cast<float*>(a.y) + (size_t)m * a.ldy + n) = v;
+        *reinterpret_cast<float4v*>(static_cast<float*>(a.y) + (size_t)split * a.ysplit + (size_t)m * a.ldy + n) = v;
       } else {
         half4v o;
         o[0] = (half_t)v[0];
@@ -294,7 +298,7 @@ static void glds_cfg(ConvArgs a, hipStream_t st) {
     a.cblk = a.C / BK;
     a.nK = a.KH * a.KW * a.cblk;
   }
-  const int grid = a.tiles_n * a.tiles_m;
+  const int grid = a.tiles_n * a.tiles_m * (a.ksplit > 1 ? a.ksplit : 1);
   const size_t lds = (size_t)NS * (BN + BM) * BK * 2;
   auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32, P3>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), (int)lds);   // per (kernel, device), launch_util.h

@@ -53,12 +53,23 @@ def wino_supported(h: int, w: int, cin: int, cout: int) -> bool:
     return cin % 16 == 0 and cout % 32 == 0 and bool(load().wino_supported(h, w, cin, cout))
 
 
-# Default K split of FC layers.  Measured (tools/ab_linear_split.py,
-# profiles/r1_v8_ab_linear_split.log): splitting never paid on these models --
-# AlexNet b500 -2.8 % (2 splits) .. -9.8 % (8), b1/b8 -20 %; ResNet50 b1024
-# within its run-to-run spread -- the fp32 partials and extra launches cost
-# more than the DMA latency they hide.  Kept selectable for other shapes.
-LINEAR_SPLITS: int = 1
+# fp16 FC layers: K split into slices in ONE launch (conv_glds grid = tiles x
+# slices, fp32 partials + combine) when the unsplit GEMM has few blocks.  The
+# round-1 version issued one launch per slice and never paid
+# (profiles/r1_v8_ab_linear_split.log); in one launch AlexNet fc6 101 -> 67 us,
+# fc7 54 -> 37, fc8 40 -> 20 at B=500 (profiles/r2_v22_fc_f16_sweep.md).
+# None = f16_linear_splits(); an int forces that split.
+LINEAR_SPLITS: int | None = None
+
+
+def f16_linear_splits(m: int, k: int, n: int) -> int:
+    """Split factor for an fp16 FC layer: ~512 blocks of the default tile,
+    at most 4 slices, slices of >= 1024 (short K does not pay the combine)."""
+    tiles = (n // 128) * -(-m // 64) if n % 128 == 0 else -(-n // 64) * -(-m // 128)
+    s = 1
+    while s < 4 and tiles * s < 512 and k % (64 * 2 * s) == 0 and k // (2 * s) >= 1024:
+        s *= 2
+    return s
 
 
 def f32_linear_splits(m: int, k: int, n: int) -> int:
@@ -89,7 +100,7 @@ def linear(x, w, bias, relu: bool = False, out_f32: bool = False, splits: int | 
         y = load().conv2d_nhwc_f32(x.view(b, 1, 1, k), w, bias, None, 1, 1, 1, 0, relu, -1, None)
         return y.view(b, n)
     if splits is None:
-        splits = LINEAR_SPLITS
+        splits = LINEAR_SPLITS if LINEAR_SPLITS is not None else f16_linear_splits(b, k, n)
     if splits > 1:
         return load().linear_splitk(x, w, bias, relu, out_f32, splits, -1)
     y = load().conv2d_nhwc(x.view(b, 1, 1, k), w, bias, None, 1, 1, 1, 0, relu, out_f32, -1, None)

@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--batch", type=int, default=500)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--variants", default="1,2,4", help="split counts forced on every FC layer")
+    ap.add_argument("--variants", default="1,auto", help="split counts forced on every FC layer ('auto': ops heuristic)")
     a = ap.parse_args()
     from idunno import ops
     from idunno.models import HipRunner, build_program
@@ -29,7 +29,7 @@ def main():
     prog = build_program(a.model)
     shard = ops.synth_images(1234, 0, a.batch, dev)
     runs, outs, keep = {}, {}, []
-    variants = [(v, int(v)) for v in a.variants.split(",")]
+    variants = [(v, None if v == "auto" else int(v)) for v in a.variants.split(",")]
     for name, forced in variants:
         ops.LINEAR_SPLITS = forced
         r = HipRunner(prog, dev)
@@ -39,7 +39,7 @@ def main():
         c, p = run()
         torch.cuda.synchronize()
         outs[name] = (c.clone(), p.clone())
-    ops.LINEAR_SPLITS = 1
+    ops.LINEAR_SPLITS = None
     first = variants[0][0]
     for name in runs:
         agree = (outs[first][0] == outs[name][0]).float().mean().item()
