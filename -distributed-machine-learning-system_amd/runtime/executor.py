@@ -237,6 +237,11 @@ class HipExecutor(Executor):
         """Release the captured graphs (under the process-wide capture lock);
         a chunk still running afterwards takes the eager path."""
         self.closed = True
+        with self.run_lock:
+            # chunks launched by submit() may still be replaying their graphs:
+            # drain the private stream before the graphs are destroyed
+            if self.stream is not None:
+                self.stream.synchronize()
         with self.lock:
             runners = list(self.runners.values())
         for r in runners:
