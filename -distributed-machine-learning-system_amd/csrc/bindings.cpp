@@ -275,6 +275,148 @@ torch::Tensor conv2d_nhwc_f32(torch::Tensor x, torch::Tensor w, torch::Tensor bi
   return y;
 }
 
+// split fp16 (fp32-accurate) conv: y = act(acc_scale * conv(x, w) + bias (+ res)).
+//   x   : [B, H, W, 2C] half, split layout ([hi x32][lo x32] per 32 channels), C % 32 == 0
+//   w   : [Cout, KH*KW*2C] half, same layout per tap, pre-scaled by 1/acc_scale
+//   res : optional [B, Ho, Wo, 2Cout] half (split);  y: split half, or fp32 [B, Ho, Wo, Cout]
+torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias, c10::optional<torch::Tensor> res,
+                           int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool relu, double acc_scale,
+                           bool out_f32, int64_t tile, c10::optional<torch::Tensor> out) {
+  CHECK_DEV(x);
+  CHECK_DEV(w);
+  CHECK_DEV(bias);
+  CHECK_CONTIG(x);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(bias);
+  CHECK_DT(x, torch::kHalf);
+  CHECK_DT(w, torch::kHalf);
+  CHECK_DT(bias, torch::kFloat);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 2 && bias.dim() == 1, "bad ranks");
+  TORCH_CHECK(w.device() == x.device() && bias.device() == x.device(), "operands on different devices");
+  TORCH_CHECK(KH >= 1 && KW >= 1 && stride >= 1 && pad >= 0, "bad conv geometry");
+  const int B = x.size(0), H = x.size(1), W = x.size(2), C2 = x.size(3);
+  TORCH_CHECK(C2 % 64 == 0, "split input needs 2C halfs with C % 32 == 0, got ", C2);
+  const int Cout = w.size(0), Kpad = w.size(1);
+  TORCH_CHECK(Kpad == KH * KW * C2, "split weight must be [Cout, KH*KW*2C]");
+  TORCH_CHECK(bias.size(0) == Cout, "bias/Cout mismatch");
+  TORCH_CHECK(Cout % 32 == 0, "split conv needs Cout % 32 == 0");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty output");
+  const long M = (long)B * Ho * Wo;
+  TORCH_CHECK(M < (1L << 31) && (long)B * H * W * C2 < (1L << 31) && M * 2 * Cout < (1L << 31),
+              "tensor too large for int32 indexing");
+  const int64_t ych = out_f32 ? Cout : 2 * Cout;
+  torch::Tensor y;
+  if (out.has_value() && out->defined()) {
+    y = *out;
+    CHECK_DEV(y);
+    CHECK_CONTIG(y);
+    CHECK_DT(y, out_f32 ? torch::kFloat : torch::kHalf);
+    TORCH_CHECK(y.device() == x.device(), "out must live on the input's device");
+    TORCH_CHECK(y.dim() == 4 && y.size(0) == B && y.size(1) == Ho && y.size(2) == Wo && y.size(3) == ych,
+                "out shape mismatch");
+  } else {
+    y = torch::empty({B, Ho, Wo, ych}, x.options().dtype(out_f32 ? torch::kFloat : torch::kHalf));
+  }
+  const half_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    auto& r = *res;
+    CHECK_DEV(r);
+    CHECK_CONTIG(r);
+    CHECK_DT(r, torch::kHalf);
+    TORCH_CHECK(r.device() == x.device(), "residual on a different device");
+    TORCH_CHECK(r.dim() == 4 && r.size(0) == B && r.size(1) == Ho && r.size(2) == Wo && r.size(3) == 2 * Cout,
+                "residual shape mismatch (split [B, Ho, Wo, 2*Cout])");
+    rp = reinterpret_cast<const half_t*>(r.data_ptr());
+  }
+  ConvArgs a{};
+  a.x = reinterpret_cast<const half_t*>(x.data_ptr());
+  a.w = reinterpret_cast<const half_t*>(w.data_ptr());
+  a.bias = bias.data_ptr<float>();
+  a.res = rp;
+  a.y = y.data_ptr();
+  a.B = B; a.H = H; a.W = W; a.C = C2;
+  a.Ho = Ho; a.Wo = Wo; a.Cout = Cout; a.ldy = (int)ych;
+  a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
+  a.M = (int)M;
+  a.Kpad = Kpad;
+  a.relu = relu ? 1 : 0;
+  a.acc_scale = (float)acc_scale;
+  a.ablate = g_conv_ablate;
+  if (M == 0) return y;
+  a.zero = zero_buffer(x.device()).data_ptr();
+  const int t = tile >= 0 ? (int)tile : conv_glds_split_pick(a.M, Cout);
+  TORCH_CHECK(conv_glds_split_launch(a, out_f32, t, cur_stream()), "unknown split conv tile id ", t);
+  check_launch("conv_glds_split");
+  return y;
+}
+
+// fp32 NHWC [.., C] <-> split [.., 2C] (C % 32 == 0)
+torch::Tensor split_from_f32(torch::Tensor x) {
+  CHECK_DEV(x);
+  CHECK_CONTIG(x);
+  CHECK_DT(x, torch::kFloat);
+  TORCH_CHECK(x.dim() >= 1 && x.size(-1) % 32 == 0, "last dim must be a multiple of 32");
+  const int C = x.size(-1);
+  auto sz = x.sizes().vec();
+  sz.back() = 2 * C;
+  auto y = torch::empty(sz, x.options().dtype(torch::kHalf));
+  const long npix = C ? x.numel() / C : 0;
+  if (npix == 0) return y;
+  split_from_f32_launch(x.data_ptr<float>(), reinterpret_cast<half_t*>(y.data_ptr()), npix, C, cur_stream());
+  check_launch("split_from_f32");
+  return y;
+}
+
+torch::Tensor f32_from_split(torch::Tensor x) {
+  CHECK_DEV(x);
+  CHECK_CONTIG(x);
+  CHECK_DT(x, torch::kHalf);
+  TORCH_CHECK(x.dim() >= 1 && x.size(-1) % 64 == 0, "last dim must be 2C with C % 32 == 0");
+  const int C = x.size(-1) / 2;
+  auto sz = x.sizes().vec();
+  sz.back() = C;
+  auto y = torch::empty(sz, x.options().dtype(torch::kFloat));
+  const long npix = x.numel() / (2 * C);
+  if (npix == 0) return y;
+  f32_from_split_launch(reinterpret_cast<const half_t*>(x.data_ptr()), y.data_ptr<float>(), npix, C, cur_stream());
+  check_launch("f32_from_split");
+  return y;
+}
+
+// NHWC max pool into the split layout; x fp32 [B,H,W,C] or split half [B,H,W,2C]
+torch::Tensor maxpool2d_split(torch::Tensor x, int64_t k, int64_t s, int64_t pad, c10::optional<torch::Tensor> out) {
+  CHECK_DEV(x);
+  CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 4, "x must be NHWC");
+  const bool in_split = x.scalar_type() == torch::kHalf;
+  TORCH_CHECK(in_split || x.scalar_type() == torch::kFloat, "x must be fp32 or split half");
+  TORCH_CHECK(k >= 1 && s >= 1 && pad >= 0 && pad < k, "bad pool geometry");
+  const int B = x.size(0), H = x.size(1), W = x.size(2), C = in_split ? x.size(3) / 2 : x.size(3);
+  TORCH_CHECK(C % 32 == 0 && (!in_split || x.size(3) == 2 * C), "channels must be a multiple of 32");
+  const int Ho = (H + 2 * pad - k) / s + 1, Wo = (W + 2 * pad - k) / s + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty output");
+  torch::Tensor y;
+  if (out.has_value() && out->defined()) {
+    y = *out;
+    CHECK_DEV(y);
+    CHECK_CONTIG(y);
+    CHECK_DT(y, torch::kHalf);
+    TORCH_CHECK(y.device() == x.device(), "out must live on the input's device");
+    TORCH_CHECK(y.dim() == 4 && y.size(0) == B && y.size(1) == Ho && y.size(2) == Wo && y.size(3) == 2 * C,
+                "out shape mismatch");
+  } else {
+    y = torch::empty({B, Ho, Wo, 2 * C}, x.options().dtype(torch::kHalf));
+  }
+  if ((long)B * Ho * Wo == 0) return y;
+  maxpool_split_launch(x.data_ptr(), in_split, reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, C, Ho, Wo, k, s, pad,
+                       cur_stream());
+  check_launch("maxpool_split");
+  return y;
+}
+
+int64_t pick_tile_split(int64_t M, int64_t Cout) { return conv_glds_split_pick((int)M, (int)Cout); }
+
 static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
 
 // fp32 FC layer y = act(x @ w.T + bias) with K split over `splits` slices in ONE
@@ -777,6 +919,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("relu"), py::arg("out_f32") = false, py::arg("tile") = -1, py::arg("out") = py::none());
   m.def("linear_splitk", &linear_splitk, "FC layer with split-K partial GEMMs + combine", py::arg("x"),
         py::arg("w"), py::arg("bias"), py::arg("relu"), py::arg("out_f32"), py::arg("splits"), py::arg("tile") = -1);
+  m.def("conv2d_split", &conv2d_split, "split-fp16 (fp32-accurate) conv: 3 f16 MFMAs per 32 channels",
+        py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
+        py::arg("pad"), py::arg("relu"), py::arg("acc_scale"), py::arg("out_f32") = false, py::arg("tile") = -1,
+        py::arg("out") = py::none());
+  m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
+  m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");
+  m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),
+        py::arg("k"), py::arg("s"), py::arg("pad"), py::arg("out") = py::none());
+  m.def("pick_tile_split", &pick_tile_split, "split conv tile heuristic for (M, Cout)");
   m.def("conv2d_nhwc_f32", &conv2d_nhwc_f32, "fp32 implicit-GEMM conv on f32 MFMA + bias (+res) (+relu)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("tile") = -1, py::arg("out") = py::none());

@@ -93,6 +93,20 @@ __device__ __forceinline__ float4v gload_f4_untracked(const void* p) {
   return v;
 }
 
+// ---- split fp16 (fp32-accurate) activations ------------------------------------
+// A value v is two halfs hi = fp16(v), lo = fp16(v - hi); a pixel of C channels
+// is 2C halfs, [hi x32][lo x32] per 32-channel block.  split_off(c) = offset of
+// channel c's hi half within its pixel (lo at +32).
+__device__ __forceinline__ int split_off(int c) { return ((c >> 5) << 6) + (c & 31); }
+
+__device__ __forceinline__ void split_f16x4(const float4v v, half4v& h, half4v& l) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    h[i] = (half_t)v[i];
+    l[i] = (half_t)(v[i] - (float)h[i]);
+  }
+}
+
 __device__ __forceinline__ void reg_tie(half4v& r) { asm volatile("" : "+v"(r)); }
 __device__ __forceinline__ void reg_tie(float4v& r) { asm volatile("" : "+v"(r)); }
 

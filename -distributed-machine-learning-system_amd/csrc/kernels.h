@@ -30,6 +30,7 @@ struct ConvArgs {
   int ksplit;        // conv_glds split-K in ONE launch (FC layers, fp32 partials): block s / tiles takes
   int kslice;        // K slice s: x and w advance by s*kslice halfs, y by s*ysplit floats; 0/1: off
   long ysplit;
+  float acc_scale;   // conv_glds SPLIT: accumulator multiplier (2^-e of the pre-scaled split weights)
 };
 
 // fp32 (reference-precision) conv: same geometry fields as ConvArgs, f32 tensors.
@@ -109,10 +110,19 @@ void preprocess_f32_launch(const uint8_t* img, float* out, long npix, const long
 void maxpool_f32_launch(const float* x, float* y, int B, int H, int W, int C, int Ho, int Wo, int k, int s,
                         int pad, hipStream_t st);
 void avgpool_f32_launch(const float* x, float* y, int B, int HW, int C, hipStream_t st);
+// split-fp16 layout conversions and pooling (elementwise_split.hip)
+void split_from_f32_launch(const float* x, half_t* y, long npix, int C, hipStream_t st);
+void f32_from_split_launch(const half_t* x, float* y, long npix, int C, hipStream_t st);
+void maxpool_split_launch(const void* x, bool in_split, half_t* y, int B, int H, int W, int C, int Ho, int Wo, int k,
+                          int s, int pad, hipStream_t st);
 
 void conv_igemm_launch(ConvArgs a, bool small, bool out_f32, int tile, hipStream_t st);
 int conv_pick_tile(int M, int Cout);
-bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);   // a.cpk > 0: pack3 stem
+bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
+// split fp16 (fp32-accurate) implicit-GEMM conv: x/res/y are split-format halfs
+// ([hi x32][lo x32] per 32 channels), y fp32 with out_f32
+bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
+int conv_glds_split_pick(int M, int Cout);   // a.cpk > 0: pack3 stem
 bool conv_big_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 bool conv_pers_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);   // false: shape unsupported
 bool conv3x3_patch_supported(int H, int W, int C, int Cout);

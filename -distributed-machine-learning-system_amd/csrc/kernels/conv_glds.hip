@@ -47,8 +47,21 @@ __device__ __forceinline__ void wait_stages(int pending_stages) {
 // the 3*KW halfs of one kernel row are contiguous in the row copy in which
 // they start 16-byte aligned; K = (kh, 16-byte chunk), ceil(3*KW/8) chunks per
 // kh (AlexNet 11x11/4: K 448 instead of 704 for NHWC4 on conv_igemm).
-template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false>
+//
+// SPLIT: fp32-accurate convolution on the f16 MFMA ("split fp16", the fp32
+// programs' fast path).  Every fp32 value v is carried as two halfs,
+// hi = fp16(v), lo = fp16(v - hi) (22 significant bits), laid out per 32
+// channels as [hi x32][lo x32], so one BK = 64 stage holds 32 channels' hi
+// and lo parts and the DMA / swizzle machinery is unchanged.  Per stage the
+// products hi*hi + hi*lo + lo*hi are summed in f32 (lo*lo, ~2^-22 relative,
+// is dropped): 3 f16 MFMAs per 32 channels = 5.3x the f32-MFMA rate.  Weights
+// are pre-scaled by 2^e (max |w| ~ 2^14, so their lo parts stay normal) and
+// the epilogue multiplies by a.acc_scale = 2^-e (exact).  Residual in, output
+// out in the same split layout (or fp32 with OUT_F32).
+template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false,
+          bool SPLIT = false>
 __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs a) {
+  static_assert(!SPLIT || BK == 64, "split stages are 32 channels x (hi, lo)");
   constexpr int NW = WN * WM;
   constexpr int NT = 64 * NW;
   constexpr int TN = BN / WN, TM = BM / WM;
@@ -173,6 +186,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
   // a full memory latency per tile (30 us of 138 on ResNet layer2 conv2,
   // profiles/r1_v8_conv_big_sweep.log)
   half4v rv[HAS_RES ? FN : 1][HAS_RES ? FM : 1];
+  half4v rl[HAS_RES && SPLIT ? FN : 1][HAS_RES && SPLIT ? FM : 1];   // SPLIT: residual lo parts
   if constexpr (HAS_RES) {
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
@@ -180,8 +194,15 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
         const int m = m0 + wm * TM + j * 16 + (lane & 15);
-        const size_t off = (m < a.M && n < a.Cout) ? (size_t)m * a.Cout + n : 0;
-        rv[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : gload_b64_untracked(a.res + off);
+        const bool ok = m < a.M && n < a.Cout;
+        if constexpr (SPLIT) {
+          const size_t off = ok ? (size_t)m * 2 * a.Cout + split_off(n) : 0;
+          rv[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : gload_b64_untracked(a.res + off);
+          rl[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : gload_b64_untracked(a.res + off + 32);
+        } else {
+          const size_t off = ok ? (size_t)m * a.Cout + n : 0;
+          rv[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : gload_b64_untracked(a.res + off);
+        }
       }
     }
   }
@@ -232,6 +253,33 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
     };
     static_assert(KK == 1 || KK == 2, "BK 32 or 64");
+    if constexpr (SPLIT) {
+      // chunk 0 = hi, chunk 1 = lo: hi*hi as soon as the hi fragments land,
+      // then hi*lo + lo*hi
+      lds_waitcnt<NR>();
+#pragma unroll
+      for (int i = 0; i < FN; ++i) lds_tie(fa[0][i]);
+#pragma unroll
+      for (int j = 0; j < FM; ++j) lds_tie(fb[0][j]);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+      lds_waitcnt<0>();
+#pragma unroll
+      for (int i = 0; i < FN; ++i) lds_tie(fa[1][i]);
+#pragma unroll
+      for (int j = 0; j < FM; ++j) lds_tie(fb[1][j]);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[0][i], fb[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[1][i], fb[0][j], acc[i][j], 0, 0, 0);
+        }
+      continue;
+    }
     if constexpr (KK == 2) {
       lds_waitcnt<NR>();                         // chunk 0 landed, chunk 1 may be in flight
       mfma_chunk(0);
@@ -246,7 +294,10 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
-      for (int j = 0; j < FM; ++j) reg_tie(rv[i][j]);
+      for (int j = 0; j < FM; ++j) {
+        reg_tie(rv[i][j]);
+        if constexpr (SPLIT) reg_tie(rl[i][j]);
+      }
   }
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
@@ -257,13 +308,23 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
     for (int j = 0; j < FM; ++j) {
       const int m = m0 + wm * TM + j * 16 + (lane & 15);
       if (m >= a.M) continue;
-      float4v v = acc[i][j] + bv;
+      float4v v;
+      if constexpr (SPLIT) v = acc[i][j] * a.acc_scale + bv;
+      else v = acc[i][j] + bv;
       if constexpr (HAS_RES) {
         const half4v r = rv[i][j];
-        v[0] += (float)r[0];
-        v[1] += (float)r[1];
-        v[2] += (float)r[2];
-        v[3] += (float)r[3];
+        if constexpr (SPLIT) {
+          const half4v q = rl[i][j];
+          v[0] += (float)r[0] + (float)q[0];
+          v[1] += (float)r[1] + (float)q[1];
+          v[2] += (float)r[2] + (float)q[2];
+          v[3] += (float)r[3] + (float)q[3];
+        } else {
+          v[0] += (float)r[0];
+          v[1] += (float)r[1];
+          v[2] += (float)r[2];
+          v[3] += (float)r[3];
+        }
       }
       if (a.relu) {
         v[0] = fmaxf(v[0], 0.f);
@@ -275,6 +336,12 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
         if (v[0] == 12345.f) *reinterpret_cast<float*>(a.y) = v[1] + v[2] + v[3];   // keep the math alive
       } else if constexpr (OUT_F32) {
         *reinterpret_cast<float4v*>(static_cast<float*>(a.y) + (size_t)split * a.ysplit + (size_t)m * a.ldy + n) = v;
+      } else if constexpr (SPLIT) {
+        half4v h, l;
+        split_f16x4(v, h, l);
+        half_t* yp = static_cast<half_t*>(a.y) + (size_t)m * a.ldy + split_off(n);
+        *reinterpret_cast<half4v*>(yp) = h;
+        *reinterpret_cast<half4v*>(yp + 32) = l;
       } else {
         half4v o;
         o[0] = (half_t)v[0];
@@ -287,7 +354,8 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
   }
 }
 
-template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false>
+template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false,
+          bool SPLIT = false>
 static void glds_cfg(ConvArgs a, hipStream_t st) {
   a.tiles_n = (a.Cout + BN - 1) / BN;
   a.tiles_m = (a.M + BM - 1) / BM;
@@ -300,7 +368,7 @@ static void glds_cfg(ConvArgs a, hipStream_t st) {
   }
   const int grid = a.tiles_n * a.tiles_m * (a.ksplit > 1 ? a.ksplit : 1);
   const size_t lds = (size_t)NS * (BN + BM) * BK * 2;
-  auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32, P3>;
+  auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32, P3, SPLIT>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), (int)lds);   // per (kernel, device), launch_util.h
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WN * WM), lds, st, a);
 }
@@ -365,6 +433,36 @@ static bool glds_dispatch_p3(ConvArgs a, int tile, hipStream_t st) {
     case 35: glds_cfg<64, 64, 64, 2, 2, 2, false, F, true>(a, st); return true;
     default: return false;
   }
+}
+
+// split fp16 (fp32-accurate) tiles: the BK = 64 shapes of the fp16 table
+template <bool R, bool F>
+static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
+  switch (tile) {
+    case 24: glds_cfg<128, 128, 64, 2, 4, 3, R, F, false, true>(a, st); return true;
+    case 26: glds_cfg<128, 128, 64, 2, 2, 2, R, F, false, true>(a, st); return true;
+    case 27: glds_cfg<64, 128, 64, 1, 4, 2, R, F, false, true>(a, st); return true;
+    case 33: glds_cfg<64, 256, 64, 1, 4, 2, R, F, false, true>(a, st); return true;
+    case 34: glds_cfg<128, 64, 64, 2, 2, 2, R, F, false, true>(a, st); return true;
+    case 35: glds_cfg<64, 64, 64, 2, 2, 2, R, F, false, true>(a, st); return true;
+    case 36: glds_cfg<128, 128, 64, 2, 4, 2, R, F, false, true>(a, st); return true;
+    case 37: glds_cfg<64, 128, 64, 1, 8, 2, R, F, false, true>(a, st); return true;
+    case 38: glds_cfg<128, 64, 64, 2, 4, 2, R, F, false, true>(a, st); return true;
+    default: return false;
+  }
+}
+
+bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
+  const bool res = a.res != nullptr;
+  if (res) return out_f32 ? glds_dispatch_split<true, true>(a, tile, st) : glds_dispatch_split<true, false>(a, tile, st);
+  return out_f32 ? glds_dispatch_split<false, true>(a, tile, st) : glds_dispatch_split<false, false>(a, tile, st);
+}
+
+// Default split tile: same shape logic as the fp16 pick (a stage is 32 channels
+// instead of 64, so a tile does 3x the MFMAs per byte staged).
+int conv_glds_split_pick(int M, int Cout) {
+  if (Cout % 128 == 0) return M >= 50000 ? 36 : 34;
+  return 27;
 }
 
 bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {

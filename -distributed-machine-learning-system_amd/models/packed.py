@@ -23,6 +23,7 @@ without a GPU).
 """
 from __future__ import annotations
 
+import math
 import threading
 from dataclasses import dataclass, field
 
@@ -47,12 +48,15 @@ class Conv:
     small: bool = False      # RGB stem packing
     wino: torch.Tensor | None = None   # fp32 3x3/s1: Winograd U = G g G^T [16, Cout, Cin]
     p3: torch.Tensor | None = None     # RGB stem on packed rows (pack_conv_weight_p3)
+    sw: torch.Tensor | None = None     # fp32 programs: split-fp16 weights (pack_split_weight)
+    s_scale: float = 1.0               # accumulator scale of ``sw`` (2^-e)
 
     def to(self, device):
         return Conv(self.w.to(device), self.b.to(device), self.cin, self.cout, self.kh, self.kw,
                     self.stride, self.pad, self.relu, self.small,
                     None if self.wino is None else self.wino.to(device),
-                    None if self.p3 is None else self.p3.to(device))
+                    None if self.p3 is None else self.p3.to(device),
+                    None if self.sw is None else self.sw.to(device), self.s_scale)
 
     @property
     def flops_per_out_pixel(self) -> int:
@@ -110,15 +114,21 @@ class Program:
 # packing
 # ---------------------------------------------------------------------------
 
-def fold_bn(w: torch.Tensor, b: torch.Tensor | None, bn: nn.BatchNorm2d | None):
-    """Fold an eval-mode BatchNorm into the preceding conv's (w, b), in fp64."""
+def fold_bn_f64(w: torch.Tensor, b: torch.Tensor | None, bn: nn.BatchNorm2d | None):
+    """Fold an eval-mode BatchNorm into the preceding conv's (w, b), fp64 result."""
     w = w.detach().double()
     b = torch.zeros(w.shape[0], dtype=torch.float64) if b is None else b.detach().double()
     if bn is None:
-        return w.float(), b.float()
+        return w, b
     scale = bn.weight.detach().double() / torch.sqrt(bn.running_var.detach().double() + bn.eps)
     w = w * scale.view(-1, 1, 1, 1)
     b = (b - bn.running_mean.detach().double()) * scale + bn.bias.detach().double()
+    return w, b
+
+
+def fold_bn(w: torch.Tensor, b: torch.Tensor | None, bn: nn.BatchNorm2d | None):
+    """Fold an eval-mode BatchNorm into the preceding conv's (w, b), in fp64."""
+    w, b = fold_bn_f64(w, b, bn)
     return w.float(), b.float()
 
 
@@ -189,6 +199,67 @@ def unpack_conv_weight(c: Conv) -> torch.Tensor:
     return w.view(c.cout, c.kh, c.kw, c.cin).permute(0, 3, 1, 2).contiguous()
 
 
+# ---------------------------------------------------------------------------
+# split fp16: fp32-accurate values as (hi, lo) half pairs (conv_glds SPLIT)
+# ---------------------------------------------------------------------------
+# A value v is carried as hi = fp16(v), lo = fp16(v - hi) (22 significant bits);
+# a pixel of C channels is 2C halfs laid out [hi x32][lo x32] per 32 channels.
+# The conv sums hi*hi + hi*lo + lo*hi on the f16 MFMA in f32.  Weights are
+# pre-scaled by 2^e so that max |w| ~ 2^14 (their lo parts stay normal halfs);
+# the kernel multiplies the accumulator by 2^-e.  On ResNet18 this is as
+# accurate as fp32 (CPU emulation: 1.2e-7 relative logit error vs fp64, fp32
+# itself 2.7e-7; tests/test_split.py).
+
+SPLIT_BLOCK = 32
+
+
+def split_eligible(cin: int, cout: int) -> bool:
+    return cin % SPLIT_BLOCK == 0 and cout % SPLIT_BLOCK == 0
+
+
+def to_split(x: torch.Tensor) -> torch.Tensor:
+    """fp32 [..., C] -> split half [..., 2C] (C % 32 == 0)."""
+    c = x.shape[-1]
+    x = x.float()
+    hi = x.half()
+    lo = (x - hi.float()).half()
+    blk = (*x.shape[:-1], c // SPLIT_BLOCK, 1, SPLIT_BLOCK)
+    return torch.cat([hi.reshape(blk), lo.reshape(blk)], dim=-2).reshape(*x.shape[:-1], 2 * c)
+
+
+def from_split(xs: torch.Tensor) -> torch.Tensor:
+    """split half [..., 2C] -> fp32 [..., C] (hi + lo in f32)."""
+    c = xs.shape[-1] // 2
+    v = xs.float().reshape(*xs.shape[:-1], c // SPLIT_BLOCK, 2, SPLIT_BLOCK)
+    return (v[..., 0, :] + v[..., 1, :]).reshape(*xs.shape[:-1], c)
+
+
+def pack_split_weight(w: torch.Tensor) -> tuple[torch.Tensor, float]:
+    """[Cout, Cin, KH, KW] -> (split weights [Cout, KH*KW*2*Cin] half, acc_scale).
+
+    K order (kh, kw, 32-channel block, hi|lo, channel); the weights are scaled
+    by 2^e (e from max |w|, so the largest is in [2^13, 2^14)) in fp64 before
+    the split, acc_scale = 2^-e undoes it exactly in the epilogue."""
+    cout, cin, kh, kw = w.shape
+    if cin % SPLIT_BLOCK:
+        raise ValueError(f"split weights need Cin % {SPLIT_BLOCK} == 0, got {cin}")
+    mx = float(w.abs().max())
+    e = 0 if mx == 0.0 else 14 - math.ceil(math.log2(mx))
+    ws = w.double().permute(0, 2, 3, 1) * (2.0 ** e)
+    hi = ws.half()
+    lo = (ws - hi.double()).half()
+    blk = (cout, kh, kw, cin // SPLIT_BLOCK, 1, SPLIT_BLOCK)
+    packed = torch.cat([hi.reshape(blk), lo.reshape(blk)], dim=4).reshape(cout, kh * kw * 2 * cin)
+    return packed.contiguous(), 2.0 ** -e
+
+
+def unpack_split_weight(c: "Conv") -> torch.Tensor:
+    """Inverse of pack_split_weight -> fp32 [Cout, Cin, KH, KW] (hi + lo, unscaled)."""
+    v = c.sw.double().reshape(c.cout, c.kh, c.kw, c.cin // SPLIT_BLOCK, 2, SPLIT_BLOCK)
+    w = (v[..., 0, :] + v[..., 1, :]).reshape(c.cout, c.kh, c.kw, c.cin) * c.s_scale
+    return w.permute(0, 3, 1, 2).float().contiguous()
+
+
 # Winograd F(2x2, 3x3) filter transform (Lavin & Gray): U = G g G^T
 WINO_G = torch.tensor([[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]], dtype=torch.float64)
 
@@ -208,14 +279,17 @@ def wino_eligible(cin: int, cout: int, kh: int, kw: int, stride: int, pad: int) 
 def make_conv(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, relu: bool, dtype: str = "fp16") -> Conv:
     w, b = fold_bn(conv.weight, conv.bias, bn)
     pw, small = pack_conv_weight(w, dtype)
+    sw, s_scale = None, 1.0
+    if dtype == "fp32" and split_eligible(conv.in_channels, conv.out_channels):
+        sw, s_scale = pack_split_weight(fold_bn_f64(conv.weight, conv.bias, bn)[0])
     if dtype == "fp32" and wino_eligible(conv.in_channels, conv.out_channels, *conv.kernel_size, conv.stride[0],
                                          conv.padding[0]):
         return Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, 3, 3, 1, 1, relu, small,
-                    wino_weight(w))
+                    wino_weight(w), None, sw, s_scale)
     p3 = pack_conv_weight_p3(w, dtype) if pack3_eligible(conv.in_channels, conv.kernel_size[1], conv.stride[0], dtype) \
         else None
     return Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, conv.kernel_size[0],
-                conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small, None, p3)
+                conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small, None, p3, sw, s_scale)
 
 
 def make_fc(lin: nn.Linear, relu: bool, perm: torch.Tensor | None = None, dtype: str = "fp16") -> Conv:
@@ -343,6 +417,10 @@ class HipRunner:
         self.pack3_f16 = False       # fp16 AlexNet conv1 on packed rows (measured net-neutral, see _logits)
         self.side_down = False       # downsample conv on a second stream (A/B: tools/ab_flag.py --attr)
         self.stem_parts: int | None = None   # fp32 ResNet: stem + maxpool on batch parts (None = 1)
+        # fp32 ResNets: residual stages on split-fp16 convs (conv_glds SPLIT:
+        # hi*hi + hi*lo + lo*hi on the f16 MFMA, fp32-accurate) instead of the
+        # f32-MFMA Winograd / direct kernels; False = the all-f32-MFMA path
+        self.split = True
         self._side: dict = {}
         # None = measured default (tools/wino_ablate.py, profiles/r2_v6_wino_variants.md):
         # variant 3 -- 4-wave blocks of 64 tiles, one 58-KiB LDS stage, two blocks
@@ -422,6 +500,16 @@ class HipRunner:
             raise ValueError("the fp32 path takes 224x224 inputs (resize on host first)")
         first = p.stem if p.kind == "resnet" else p.features[0][1]
         nb = batch if start is not None else img_u8.shape[0]
+        if p.kind == "resnet" and self.split and self._split_ok():
+            # fp32 stem -> max pool straight into the split layout -> split
+            # residual stages (the last conv writes fp32) -> fp32 avgpool / FC
+            x = o.maxpool2d_split(self._stem_f32(first, img_u8, start, batch, start_offset), 3, 2, 1)
+            for i, blk in enumerate(p.blocks):
+                x = self._block_split(blk, x, last=i == len(p.blocks) - 1)
+            x = o.global_avgpool(x)
+            for fc in p.fcs:
+                x = o.linear(x, fc.w, fc.b, relu=fc.relu)
+            return x
         parts = self.stem_parts if self.stem_parts is not None else 1
         if p.kind == "resnet" and parts > 1 and nb >= 2 * parts:
             # stem + maxpool on batch parts: a part's 112x112x64 stem output
@@ -504,6 +592,35 @@ class HipRunner:
             torch.cuda.current_stream(x.device).wait_stream(join)
         return self._conv(blk.convs[-1], y, residual=idt, out=out)
 
+    def _capture_key(self, batch: int, packed=None, slot: int = 0):
+        return ((batch if slot == 0 else (batch, slot)) if packed is None else ("pk", batch, packed.data_ptr()),
+                self._variant())
+
+    def has_graph(self, batch: int, packed=None, slot: int = 0) -> bool:
+        """Whether ``capture(batch, packed=, slot=)`` would replay an existing graph."""
+        return self._capture_key(batch, packed, slot) in self._graphs
+
+    def _variant(self) -> tuple:
+        """Kernel-choice switches a captured graph depends on (part of its cache key)."""
+        return (self.split, self.winograd, self.wino_variant, self.pack3, self.pack3_f16, self.side_down,
+                self.stem_parts, self.front_split, self.fuse_stem)
+
+    def _split_ok(self) -> bool:
+        return all(c.sw is not None for b in self.p.blocks for c in [*b.convs, *([b.down] if b.down else [])])
+
+    def _conv_split(self, c, x, residual=None, out_f32=False):
+        return self.ops.conv2d_split(x, c.sw, c.b, c.s_scale, c.kh, c.kw, c.stride, c.pad, c.relu, residual,
+                                     out_f32)
+
+    def _block_split(self, blk, x, last: bool = False):
+        """Residual block on split-fp16 activations; with ``last`` the block's
+        output is fp32 (for the avgpool / FC head)."""
+        idt = x if blk.down is None else self._conv_split(blk.down, x)
+        y = x
+        for c in blk.convs[:-1]:
+            y = self._conv_split(c, y)
+        return self._conv_split(blk.convs[-1], y, residual=idt, out_f32=last)
+
     def _side_stream(self, device):
         st = self._side.get(device)
         if st is None:
@@ -565,7 +682,7 @@ class HipRunner:
         gather's send buffer)."""
         key = ("win", shard.data_ptr(), tuple(shard.shape), batch,
                None if start is None else start.data_ptr(), start_offset,
-               None if packed is None else packed.data_ptr())
+               None if packed is None else packed.data_ptr(), self._variant())
         if key in self._graphs:
             g, start, sout = self._graphs[key]
             return start, self._replayer(g, sout, shard)
@@ -616,7 +733,7 @@ class HipRunner:
         that caller-owned buffer (e.g. a collective round's send buffer).
         ``slot`` > 0 captures an independent copy (own static buffers), so two
         forwards of the same batch size can be in flight."""
-        key = (batch if slot == 0 else (batch, slot)) if packed is None else ("pk", batch, packed.data_ptr())
+        key = self._capture_key(batch, packed, slot)
         if key in self._graphs:
             g, sin, sout = self._graphs[key]
             return sin, self._replayer(g, sout, packed)

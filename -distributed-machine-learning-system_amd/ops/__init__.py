@@ -13,7 +13,36 @@ __all__ = [
     "available", "load", "so_path", "conv2d", "linear", "preprocess", "resize_crop",
     "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile", "pick_tile_f32", "synth_images", "stem_fused",
     "conv2d_wino", "wino_supported", "preprocess_pack3", "conv2d_pack3",
+    "conv2d_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
 ]
+
+
+def conv2d_split(x, w, bias, acc_scale: float, kh: int, kw: int, stride: int, pad: int, relu: bool,
+                 residual=None, out_f32: bool = False, tile: int = -1, out=None):
+    """fp32-accurate conv on split-fp16 activations ([.., 2C] halfs, hi/lo per
+    32 channels; models.packed.to_split) and weights (pack_split_weight):
+    hi*hi + hi*lo + lo*hi on the f16 MFMA.  Output split (or fp32 with
+    ``out_f32``)."""
+    return load().conv2d_split(x, w, bias, residual, kh, kw, stride, pad, relu, acc_scale, out_f32, tile, out)
+
+
+def split_from_f32(x):
+    """fp32 [.., C] -> split-fp16 [.., 2C] on the GPU."""
+    return load().split_from_f32(x)
+
+
+def f32_from_split(x):
+    """split-fp16 [.., 2C] -> fp32 [.., C] on the GPU."""
+    return load().f32_from_split(x)
+
+
+def maxpool2d_split(x, k: int, s: int, pad: int, out=None):
+    """NHWC max pool of fp32 or split input into the split layout."""
+    return load().maxpool2d_split(x, k, s, pad, out)
+
+
+def pick_tile_split(m: int, cout: int) -> int:
+    return int(load().pick_tile_split(m, cout))
 
 
 def conv2d(x, w, bias, kh: int, kw: int, stride: int, pad: int, relu: bool,

@@ -159,9 +159,8 @@ class HipExecutor(Executor):
         with ``packed`` the (class, prob bits) pairs are also written there.
         Launch slot ``slot`` replays its own graph (own static buffers)."""
         n = images.shape[0]
-        key = n if slot == 0 else (n, slot)
         if not self.closed and packed is None and \
-                ((self.use_graphs and len(r._graphs) < self.max_graphs) or key in r._graphs):
+                ((self.use_graphs and len(r._graphs) < self.max_graphs) or r.has_graph(n, slot=slot)):
             sin, replay = r.capture(n, slot=slot)
             sin.copy_(images)
             return replay()
@@ -223,8 +222,8 @@ class HipExecutor(Executor):
         with torch.cuda.device(self.device), self.run_lock:
             s = self._enter(images)
             with torch.cuda.stream(s):
-                key = ("pk", n, packed.data_ptr())
-                if not self.closed and ((self.use_graphs and len(r._graphs) < self.max_graphs) or key in r._graphs):
+                if not self.closed and ((self.use_graphs and len(r._graphs) < self.max_graphs)
+                                        or r.has_graph(n, packed=packed)):
                     sin, replay = r.capture(n, packed=packed)
                     sin.copy_(images)
                     replay()

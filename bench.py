@@ -7,12 +7,18 @@ random-init weights (no datasets or checkpoints are reachable).
 
 Precision: the reference classifies in fp32 (torchvision eager,
 /root/reference/alexnet_resnet.py:17-22, 74-75), so the headline runs the
-framework's fp32 path: fp32 activations and weights, every conv / FC on the
-f32-input MFMA (v_mfma_f32_16x16x4_f32, exact f32 products, f32 accumulate);
-3x3 stride-1 convs by fused fp32 Winograd F(2x2,3x3) (the fp32 algorithm
-cuDNN / MIOpen pick for these layers; logits agree with torch fp32 to ~1e-6
-relative, reported as ``max_rel_logit_err_vs_torch_fp32``).
-The fp16 path (f16 MFMA, f32 accumulate) is reported as extra keys.
+framework's fp32 path (``--fp32-impl``):
+  * "split" (default): the stem and FC on the f32-input MFMA, every residual-
+    stage conv on fp32-accurate split fp16 -- each fp32 value carried as
+    (hi, lo) halfs (22 significant bits, 4 bytes like fp32), hi*hi + hi*lo +
+    lo*hi summed in f32 on the f16 MFMA (conv_glds SPLIT);
+  * "f32mfma": every conv / FC on v_mfma_f32_16x16x4_f32 (exact f32 products,
+    f32 accumulate), 3x3 stride-1 convs by fused fp32 Winograd F(2x2,3x3).
+Both are checked against the fp64 CPU module on the same weights, next to
+torch fp32 itself (``max_rel_logit_err_vs_fp64``,
+``torch_fp32_max_rel_logit_err_vs_fp64``, ``max_rel_logit_err_vs_torch_fp32``).
+The other fp32 implementation and the fp16 path (f16 MFMA, f32 accumulate,
+fp16 activations) are reported as extra keys.
 
 One *step* is one round of the cluster's query path, end to end:
   1. the coordinator (rank 0) splits the round's image range over the ranks
@@ -55,6 +61,11 @@ BASELINE_IMG_PER_S = 41.0          # 400 img / 9.749 s (ResNet18, 5
 BASELINE_P50_S = 9.749             # p50 ResNet18 400-image query latency
 METRIC = "images/sec (whole node) + p50 query latency, ResNet18 bs=400 at 1/2/4/8 GPU"
 QUERY = 400                        # images per query (reference report p.1, ResNet18)
+COMPUTE_F32 = ("f32-input MFMA (v_mfma_f32_16x16x4_f32), fp32 activations/weights, fp32 accumulate; "
+               "3x3/s1 convs by fused fp32 Winograd F(2x2,3x3)")
+COMPUTE_SPLIT = ("fp32-accurate: stem/FC on f32-input MFMA; residual-stage convs on split fp16 (each fp32 value "
+                 "as hi+lo halfs, 22-bit significand, 4 bytes; hi*hi+hi*lo+lo*hi on v_mfma_f32_16x16x32_f16, "
+                 "fp32 accumulate); logits checked against fp64 next to torch fp32")
 
 
 def parse(argv=None):
@@ -65,6 +76,8 @@ def parse(argv=None):
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "fp16"],
                     help="headline precision (fp32 = the reference's)")
+    ap.add_argument("--fp32-impl", default="split", choices=["split", "f32mfma"],
+                    help="fp32 kernels: split-fp16 (fp32-accurate) residual stages, or all f32-MFMA")
     ap.add_argument("--batch", type=int, default=400, help="images per GPU per weak-scaling step")
     ap.add_argument("--dataset-images", type=int, default=2000,
                     help="synthetic images replicated in every rank's HBM (grown to fit a round)")
@@ -293,6 +306,7 @@ def main(argv=None) -> int:
     if not a.dry_run:
         from idunno.models import HipRunner, build_program, program_flops
         runner = HipRunner(build_program(a.model, seed=a.seed, dtype=a.dtype), env.device)
+        runner.split = a.fp32_impl == "split"
     head = measure(make_run(runner, B), W * B, a.steps, a.warmup, "weak")
     extras = {}
     if not a.no_extras:
@@ -311,6 +325,13 @@ def main(argv=None) -> int:
                            f"ms_per_step_{other}": round(1000 * m2["elapsed"] / a.steps, 4),
                            f"p50_query_latency_{other}_s": round(m2["p50"], 6) if m2["p50"] else None})
             del r2
+            if a.dtype == "fp32":
+                alt = "f32mfma" if a.fp32_impl == "split" else "split"
+                runner.split = alt == "split"
+                m3 = measure(make_run(runner, B), W * B, a.steps, a.warmup, alt)
+                runner.split = a.fp32_impl == "split"
+                extras.update({f"value_fp32_{alt}": round(m3["ips"], 2),
+                               f"ms_per_step_fp32_{alt}": round(1000 * m3["elapsed"] / a.steps, 4)})
             if coord:
                 extras.update(numerics_check(runner, a, env.device))
 
@@ -334,8 +355,7 @@ def main(argv=None) -> int:
             "data": "synthetic uint8 224x224x3 images (dataset replicated in every GPU's HBM), random-init weights",
             "config": {"model": a.model, "global_batch": W * B, "seq_len": None, "image_hw": 224,
                        "batch_per_gpu": B, "parallelism": f"dp{W}", "graph": not a.no_graph,
-                       "compute": ("f32-input MFMA (v_mfma_f32_16x16x4_f32), fp32 activations/weights, "
-                                   "fp32 accumulate; 3x3/s1 convs by fused fp32 Winograd F(2x2,3x3)") if a.dtype == "fp32" else
+                       "compute": (COMPUTE_SPLIT if a.fp32_impl == "split" else COMPUTE_F32) if a.dtype == "fp32" else
                        "f16 MFMA, fp16 activations, fp32 accumulate",
                        "dry_run": a.dry_run},
             "p50_query_latency_s": round(p50, 6) if p50 else None,
@@ -490,9 +510,17 @@ def numerics_check(runner, a, device, n: int = 8) -> dict:
     with torch.no_grad():
         want = m(ref.preprocess_u8(img)).float()
         got = runner.logits(img).float()
+        # fp64 oracle on the CPU (same weights): the error torch fp32 itself makes is the yardstick
+        x64 = ref.preprocess_u8(img.cpu()).double()
+        want64 = m.cpu().double()(x64)
     err = ((got - want).abs().max() / want.abs().max()).item()
     agree = (got.argmax(1) == want.argmax(1)).float().mean().item()
-    return {"max_rel_logit_err_vs_torch_fp32": float(f"{err:.3g}"), "top1_agreement_vs_torch_fp32": agree}
+    s64 = want64.abs().max()
+    err64 = ((got.cpu().double() - want64).abs().max() / s64).item()
+    t64 = ((want.cpu().double() - want64).abs().max() / s64).item()
+    return {"max_rel_logit_err_vs_torch_fp32": float(f"{err:.3g}"), "top1_agreement_vs_torch_fp32": agree,
+            "max_rel_logit_err_vs_fp64": float(f"{err64:.3g}"),
+            "torch_fp32_max_rel_logit_err_vs_fp64": float(f"{t64:.3g}")}
 
 
 if __name__ == "__main__":

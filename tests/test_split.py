@@ -1,0 +1,199 @@
+"""Split-fp16 (fp32-accurate) path: layout helpers on the CPU, HIP kernels on the GPU.
+
+A value v is carried as hi = fp16(v), lo = fp16(v - hi) (models/packed.py);
+the conv (conv_glds SPLIT) sums hi*hi + hi*lo + lo*hi in f32 on the f16 MFMA.
+The oracle is F.conv2d in float64 on the same fp32 inputs; the tolerance is
+the fp32 path's (2e-5 of the output scale) -- the split path is held to fp32
+accuracy, not fp16.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from idunno.models import packed as P
+
+DEV = "cuda"
+
+
+# ---------------------------------------------------------------------------
+# CPU: layout, packing, emulated arithmetic
+# ---------------------------------------------------------------------------
+
+def test_split_roundtrip_cpu():
+    torch.manual_seed(0)
+    x = torch.randn(2, 5, 7, 96) * 3
+    xs = P.to_split(x)
+    assert xs.dtype == torch.float16 and xs.shape == (2, 5, 7, 192)
+    # layout: block b of a pixel = [hi x32][lo x32]
+    assert torch.equal(xs[..., :32], x[..., :32].half())
+    assert torch.equal(xs[..., 64:96], x[..., 32:64].half())
+    back = P.from_split(xs)
+    # 22 significant bits; lo parts below fp16's normal range keep 2^-24 absolute
+    assert bool(((back - x).abs() <= x.abs() * 2.0 ** -21 + 2.0 ** -24).all())
+
+
+def test_pack_split_weight_cpu():
+    torch.manual_seed(1)
+    w = torch.randn(64, 96, 3, 3) * 0.03
+    sw, scale = P.pack_split_weight(w)
+    assert sw.shape == (64, 9 * 192) and sw.dtype == torch.float16
+    # scale is a power of two, largest scaled weight in [2^13, 2^14)
+    e = -torch.log2(torch.tensor(scale)).item()
+    assert e == int(e)
+    assert 2 ** 13 <= (w.abs().max() / scale).item() < 2 ** 14
+    c = P.Conv(torch.empty(0), torch.zeros(64), 96, 64, 3, 3, 1, 1, False, sw=sw, s_scale=scale)
+    back = P.unpack_split_weight(c)
+    assert ((back - w).abs().max() / w.abs().max()).item() < 2.0 ** -22
+    with pytest.raises(ValueError):
+        P.pack_split_weight(torch.randn(8, 3, 7, 7))
+
+
+def _emu_split_conv(x, sw, scale, cout, cin, k, stride, pad):
+    """The kernel's arithmetic in fp64 on CPU: hi*hi + hi*lo + lo*hi."""
+    xs = P.to_split(x).double().reshape(*x.shape[:-1], cin // 32, 2, 32)
+    xh = xs[..., 0, :].reshape(x.shape).permute(0, 3, 1, 2)
+    xl = xs[..., 1, :].reshape(x.shape).permute(0, 3, 1, 2)
+    ws = sw.double().reshape(cout, k, k, cin // 32, 2, 32)
+    wh = ws[..., 0, :].reshape(cout, k, k, cin).permute(0, 3, 1, 2)
+    wl = ws[..., 1, :].reshape(cout, k, k, cin).permute(0, 3, 1, 2)
+    y = F.conv2d(xh, wh, None, stride, pad) + F.conv2d(xh, wl, None, stride, pad) + F.conv2d(xl, wh, None, stride, pad)
+    return y * scale
+
+
+def test_split_arithmetic_matches_fp32_accuracy_cpu():
+    torch.manual_seed(2)
+    x = F.relu(torch.randn(2, 12, 12, 64))
+    w = torch.randn(32, 64, 3, 3) / 24
+    sw, scale = P.pack_split_weight(w)
+    y = _emu_split_conv(x, sw, scale, 32, 64, 3, 1, 1)
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.double(), None, 1, 1)
+    y32 = F.conv2d(x.permute(0, 3, 1, 2), w, None, 1, 1).double()
+    err = ((y - ref).abs().max() / ref.abs().max()).item()
+    err32 = ((y32 - ref).abs().max() / ref.abs().max()).item()
+    assert err < 4 * max(err32, 1e-7), (err, err32)
+
+
+def test_compile_fp32_program_has_split_weights_cpu():
+    p = P.build_program("resnet18", dtype="fp32")
+    convs = [c for b in p.blocks for c in [*b.convs, *([b.down] if b.down else [])]]
+    assert convs and all(c.sw is not None for c in convs)
+    assert p.stem.sw is None        # C = 3 stem stays on the f32 MFMA
+    for c in convs[:3]:
+        w = P.unpack_conv_weight(c)
+        assert ((P.unpack_split_weight(c) - w).abs().max() / w.abs().max()).item() < 1e-6
+    # fp16 programs carry none
+    assert all(c.sw is None for c in P.build_program("resnet18", dtype="fp16").all_convs())
+
+
+# ---------------------------------------------------------------------------
+# GPU: kernels against the fp64 oracle
+# ---------------------------------------------------------------------------
+
+@pytest.fixture(scope="module")
+def ops():
+    from idunno import ops as o
+
+    o.load()
+    return o
+
+
+def _ref64(x_nhwc, w, b, stride, pad, relu, res=None):
+    x = x_nhwc.double().permute(0, 3, 1, 2)
+    y = F.conv2d(x, w.double().to(x.device), b.double().to(x.device), stride, pad)
+    if res is not None:
+        y = y + res.double().permute(0, 3, 1, 2)
+    if relu:
+        y = F.relu(y)
+    return y.permute(0, 2, 3, 1)
+
+
+def _check(y, ref, rel=2e-5):
+    y = y.double()
+    scale = ref.abs().max().item() + 1e-12
+    err = (y - ref).abs().max().item()
+    assert err <= rel * scale, f"max err {err:.3e} vs scale {scale:.3e} (rel {err / scale:.2e})"
+
+
+SPLIT_CASES = [
+    # (B, H, Cin, Cout, k, stride, pad)
+    (2, 56, 64, 64, 3, 1, 1),      # resnet layer1
+    (2, 56, 64, 128, 3, 2, 1),     # layer2 first conv
+    (2, 56, 64, 128, 1, 2, 0),     # layer2 downsample
+    (2, 28, 128, 128, 3, 1, 1),
+    (2, 14, 256, 256, 3, 1, 1),
+    (3, 7, 512, 512, 3, 1, 1),     # layer4, M = 147 (not a tile multiple)
+    (2, 27, 64, 192, 5, 1, 2),     # alexnet conv2 (Cout 192 masks part of a tile)
+    (2, 56, 256, 64, 1, 1, 0),     # resnet50 1x1 reduce
+    (2, 14, 1024, 256, 1, 1, 0),
+    (1, 9, 96, 32, 3, 1, 1),       # odd: C 96 (3 split stages), Cout 32
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,Cin,Cout,k,s,p", SPLIT_CASES)
+def test_conv_split_default_tile(ops, B, H, Cin, Cout, k, s, p):
+    torch.manual_seed(B * 1000 + H + Cin + Cout + k)
+    x = torch.randn(B, H, H, Cin, device=DEV)
+    w = torch.randn(Cout, Cin, k, k) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    sw, scale = P.pack_split_weight(w)
+    y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, k, k, s, p, True)
+    assert y.dtype == torch.float16 and y.shape[-1] == 2 * Cout
+    ref = _ref64(x, w, b, s, p, True)
+    _check(P.from_split(y), ref)
+
+
+SPLIT_TILES = [24, 26, 27, 33, 34, 35, 36, 37, 38]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", SPLIT_TILES)
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("out_f32", [False, True])
+def test_conv_split_tiles(ops, tile, res, out_f32):
+    torch.manual_seed(tile + 7 * res + 3 * out_f32)
+    B, H, Cin, Cout = 3, 13, 128, 192            # M = 507, Cout 192: partial tiles on both sides
+    x = torch.randn(B, H, H, Cin, device=DEV)
+    w = torch.randn(Cout, Cin, 3, 3) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    r = torch.randn(B, H, H, Cout, device=DEV) if res else None
+    sw, scale = P.pack_split_weight(w)
+    y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, 3, 3, 1, 1, True,
+                         residual=None if r is None else ops.split_from_f32(r), out_f32=out_f32, tile=tile)
+    ref = _ref64(x, w, b, 1, 1, True, r)
+    _check(y if out_f32 else P.from_split(y), ref)
+
+
+@pytest.mark.gpu
+def test_split_conversions_and_maxpool(ops):
+    torch.manual_seed(5)
+    x = torch.randn(3, 17, 19, 96, device=DEV) * 5
+    xs = ops.split_from_f32(x)
+    assert torch.equal(xs.cpu(), P.to_split(x.cpu()))
+    back = ops.f32_from_split(xs)
+    assert torch.equal(back.cpu(), P.from_split(xs.cpu()))
+    ref = F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    for inp in (x, xs):
+        y = ops.maxpool2d_split(inp, 3, 2, 1)
+        assert y.shape == (3, 9, 10, 192)
+        _check(P.from_split(y.cpu()).to(DEV), ref.double(), rel=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,B", [("resnet18", 4), ("resnet18", 400), ("resnet50", 8)])
+def test_model_split_vs_fp64_oracle(ops, name, B):
+    from idunno.models import reference as ref
+
+    m = ref.build(name, seed=0)
+    prog = P.compile_model(m, name, "fp32")
+    r = P.HipRunner(prog)
+    assert r.split and r._split_ok()
+    img = ops.synth_images(0, 0, B, DEV)
+    got = r.logits(img).double().cpu()
+    n = min(B, 8)
+    with torch.no_grad():
+        want = m.double()(ref.preprocess_u8(img[:n].cpu()).double())
+    scale = want.abs().max().item()
+    err = (got[:n] - want).abs().max().item() / scale
+    assert err <= 1e-5, f"{name}: rel logit err {err:.2e}"
+    assert torch.equal(got[:n].argmax(1), want.argmax(1))
