@@ -557,6 +557,61 @@ torch::Tensor conv2d_pack3(torch::Tensor x3, torch::Tensor w, torch::Tensor bias
   return y;
 }
 
+// split-fp16 RGB stem on packed rows: x3 [B, H, 2*nc, wp] half (preprocess_pack3_split:
+// nc hi copies, then nc lo copies), w [Cout, nK * 64] half (models/packed.py
+// pack_split_weight_p3: per stage 32 K elements as [hi x32][lo x32]); fp32 output.
+torch::Tensor conv2d_pack3_split(torch::Tensor x3, torch::Tensor w, torch::Tensor bias, int64_t W, int64_t KH,
+                                 int64_t KW, int64_t stride, int64_t pad, bool relu, double acc_scale, int64_t tile) {
+  CHECK_DEV(x3);
+  CHECK_DEV(w);
+  CHECK_DEV(bias);
+  CHECK_CONTIG(x3);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(bias);
+  CHECK_DT(x3, torch::kHalf);
+  CHECK_DT(w, torch::kHalf);
+  CHECK_DT(bias, torch::kFloat);
+  TORCH_CHECK(x3.dim() == 4 && w.dim() == 2 && bias.dim() == 1, "bad ranks");
+  TORCH_CHECK(w.device() == x3.device() && bias.device() == x3.device(), "operands on different devices");
+  TORCH_CHECK(KH >= 1 && KW >= 5 && stride >= 1 && pad >= 0 && W >= 1, "pack3 stem geometry: KW >= 5");
+  int nc, wp, cpk;
+  pack3_geometry((int)W, (int)KW, (int)stride, (int)pad, 2, nc, wp, cpk);
+  TORCH_CHECK(nc <= 4, "pack3 stem: stride needs at most 4 row copies");
+  const int B = x3.size(0), H = x3.size(1);
+  TORCH_CHECK(x3.size(2) == 2 * nc && x3.size(3) == wp, "x3 must be [B, H, ", 2 * nc, ", ", wp,
+              "] (preprocess_pack3_split)");
+  const int Cout = w.size(0), Kpad = w.size(1);
+  const int nK = (KH * cpk + 3) / 4;                 // 4 input chunks (32 halfs) per split stage
+  TORCH_CHECK(Kpad == nK * 64, "split pack3 weight must be [Cout, ", nK * 64, "]");
+  TORCH_CHECK(bias.size(0) == Cout && Cout % 64 == 0, "bias/Cout mismatch or Cout % 64");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = ((int)W + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty output");
+  const long M = (long)B * Ho * Wo;
+  TORCH_CHECK(M < (1L << 31) && (long)B * H * 2 * nc * wp < (1L << 31) && M * Cout < (1L << 31),
+              "tensor too large for int32 indexing");
+  auto y = torch::empty({B, Ho, Wo, Cout}, x3.options().dtype(torch::kFloat));
+  if (M == 0) return y;
+  ConvArgs a{};
+  a.x = reinterpret_cast<const half_t*>(x3.data_ptr());
+  a.w = reinterpret_cast<const half_t*>(w.data_ptr());
+  a.bias = bias.data_ptr<float>();
+  a.res = nullptr;
+  a.y = y.data_ptr();
+  a.B = B; a.H = H; a.W = (int)W; a.C = 3;
+  a.Ho = Ho; a.Wo = Wo; a.Cout = Cout; a.ldy = Cout;
+  a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
+  a.M = (int)M;
+  a.Kpad = Kpad;
+  a.relu = relu ? 1 : 0;
+  a.acc_scale = (float)acc_scale;
+  a.nc = nc; a.wp = wp; a.cpk = cpk;
+  a.zero = zero_buffer(x3.device()).data_ptr();
+  const int t = tile >= 0 ? (int)tile : 27;
+  TORCH_CHECK(conv_glds_split_p3_launch(a, t, cur_stream()), "unsupported split pack3 tile id ", t);
+  check_launch("conv_glds_split_pack3");
+  return y;
+}
+
 static int g_wino_ablate_host = 0;
 static void set_wino_ablation_host(int64_t mode) {
   g_wino_ablate_host = (int)mode;
@@ -753,6 +808,44 @@ torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias,
   return y;
 }
 
+// uint8 [B,H,W,3] -> split-fp16 [B,Hp,Wp,128] = maxpool3x3/2(relu(conv7x7/2(normalise(img)) + bias)),
+// fp32-accurate; w = [2, 64, 7*32] half (models/packed.py pack_stem_split), acc_scale = 2^-e
+torch::Tensor stem_split(torch::Tensor img, torch::Tensor w, torch::Tensor bias, double acc_scale,
+                         c10::optional<torch::Tensor> start, int64_t batch, int64_t start_offset, int64_t window,
+                         int64_t sub) {
+  CHECK_DEV(img);
+  CHECK_DEV(w);
+  CHECK_DEV(bias);
+  CHECK_CONTIG(img);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(bias);
+  CHECK_DT(img, torch::kUInt8);
+  CHECK_DT(w, torch::kHalf);
+  CHECK_DT(bias, torch::kFloat);
+  TORCH_CHECK(w.device() == img.device() && bias.device() == img.device(), "operands on different devices");
+  TORCH_CHECK(img.dim() == 4 && img.size(3) == 3, "img must be [B, H, W, 3] uint8");
+  TORCH_CHECK(w.dim() == 3 && w.size(0) == 2 && w.size(1) == 64 && w.size(2) == 7 * 32,
+              "split stem weight must be [2, 64, 7*32]");
+  TORCH_CHECK(bias.numel() == 64, "bias must have 64 entries");
+  const int H = img.size(1), W = img.size(2);
+  int B;
+  long long max_start;
+  const long long* sp = window_args(img, start, batch, window, sub, B, max_start);
+  TORCH_CHECK(H >= 7 && W >= 7, "image too small");
+  TORCH_CHECK((long)B * H * W * 3 < (1L << 31), "batch too large");
+  const int Hc = (H + 6 - 7) / 2 + 1, Wc = (W + 6 - 7) / 2 + 1;
+  const int Hp = (Hc + 2 - 3) / 2 + 1, Wp = (Wc + 2 - 3) / 2 + 1;
+  TORCH_CHECK((long)B * Hp * Wp * 128 < (1L << 31), "batch too large");
+  auto y = torch::empty({B, Hp, Wp, 128}, img.options().dtype(torch::kHalf));
+  if (B) {
+    stem_split_launch(img.data_ptr<uint8_t>(), reinterpret_cast<const half_t*>(w.data_ptr()), bias.data_ptr<float>(),
+                      (float)acc_scale, reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp, start_offset, max_start,
+                      sp ? sub : 0, cur_stream());
+    check_launch("stem_split");
+  }
+  return y;
+}
+
 torch::Tensor preprocess(torch::Tensor img, c10::optional<torch::Tensor> start, int64_t batch, int64_t start_offset,
                          int64_t window, int64_t sub, bool f32) {
   CHECK_DEV(img);
@@ -803,6 +896,31 @@ torch::Tensor preprocess_pack3(torch::Tensor img, int64_t KW, int64_t stride, in
     preprocess_pack3_f32_launch(img.data_ptr<uint8_t>(), out.data_ptr<float>(), B, H, W, (int)pad, nc, wp, sp,
                                 start_offset, max_start, sp ? sub : 0, cur_stream());
   check_launch("preprocess_pack3_f32");
+  return out;
+}
+
+// uint8 HWC -> split-fp16 packed-row stem input [B, H, 2*nc, wp] (hi copies, lo copies)
+torch::Tensor preprocess_pack3_split(torch::Tensor img, int64_t KW, int64_t stride, int64_t pad,
+                                     c10::optional<torch::Tensor> start, int64_t batch, int64_t start_offset,
+                                     int64_t window, int64_t sub) {
+  CHECK_DEV(img);
+  CHECK_CONTIG(img);
+  CHECK_DT(img, torch::kUInt8);
+  TORCH_CHECK(img.dim() == 4 && img.size(3) == 3, "img must be [B, H, W, 3] uint8");
+  TORCH_CHECK(KW >= 5 && stride >= 1 && pad >= 0, "pack3 stem geometry: KW >= 5");
+  int B;
+  long long max_start;
+  const long long* sp = window_args(img, start, batch, window, sub, B, max_start);
+  const int H = img.size(1), W = img.size(2);
+  int nc, wp, cpk;
+  pack3_geometry(W, (int)KW, (int)stride, (int)pad, 2, nc, wp, cpk);
+  TORCH_CHECK(nc <= 4, "pack3 stem: stride needs at most 4 row copies");
+  TORCH_CHECK((long)B * H * 2 * nc * wp < (1L << 31), "tensor too large for int32 indexing");
+  auto out = torch::empty({B, H, 2 * nc, wp}, img.options().dtype(torch::kHalf));
+  if (B == 0) return out;
+  preprocess_pack3_split_launch(img.data_ptr<uint8_t>(), reinterpret_cast<half_t*>(out.data_ptr()), B, H, W,
+                                (int)pad, nc, wp, sp, start_offset, max_start, sp ? sub : 0, cur_stream());
+  check_launch("preprocess_pack3_split");
   return out;
 }
 
@@ -923,6 +1041,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("acc_scale"), py::arg("out_f32") = false, py::arg("tile") = -1,
         py::arg("out") = py::none());
+  m.def("conv2d_pack3_split", &conv2d_pack3_split, "split-fp16 RGB stem conv on packed rows, fp32 out",
+        py::arg("x3"), py::arg("w"), py::arg("bias"), py::arg("W"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
+        py::arg("pad"), py::arg("relu"), py::arg("acc_scale"), py::arg("tile") = -1);
+  m.def("preprocess_pack3_split", &preprocess_pack3_split, "uint8 HWC -> split-fp16 packed-row stem input",
+        py::arg("img"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("start") = py::none(),
+        py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1, py::arg("sub") = 0);
+  m.def("stem_split", &stem_split, "fp32-accurate fused split-fp16 ResNet stem (normalise+conv7x7/2+relu+maxpool)",
+        py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("acc_scale"), py::arg("start") = py::none(),
+        py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1, py::arg("sub") = 0);
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");
   m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),

@@ -104,6 +104,10 @@ void preprocess_pack3_f32_launch(const uint8_t* img, float* out, int B, int H, i
 void preprocess_pack3_f16_launch(const uint8_t* img, half_t* out, int B, int H, int W, int pad, int nc, int wp,
                                  const long long* start_idx, long long start_off, long long max_start,
                                  long long sub, hipStream_t st);
+// split-fp16 packed rows [B][H][2][nc][wp] (plane 0 hi, plane 1 lo) for conv_glds P3+SPLIT
+void preprocess_pack3_split_launch(const uint8_t* img, half_t* out, int B, int H, int W, int pad, int nc, int wp,
+                                   const long long* start_idx, long long start_off, long long max_start,
+                                   long long sub, hipStream_t st);
 void preprocess_f32_launch(const uint8_t* img, float* out, long npix, const long long* start_idx,
                            long long start_off, long long max_start, long long sub, long pix_per_img,
                            hipStream_t st);
@@ -122,7 +126,9 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 // split fp16 (fp32-accurate) implicit-GEMM conv: x/res/y are split-format halfs
 // ([hi x32][lo x32] per 32 channels), y fp32 with out_f32
 bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
-int conv_glds_split_pick(int M, int Cout);   // a.cpk > 0: pack3 stem
+int conv_glds_split_pick(int M, int Cout);
+// split-fp16 RGB stem on packed rows (a.cpk > 0, x from preprocess_pack3_split): fp32 output
+bool conv_glds_split_p3_launch(ConvArgs a, int tile, hipStream_t st);   // a.cpk > 0: pack3 stem
 bool conv_big_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 bool conv_pers_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);   // false: shape unsupported
 bool conv3x3_patch_supported(int H, int W, int C, int Cout);
@@ -134,6 +140,11 @@ void conv3x3_c64_launch(const half_t* x, const half_t* w, const float* bias, con
 void conv3x3_patch_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
                           const void* zero, int B, int H, int W, int C, int Cout, int relu, hipStream_t st);
 int conv_glds_pick(int M, int Cout);
+// split-fp16 (fp32-accurate) fused stem: w = [2][64][7*32] (hi, lo; pre-scaled by
+// 1/acc_scale), y = split layout [B][Hp][Wp][128]
+void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, float acc_scale, half_t* y, int B,
+                       int H, int W, const long long* start_idx, long long start_off, long long max_start,
+                       long long sub, hipStream_t st);
 void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, half_t* y, int B, int H, int W,
                        const long long* start_idx, long long start_off, long long max_start, long long sub,
                        hipStream_t st);

@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
   // of wider rows when the caller splits K, e.g. linear_splitk)
   const int ldx = a.ldx ? a.ldx : a.C;
   int b_base[GB], b_ih0[GB], b_iw0[GB], b_ch[GB];
-  const int prow = a.nc * a.wp;                       // P3: halfs per image row (all copies)
+  const int prow = a.nc * a.wp * (SPLIT ? 2 : 1);     // P3: halfs per image row (all copies, both planes)
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int row = (wave + NW * j) * RPI + lrow;
@@ -148,11 +148,20 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
     for (int j = 0; j < GB; ++j) {
       if constexpr (P3) {
         // this lane's chunk of stage i_s: flat chunk q = i_s*CPR + ch over (kh, chunk)
-        const int q = i_s * CPR + b_ch[j] / 8;
+        // SPLIT: chunks 0-3 of a stage are the hi plane's flat chunks
+        // 4*i_s .. +3, chunks 4-7 the lo plane's same chunks
+        int q, poff = 0;
+        if constexpr (SPLIT) {
+          const int cc = b_ch[j] / 8;
+          q = i_s * 4 + (cc & 3);
+          poff = (cc >> 2) * a.nc * a.wp;
+        } else {
+          q = i_s * CPR + b_ch[j] / 8;
+        }
         const int kh = q / a.cpk, jj = q - kh * a.cpk;
         const int ih = b_ih0[j] + kh;
         const bool ok = kh < a.KH && (unsigned)ih < (unsigned)a.H;
-        const half_t* src = ok ? xin + b_base[j] + ih * prow + 8 * jj : zero;
+        const half_t* src = ok ? xin + b_base[j] + ih * prow + 8 * jj + poff : zero;
         __builtin_amdgcn_global_load_lds((glb_void_t*)src,
                                          (lds_void_t*)(base + A_BYTES + (wave + NW * j) * 1024), 16, 0, 0);
         continue;
@@ -185,24 +194,21 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
   // retire them long before the epilogue, whose own load would otherwise expose
   // a full memory latency per tile (30 us of 138 on ResNet layer2 conv2,
   // profiles/r1_v8_conv_big_sweep.log)
+  //
+  // SPLIT loads its residual (hi and lo: twice the registers) only after the
+  // main loop instead: held across the loop it took the 128x128 8-wave tile
+  // from 112 to 140 VGPRs, one block per CU instead of two, +25-50 % time.
   half4v rv[HAS_RES ? FN : 1][HAS_RES ? FM : 1];
   half4v rl[HAS_RES && SPLIT ? FN : 1][HAS_RES && SPLIT ? FM : 1];   // SPLIT: residual lo parts
-  if constexpr (HAS_RES) {
+  if constexpr (HAS_RES && !SPLIT) {
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
       const int n = n0 + wn * TN + i * 16 + (lane >> 4) * 4;
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
         const int m = m0 + wm * TM + j * 16 + (lane & 15);
-        const bool ok = m < a.M && n < a.Cout;
-        if constexpr (SPLIT) {
-          const size_t off = ok ? (size_t)m * 2 * a.Cout + split_off(n) : 0;
-          rv[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : gload_b64_untracked(a.res + off);
-          rl[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : gload_b64_untracked(a.res + off + 32);
-        } else {
-          const size_t off = ok ? (size_t)m * a.Cout + n : 0;
-          rv[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : gload_b64_untracked(a.res + off);
-        }
+        const size_t off = (m < a.M && n < a.Cout) ? (size_t)m * a.Cout + n : 0;
+        rv[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : gload_b64_untracked(a.res + off);
       }
     }
   }
@@ -289,15 +295,30 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
   }
 
   // ---- epilogue: bias (+residual) (+ReLU), NHWC store --------------------
-  if constexpr (HAS_RES) {
+  if constexpr (HAS_RES && SPLIT) {
+    // the ring is drained (last wait was vmcnt(0)): ordinary tracked loads
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int n = n0 + wn * TN + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int m = m0 + wm * TM + j * 16 + (lane & 15);
+        const size_t off = (m < a.M && n < a.Cout) ? (size_t)m * 2 * a.Cout + split_off(n) : 0;
+        if (a.ablate & 2) {
+          rv[i][j] = half4v{0, 0, 0, 0};
+          rl[i][j] = half4v{0, 0, 0, 0};
+        } else {
+          rv[i][j] = *reinterpret_cast<const half4v*>(a.res + off);
+          rl[i][j] = *reinterpret_cast<const half4v*>(a.res + off + 32);
+        }
+      }
+    }
+  } else if constexpr (HAS_RES) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (already retired by the ring's last wait)
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
-      for (int j = 0; j < FM; ++j) {
-        reg_tie(rv[i][j]);
-        if constexpr (SPLIT) reg_tie(rl[i][j]);
-      }
+      for (int j = 0; j < FM; ++j) reg_tie(rv[i][j]);
   }
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
@@ -361,7 +382,8 @@ static void glds_cfg(ConvArgs a, hipStream_t st) {
   a.tiles_m = (a.M + BM - 1) / BM;
   if (P3) {
     a.cblk = 1;
-    a.nK = (a.KH * a.cpk + BK / 8 - 1) / (BK / 8);
+    const int cps = SPLIT ? BK / 16 : BK / 8;          // input chunks per stage (SPLIT: hi + lo of 4)
+    a.nK = (a.KH * a.cpk + cps - 1) / cps;
   } else {
     a.cblk = a.C / BK;
     a.nK = a.KH * a.KW * a.cblk;
@@ -463,6 +485,18 @@ bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) 
 int conv_glds_split_pick(int M, int Cout) {
   if (Cout % 128 == 0) return M >= 50000 ? 36 : 34;
   return 27;
+}
+
+bool conv_glds_split_p3_launch(ConvArgs a, int tile, hipStream_t st) {
+  if (a.res != nullptr || a.cpk <= 0) return false;
+  switch (tile) {
+    case 23: glds_cfg<64, 64, 64, 2, 2, 3, false, true, true, true>(a, st); return true;
+    case 27: glds_cfg<64, 128, 64, 1, 4, 2, false, true, true, true>(a, st); return true;
+    case 33: glds_cfg<64, 256, 64, 1, 4, 2, false, true, true, true>(a, st); return true;
+    case 35: glds_cfg<64, 64, 64, 2, 2, 2, false, true, true, true>(a, st); return true;
+    case 37: glds_cfg<64, 128, 64, 1, 8, 2, false, true, true, true>(a, st); return true;
+    default: return false;
+  }
 }
 
 bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {

@@ -60,7 +60,9 @@ __global__ void preprocess_f32_kernel(const uint8_t* __restrict__ img, float* __
 // Ek-pad .., loaded once (aligned dwords realigned with v_alignbyte away from
 // the row ends) and normalised through an LDS table of the 256 x 3 byte values
 // (same arithmetic as preprocess_f32, one division per table entry).
-template <typename T, int NC>
+// SPLIT (T = half): split-fp16 stem input [b][y][2][c][wp]: plane 0 = hi =
+// fp16(v), plane 1 = lo = fp16(v - hi) of the same copies (conv_glds P3+SPLIT).
+template <typename T, int NC, bool SPLIT = false>
 __global__ void __launch_bounds__(256) preprocess_pack3_kernel(
     const uint8_t* __restrict__ img, T* __restrict__ out, int B, int H, int W, int pad, int wp,
     const long long* __restrict__ start_idx, long long start_off, long long max_start, long long sub) {
@@ -116,6 +118,23 @@ __global__ void __launch_bounds__(256) preprocess_pack3_kernel(
   const int nch = min(3, (wp - 3 * E * k) / E);        // chunks of this group inside the row
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
+    if constexpr (SPLIT) {
+      T* dst = out + (r * 2 * NC + c) * wp + 3 * E * k;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        if (j >= nch) break;
+        half8v h, l;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = v[c * G + 8 * j + e];
+          h[e] = (half_t)x;
+          l[e] = (half_t)(x - (float)h[e]);
+        }
+        *reinterpret_cast<half8v*>(dst + 8 * j) = h;
+        *reinterpret_cast<half8v*>(dst + NC * wp + 8 * j) = l;
+      }
+      continue;
+    }
     T* dst = out + (r * NC + c) * wp + 3 * E * k;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -151,6 +170,16 @@ void preprocess_pack3_f32_launch(const uint8_t* img, float* out, int B, int H, i
                                  const long long* start_idx, long long start_off, long long max_start,
                                  long long sub, hipStream_t st) {
   pack3_launch<float>(img, out, B, H, W, pad, nc, wp, start_idx, start_off, max_start, sub, st);
+}
+
+void preprocess_pack3_split_launch(const uint8_t* img, half_t* out, int B, int H, int W, int pad, int nc, int wp,
+                                   const long long* start_idx, long long start_off, long long max_start,
+                                   long long sub, hipStream_t st) {
+  const long total = (long)B * H * ((wp + 23) / 24);
+  auto kern = nc == 4 ? preprocess_pack3_kernel<half_t, 4, true>
+              : nc == 2 ? preprocess_pack3_kernel<half_t, 2, true> : preprocess_pack3_kernel<half_t, 1, true>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, img, out, B, H, W, pad, wp,
+                     start_idx, start_off, max_start, sub);
 }
 
 void preprocess_pack3_f16_launch(const uint8_t* img, half_t* out, int B, int H, int W, int pad, int nc, int wp,

@@ -338,4 +338,230 @@ void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, h
                      max_start, sub);
 }
 
+// ============================================================================
+// Split-fp16 (fp32-accurate) fused stem: same tiling as stem_fused_kernel, for
+// the fp32 programs.  Every value is carried as hi + lo halfs (common.h
+// split_f16x4): the normalised patch is stored twice (hi plane, lo plane), the
+// weights come as hi and lo fragments pre-scaled by 2^e, and each K stage runs
+// hi*hi + hi*lo + lo*hi (3 f16 MFMAs).  The pool runs on the f32 accumulators
+// (DPP horizontal 3-max, f32 LDS tile for the vertical 3-max); the 2^-e scale,
+// bias and ReLU are applied after the max (all commute with it) and the
+// pooled result is written in the split layout [B][Hp][Wp][128 halfs].
+// Replaces preprocess_pack3_split + conv2d_pack3_split + maxpool_split (three
+// passes over ~3 GB at B = 400).
+namespace stem_s {
+constexpr int PLANE = stem::PATCH_BYTES;                  // lo plane follows the hi plane
+constexpr int PATCH2 = 2 * stem::PATCH_BYTES;             // 28704
+constexpr int HP_BYTES = stem::CRY * stem::PTX * 256;     // [conv row][pooled col][64 ch] f32 = 30464
+constexpr int LDS = PATCH2 + HP_BYTES;                    // 59168: 2 workgroups per CU
+constexpr int WGS = 2;
+}  // namespace stem_s
+
+// f32 tile offset of 4-channel chunk c (0..15) of (conv row r, pooled col px),
+// chunk XOR-swizzled by px
+__device__ __forceinline__ int hp32_off(int r, int px, int c) { return (r * stem::PTX + px) * 256 + ((c ^ px) << 4); }
+
+// registers -> normalised split patch (hi plane, lo plane) in LDS
+__device__ __forceinline__ void store_patch_split(char* patch, const StemGeom& g, int t, int tid, const Quads& q) {
+  using namespace stem;
+  int b, py0, px0;
+  tile_coords(g, t, b, py0, px0);
+  const int ixa = (px0 * PS - PP) * CS - CP - 3;
+#pragma unroll
+  for (int k = 0; k < QPT; ++k) {
+    const int i = tid + 256 * k;
+    if (i >= NQUAD) continue;
+    const int r = i / QPR, qc = i - r * QPR;
+    float f[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) f[j] = (float)((q.d[k][j >> 2] >> (8 * (j & 3))) & 0xFFu);
+    const int x0 = ixa + 4 * qc;
+    const bool edge = !(q.ok[k] && x0 >= 0 && x0 + 3 < g.W);
+    half4v ph[4], pl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float2v rg = float2v{f[3 * j], f[3 * j + 1]} * kScaleRG + kShiftRG;
+      const float bb = f[3 * j + 2] * kSB + kCB;
+      float4v v = float4v{rg[0], rg[1], bb, 0.f};
+      if (edge && (!q.ok[k] || (unsigned)(x0 + j) >= (unsigned)g.W)) v = float4v{0.f, 0.f, 0.f, 0.f};
+      split_f16x4(v, ph[j], pl[j]);
+    }
+    char* d = patch + (r * IPC + 4 * qc + PCO - 3) * 8;
+    *reinterpret_cast<half4v*>(d) = ph[0];
+    *reinterpret_cast<half8v*>(d + 8) = __builtin_shufflevector(ph[1], ph[2], 0, 1, 2, 3, 4, 5, 6, 7);
+    *reinterpret_cast<half4v*>(d + 24) = ph[3];
+    d += stem_s::PLANE;
+    *reinterpret_cast<half4v*>(d) = pl[0];
+    *reinterpret_cast<half8v*>(d + 8) = __builtin_shufflevector(pl[1], pl[2], 0, 1, 2, 3, 4, 5, 6, 7);
+    *reinterpret_cast<half4v*>(d + 24) = pl[3];
+  }
+}
+
+// f32 of lane l + N of the same 16-lane row (DPP row_shl:N)
+template <int N>
+__device__ __forceinline__ float row_shl_f32(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x100 | N, 0xF, 0xF, true));
+}
+
+__global__ void __launch_bounds__(256, stem_s::WGS)
+stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w, const float* __restrict__ bias,
+                  float acc_scale, half_t* __restrict__ y, const StemGeom g, const long long* __restrict__ start_idx,
+                  long long start_off, long long max_start, long long sub) {
+  using namespace stem;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (start_idx != nullptr) {
+    long long s = *start_idx - start_off;
+    s = (s < 0 ? 0 : (s > max_start ? max_start : s)) + sub;
+    img += (size_t)s * g.H * g.W * 3;
+  }
+  char* patch = smem;
+  char* hp = smem + stem_s::PATCH2;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  int t = blockIdx.x;
+  if (t >= g.ntiles) return;   // whole workgroup exits together (uniform)
+
+  Quads q;
+  load_quads(img, g, t, tid, q);
+
+  // ---- A fragments: hi and lo weights [2][cout][kh][32], registers, once ----
+  const int frow = lane & 15, fch = lane >> 4;
+  const int ch0 = (wave % NCH) * NIW;
+  half8v fah[KH][NIW], fal[KH][NIW];
+#pragma unroll
+  for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+    for (int i = 0; i < NIW; ++i) {
+      const size_t o = (size_t)((ch0 + i) * 16 + frow) * (KH * 32) + kh * 32 + fch * 8;
+      fah[kh][i] = *reinterpret_cast<const half8v*>(w + o);
+      fal[kh][i] = *reinterpret_cast<const half8v*>(w + 64 * KH * 32 + o);
+    }
+
+  store_patch_split(patch, g, t, tid, q);
+  int tn = t + gridDim.x;
+  if (tn < g.ntiles) load_quads(img, g, tn, tid, q);
+  __syncthreads();
+
+  // vertical-pool item: 8-channel chunk c8, pooled column vpx, pooled rows 2*vpy2, 2*vpy2+1
+  const int c8 = tid & 7, vpx = (tid >> 3) % PTX, vpy2 = tid / (8 * PTX);
+  float4v pb0 = float4v{0.f, 0.f, 0.f, 0.f}, pb1 = pb0;
+  if (tid < NVP) {
+    pb0 = *reinterpret_cast<const float4v*>(bias + c8 * 8);
+    pb1 = *reinterpret_cast<const float4v*>(bias + c8 * 8 + 4);
+  }
+  const int cx = frow;
+
+  while (true) {
+    int b, py0, px0;
+    tile_coords(g, t, b, py0, px0);
+    const int oy0 = py0 * PS - PP, ox0 = px0 * PS - PP;
+    const bool colv = cx < CRX && (unsigned)(ox0 + cx) < (unsigned)g.Wc;
+    const bool interior = ox0 >= 0 && ox0 + CRX <= g.Wc;
+
+    for (int f = wave / NCH; f < CRY; f += 4 / NCH) {
+      const char* pb = patch + ((2 * f) * IPC + 2 * cx + 2 * fch + PCO) * 8;
+      float4v acc[NIW];
+#pragma unroll
+      for (int i = 0; i < NIW; ++i) acc[i] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < KH; ++kh) {
+        const half8v bh = *reinterpret_cast<const half8v*>(pb + kh * IPC * 8);
+        const half8v bl = *reinterpret_cast<const half8v*>(pb + stem_s::PLANE + kh * IPC * 8);
+#pragma unroll
+        for (int i = 0; i < NIW; ++i) {
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[kh][i], bh, acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[kh][i], bl, acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh][i], bh, acc[i], 0, 0, 0);
+        }
+      }
+      // horizontal 3-max on the raw f32 accumulators; outside the image the
+      // conv output is the pool's -inf padding
+      float4v o[NIW];
+      const bool rowv = (unsigned)(oy0 + f) < (unsigned)g.Hc;   // wave-uniform
+#pragma unroll
+      for (int i = 0; i < NIW; ++i) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc[i][e];
+          if (!rowv || (!interior && !colv)) v = -INFINITY;
+          o[i][e] = fmaxf(v, fmaxf(row_shl_f32<1>(v), row_shl_f32<2>(v)));
+        }
+      }
+      if (!(cx & 1) && cx < 2 * PTX) {
+        const int px = cx >> 1;
+#pragma unroll
+        for (int i = 0; i < NIW; ++i)
+          *reinterpret_cast<float4v*>(hp + hp32_off(f, px, 4 * (ch0 + i) + fch)) = o[i];
+      }
+    }
+    __syncthreads();   // pooled-column tile complete; patch(t) no longer read
+
+    const int tnext = tn;
+    if (tnext < g.ntiles) {
+      store_patch_split(patch, g, tnext, tid, q);
+      tn = tnext + gridDim.x;
+      if (tn < g.ntiles) load_quads(img, g, tn, tid, q);
+    }
+
+    // ---- vertical 3-max over conv rows 4*vpy2 .. 4*vpy2+4 -> 2 pooled rows ----
+    if (tid < NVP) {
+      const int r0 = 4 * vpy2;
+      float4v a[5][2];
+#pragma unroll
+      for (int r = 0; r < 5; ++r) {
+        a[r][0] = *reinterpret_cast<const float4v*>(hp + hp32_off(r0 + r, vpx, 2 * c8));
+        a[r][1] = *reinterpret_cast<const float4v*>(hp + hp32_off(r0 + r, vpx, 2 * c8 + 1));
+      }
+      const int ox = px0 + vpx, oy = py0 + 2 * vpy2;
+      if (ox < g.Wp) {
+#pragma unroll
+        for (int hr = 0; hr < 2; ++hr) {
+          if (oy + hr >= g.Hp) break;
+          const int rr = 2 * hr;
+          float4v m0, m1;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            m0[e] = fmaxf(fmaxf(a[rr][0][e], a[rr + 1][0][e]), a[rr + 2][0][e]);
+            m1[e] = fmaxf(fmaxf(a[rr][1][e], a[rr + 1][1][e]), a[rr + 2][1][e]);
+            m0[e] = fmaxf(m0[e] * acc_scale + pb0[e], 0.f);
+            m1[e] = fmaxf(m1[e] * acc_scale + pb1[e], 0.f);
+          }
+          half4v h0, l0, h1, l1;
+          split_f16x4(m0, h0, l0);
+          split_f16x4(m1, h1, l1);
+          half_t* dst = y + (((size_t)b * g.Hp + oy + hr) * g.Wp + ox) * 128 + split_off(8 * c8);
+          *reinterpret_cast<half8v*>(dst) = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+          *reinterpret_cast<half8v*>(dst + 32) = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      }
+    }
+    __syncthreads();   // tile reads done; patch(tnext) visible
+    if (tnext >= g.ntiles) break;
+    t = tnext;
+  }
+}
+
+void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, float acc_scale, half_t* y, int B,
+                       int H, int W, const long long* start_idx, long long start_off, long long max_start,
+                       long long sub, hipStream_t st) {
+  using namespace stem;
+  StemGeom g;
+  g.B = B;
+  g.H = H;
+  g.W = W;
+  g.Hc = (H + 2 * CP - KH) / CS + 1;
+  g.Wc = (W + 2 * CP - KH) / CS + 1;
+  g.Hp = (g.Hc + 2 * PP - PK) / PS + 1;
+  g.Wp = (g.Wc + 2 * PP - PK) / PS + 1;
+  g.tiles_x = (g.Wp + PTX - 1) / PTX;
+  g.tiles_y = (g.Hp + PTY - 1) / PTY;
+  g.ntiles = B * g.tiles_x * g.tiles_y;
+  g.ablate = 0;
+  const int per = stem_s::WGS * device_cu_count();
+  const int grid = g.ntiles < per ? g.ntiles : per;
+  ensure_lds_attr(reinterpret_cast<const void*>(stem_split_kernel), stem_s::LDS);
+  hipLaunchKernelGGL(stem_split_kernel, dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias, acc_scale, y, g,
+                     start_idx, start_off, max_start, sub);
+}
+
 }  // namespace idunno

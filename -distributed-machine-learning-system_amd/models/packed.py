@@ -49,14 +49,18 @@ class Conv:
     wino: torch.Tensor | None = None   # fp32 3x3/s1: Winograd U = G g G^T [16, Cout, Cin]
     p3: torch.Tensor | None = None     # RGB stem on packed rows (pack_conv_weight_p3)
     sw: torch.Tensor | None = None     # fp32 programs: split-fp16 weights (pack_split_weight)
-    s_scale: float = 1.0               # accumulator scale of ``sw`` (2^-e)
+    s_scale: float = 1.0               # accumulator scale of ``sw`` / ``sp3`` (2^-e)
+    sp3: torch.Tensor | None = None    # fp32 RGB stems: split-fp16 packed-row weights (pack_split_weight_p3)
+    fs: torch.Tensor | None = None     # fp32 ResNet 7x7/2 stem: fused split stem weights (pack_stem_split)
 
     def to(self, device):
         return Conv(self.w.to(device), self.b.to(device), self.cin, self.cout, self.kh, self.kw,
                     self.stride, self.pad, self.relu, self.small,
                     None if self.wino is None else self.wino.to(device),
                     None if self.p3 is None else self.p3.to(device),
-                    None if self.sw is None else self.sw.to(device), self.s_scale)
+                    None if self.sw is None else self.sw.to(device), self.s_scale,
+                    None if self.sp3 is None else self.sp3.to(device),
+                    None if self.fs is None else self.fs.to(device))
 
     @property
     def flops_per_out_pixel(self) -> int:
@@ -243,14 +247,57 @@ def pack_split_weight(w: torch.Tensor) -> tuple[torch.Tensor, float]:
     cout, cin, kh, kw = w.shape
     if cin % SPLIT_BLOCK:
         raise ValueError(f"split weights need Cin % {SPLIT_BLOCK} == 0, got {cin}")
-    mx = float(w.abs().max())
-    e = 0 if mx == 0.0 else 14 - math.ceil(math.log2(mx))
+    e = _split_scale(w)
     ws = w.double().permute(0, 2, 3, 1) * (2.0 ** e)
     hi = ws.half()
     lo = (ws - hi.double()).half()
     blk = (cout, kh, kw, cin // SPLIT_BLOCK, 1, SPLIT_BLOCK)
     packed = torch.cat([hi.reshape(blk), lo.reshape(blk)], dim=4).reshape(cout, kh * kw * 2 * cin)
     return packed.contiguous(), 2.0 ** -e
+
+
+def _split_scale(w: torch.Tensor) -> int:
+    mx = float(w.abs().max())
+    return 0 if mx == 0.0 else 14 - math.ceil(math.log2(mx))
+
+
+def pack_split_weight_p3(w: torch.Tensor) -> tuple[torch.Tensor, float]:
+    """RGB stem [Cout, 3, KH, KW] -> split-fp16 packed-row weights (conv_glds
+    P3+SPLIT): K = (kh, f = 3*kw + c) over cpk = ceil(3*KW/8) 8-half chunks per
+    kernel row (preprocess_pack3_split's order), padded to whole stages of 32
+    K elements, each stage [hi x32][lo x32]; scaled by 2^e like pack_split_weight."""
+    cout, cin, kh, kw = w.shape
+    if cin != 3 or kw < 5:
+        raise ValueError("packed-row stems take 3 input channels and KW >= 5")
+    cpk = (3 * kw + 7) // 8
+    k = kh * cpk * 8
+    nk = (k + 31) // 32
+    rows = torch.zeros(cout, kh, 8 * cpk, dtype=torch.float64)
+    rows[:, :, :3 * kw] = w.double().permute(0, 2, 3, 1).reshape(cout, kh, 3 * kw)
+    flat = torch.zeros(cout, nk * 32, dtype=torch.float64)
+    flat[:, :k] = rows.reshape(cout, -1)
+    e = _split_scale(w)
+    flat = flat * (2.0 ** e)
+    hi = flat.half()
+    lo = (flat - hi.double()).half()
+    packed = torch.cat([hi.reshape(cout, nk, 1, 32), lo.reshape(cout, nk, 1, 32)], dim=2).reshape(cout, nk * 64)
+    return packed.contiguous(), 2.0 ** -e
+
+
+def pack_stem_split(w: torch.Tensor) -> tuple[torch.Tensor, float]:
+    """ResNet stem [64, 3, 7, 7] -> fused split stem weights [2, 64, 7*32] half
+    (hi, lo) for stem_split_kernel: per kernel row 8 taps x 4 channels (tap 7
+    and channel 3 zero), scaled by 2^e like pack_split_weight."""
+    cout, cin, kh, kw = w.shape
+    if (cout, cin, kh, kw) != (64, 3, 7, 7):
+        raise ValueError("the fused split stem takes a [64, 3, 7, 7] conv")
+    p = torch.zeros(cout, kh, 8, 4, dtype=torch.float64)
+    p[:, :, :kw, :cin] = w.double().permute(0, 2, 3, 1)
+    e = _split_scale(w)
+    p = p.reshape(cout, kh * 32) * (2.0 ** e)
+    hi = p.half()
+    lo = (p - hi.double()).half()
+    return torch.stack([hi, lo]).contiguous(), 2.0 ** -e
 
 
 def unpack_split_weight(c: "Conv") -> torch.Tensor:
@@ -288,8 +335,15 @@ def make_conv(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, relu: bool, dtype: str
                     wino_weight(w), None, sw, s_scale)
     p3 = pack_conv_weight_p3(w, dtype) if pack3_eligible(conv.in_channels, conv.kernel_size[1], conv.stride[0], dtype) \
         else None
+    sp3 = None
+    if dtype == "fp32" and pack3_eligible(conv.in_channels, conv.kernel_size[1], conv.stride[0], "fp16") \
+            and conv.out_channels % 64 == 0:
+        sp3, s_scale = pack_split_weight_p3(fold_bn_f64(conv.weight, conv.bias, bn)[0])
+    fs = None
+    if dtype == "fp32" and tuple(conv.weight.shape) == (64, 3, 7, 7) and conv.stride[0] == 2 and conv.padding[0] == 3:
+        fs, _ = pack_stem_split(fold_bn_f64(conv.weight, conv.bias, bn)[0])   # same 2^-e as sp3
     return Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, conv.kernel_size[0],
-                conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small, None, p3, sw, s_scale)
+                conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small, None, p3, sw, s_scale, sp3, fs)
 
 
 def make_fc(lin: nn.Linear, relu: bool, perm: torch.Tensor | None = None, dtype: str = "fp16") -> Conv:
@@ -501,9 +555,13 @@ class HipRunner:
         first = p.stem if p.kind == "resnet" else p.features[0][1]
         nb = batch if start is not None else img_u8.shape[0]
         if p.kind == "resnet" and self.split and self._split_ok():
-            # fp32 stem -> max pool straight into the split layout -> split
-            # residual stages (the last conv writes fp32) -> fp32 avgpool / FC
-            x = o.maxpool2d_split(self._stem_f32(first, img_u8, start, batch, start_offset), 3, 2, 1)
+            # fused split stem (uint8 -> normalise -> conv7x7/2 -> ReLU -> max
+            # pool, split out; or stem conv + max pool into the split layout)
+            # -> split residual stages (the last conv writes fp32) -> fp32 avgpool / FC
+            if self.fuse_stem and first.fs is not None and first.relu:
+                x = o.stem_split(img_u8, first.fs, first.b, first.s_scale, start, batch, start_offset)
+            else:
+                x = o.maxpool2d_split(self._stem_f32(first, img_u8, start, batch, start_offset), 3, 2, 1)
             for i, blk in enumerate(p.blocks):
                 x = self._block_split(blk, x, last=i == len(p.blocks) - 1)
             x = o.global_avgpool(x)
@@ -550,6 +608,12 @@ class HipRunner:
     def _stem_f32(self, first, img_u8, start, batch, start_offset, window: int = -1, sub: int = 0):
         """fp32 RGB stem conv (+ReLU) of a window / part of the images."""
         o = self.ops
+        if self.split and first.sp3 is not None:
+            # split-fp16 packed rows (fp32-accurate) on the f16 MFMA, fp32 output
+            x3 = o.preprocess_pack3_split(img_u8, first.kw, first.stride, first.pad, start, batch, start_offset,
+                                          window, sub)
+            return o.conv2d_pack3_split(x3, first.sp3, first.b, first.s_scale, img_u8.shape[2], first.kh, first.kw,
+                                        first.stride, first.pad, first.relu)
         if self.pack3 and first.p3 is not None:
             # packed rows: K 176 vs 224 for the 7x7/2, 400 vs 528 for the 11x11/4
             x3 = o.preprocess_pack3(img_u8, first.kw, first.stride, first.pad, start, batch, start_offset, window,

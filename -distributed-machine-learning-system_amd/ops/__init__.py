@@ -13,7 +13,7 @@ __all__ = [
     "available", "load", "so_path", "conv2d", "linear", "preprocess", "resize_crop",
     "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile", "pick_tile_f32", "synth_images", "stem_fused",
     "conv2d_wino", "wino_supported", "preprocess_pack3", "conv2d_pack3",
-    "conv2d_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
+    "conv2d_split", "stem_split", "preprocess_pack3_split", "conv2d_pack3_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
 ]
 
 
@@ -24,6 +24,27 @@ def conv2d_split(x, w, bias, acc_scale: float, kh: int, kw: int, stride: int, pa
     hi*hi + hi*lo + lo*hi on the f16 MFMA.  Output split (or fp32 with
     ``out_f32``)."""
     return load().conv2d_split(x, w, bias, residual, kh, kw, stride, pad, relu, acc_scale, out_f32, tile, out)
+
+
+def preprocess_pack3_split(img_u8, kw: int, stride: int, pad: int, start=None, batch: int = -1,
+                           start_offset: int = 0, window: int = -1, sub: int = 0):
+    """uint8 [B,H,W,3] -> split-fp16 packed-row stem input [B, H, 2*nc, wp]."""
+    return load().preprocess_pack3_split(img_u8, kw, stride, pad, start, batch, start_offset, window, sub)
+
+
+def conv2d_pack3_split(x3, w, bias, acc_scale: float, width: int, kh: int, kw: int, stride: int, pad: int,
+                       relu: bool, tile: int = -1):
+    """fp32-accurate RGB stem conv on split packed rows (conv_glds P3+SPLIT),
+    fp32 output; ``w``, ``acc_scale`` = models.packed.pack_split_weight_p3(w)."""
+    return load().conv2d_pack3_split(x3, w, bias, width, kh, kw, stride, pad, relu, acc_scale, tile)
+
+
+def stem_split(img_u8, w, bias, acc_scale: float, start=None, batch: int = -1, start_offset: int = 0,
+               window: int = -1, sub: int = 0):
+    """fp32-accurate fused ResNet stem on split fp16: uint8 [B,224,224,3] ->
+    split [B,56,56,128] (normalise, conv 7x7/2 + bias, ReLU, max pool 3x3/2);
+    ``w``, ``acc_scale`` = models.packed.pack_stem_split(w)."""
+    return load().stem_split(img_u8, w, bias, acc_scale, start, batch, start_offset, window, sub)
 
 
 def split_from_f32(x):

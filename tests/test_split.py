@@ -48,6 +48,28 @@ def test_pack_split_weight_cpu():
         P.pack_split_weight(torch.randn(8, 3, 7, 7))
 
 
+def _unpack_split_p3(sp3, scale, cout, kh, kw):
+    cpk = (3 * kw + 7) // 8
+    v = sp3.double().reshape(cout, -1, 2, 32)
+    flat = (v[:, :, 0] + v[:, :, 1]).reshape(cout, -1)[:, :kh * cpk * 8] * scale
+    return flat.reshape(cout, kh, 8 * cpk)[:, :, :3 * kw].reshape(cout, kh, kw, 3).permute(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("kh,kw", [(7, 7), (11, 11)])
+def test_pack_split_weight_p3_cpu(kh, kw):
+    torch.manual_seed(kh)
+    w = torch.randn(64, 3, kh, kw) * 0.05
+    sp3, scale = P.pack_split_weight_p3(w)
+    nk = (kh * ((3 * kw + 7) // 8) * 8 + 31) // 32
+    assert sp3.shape == (64, nk * 64) and sp3.dtype == torch.float16
+    back = _unpack_split_p3(sp3, scale, 64, kh, kw)
+    assert ((back - w.double()).abs().max() / w.abs().max()).item() < 2.0 ** -22
+    p = P.build_program("resnet18", dtype="fp32")
+    assert p.stem.sp3 is not None
+    assert P.build_program("alexnet", dtype="fp32").features[0][1].sp3 is not None
+    assert p.stem.fs is not None and p.stem.fs.shape == (2, 64, 224)
+
+
 def _emu_split_conv(x, sw, scale, cout, cin, k, stride, pad):
     """The kernel's arithmetic in fp64 on CPU: hi*hi + hi*lo + lo*hi."""
     xs = P.to_split(x).double().reshape(*x.shape[:-1], cin // 32, 2, 32)
@@ -162,6 +184,43 @@ def test_conv_split_tiles(ops, tile, res, out_f32):
                          residual=None if r is None else ops.split_from_f32(r), out_f32=out_f32, tile=tile)
     ref = _ref64(x, w, b, 1, 1, True, r)
     _check(y if out_f32 else P.from_split(y), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kh,stride,pad,B", [(7, 2, 3, 3), (11, 4, 2, 2)])
+@pytest.mark.parametrize("tile", [-1, 23, 27, 33, 35, 37])
+def test_stem_pack3_split(ops, kh, stride, pad, B, tile):
+    from idunno.models import reference as ref
+
+    torch.manual_seed(kh + tile)
+    img = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=DEV)
+    w = torch.randn(64, 3, kh, kh) / (3 * kh * kh) ** 0.5
+    b = torch.randn(64) * 0.1
+    sp3, scale = P.pack_split_weight_p3(w)
+    x3 = ops.preprocess_pack3_split(img, kh, stride, pad)
+    y = ops.conv2d_pack3_split(x3, sp3.to(DEV), b.to(DEV), scale, 224, kh, kh, stride, pad, True, tile=tile)
+    assert y.dtype == torch.float32
+    x = ref.preprocess_u8(img).permute(0, 2, 3, 1)
+    _check(y, _ref64(x, w, b, stride, pad, True))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,hw", [(3, 224), (2, 100), (1, 37)])
+def test_stem_split_fused(ops, B, hw):
+    """uint8 -> normalise -> conv7x7/2 -> +bias -> ReLU -> maxpool3x3/2, split out."""
+    from idunno.models import reference as ref
+
+    torch.manual_seed(B + hw)
+    img = torch.randint(0, 256, (B, hw, hw, 3), dtype=torch.uint8, device=DEV)
+    w = torch.randn(64, 3, 7, 7) / (3 * 49) ** 0.5
+    b = torch.randn(64) * 0.1
+    fs, scale = P.pack_stem_split(w)
+    y = ops.stem_split(img, fs.to(DEV), b.to(DEV), scale)
+    x = ref.preprocess_u8(img).permute(0, 2, 3, 1)
+    want = _ref64(x, w, b, 2, 3, True).permute(0, 3, 1, 2)
+    want = F.max_pool2d(want, 3, 2, 1).permute(0, 2, 3, 1)
+    assert y.shape == (*want.shape[:3], 128)
+    _check(P.from_split(y), want)
 
 
 @pytest.mark.gpu
