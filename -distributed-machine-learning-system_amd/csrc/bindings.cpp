@@ -275,6 +275,8 @@ torch::Tensor conv2d_nhwc_f32(torch::Tensor x, torch::Tensor w, torch::Tensor bi
   return y;
 }
 
+static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
+
 // split fp16 (fp32-accurate) conv: y = act(acc_scale * conv(x, w) + bias (+ res)).
 //   x   : [B, H, W, 2C] half, split layout ([hi x32][lo x32] per 32 channels), C % 32 == 0
 //   w   : [Cout, KH*KW*2C] half, same layout per tap, pre-scaled by 1/acc_scale
@@ -351,6 +353,64 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   return y;
 }
 
+// fp32-accurate FC on split fp16: y = act(acc_scale * x @ w.T + bias)
+//   x [M, 2K] split, w [N, 2K] split (pack_split_weight of [N, K, 1, 1]); K % 32 == 0.
+// K is cut into `splits` slices in ONE conv_glds launch (fp32 partials) + the
+// combine, which writes fp32 [M, N] or split [M, 2N] (N % 32 == 0).
+torch::Tensor linear_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias, double acc_scale, bool relu,
+                           bool out_f32, int64_t splits, int64_t tile) {
+  CHECK_DEV(x);
+  CHECK_DEV(w);
+  CHECK_DEV(bias);
+  CHECK_CONTIG(x);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(bias);
+  CHECK_DT(x, torch::kHalf);
+  CHECK_DT(w, torch::kHalf);
+  CHECK_DT(bias, torch::kFloat);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && bias.dim() == 1, "bad ranks");
+  TORCH_CHECK(w.device() == x.device() && bias.device() == x.device(), "operands on different devices");
+  const int64_t M = x.size(0), K2 = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K2 && bias.size(0) == N, "shape mismatch");
+  TORCH_CHECK(out_f32 ? N % 4 == 0 : N % 32 == 0, "N must be a multiple of 4 (fp32 out) / 32 (split out)");
+  TORCH_CHECK(splits >= 1 && splits <= 16 && K2 % (64 * splits) == 0, "K must split into multiples of 32");
+  TORCH_CHECK(splits * M * N < (1L << 31) && M * K2 < (1L << 31), "too large for int32 indexing");
+  auto part = torch::empty({splits, M, N}, x.options().dtype(torch::kFloat));
+  auto y = out_f32 ? torch::empty({M, N}, x.options().dtype(torch::kFloat))
+                   : torch::empty({M, 2 * N}, x.options().dtype(torch::kHalf));
+  if (M == 0) return y;
+  const int64_t Ks2 = K2 / splits;
+  auto zb = zero_f32(x.device(), N);
+  ConvArgs a{};
+  a.x = reinterpret_cast<const half_t*>(x.data_ptr());
+  a.w = reinterpret_cast<const half_t*>(w.data_ptr());
+  a.bias = zb.data_ptr<float>();
+  a.res = nullptr;
+  a.y = part.data_ptr<float>();
+  a.B = (int)M; a.H = 1; a.W = 1; a.C = (int)Ks2; a.ldx = (int)K2;
+  a.Ho = 1; a.Wo = 1; a.Cout = (int)N; a.ldy = (int)N;
+  a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0;
+  a.M = (int)M;
+  a.Kpad = (int)K2;
+  a.relu = 0;
+  a.acc_scale = (float)acc_scale;
+  a.zero = zero_buffer(x.device()).data_ptr();
+  a.ksplit = (int)splits;
+  a.kslice = (int)Ks2;
+  a.ysplit = (long)(M * N);
+  const int t = tile >= 0 ? (int)tile : conv_glds_split_pick((int)M, (int)N);
+  TORCH_CHECK(conv_glds_split_launch(a, true, t, cur_stream()), "unknown split conv tile id ", t);
+  check_launch("linear_split");
+  if (out_f32)
+    splitk_reduce_launch(part.data_ptr<float>(), (int)splits, (long)(M * N), (int)N, bias.data_ptr<float>(),
+                         relu ? 1 : 0, y.data_ptr(), true, cur_stream());
+  else
+    splitk_reduce_split_launch(part.data_ptr<float>(), (int)splits, (long)(M * N), (int)N, bias.data_ptr<float>(),
+                               relu ? 1 : 0, reinterpret_cast<half_t*>(y.data_ptr()), cur_stream());
+  check_launch("splitk_reduce");
+  return y;
+}
+
 // fp32 NHWC [.., C] <-> split [.., 2C] (C % 32 == 0)
 torch::Tensor split_from_f32(torch::Tensor x) {
   CHECK_DEV(x);
@@ -416,8 +476,6 @@ torch::Tensor maxpool2d_split(torch::Tensor x, int64_t k, int64_t s, int64_t pad
 }
 
 int64_t pick_tile_split(int64_t M, int64_t Cout) { return conv_glds_split_pick((int)M, (int)Cout); }
-
-static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
 
 // fp32 FC layer y = act(x @ w.T + bias) with K split over `splits` slices in ONE
 // conv_f32 launch (grid = tiles x splits, fp32 partials) + the split-K combine.
@@ -1050,6 +1108,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_split", &stem_split, "fp32-accurate fused split-fp16 ResNet stem (normalise+conv7x7/2+relu+maxpool)",
         py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("acc_scale"), py::arg("start") = py::none(),
         py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1, py::arg("sub") = 0);
+  m.def("linear_split", &linear_split, "fp32-accurate FC on split fp16, split-K in one launch + combine",
+        py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("acc_scale"), py::arg("relu"), py::arg("out_f32"),
+        py::arg("splits"), py::arg("tile") = -1);
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");
   m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),

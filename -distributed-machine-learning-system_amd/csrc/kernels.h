@@ -157,6 +157,9 @@ void maxpool_launch(const half_t* x, half_t* y, int B, int H, int W, int C, int 
 void avgpool_launch(const half_t* x, half_t* y, int B, int HW, int C, hipStream_t st);
 void synth_images_launch(uint8_t* out, uint64_t seed, long start, long n, long bytes_per_img,
                          hipStream_t st);
+// split-K combine into the split-fp16 layout [M][2N] (N % 32 == 0)
+void splitk_reduce_split_launch(const float* part, int S, long MN, int N, const float* bias, int relu, half_t* y,
+                                hipStream_t st);
 void splitk_reduce_launch(const float* part, int S, long MN, int N, const float* bias, int relu, void* y,
                           bool out_f32, hipStream_t st);
 void softmax_top1_launch(const float* logits, int ld, int N, int rows, int* cls, float* prob, int* packed,

@@ -227,7 +227,13 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, int S, long
     v[2] = fmaxf(v[2], 0.f);
     v[3] = fmaxf(v[3], 0.f);
   }
-  if (out_f32) {
+  if (out_f32 == 2) {                     // split-fp16 layout [M][2N] (N % 32 == 0)
+    half4v h, l;
+    split_f16x4(v, h, l);
+    half_t* yp = static_cast<half_t*>(y) + (i / N) * 2 * N + split_off(n);
+    *reinterpret_cast<half4v*>(yp) = h;
+    *reinterpret_cast<half4v*>(yp + 32) = l;
+  } else if (out_f32) {
     *reinterpret_cast<float4v*>(static_cast<float*>(y) + i) = v;
   } else {
     half4v o;
@@ -237,6 +243,13 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, int S, long
     o[3] = (half_t)v[3];
     *reinterpret_cast<half4v*>(static_cast<half_t*>(y) + i) = o;
   }
+}
+
+void splitk_reduce_split_launch(const float* part, int S, long MN, int N, const float* bias, int relu, half_t* y,
+                                hipStream_t st) {
+  const long threads = (MN + 3) / 4;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, part, S, MN, N,
+                     bias, relu, (void*)y, 2);
 }
 
 void splitk_reduce_launch(const float* part, int S, long MN, int N, const float* bias, int relu, void* y,

@@ -353,8 +353,14 @@ def make_fc(lin: nn.Linear, relu: bool, perm: torch.Tensor | None = None, dtype:
     k = w.shape[1]
     if k % 64 != 0:
         raise ValueError(f"FC in_features={k} must be a multiple of 64")
+    sw, s_scale = None, 1.0
+    if dtype == "fp32" and k % SPLIT_BLOCK == 0:
+        w64 = lin.weight.detach().double()
+        if perm is not None:
+            w64 = w64[:, perm]
+        sw, s_scale = pack_split_weight(w64.reshape(w.shape[0], k, 1, 1))
     return Conv((w if dtype == "fp32" else w.half()).contiguous(), lin.bias.detach().float().contiguous(), k, w.shape[0], 1, 1, 1,
-                0, relu, False)
+                0, relu, False, sw=sw, s_scale=s_scale)
 
 
 def compile_model(m: nn.Module, name: str, dtype: str = "fp16") -> Program:
@@ -591,6 +597,8 @@ class HipRunner:
             for fc in p.fcs:
                 x = o.linear(x, fc.w, fc.b, relu=fc.relu)
             return x
+        if p.kind == "alexnet" and self.split and self._split_ok():
+            return self._alexnet_split(first, img_u8, start, batch, start_offset)
         x = self._stem_f32(first, img_u8, start, batch, start_offset)
         if p.kind == "resnet":
             x = o.maxpool2d(x, 3, 2, 1)
@@ -670,7 +678,23 @@ class HipRunner:
                 self.stem_parts, self.front_split, self.fuse_stem)
 
     def _split_ok(self) -> bool:
-        return all(c.sw is not None for b in self.p.blocks for c in [*b.convs, *([b.down] if b.down else [])])
+        p = self.p
+        if p.kind == "alexnet":
+            return all(v.sw is not None for k, v in p.features[1:] if k == "conv") and \
+                all(f.sw is not None for f in p.fcs)
+        return all(c.sw is not None for b in p.blocks for c in [*b.convs, *([b.down] if b.down else [])])
+
+    def _alexnet_split(self, first, img_u8, start, batch, start_offset):
+        """fp32-accurate AlexNet: split packed-row conv1 (fp32 out) -> pools into
+        the split layout -> split convs 2-5 -> split FCs (split-K), fp32 logits."""
+        o, p = self.ops, self.p
+        x = self._stem_f32(first, img_u8, start, batch, start_offset)
+        for k, v in p.features[1:]:
+            x = self._conv_split(v, x) if k == "conv" else o.maxpool2d_split(x, *v)
+        x = x.reshape(x.shape[0], -1)         # split [B, 6*6*2*256]: the split layout of the NHWC flatten
+        for i, fc in enumerate(p.fcs):
+            x = o.linear_split(x, fc.sw, fc.b, fc.s_scale, relu=fc.relu, out_f32=i == len(p.fcs) - 1)
+        return x
 
     def _conv_split(self, c, x, residual=None, out_f32=False):
         return self.ops.conv2d_split(x, c.sw, c.b, c.s_scale, c.kh, c.kw, c.stride, c.pad, c.relu, residual,

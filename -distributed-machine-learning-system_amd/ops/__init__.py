@@ -13,7 +13,7 @@ __all__ = [
     "available", "load", "so_path", "conv2d", "linear", "preprocess", "resize_crop",
     "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile", "pick_tile_f32", "synth_images", "stem_fused",
     "conv2d_wino", "wino_supported", "preprocess_pack3", "conv2d_pack3",
-    "conv2d_split", "stem_split", "preprocess_pack3_split", "conv2d_pack3_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
+    "conv2d_split", "linear_split", "stem_split", "preprocess_pack3_split", "conv2d_pack3_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
 ]
 
 
@@ -45,6 +45,25 @@ def stem_split(img_u8, w, bias, acc_scale: float, start=None, batch: int = -1, s
     split [B,56,56,128] (normalise, conv 7x7/2 + bias, ReLU, max pool 3x3/2);
     ``w``, ``acc_scale`` = models.packed.pack_stem_split(w)."""
     return load().stem_split(img_u8, w, bias, acc_scale, start, batch, start_offset, window, sub)
+
+
+def split_linear_splits(m: int, k: int, n: int) -> int:
+    """Split-K factor for a split-fp16 FC layer: ~1024 blocks of the default
+    tile, slices of >= 512 input features, at most 8."""
+    tiles = -(-m // 64) * (n // 128) if n % 128 == 0 else -(-m // 128) * -(-n // 64)
+    s = 1
+    while s < 8 and tiles * s < 1024 and k % (64 * s) == 0 and k // (2 * s) >= 512:
+        s *= 2
+    return s
+
+
+def linear_split(x, w, bias, acc_scale: float, relu: bool = False, out_f32: bool = False, splits: int | None = None):
+    """fp32-accurate y = act(x @ w.T + bias) on split fp16: x [M, 2K] split,
+    w [N, 2K] split (models.packed.pack_split_weight of [N, K, 1, 1]); output
+    split [M, 2N], or fp32 [M, N] with ``out_f32``.  K slices in one launch."""
+    m, k2 = x.shape
+    s = split_linear_splits(m, k2 // 2, w.shape[0]) if splits is None else splits
+    return load().linear_split(x, w, bias, acc_scale, relu, out_f32, s, -1)
 
 
 def split_from_f32(x):

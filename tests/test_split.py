@@ -239,7 +239,29 @@ def test_split_conversions_and_maxpool(ops):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,B", [("resnet18", 4), ("resnet18", 400), ("resnet50", 8)])
+@pytest.mark.parametrize("M,K,N,out_f32,relu,splits", [
+    (500, 9216, 4096, False, True, None),    # alexnet fc6 (auto split)
+    (500, 4096, 1000, True, False, None),    # fc8: N 1000, fp32 logits
+    (7, 512, 96, False, False, 1),
+    (33, 1024, 256, True, True, 4),
+])
+def test_linear_split(ops, M, K, N, out_f32, relu, splits):
+    torch.manual_seed(M + K + N)
+    x = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K) / K ** 0.5
+    b = torch.randn(N) * 0.1
+    sw, scale = P.pack_split_weight(w.reshape(N, K, 1, 1))
+    y = ops.linear_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, relu=relu, out_f32=out_f32,
+                         splits=splits)
+    ref = x.double() @ w.double().t().to(DEV) + b.double().to(DEV)
+    if relu:
+        ref = F.relu(ref)
+    _check(y if out_f32 else P.from_split(y), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,B", [("resnet18", 4), ("resnet18", 400), ("resnet50", 8), ("alexnet", 6),
+                                    ("alexnet", 500)])
 def test_model_split_vs_fp64_oracle(ops, name, B):
     from idunno.models import reference as ref
 
