@@ -277,6 +277,11 @@ torch::Tensor conv2d_nhwc_f32(torch::Tensor x, torch::Tensor w, torch::Tensor bi
 
 static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
 
+// Whether auto selection routes split 3x3/s1 64->64 convs (ResNet layer1) to the
+// row-streaming register-weight kernel (tile 50 of conv2d_split, conv3x3_split.hip).
+static bool g_split_c64_default = true;
+void set_split_c64_default(bool on) { g_split_c64_default = on; }
+
 // split fp16 (fp32-accurate) conv: y = act(acc_scale * conv(x, w) + bias (+ res)).
 //   x   : [B, H, W, 2C] half, split layout ([hi x32][lo x32] per 32 channels), C % 32 == 0
 //   w   : [Cout, KH*KW*2C] half, same layout per tap, pre-scaled by 1/acc_scale
@@ -347,6 +352,15 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   a.ablate = g_conv_ablate;
   if (M == 0) return y;
   a.zero = zero_buffer(x.device()).data_ptr();
+  const bool c64_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 &&
+                      conv3x3_split_c64_supported(H, W, C2 / 2, Cout);
+  if (tile == 50 || (tile < 0 && c64_ok && g_split_c64_default)) {
+    TORCH_CHECK(c64_ok, "tile 50 (row-streaming split 3x3 64->64 conv) does not support this shape");
+    conv3x3_split_c64_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W, a.relu,
+                             a.acc_scale, cur_stream());
+    check_launch("conv3x3_split_c64");
+    return y;
+  }
   const int t = tile >= 0 ? (int)tile : conv_glds_split_pick(a.M, Cout);
   TORCH_CHECK(conv_glds_split_launch(a, out_f32, t, cur_stream()), "unknown split conv tile id ", t);
   check_launch("conv_glds_split");
@@ -1111,6 +1125,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_split", &linear_split, "fp32-accurate FC on split fp16, split-K in one launch + combine",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("acc_scale"), py::arg("relu"), py::arg("out_f32"),
         py::arg("splits"), py::arg("tile") = -1);
+  m.def("set_split_c64_default", &set_split_c64_default,
+        "A/B: route split 3x3 64->64 convs to the row-streaming kernel (tile 50; default on)");
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");
   m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),

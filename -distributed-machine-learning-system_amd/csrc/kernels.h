@@ -127,6 +127,10 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 // ([hi x32][lo x32] per 32 channels), y fp32 with out_f32
 bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 int conv_glds_split_pick(int M, int Cout);
+// split 3x3/s1/p1 64 -> 64 conv, weights in registers, input rows streamed through an LDS ring
+bool conv3x3_split_c64_supported(int H, int W, int C, int Cout);
+void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
+                              const void* zero, int B, int H, int W, int relu, float acc_scale, hipStream_t st);
 // split-fp16 RGB stem on packed rows (a.cpk > 0, x from preprocess_pack3_split): fp32 output
 bool conv_glds_split_p3_launch(ConvArgs a, int tile, hipStream_t st);   // a.cpk > 0: pack3 stem
 bool conv_big_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);

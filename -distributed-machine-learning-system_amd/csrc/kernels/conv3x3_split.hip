@@ -1,0 +1,265 @@
+// Row-streaming 3x3 / stride-1 / pad-1 conv, 64 -> 64 channels, on split fp16
+// (fp32-accurate, see conv_glds.hip SPLIT): ResNet layer1 (56x56x64).
+//
+// Why a kernel of its own: as an implicit GEMM (conv_glds SPLIT) every input
+// pixel is DMA'd from L2 once per tap, 9x; at C = 64 the layer is bound by
+// that L2 -> LDS stream (~11 TB/s at 28 % of the f16 MFMA peak).  Here
+//   * the weights live in REGISTERS: wave w owns output channels 16w..16w+15
+//     and holds their 9 taps x 2 channel blocks x (hi, lo) A fragments
+//     (36 x half8v = 144 VGPRs) for the whole launch;
+//   * the input streams through LDS one image row at a time: a 4-row ring
+//     (rows y-1, y, y+1 in use, row y+2 landing by LDS-DMA while row y
+//     computes), so each input row is fetched once per band of rows instead
+//     of 9 times;
+//   * an output row is 4 pixel fragments of 16 (49 <= W <= 62); per (tap,
+//     channel block, fragment) a wave reads the hi and lo B fragments and
+//     issues 3 MFMAs (hi*hi + hi*lo + lo*hi), the reads of the next two such
+//     groups in flight behind them (3-deep register ring, counted lgkmcnt);
+//   * the residual of the row is loaded into registers when the row starts.
+// LDS pixel rows are 256 B (64 channels x (hi, lo) halfs: 16 chunks of 16 B);
+// chunk c of LDS column col sits in slot c ^ ((2*col) & 15), which makes the
+// B-fragment reads (lane = pixel col + 16 * k-group) conflict-free for every
+// tap shift (exhaustive check in tests/test_split.py).
+// Persistent: a work item is a band of BAND output rows of one image.
+#include "../kernels.h"
+#include "../launch_util.h"
+
+namespace idunno {
+
+namespace c64s {
+constexpr int C = 64;              // channels in and out
+constexpr int PIX = 2 * C;         // halfs per pixel (split)
+constexpr int RC = 66;             // LDS columns per ring row (W + 2 <= 64 read + 2 of masked lanes)
+constexpr int RB = RC * 256;       // bytes per ring row
+constexpr int RING = 4;
+constexpr int LDS = RING * RB;     // 67,584 B: 2 workgroups per CU
+constexpr int BAND = 8;            // output rows per work item
+constexpr int NF = 4;              // pixel fragments per row (49 <= W <= 62: all 4 store)
+constexpr int NST = 2 * NF;        // epilogue store instructions per wave and row
+}  // namespace c64s
+
+struct C64sArgs {
+  const half_t* x;      // split [B][H][W][128]
+  const half_t* w;      // split weights [64][9 * 128] (pack_split_weight)
+  const float* bias;    // [64]
+  const half_t* res;    // split [B][H][W][128] or nullptr
+  half_t* y;            // split [B][H][W][128]
+  const void* zero;     // >= 16 zero bytes
+  int B, H, W, relu, nbands, ntasks;
+  float acc_scale;
+};
+
+__device__ __forceinline__ int c64s_slot(int chunk, int col) { return chunk ^ ((2 * col) & 15); }
+
+// ds_read_b128 with an immediate byte offset (invisible to the wait-count pass, see common.h)
+template <int OFF>
+__device__ __forceinline__ half8v lds_read_b128_off(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset range");
+  half8v v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF) : "memory");
+  return v;
+}
+
+// fragment f's read (f = 0..3, constant after unrolling): immediate offset 4096 * f
+__device__ __forceinline__ half8v lds_read_frag(uint32_t addr, int f) {
+  switch (f) {
+    case 0: return lds_read_b128_off<0>(addr);
+    case 1: return lds_read_b128_off<4096>(addr);
+    case 2: return lds_read_b128_off<8192>(addr);
+    default: return lds_read_b128_off<12288>(addr);
+  }
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+// DMA input row iy of image b into ring slot rs (zeros outside the image);
+// every wave issues exactly 4 DMA instructions
+__device__ __forceinline__ void c64s_load_row(const C64sArgs& a, char* ring, int b, int iy, int rs, int tid) {
+  using namespace c64s;
+  const bool rowv = (unsigned)iy < (unsigned)a.H;
+  const half_t* zero = static_cast<const half_t*>(a.zero);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = r * 256 + tid;                // 16-byte chunk of the LDS row (lane-linear)
+    const int col = i >> 4, slot = i & 15;
+    const int ix = col - 1;
+    const bool ok = rowv && (unsigned)ix < (unsigned)a.W;
+    const half_t* src = ok ? a.x + (((size_t)b * a.H + iy) * a.W + ix) * PIX + (c64s_slot(slot, col) << 3) : zero;
+    __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(ring + rs * RB + (r * 256 + (tid & ~63)) * 16),
+                                     16, 0, 0);
+  }
+}
+
+template <bool HAS_RES>
+__global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArgs a) {
+  using namespace c64s;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15, q = lane >> 4;
+  if ((int)blockIdx.x >= a.ntasks) return;   // uniform
+
+  // ---- A fragments of this wave's 16 couts: [tap][block][hi|lo] ----
+  half8v fa[9][2][2];
+  {
+    const half_t* wr = a.w + (size_t)(wave * 16 + frow) * (9 * PIX) + q * 8;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) fa[t][cb][p] = *reinterpret_cast<const half8v*>(wr + t * PIX + cb * 64 + p * 32);
+  }
+  const int n0 = wave * 16 + 4 * q;            // this lane's 4 output channels (C/D layout)
+  const float4v bv = *reinterpret_cast<const float4v*>(a.bias + n0);
+  const uint32_t ring = lds_addr(smem);
+  // per-lane LDS byte offset of column frow + kw, chunk 4c + q:
+  //   col*256 + (slot << 4), slot = (4c + q) ^ x, x = (2*col) & 15
+  // = loff[kw] ^ (c << 6): bits 6-7 hold c ^ (x >> 2), bits 4-5 q ^ (x & 3)
+  uint32_t loff[3];
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw) {
+    const int col = frow + kw, x = (2 * col) & 15;
+    loff[kw] = (uint32_t)(col * 256 + (((x >> 2) & 3) << 6) + (((q ^ x) & 3) << 4));
+  }
+
+  for (int task = blockIdx.x; task < a.ntasks; task += gridDim.x) {
+    const int b = task / a.nbands;
+    const int y0 = (task - b * a.nbands) * BAND;
+    const int y1 = min(y0 + BAND, a.H);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();              // previous item's ring reads are done
+    c64s_load_row(a, smem, b, y0 - 1, (y0 + 3) & 3, tid);
+    c64s_load_row(a, smem, b, y0, y0 & 3, tid);
+    c64s_load_row(a, smem, b, y0 + 1, (y0 + 1) & 3, tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int y = y0; y < y1; ++y) {
+      // row y+1 landed: its DMA (issued one row ago) is older than this wave's
+      // last NST epilogue stores; then the barrier publishes everyone's DMA
+      // and ends every wave's reads of row y-2, whose slot row y+2 now takes
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+      __builtin_amdgcn_s_barrier();
+      if (y + 2 <= y1) c64s_load_row(a, smem, b, y + 2, (y + 2) & 3, tid);
+      // residual of row y -> registers now (untracked loads, retired by the
+      // epilogue's vmcnt(0)): a load issued in the epilogue exposed a full
+      // memory latency per row (+25 % on the residual variant)
+      const size_t rowpix = ((size_t)b * a.H + y) * a.W;
+      half4v rh[HAS_RES ? NF : 1], rl[HAS_RES ? NF : 1];
+      if constexpr (HAS_RES) {
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          const int ox = min(16 * f + frow, a.W - 1);
+          const size_t off = (rowpix + ox) * PIX + split_off(n0);
+          rh[f] = gload_b64_untracked(a.res + off);
+          rl[f] = gload_b64_untracked(a.res + off + 32);
+        }
+      }
+      float4v acc[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) acc[f] = float4v{0.f, 0.f, 0.f, 0.f};
+      // 72 groups g = (tap t, block cb, pixel fragment F): 2 B reads (hi, lo),
+      // 3 MFMAs; a 3-deep register ring keeps the reads of groups g+1, g+2 in
+      // flight behind group g's MFMAs (counted lgkmcnt)
+      half8v bf[3][2];
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) asm volatile("" : "+v"(loff[kw]));
+      uint32_t rowb[3];
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) rowb[kh] = ring + (uint32_t)(((y - 1 + kh) & 3) * RB);
+      auto issue = [&](int g, int buf) {
+        const int t = g >> 3, cb = (g >> 2) & 1, F = g & 3;
+        const int kh = t / 3, kw = t - 3 * kh;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          bf[buf][p] = lds_read_frag(rowb[kh] + (loff[kw] ^ (uint32_t)((2 * cb + p) << 6)), F);
+      };
+      issue(0, 0);
+      issue(1, 1);
+#pragma unroll
+      for (int g = 0; g < 72; ++g) {
+        const int buf = g % 3;
+        if (g + 2 < 72) {
+          issue(g + 2, (g + 2) % 3);
+          lds_waitcnt<4>();
+        } else if (g + 1 < 72) {
+          lds_waitcnt<2>();
+        } else {
+          lds_waitcnt<0>();
+        }
+        lds_tie(bf[buf][0]);
+        lds_tie(bf[buf][1]);
+        const int t = g >> 3, cb = (g >> 2) & 1, F = g & 3;
+        float4v& c = acc[F];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][cb][0], bf[buf][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][cb][0], bf[buf][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][cb][1], bf[buf][0], c, 0, 0, 0);
+      }
+      // ---- epilogue: scale, bias (+ residual), ReLU, split store ----
+      if constexpr (HAS_RES) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          reg_tie(rh[f]);
+          reg_tie(rl[f]);
+        }
+      }
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int ox = 16 * f + frow;
+        if (ox >= a.W) continue;
+        const size_t off = (rowpix + ox) * PIX + split_off(n0);
+        float4v v = acc[f] * a.acc_scale + bv;
+        if constexpr (HAS_RES) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)rh[f][e] + (float)rl[f][e];
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        half4v h, l;
+        split_f16x4(v, h, l);
+        *reinterpret_cast<half4v*>(a.y + off) = h;
+        *reinterpret_cast<half4v*>(a.y + off + 32) = l;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// W in [49, 62]: every one of the 4 pixel fragments has a valid column, so
+// each wave issues exactly NST epilogue stores per row (counted vmcnt above)
+bool conv3x3_split_c64_supported(int H, int W, int C, int Cout) {
+  return C == 64 && Cout == 64 && W >= 49 && W <= 62 && H >= 1;
+}
+
+void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
+                              const void* zero, int B, int H, int W, int relu, float acc_scale, hipStream_t st) {
+  using namespace c64s;
+  C64sArgs a;
+  a.x = x;
+  a.w = w;
+  a.bias = bias;
+  a.res = res;
+  a.y = y;
+  a.zero = zero;
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  a.relu = relu;
+  a.acc_scale = acc_scale;
+  a.nbands = (H + BAND - 1) / BAND;
+  a.ntasks = B * a.nbands;
+  const int per = 2 * device_cu_count();
+  const int grid = a.ntasks < per ? a.ntasks : per;
+  if (res) {
+    ensure_lds_attr(reinterpret_cast<const void*>(conv3x3_split_c64_kernel<true>), LDS);
+    hipLaunchKernelGGL(conv3x3_split_c64_kernel<true>, dim3(grid), dim3(256), LDS, st, a);
+  } else {
+    ensure_lds_attr(reinterpret_cast<const void*>(conv3x3_split_c64_kernel<false>), LDS);
+    hipLaunchKernelGGL(conv3x3_split_c64_kernel<false>, dim3(grid), dim3(256), LDS, st, a);
+  }
+}
+
+}  // namespace idunno

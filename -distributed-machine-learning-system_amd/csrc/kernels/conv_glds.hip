@@ -461,7 +461,11 @@ static bool glds_dispatch_p3(ConvArgs a, int tile, hipStream_t st) {
 template <bool R, bool F>
 static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
   switch (tile) {
+    case 14: glds_cfg<128, 256, 64, 2, 4, 3, R, F, false, true>(a, st); return true;
+    case 17: glds_cfg<256, 128, 64, 4, 2, 3, R, F, false, true>(a, st); return true;
     case 24: glds_cfg<128, 128, 64, 2, 4, 3, R, F, false, true>(a, st); return true;
+    case 25: glds_cfg<256, 128, 64, 4, 2, 2, R, F, false, true>(a, st); return true;
+    case 30: glds_cfg<128, 256, 64, 2, 4, 2, R, F, false, true>(a, st); return true;
     case 26: glds_cfg<128, 128, 64, 2, 2, 2, R, F, false, true>(a, st); return true;
     case 27: glds_cfg<64, 128, 64, 1, 4, 2, R, F, false, true>(a, st); return true;
     case 33: glds_cfg<64, 256, 64, 1, 4, 2, R, F, false, true>(a, st); return true;

@@ -48,6 +48,19 @@ def test_pack_split_weight_cpu():
         P.pack_split_weight(torch.randn(8, 3, 7, 7))
 
 
+def test_c64_split_lds_swizzle_conflict_free_cpu():
+    """conv3x3_split.hip: chunk c of LDS column col in slot c ^ ((2*col) & 15);
+    every ds_read_b128 lane group (lane = pixel + 16 * k-group) hits 16
+    distinct 16-byte slots for every column base (tap shift) and chunk base."""
+    groups = [[*range(0, 4), *range(12, 16), *range(20, 28)], [*range(4, 12), *range(16, 20), *range(28, 32)]]
+    groups += [[lane + 32 for lane in g] for g in groups]
+    for base in range(16):
+        for c0 in range(0, 16, 4):
+            for g in groups:
+                slots = {((c0 + (lane >> 4)) ^ ((2 * (base + (lane & 15))) & 15)) for lane in g}
+                assert len(slots) == 16, (base, c0, g)
+
+
 def _unpack_split_p3(sp3, scale, cout, kh, kw):
     cpk = (3 * kw + 7) // 8
     v = sp3.double().reshape(cout, -1, 2, 32)
@@ -165,7 +178,23 @@ def test_conv_split_default_tile(ops, B, H, Cin, Cout, k, s, p):
     _check(P.from_split(y), ref)
 
 
-SPLIT_TILES = [24, 26, 27, 33, 34, 35, 36, 37, 38]
+SPLIT_TILES = [14, 17, 24, 25, 26, 27, 30, 33, 34, 35, 36, 37, 38]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,W", [(2, 56, 56), (3, 13, 49), (1, 9, 62)])
+@pytest.mark.parametrize("res", [False, True])
+def test_conv_split_c64_rows(ops, B, H, W, res):
+    """Row-streaming register-weight 3x3 64->64 kernel (tile 50)."""
+    torch.manual_seed(B * H + W + res)
+    x = torch.randn(B, H, W, 64, device=DEV)
+    w = torch.randn(64, 64, 3, 3) / 24
+    b = torch.randn(64) * 0.1
+    r = torch.randn(B, H, W, 64, device=DEV) if res else None
+    sw, scale = P.pack_split_weight(w)
+    y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, 3, 3, 1, 1, True,
+                         residual=None if r is None else ops.split_from_f32(r), tile=50)
+    _check(P.from_split(y), _ref64(x, w, b, 1, 1, True, r))
 
 
 @pytest.mark.gpu

@@ -24,7 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=400)
     ap.add_argument("--model", default="resnet18")
-    ap.add_argument("--tiles", default="24,26,27,33,34,35,36,37,38")
+    ap.add_argument("--tiles", default="14,17,24,25,26,27,30,33,34,35,36,37,38")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     from idunno import ops
