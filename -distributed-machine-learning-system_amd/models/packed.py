@@ -481,6 +481,9 @@ class HipRunner:
         # hi*hi + hi*lo + lo*hi on the f16 MFMA, fp32-accurate) instead of the
         # f32-MFMA Winograd / direct kernels; False = the all-f32-MFMA path
         self.split = True
+        # split path: fused stem + layer1 on this many batch parts (None = 1;
+        # A/B: tools/ab_flag.py --attr split_front --values 1,2)
+        self.split_front: int | None = None
         self._side: dict = {}
         # None = measured default (tools/wino_ablate.py, profiles/r2_v6_wino_variants.md):
         # variant 3 -- 4-wave blocks of 64 tiles, one 58-KiB LDS stage, two blocks
@@ -564,11 +567,16 @@ class HipRunner:
             # fused split stem (uint8 -> normalise -> conv7x7/2 -> ReLU -> max
             # pool, split out; or stem conv + max pool into the split layout)
             # -> split residual stages (the last conv writes fp32) -> fp32 avgpool / FC
-            if self.fuse_stem and first.fs is not None and first.relu:
+            fused = self.fuse_stem and first.fs is not None and first.relu
+            parts = self.split_front or 1
+            nfront = self._front_blocks() if fused and parts > 1 and nb >= 2 * parts else 0
+            if nfront:
+                x = self._split_front_split(img_u8, start, batch, start_offset, nfront, parts)
+            elif fused:
                 x = o.stem_split(img_u8, first.fs, first.b, first.s_scale, start, batch, start_offset)
             else:
                 x = o.maxpool2d_split(self._stem_f32(first, img_u8, start, batch, start_offset), 3, 2, 1)
-            for i, blk in enumerate(p.blocks):
+            for i, blk in enumerate(p.blocks[nfront:], nfront):
                 x = self._block_split(blk, x, last=i == len(p.blocks) - 1)
             x = o.global_avgpool(x)
             for fc in p.fcs:
@@ -674,7 +682,7 @@ class HipRunner:
 
     def _variant(self) -> tuple:
         """Kernel-choice switches a captured graph depends on (part of its cache key)."""
-        return (self.split, self.winograd, self.wino_variant, self.pack3, self.pack3_f16, self.side_down,
+        return (self.split, self.split_front, self.winograd, self.wino_variant, self.pack3, self.pack3_f16, self.side_down,
                 self.stem_parts, self.front_split, self.fuse_stem)
 
     def _split_ok(self) -> bool:
@@ -696,18 +704,44 @@ class HipRunner:
             x = o.linear_split(x, fc.sw, fc.b, fc.s_scale, relu=fc.relu, out_f32=i == len(p.fcs) - 1)
         return x
 
-    def _conv_split(self, c, x, residual=None, out_f32=False):
+    def _conv_split(self, c, x, residual=None, out_f32=False, out=None):
         return self.ops.conv2d_split(x, c.sw, c.b, c.s_scale, c.kh, c.kw, c.stride, c.pad, c.relu, residual,
-                                     out_f32)
+                                     out_f32, out=out)
 
-    def _block_split(self, blk, x, last: bool = False):
+    def _block_split(self, blk, x, last: bool = False, out=None):
         """Residual block on split-fp16 activations; with ``last`` the block's
-        output is fp32 (for the avgpool / FC head)."""
+        output is fp32 (for the avgpool / FC head); into ``out`` when given."""
         idt = x if blk.down is None else self._conv_split(blk.down, x)
         y = x
         for c in blk.convs[:-1]:
             y = self._conv_split(c, y)
-        return self._conv_split(blk.convs[-1], y, residual=idt, out_f32=last)
+        return self._conv_split(blk.convs[-1], y, residual=idt, out_f32=last, out=out)
+
+    def _split_front_split(self, img_u8, start, batch, start_offset, nfront, parts):
+        """Fused split stem + the first ``nfront`` (full-resolution) blocks on
+        ``parts`` batch parts, so a part's activations can stay in the 256-MB
+        Infinity Cache between kernels; the last block writes its slice of the
+        full-batch output."""
+        o, s = self.ops, self.p.stem
+        B = batch if start is not None else img_u8.shape[0]
+        n = -(-B // parts)
+        out = None
+        for sub in range(0, B, n):
+            nb = min(n, B - sub)
+            if start is not None:
+                x = o.stem_split(img_u8, s.fs, s.b, s.s_scale, start, nb, start_offset, window=B, sub=sub)
+            else:
+                x = o.stem_split(img_u8[sub:sub + nb], s.fs, s.b, s.s_scale)
+            for bi in range(nfront):
+                blk = self.p.blocks[bi]
+                if bi < nfront - 1:
+                    x = self._block_split(blk, x)
+                    continue
+                if out is None:
+                    out = torch.empty((B, x.shape[1], x.shape[2], 2 * blk.convs[-1].cout), dtype=torch.float16,
+                                      device=x.device)
+                self._block_split(blk, x, out=out[sub:sub + nb])
+        return out
 
     def _side_stream(self, device):
         st = self._side.get(device)
