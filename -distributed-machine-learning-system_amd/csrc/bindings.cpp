@@ -281,6 +281,13 @@ static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
 // row-streaming register-weight kernel (tile 50 of conv2d_split, conv3x3_split.hip).
 static bool g_split_c64_default = true;
 void set_split_c64_default(bool on) { g_split_c64_default = on; }
+// split convs: tile order (0 m-major, 1 n-major, -1 auto heuristic)
+static int g_split_norder = -1;
+void set_split_norder(int64_t mode) { g_split_norder = (int)mode; }
+static int split_norder(int tiles_n, long kpad) {
+  if (g_split_norder >= 0) return g_split_norder;
+  return 0;
+}
 
 // split fp16 (fp32-accurate) conv: y = act(acc_scale * conv(x, w) + bias (+ res)).
 //   x   : [B, H, W, 2C] half, split layout ([hi x32][lo x32] per 32 channels), C % 32 == 0
@@ -362,6 +369,7 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     return y;
   }
   const int t = tile >= 0 ? (int)tile : conv_glds_split_pick(a.M, Cout);
+  a.norder = split_norder((Cout + 127) / 128, Kpad);
   TORCH_CHECK(conv_glds_split_launch(a, out_f32, t, cur_stream()), "unknown split conv tile id ", t);
   check_launch("conv_glds_split");
   return y;
@@ -1127,6 +1135,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splits"), py::arg("tile") = -1);
   m.def("set_split_c64_default", &set_split_c64_default,
         "A/B: route split 3x3 64->64 convs to the row-streaming kernel (tile 50; default on)");
+  m.def("set_split_norder", &set_split_norder, "A/B: split conv tile order (0 m-major, 1 n-major, -1 auto)");
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");
   m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),

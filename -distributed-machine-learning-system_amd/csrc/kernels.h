@@ -31,6 +31,7 @@ struct ConvArgs {
   int kslice;        // K slice s: x and w advance by s*kslice halfs, y by s*ysplit floats; 0/1: off
   long ysplit;
   float acc_scale;   // conv_glds SPLIT: accumulator multiplier (2^-e of the pre-scaled split weights)
+  int norder;        // conv_glds: 1 = n-major tile order (tn = lid / tiles_m), 0 = m-major
 };
 
 // fp32 (reference-precision) conv: same geometry fields as ConvArgs, f32 tensors.

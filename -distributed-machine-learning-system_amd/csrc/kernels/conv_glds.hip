@@ -85,7 +85,10 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
   const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
   const int lid_all = xcd_remap(blockIdx.x, nwg * nsplit);
   const int split = lid_all / nwg, lid = lid_all - split * nwg;
-  const int tm = lid / a.tiles_n, tn = lid % a.tiles_n;
+  // norder: n-major tile order (an XCD's resident blocks share one weight
+  // panel, pixel panels stream) instead of m-major (they share pixel panels)
+  const int tm = a.norder ? lid % a.tiles_m : lid / a.tiles_n;
+  const int tn = a.norder ? lid / a.tiles_m : lid % a.tiles_n;
   const int n0 = tn * BN, m0 = tm * BM;
   const half_t* const xin = a.x + (size_t)split * a.kslice;        // split-K: this block's K slice
   const half_t* const win = a.w + (size_t)split * a.kslice;
