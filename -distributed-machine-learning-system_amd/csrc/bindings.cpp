@@ -281,6 +281,10 @@ static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
 // row-streaming register-weight kernel (tile 50 of conv2d_split, conv3x3_split.hip).
 static bool g_split_c64_default = true;
 void set_split_c64_default(bool on) { g_split_c64_default = on; }
+// Whether auto selection routes split 3x3/s1 convs with Cout % 128 == 0 to the
+// halo-patch kernel (tile 60, conv3x3_patch_split.hip).
+static bool g_split_patch_default = false;
+void set_split_patch_default(bool on) { g_split_patch_default = on; }
 // split convs: tile order (0 m-major, 1 n-major, -1 auto heuristic)
 static int g_split_norder = -1;
 void set_split_norder(int64_t mode) { g_split_norder = (int)mode; }
@@ -366,6 +370,15 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     conv3x3_split_c64_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W, a.relu,
                              a.acc_scale, cur_stream());
     check_launch("conv3x3_split_c64");
+    return y;
+  }
+  const bool patch_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && Cout % 128 == 0 &&
+                        conv3x3_patch_split_supported(B, H, W, C2 / 2, Cout);
+  if ((tile >= 60 && tile <= 62) || (tile < 0 && patch_ok && g_split_patch_default)) {
+    TORCH_CHECK(patch_ok, "tiles 60-62 (split 3x3 patch conv) do not support this shape");
+    conv3x3_patch_split_launch(a.x, a.w, a.bias, a.res, a.y, out_f32, a.zero, B, H, W, C2 / 2, Cout, a.relu,
+                               a.acc_scale, tile >= 60 ? (int)tile - 58 : 2, cur_stream());
+    check_launch("conv3x3_patch_split");
     return y;
   }
   const int t = tile >= 0 ? (int)tile : conv_glds_split_pick(a.M, Cout);
@@ -1136,6 +1149,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_split_c64_default", &set_split_c64_default,
         "A/B: route split 3x3 64->64 convs to the row-streaming kernel (tile 50; default on)");
   m.def("set_split_norder", &set_split_norder, "A/B: split conv tile order (0 m-major, 1 n-major, -1 auto)");
+  m.def("set_split_patch_default", &set_split_patch_default,
+        "A/B: route split 3x3/s1 convs (Cout % 128 == 0) to the halo-patch kernel (tile 60)");
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");
   m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),
