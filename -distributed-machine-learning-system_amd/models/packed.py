@@ -454,6 +454,10 @@ def emulate(p: Program, img_u8: torch.Tensor) -> torch.Tensor:
 _CAPTURE_LOCK = threading.Lock()
 
 
+def x_is_cuda(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
 class HipRunner:
     """Runs a packed Program through the gfx950 kernels.
 
@@ -484,6 +488,9 @@ class HipRunner:
         # split path: fused stem + layer1 on this many batch parts (None = 1;
         # A/B: tools/ab_flag.py --attr split_front --values 1,2)
         self.split_front: int | None = None
+        # split path: the batch as this many streams' halves (None = 1; A/B:
+        # tools/ab_flag.py --attr split_streams --values 1,2)
+        self.split_streams: int | None = None
         self._side: dict = {}
         # None = measured default (tools/wino_ablate.py, profiles/r2_v6_wino_variants.md):
         # variant 3 -- 4-wave blocks of 64 tiles, one 58-KiB LDS stage, two blocks
@@ -568,6 +575,8 @@ class HipRunner:
             # pool, split out; or stem conv + max pool into the split layout)
             # -> split residual stages (the last conv writes fp32) -> fp32 avgpool / FC
             fused = self.fuse_stem and first.fs is not None and first.relu
+            if fused and (self.split_streams or 1) > 1 and nb >= 64 and x_is_cuda(img_u8):
+                return self._split_dual_stream(img_u8, start, batch, start_offset, nb)
             parts = self.split_front or 1
             nfront = self._front_blocks() if fused and parts > 1 and nb >= 2 * parts else 0
             if nfront:
@@ -682,7 +691,7 @@ class HipRunner:
 
     def _variant(self) -> tuple:
         """Kernel-choice switches a captured graph depends on (part of its cache key)."""
-        return (self.split, self.split_front, self.winograd, self.wino_variant, self.pack3, self.pack3_f16, self.side_down,
+        return (self.split, self.split_front, self.split_streams, self.winograd, self.wino_variant, self.pack3, self.pack3_f16, self.side_down,
                 self.stem_parts, self.front_split, self.fuse_stem)
 
     def _split_ok(self) -> bool:
@@ -716,6 +725,37 @@ class HipRunner:
         for c in blk.convs[:-1]:
             y = self._conv_split(c, y)
         return self._conv_split(blk.convs[-1], y, residual=idt, out_f32=last, out=out)
+
+    def _split_part(self, img_u8, start, nb, start_offset, window, sub):
+        """Whole split ResNet forward of images [sub, sub + nb) of the window."""
+        o, p, s = self.ops, self.p, self.p.stem
+        if start is not None:
+            x = o.stem_split(img_u8, s.fs, s.b, s.s_scale, start, nb, start_offset, window=window, sub=sub)
+        else:
+            x = o.stem_split(img_u8[sub:sub + nb], s.fs, s.b, s.s_scale)
+        for i, blk in enumerate(p.blocks):
+            x = self._block_split(blk, x, last=i == len(p.blocks) - 1)
+        x = o.global_avgpool(x)
+        for fc in p.fcs:
+            x = o.linear(x, fc.w, fc.b, relu=fc.relu)
+        return x
+
+    def _split_dual_stream(self, img_u8, start, batch, start_offset, nb):
+        """The batch as two halves on two streams (fork/join, kept as parallel
+        branches by hipGraph capture): one half's blocks fill the other's
+        partial last wave of workgroups (layers 3-4 run 1.6-2.4 waves of blocks)."""
+        cur = torch.cuda.current_stream(img_u8.device)
+        side = self._side_stream(img_u8.device)
+        side.wait_stream(cur)
+        n0 = nb // 2
+        window = nb if start is not None else -1
+        l0 = self._split_part(img_u8, start, n0, start_offset, window, 0)
+        with torch.cuda.stream(side):
+            l1 = self._split_part(img_u8, start, nb - n0, start_offset, window, n0)
+        img_u8.record_stream(side)
+        l1.record_stream(cur)
+        cur.wait_stream(side)
+        return torch.cat([l0, l1])
 
     def _split_front_split(self, img_u8, start, batch, start_offset, nfront, parts):
         """Fused split stem + the first ``nfront`` (full-resolution) blocks on

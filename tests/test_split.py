@@ -337,6 +337,11 @@ def test_model_split_vs_fp64_oracle(ops, name, B):
         r.split_front = 2                      # stem + layer1 on batch parts: same numbers
         assert torch.equal(r.logits(img).double().cpu(), got)
         r.split_front = None
+    if name.startswith("resnet") and B >= 64:
+        r.split_streams = 2                    # two half-batch streams: same numbers
+        assert torch.equal(r.logits(img).double().cpu(), got)
+        torch.cuda.synchronize()
+        r.split_streams = None
     n = min(B, 8)
     with torch.no_grad():
         want = m.double()(ref.preprocess_u8(img[:n].cpu()).double())
