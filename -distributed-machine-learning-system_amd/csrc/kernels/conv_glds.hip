@@ -465,6 +465,9 @@ template <bool R, bool F>
 static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
   switch (tile) {
     case 14: glds_cfg<128, 256, 64, 2, 4, 3, R, F, false, true>(a, st); return true;
+    case 15: glds_cfg<64, 128, 64, 1, 4, 3, R, F, false, true>(a, st); return true;    // 72 KiB, 2 stages ahead
+    case 16: glds_cfg<128, 64, 64, 2, 2, 3, R, F, false, true>(a, st); return true;    // 72 KiB, 2 stages ahead
+    case 41: glds_cfg<128, 64, 64, 2, 4, 3, R, F, false, true>(a, st); return true;    // 8 waves, 72 KiB, 2 ahead
     case 17: glds_cfg<256, 128, 64, 4, 2, 3, R, F, false, true>(a, st); return true;
     case 24: glds_cfg<128, 128, 64, 2, 4, 3, R, F, false, true>(a, st); return true;
     case 25: glds_cfg<256, 128, 64, 4, 2, 2, R, F, false, true>(a, st); return true;
