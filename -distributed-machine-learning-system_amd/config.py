@@ -32,6 +32,7 @@ class ClusterConfig:
     max_chunk: int = 1024                    # largest per-worker batch (HBM is not the limit)
     dataset_size: int = 10000                # reference dataset: 10,000 images (report p.1)
     dtype: str = "fp32"                      # executor precision: "fp32" (the reference's) | "fp16"
+    fp32_impl: str = "split"                 # fp32 kernels: "split" (split-fp16, fp32-accurate) | "f32mfma"
     prefetch: bool = True                    # stage the next queued chunk while one computes
     model_seed: int = 0
     data_seed: int = 1234

@@ -33,7 +33,7 @@ constexpr int RC = 66;             // LDS columns per ring row (W + 2 <= 64 read
 constexpr int RB = RC * 256;       // bytes per ring row
 constexpr int RING = 4;
 constexpr int LDS = RING * RB;     // 67,584 B: 2 workgroups per CU
-constexpr int BAND = 8;            // output rows per work item
+constexpr int BAND = 8;            // output rows per work item (at most; fewer for small batches)
 constexpr int NF = 4;              // pixel fragments per row (49 <= W <= 62: all 4 store)
 constexpr int NST = 2 * NF;        // epilogue store instructions per wave and row
 }  // namespace c64s
@@ -45,7 +45,7 @@ struct C64sArgs {
   const half_t* res;    // split [B][H][W][128] or nullptr
   half_t* y;            // split [B][H][W][128]
   const void* zero;     // >= 16 zero bytes
-  int B, H, W, relu, nbands, ntasks;
+  int B, H, W, relu, band, nbands, ntasks;
   float acc_scale;
 };
 
@@ -126,8 +126,8 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
 
   for (int task = blockIdx.x; task < a.ntasks; task += gridDim.x) {
     const int b = task / a.nbands;
-    const int y0 = (task - b * a.nbands) * BAND;
-    const int y1 = min(y0 + BAND, a.H);
+    const int y0 = (task - b * a.nbands) * a.band;
+    const int y1 = min(y0 + a.band, a.H);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();              // previous item's ring reads are done
     c64s_load_row(a, smem, b, y0 - 1, (y0 + 3) & 3, tid);
@@ -249,9 +249,14 @@ void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bia
   a.W = W;
   a.relu = relu;
   a.acc_scale = acc_scale;
-  a.nbands = (H + BAND - 1) / BAND;
-  a.ntasks = B * a.nbands;
   const int per = 2 * device_cu_count();
+  // rows per work item: BAND, or fewer so that a small batch still makes ~2
+  // work items per resident workgroup (each item re-reads 2 halo rows)
+  int band = BAND;
+  while (band > 1 && (long)B * ((H + band - 1) / band) < 2L * per) band /= 2;
+  a.band = band;
+  a.nbands = (H + band - 1) / band;
+  a.ntasks = B * a.nbands;
   const int grid = a.ntasks < per ? a.ntasks : per;
   if (res) {
     ensure_lds_attr(reinterpret_cast<const void*>(conv3x3_split_c64_kernel<true>), LDS);

@@ -50,7 +50,8 @@ def run_node(a) -> int:
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
-    ex = make_executor(a.executor, dev if dev.type == "cuda" else None, seed=cfg.model_seed, dtype=cfg.dtype)
+    ex = make_executor(a.executor, dev if dev.type == "cuda" else None, seed=cfg.model_seed, dtype=cfg.dtype,
+                       fp32_impl=cfg.fp32_impl)
     if cfg.collective_rounds is None:
         # one node per process and per GPU: queries run as RCCL rounds by default
         # (RCCL needs a distinct GPU per rank; nodes sharing a GPU use the TCP path)

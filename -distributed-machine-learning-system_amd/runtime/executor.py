@@ -116,7 +116,7 @@ class HipExecutor(Executor):
     one critical section (results of two chunks must never mix)."""
 
     def __init__(self, device="cuda", seed: int = 0, use_graphs: bool = True, max_graphs: int = 16,
-                 dtype: str = "fp32"):
+                 dtype: str = "fp32", fp32_impl: str = "split"):
         from .. import ops
         from ..models import HipRunner, build_program
 
@@ -124,6 +124,9 @@ class HipExecutor(Executor):
         self.device = torch.device(device)
         self.seed = seed
         self.dtype = dtype
+        if fp32_impl not in ("split", "f32mfma"):
+            raise ValueError(f"fp32_impl must be 'split' or 'f32mfma', got {fp32_impl!r}")
+        self.fp32_impl = fp32_impl      # fp32 programs: split-fp16 kernels or the all-f32-MFMA kernels
         self.use_graphs = use_graphs
         self.max_graphs = max_graphs
         self._HipRunner, self._build = HipRunner, build_program
@@ -146,6 +149,7 @@ class HipExecutor(Executor):
             if r is None:
                 with torch.cuda.device(self.device):
                     r = self._HipRunner(self._build(name, seed=self.seed, dtype=self.dtype), self.device)
+                    r.split = self.fp32_impl == "split"
                 self.runners[name] = r
         return r
 
@@ -247,12 +251,12 @@ class HipExecutor(Executor):
             r.close()
 
 
-def make_executor(kind: str, device=None, seed: int = 0, dtype: str = "fp32") -> Executor:
+def make_executor(kind: str, device=None, seed: int = 0, dtype: str = "fp32", fp32_impl: str = "split") -> Executor:
     kind = kind.lower()
     if kind == "auto":
         kind = "hip" if torch.cuda.is_available() else "torch"
     if kind == "hip":
-        return HipExecutor(device or "cuda", seed=seed, dtype=dtype)
+        return HipExecutor(device or "cuda", seed=seed, dtype=dtype, fp32_impl=fp32_impl)
     if kind == "torch":
         return TorchExecutor(device or "cpu", seed=seed)
     if kind == "fake":

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--kill-coordinator-at-frac", type=float, default=0.0,
                     help="kill the coordinator once this fraction of both jobs' images is done")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--fp32-impl", default="split", choices=["split", "f32mfma"])
     ap.add_argument("--reference-pacing", action="store_true",
                     help="the reference's sleeps: 20 s between a job's queries (:1109), 3 s before each "
                          "chunk (:594), for apples-to-apples query latency (SURVEY.md §7.2 step 7)")
@@ -58,7 +59,7 @@ def main():
 
     def exf(i):
         if a.executor == "hip":
-            return HipExecutor(f"cuda:{i % ngpu}", seed=0)
+            return HipExecutor(f"cuda:{i % ngpu}", seed=0, fp32_impl=a.fp32_impl)
         if a.executor == "torch":
             return TorchExecutor("cpu")
         return FakeExecutor()
@@ -75,7 +76,8 @@ def main():
                      metadata_period_s=0.5, rpc_timeout_s=30.0).start()
     if a.reference_pacing:        # after the cluster is up: the warm-up below runs unpaced
         pacing = dict(client_query_interval_s=20.0, worker_start_delay_s=3.0)
-    out = {"nodes": a.nodes, "gpus": ngpu, "executor": a.executor, "images_per_job": a.images}
+    out = {"nodes": a.nodes, "gpus": ngpu, "executor": a.executor, "images_per_job": a.images,
+           "fp32_impl": a.fp32_impl}
     try:
         cl = c.client(c.cfg.node_name(a.nodes - 2))
         # warm-up: capture graphs for the chunk sizes the fair-time split will produce
