@@ -34,6 +34,8 @@ class ClusterConfig:
     dtype: str = "fp32"                      # executor precision: "fp32" (the reference's) | "fp16"
     fp32_impl: str = "split"                 # fp32 kernels: "split" (split-fp16, fp32-accurate) | "f32mfma"
     prefetch: bool = True                    # stage the next queued chunk while one computes
+    quick_start_wait_s: float = 0.005        # worker: wait this long for a just-queued prefetch before
+                                             # answering the finished chunk first
     model_seed: int = 0
     data_seed: int = 1234
 

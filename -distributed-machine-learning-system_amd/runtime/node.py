@@ -678,6 +678,14 @@ class Node:
         with self._pf_lock:
             fut = self._pf.get(key)
         if fut is not None:
+            # the prefetch was queued a moment ago (start_chunk of the previous
+            # chunk): a synthesised or cached stage completes within a few ms, so
+            # give it that long before treating it as slow -- answering the
+            # finished chunk first would leave the GPU idle while this one stages
+            try:
+                fut.result(timeout=self.cfg.quick_start_wait_s)
+            except Exception:  # noqa: BLE001  (timeout, or a failed prefetch start_chunk reports)
+                pass
             return fut.done()
         cached = getattr(self.source, "cached", None)
         return cached is None or cached(*key)
