@@ -63,9 +63,9 @@ METRIC = "images/sec (whole node) + p50 query latency, ResNet18 bs=400 at 1/2/4/
 QUERY = 400                        # images per query (reference report p.1, ResNet18)
 COMPUTE_F32 = ("f32-input MFMA (v_mfma_f32_16x16x4_f32), fp32 activations/weights, fp32 accumulate; "
                "3x3/s1 convs by fused fp32 Winograd F(2x2,3x3)")
-COMPUTE_SPLIT = ("fp32-accurate: stem/FC on f32-input MFMA; residual-stage convs on split fp16 (each fp32 value "
-                 "as hi+lo halfs, 22-bit significand, 4 bytes; hi*hi+hi*lo+lo*hi on v_mfma_f32_16x16x32_f16, "
-                 "fp32 accumulate); logits checked against fp64 next to torch fp32")
+COMPUTE_SPLIT = ("fp32-accurate: every conv (fused stem, residual stages) on split fp16 (each fp32 value as "
+                 "hi+lo halfs, 22-bit significand, 4 bytes; hi*hi+hi*lo+lo*hi on v_mfma_f32_16x16x32_f16, "
+                 "fp32 accumulate), FC on the f32-input MFMA; logits checked against fp64 next to torch fp32")
 
 
 def parse(argv=None):
@@ -355,6 +355,7 @@ def main(argv=None) -> int:
             "data": "synthetic uint8 224x224x3 images (dataset replicated in every GPU's HBM), random-init weights",
             "config": {"model": a.model, "global_batch": W * B, "seq_len": None, "image_hw": 224,
                        "batch_per_gpu": B, "parallelism": f"dp{W}", "graph": not a.no_graph,
+                       "fp32_impl": a.fp32_impl if a.dtype == "fp32" else None,
                        "compute": (COMPUTE_SPLIT if a.fp32_impl == "split" else COMPUTE_F32) if a.dtype == "fp32" else
                        "f16 MFMA, fp16 activations, fp32 accumulate",
                        "dry_run": a.dry_run},
