@@ -8,10 +8,10 @@ random-init weights (no datasets or checkpoints are reachable).
 Precision: the reference classifies in fp32 (torchvision eager,
 /root/reference/alexnet_resnet.py:17-22, 74-75), so the headline runs the
 framework's fp32 path (``--fp32-impl``):
-  * "split" (default): the stem and FC on the f32-input MFMA, every residual-
-    stage conv on fp32-accurate split fp16 -- each fp32 value carried as
-    (hi, lo) halfs (22 significant bits, 4 bytes like fp32), hi*hi + hi*lo +
-    lo*hi summed in f32 on the f16 MFMA (conv_glds SPLIT);
+  * "split" (default): every conv (the fused stem, the residual stages) on
+    fp32-accurate split fp16 -- each fp32 value carried as (hi, lo) halfs (22
+    significant bits, 4 bytes like fp32), hi*hi + hi*lo + lo*hi summed in f32
+    on the f16 MFMA -- and the FC on the f32-input MFMA;
   * "f32mfma": every conv / FC on v_mfma_f32_16x16x4_f32 (exact f32 products,
     f32 accumulate), 3x3 stride-1 convs by fused fp32 Winograd F(2x2,3x3).
 Both are checked against the fp64 CPU module on the same weights, next to
