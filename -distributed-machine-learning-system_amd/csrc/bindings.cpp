@@ -902,24 +902,29 @@ torch::Tensor stem_fused(torch::Tensor img, torch::Tensor w, torch::Tensor bias,
 }
 
 // uint8 [B,H,W,3] -> split-fp16 [B,Hp,Wp,128] = maxpool3x3/2(relu(conv7x7/2(normalise(img)) + bias)),
-// fp32-accurate; w = [2, 64, 7*32] half (models/packed.py pack_stem_split), acc_scale = 2^-e
-torch::Tensor stem_split(torch::Tensor img, torch::Tensor w, torch::Tensor bias, double acc_scale,
+// fp32-accurate; (w, bias, psum, acc_scale) = models/packed.py pack_stem_split
+torch::Tensor stem_split(torch::Tensor img, torch::Tensor w, torch::Tensor bias, torch::Tensor psum, double acc_scale,
                          c10::optional<torch::Tensor> start, int64_t batch, int64_t start_offset, int64_t window,
                          int64_t sub) {
   CHECK_DEV(img);
   CHECK_DEV(w);
   CHECK_DEV(bias);
+  CHECK_DEV(psum);
   CHECK_CONTIG(img);
   CHECK_CONTIG(w);
   CHECK_CONTIG(bias);
+  CHECK_CONTIG(psum);
   CHECK_DT(img, torch::kUInt8);
   CHECK_DT(w, torch::kHalf);
   CHECK_DT(bias, torch::kFloat);
-  TORCH_CHECK(w.device() == img.device() && bias.device() == img.device(), "operands on different devices");
+  CHECK_DT(psum, torch::kFloat);
+  TORCH_CHECK(w.device() == img.device() && bias.device() == img.device() && psum.device() == img.device(),
+              "operands on different devices");
   TORCH_CHECK(img.dim() == 4 && img.size(3) == 3, "img must be [B, H, W, 3] uint8");
   TORCH_CHECK(w.dim() == 3 && w.size(0) == 2 && w.size(1) == 64 && w.size(2) == 7 * 32,
               "split stem weight must be [2, 64, 7*32]");
   TORCH_CHECK(bias.numel() == 64, "bias must have 64 entries");
+  TORCH_CHECK(psum.numel() == 8 * 8 * 64, "psum must be [8, 8, 64]");
   const int H = img.size(1), W = img.size(2);
   int B;
   long long max_start;
@@ -932,8 +937,8 @@ torch::Tensor stem_split(torch::Tensor img, torch::Tensor w, torch::Tensor bias,
   auto y = torch::empty({B, Hp, Wp, 128}, img.options().dtype(torch::kHalf));
   if (B) {
     stem_split_launch(img.data_ptr<uint8_t>(), reinterpret_cast<const half_t*>(w.data_ptr()), bias.data_ptr<float>(),
-                      (float)acc_scale, reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp, start_offset, max_start,
-                      sp ? sub : 0, cur_stream());
+                      psum.data_ptr<float>(), (float)acc_scale, reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp,
+                      start_offset, max_start, sp ? sub : 0, cur_stream());
     check_launch("stem_split");
   }
   return y;
@@ -1141,7 +1146,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("img"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("start") = py::none(),
         py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1, py::arg("sub") = 0);
   m.def("stem_split", &stem_split, "fp32-accurate fused split-fp16 ResNet stem (normalise+conv7x7/2+relu+maxpool)",
-        py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("acc_scale"), py::arg("start") = py::none(),
+        py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("psum"), py::arg("acc_scale"), py::arg("start") = py::none(),
         py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1, py::arg("sub") = 0);
   m.def("linear_split", &linear_split, "fp32-accurate FC on split fp16, split-K in one launch + combine",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("acc_scale"), py::arg("relu"), py::arg("out_f32"),
@@ -1151,6 +1156,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_split_norder", &set_split_norder, "A/B: split conv tile order (0 m-major, 1 n-major, -1 auto)");
   m.def("set_split_patch_default", &set_split_patch_default,
         "A/B: route split 3x3/s1 convs (Cout % 128 == 0) to the halo-patch kernel (tile 60)");
+  m.def("set_stem_split_niw", [](int64_t n) { set_stem_split_niw((int)n); },
+        "A/B: fused split stem, 16-cout A fragments per wave (1 default: 3 workgroups/CU; 2)");
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");
   m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),

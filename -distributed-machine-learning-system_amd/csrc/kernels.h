@@ -150,11 +150,13 @@ void conv3x3_c64_launch(const half_t* x, const half_t* w, const float* bias, con
 void conv3x3_patch_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
                           const void* zero, int B, int H, int W, int C, int Cout, int relu, hipStream_t st);
 int conv_glds_pick(int M, int Cout);
-// split-fp16 (fp32-accurate) fused stem: w = [2][64][7*32] (hi, lo; pre-scaled by
-// 1/acc_scale), y = split layout [B][Hp][Wp][128]
-void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, float acc_scale, half_t* y, int B,
-                       int H, int W, const long long* start_idx, long long start_off, long long max_start,
-                       long long sub, hipStream_t st);
+// split-fp16 (fp32-accurate) fused stem, exact-u8 form: w = [2][64][7*32] hi/lo of
+// w * s_c (pre-scaled by 1/acc_scale), bias = folded bias + full sum of w * c_c,
+// psum = [8][8][64] 2D prefix sums of w * c_c over (kh, kw); y = split [B][Hp][Wp][128]
+void set_stem_split_niw(int n);   // A/B: 16-cout fragments per wave (1 default, 2)
+void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
+                       half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,
+                       long long max_start, long long sub, hipStream_t st);
 void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, half_t* y, int B, int H, int W,
                        const long long* start_idx, long long start_off, long long max_start, long long sub,
                        hipStream_t st);

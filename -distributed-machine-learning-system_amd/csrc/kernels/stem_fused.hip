@@ -340,29 +340,33 @@ void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, h
 
 // ============================================================================
 // Split-fp16 (fp32-accurate) fused stem: same tiling as stem_fused_kernel, for
-// the fp32 programs.  Every value is carried as hi + lo halfs (common.h
-// split_f16x4): the normalised patch is stored twice (hi plane, lo plane), the
-// weights come as hi and lo fragments pre-scaled by 2^e, and each K stage runs
-// hi*hi + hi*lo + lo*hi (3 f16 MFMAs).  The pool runs on the f32 accumulators
-// (DPP horizontal 3-max, f32 LDS tile for the vertical 3-max); the 2^-e scale,
-// bias and ReLU are applied after the max (all commute with it) and the
-// pooled result is written in the split layout [B][Hp][Wp][128 halfs].
-// Replaces preprocess_pack3_split + conv2d_pack3_split + maxpool_split (three
-// passes over ~3 GB at B = 400).
+// the fp32 programs.  Exact-u8 formulation: the normalised input is
+// x = u * s_c + c_c (u the uint8 byte, s_c = 1/(255 std_c), c_c = -mean_c/std_c),
+// so conv(x) = conv'(u) + C(oy, ox) with w' = w * s_c and C the sum of
+// w * c_c over the taps that fall inside the image.  u is an integer <= 255 and
+// therefore EXACT in fp16: the B operand needs no lo part, and each K stage is
+// w'_hi*u + w'_lo*u -- 2 f16 MFMAs instead of 3, one patch plane instead of two,
+// and the patch store is a byte -> half conversion.  C(oy, ox) is the bias for
+// interior pixels (host-folded) plus a border delta from a 2D prefix-sum table
+// of w * c over (kh, kw), added to the accumulators before the max pool (it
+// depends on the position).  Then as before: DPP horizontal 3-max on the f32
+// accumulators, f32 LDS vertical 3-max, x 2^-e, + bias, ReLU, split store
+// [B][Hp][Wp][128 halfs].  Replaces preprocess_pack3_split + conv2d_pack3_split
+// + maxpool_split (three passes over ~3 GB at B = 400).
 namespace stem_s {
-constexpr int PLANE = stem::PATCH_BYTES;                  // lo plane follows the hi plane
-constexpr int PATCH2 = 2 * stem::PATCH_BYTES;             // 28704
 constexpr int HP_BYTES = stem::CRY * stem::PTX * 256;     // [conv row][pooled col][64 ch] f32 = 30464
-constexpr int LDS = PATCH2 + HP_BYTES;                    // 59168: 2 workgroups per CU
-constexpr int WGS = 2;
+constexpr int LDS = stem::PATCH_BYTES + HP_BYTES;         // 44816
 }  // namespace stem_s
+static int g_stem_split_niw = 1;   // measured: 399 vs 461 us at B = 400 (profiles/r2_v28_stem_split_u8.md)
+void set_stem_split_niw(int n) { g_stem_split_niw = n == 1 ? 1 : 2; }
 
 // f32 tile offset of 4-channel chunk c (0..15) of (conv row r, pooled col px),
 // chunk XOR-swizzled by px
 __device__ __forceinline__ int hp32_off(int r, int px, int c) { return (r * stem::PTX + px) * 256 + ((c ^ px) << 4); }
 
-// registers -> normalised split patch (hi plane, lo plane) in LDS
-__device__ __forceinline__ void store_patch_split(char* patch, const StemGeom& g, int t, int tid, const Quads& q) {
+// registers -> u8 values as fp16 in LDS ([row][col][4], channel 3 and
+// out-of-image pixels 0)
+__device__ __forceinline__ void store_patch_u8(char* patch, const StemGeom& g, int t, int tid, const Quads& q) {
   using namespace stem;
   int b, py0, px0;
   tile_coords(g, t, b, py0, px0);
@@ -372,28 +376,20 @@ __device__ __forceinline__ void store_patch_split(char* patch, const StemGeom& g
     const int i = tid + 256 * k;
     if (i >= NQUAD) continue;
     const int r = i / QPR, qc = i - r * QPR;
-    float f[12];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) f[j] = (float)((q.d[k][j >> 2] >> (8 * (j & 3))) & 0xFFu);
     const int x0 = ixa + 4 * qc;
     const bool edge = !(q.ok[k] && x0 >= 0 && x0 + 3 < g.W);
-    half4v ph[4], pl[4];
+    half4v px[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float2v rg = float2v{f[3 * j], f[3 * j + 1]} * kScaleRG + kShiftRG;
-      const float bb = f[3 * j + 2] * kSB + kCB;
-      float4v v = float4v{rg[0], rg[1], bb, 0.f};
-      if (edge && (!q.ok[k] || (unsigned)(x0 + j) >= (unsigned)g.W)) v = float4v{0.f, 0.f, 0.f, 0.f};
-      split_f16x4(v, ph[j], pl[j]);
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) px[j][ch] = (half_t)(float)((q.d[k][(3 * j + ch) >> 2] >> (8 * ((3 * j + ch) & 3))) & 0xFFu);
+      px[j][3] = (half_t)0.f;
+      if (edge && (!q.ok[k] || (unsigned)(x0 + j) >= (unsigned)g.W)) px[j] = half4v{0, 0, 0, 0};
     }
     char* d = patch + (r * IPC + 4 * qc + PCO - 3) * 8;
-    *reinterpret_cast<half4v*>(d) = ph[0];
-    *reinterpret_cast<half8v*>(d + 8) = __builtin_shufflevector(ph[1], ph[2], 0, 1, 2, 3, 4, 5, 6, 7);
-    *reinterpret_cast<half4v*>(d + 24) = ph[3];
-    d += stem_s::PLANE;
-    *reinterpret_cast<half4v*>(d) = pl[0];
-    *reinterpret_cast<half8v*>(d + 8) = __builtin_shufflevector(pl[1], pl[2], 0, 1, 2, 3, 4, 5, 6, 7);
-    *reinterpret_cast<half4v*>(d + 24) = pl[3];
+    *reinterpret_cast<half4v*>(d) = px[0];
+    *reinterpret_cast<half8v*>(d + 8) = __builtin_shufflevector(px[1], px[2], 0, 1, 2, 3, 4, 5, 6, 7);
+    *reinterpret_cast<half4v*>(d + 24) = px[3];
   }
 }
 
@@ -403,10 +399,20 @@ __device__ __forceinline__ float row_shl_f32(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x100 | N, 0xF, 0xF, true));
 }
 
-__global__ void __launch_bounds__(256, stem_s::WGS)
+// valid kernel-tap range [lo, hi) of conv output coordinate o (stride 2, pad 3)
+__device__ __forceinline__ void tap_range(int o, int n, int& lo, int& hi) {
+  lo = max(0, stem::CP - stem::CS * o);
+  hi = min(stem::KH, n + stem::CP - stem::CS * o);
+}
+
+// NIWS: 16-cout A fragments per wave (2: two waves share a conv row, 2
+// workgroups per CU by registers; 1: every wave takes all rows for its 16
+// couts, half the A registers, 3 workgroups per CU)
+template <int NIWS>
+__global__ void __launch_bounds__(256, NIWS == 1 ? 3 : 2)
 stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w, const float* __restrict__ bias,
-                  float acc_scale, half_t* __restrict__ y, const StemGeom g, const long long* __restrict__ start_idx,
-                  long long start_off, long long max_start, long long sub) {
+                  const float* __restrict__ psum, float acc_scale, half_t* __restrict__ y, const StemGeom g,
+                  const long long* __restrict__ start_idx, long long start_off, long long max_start, long long sub) {
   using namespace stem;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (start_idx != nullptr) {
@@ -415,7 +421,7 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
     img += (size_t)s * g.H * g.W * 3;
   }
   char* patch = smem;
-  char* hp = smem + stem_s::PATCH2;
+  char* hp = smem + PATCH_BYTES;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
   int t = blockIdx.x;
@@ -424,7 +430,8 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
   Quads q;
   load_quads(img, g, t, tid, q);
 
-  // ---- A fragments: hi and lo weights [2][cout][kh][32], registers, once ----
+  // ---- A fragments: hi and lo of w' = w * s_c, [2][cout][kh][32], registers, once ----
+  constexpr int NIW = NIWS, NCH = 4 / NIWS;
   const int frow = lane & 15, fch = lane >> 4;
   const int ch0 = (wave % NCH) * NIW;
   half8v fah[KH][NIW], fal[KH][NIW];
@@ -436,8 +443,9 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
       fah[kh][i] = *reinterpret_cast<const half8v*>(w + o);
       fal[kh][i] = *reinterpret_cast<const half8v*>(w + 64 * KH * 32 + o);
     }
+  const float inv_scale = 1.f / acc_scale;           // 2^e: border deltas in accumulator units
 
-  store_patch_split(patch, g, t, tid, q);
+  store_patch_u8(patch, g, t, tid, q);
   int tn = t + gridDim.x;
   if (tn < g.ntiles) load_quads(img, g, tn, tid, q);
   __syncthreads();
@@ -457,6 +465,9 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
     const int oy0 = py0 * PS - PP, ox0 = px0 * PS - PP;
     const bool colv = cx < CRX && (unsigned)(ox0 + cx) < (unsigned)g.Wc;
     const bool interior = ox0 >= 0 && ox0 + CRX <= g.Wc;
+    // conv columns of this lane whose taps leave the image: border delta needed
+    int wlo, whi;
+    tap_range(ox0 + cx, g.W, wlo, whi);
 
     for (int f = wave / NCH; f < CRY; f += 4 / NCH) {
       const char* pb = patch + ((2 * f) * IPC + 2 * cx + 2 * fch + PCO) * 8;
@@ -465,19 +476,34 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
       for (int i = 0; i < NIW; ++i) acc[i] = float4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kh = 0; kh < KH; ++kh) {
-        const half8v bh = *reinterpret_cast<const half8v*>(pb + kh * IPC * 8);
-        const half8v bl = *reinterpret_cast<const half8v*>(pb + stem_s::PLANE + kh * IPC * 8);
+        const half8v bu = *reinterpret_cast<const half8v*>(pb + kh * IPC * 8);
 #pragma unroll
         for (int i = 0; i < NIW; ++i) {
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[kh][i], bh, acc[i], 0, 0, 0);
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[kh][i], bl, acc[i], 0, 0, 0);
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh][i], bh, acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[kh][i], bu, acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh][i], bu, acc[i], 0, 0, 0);
         }
       }
-      // horizontal 3-max on the raw f32 accumulators; outside the image the
-      // conv output is the pool's -inf padding
+      const int oy = oy0 + f;
+      const bool rowv = (unsigned)oy < (unsigned)g.Hc;    // wave-uniform
+      int hlo, hhi;
+      tap_range(oy, g.H, hlo, hhi);
+      if (rowv && (hlo > 0 || hhi < KH || wlo > 0 || whi < KH)) {
+        // border pixel: add (sum of w*c over its valid taps) - (the full sum in
+        // the bias), from the 2D prefix sums psum[kh][kw][64] (kh, kw in 0..7)
+#pragma unroll
+        for (int i = 0; i < NIW; ++i) {
+          const int co = (ch0 + i) * 16 + fch * 4;
+          const float4v s_hh = *reinterpret_cast<const float4v*>(psum + (hhi * 8 + whi) * 64 + co);
+          const float4v s_lh = *reinterpret_cast<const float4v*>(psum + (hlo * 8 + whi) * 64 + co);
+          const float4v s_hl = *reinterpret_cast<const float4v*>(psum + (hhi * 8 + wlo) * 64 + co);
+          const float4v s_ll = *reinterpret_cast<const float4v*>(psum + (hlo * 8 + wlo) * 64 + co);
+          const float4v s_ff = *reinterpret_cast<const float4v*>(psum + (7 * 8 + 7) * 64 + co);
+          acc[i] += (s_hh - s_lh - s_hl + s_ll - s_ff) * inv_scale;
+        }
+      }
+      // horizontal 3-max on the f32 accumulators; outside the image the conv
+      // output is the pool's -inf padding
       float4v o[NIW];
-      const bool rowv = (unsigned)(oy0 + f) < (unsigned)g.Hc;   // wave-uniform
 #pragma unroll
       for (int i = 0; i < NIW; ++i) {
 #pragma unroll
@@ -498,7 +524,7 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
 
     const int tnext = tn;
     if (tnext < g.ntiles) {
-      store_patch_split(patch, g, tnext, tid, q);
+      store_patch_u8(patch, g, tnext, tid, q);
       tn = tnext + gridDim.x;
       if (tn < g.ntiles) load_quads(img, g, tn, tid, q);
     }
@@ -512,11 +538,11 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
         a[r][0] = *reinterpret_cast<const float4v*>(hp + hp32_off(r0 + r, vpx, 2 * c8));
         a[r][1] = *reinterpret_cast<const float4v*>(hp + hp32_off(r0 + r, vpx, 2 * c8 + 1));
       }
-      const int ox = px0 + vpx, oy = py0 + 2 * vpy2;
+      const int ox = px0 + vpx, oyp = py0 + 2 * vpy2;
       if (ox < g.Wp) {
 #pragma unroll
         for (int hr = 0; hr < 2; ++hr) {
-          if (oy + hr >= g.Hp) break;
+          if (oyp + hr >= g.Hp) break;
           const int rr = 2 * hr;
           float4v m0, m1;
 #pragma unroll
@@ -529,7 +555,7 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
           half4v h0, l0, h1, l1;
           split_f16x4(m0, h0, l0);
           split_f16x4(m1, h1, l1);
-          half_t* dst = y + (((size_t)b * g.Hp + oy + hr) * g.Wp + ox) * 128 + split_off(8 * c8);
+          half_t* dst = y + (((size_t)b * g.Hp + oyp + hr) * g.Wp + ox) * 128 + split_off(8 * c8);
           *reinterpret_cast<half8v*>(dst) = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
           *reinterpret_cast<half8v*>(dst + 32) = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
         }
@@ -541,9 +567,9 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
   }
 }
 
-void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, float acc_scale, half_t* y, int B,
-                       int H, int W, const long long* start_idx, long long start_off, long long max_start,
-                       long long sub, hipStream_t st) {
+void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
+                       half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,
+                       long long max_start, long long sub, hipStream_t st) {
   using namespace stem;
   StemGeom g;
   g.B = B;
@@ -557,11 +583,15 @@ void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, f
   g.tiles_y = (g.Hp + PTY - 1) / PTY;
   g.ntiles = B * g.tiles_x * g.tiles_y;
   g.ablate = 0;
-  const int per = stem_s::WGS * device_cu_count();
+  const int wgs = g_stem_split_niw == 1 ? 3 : 2;
+  const int per = wgs * device_cu_count();
   const int grid = g.ntiles < per ? g.ntiles : per;
-  ensure_lds_attr(reinterpret_cast<const void*>(stem_split_kernel), stem_s::LDS);
-  hipLaunchKernelGGL(stem_split_kernel, dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias, acc_scale, y, g,
-                     start_idx, start_off, max_start, sub);
+  if (g_stem_split_niw == 1)
+    hipLaunchKernelGGL(stem_split_kernel<1>, dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias, psum, acc_scale,
+                       y, g, start_idx, start_off, max_start, sub);
+  else
+    hipLaunchKernelGGL(stem_split_kernel<2>, dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias, psum, acc_scale,
+                       y, g, start_idx, start_off, max_start, sub);
 }
 
 }  // namespace idunno

@@ -52,6 +52,9 @@ class Conv:
     s_scale: float = 1.0               # accumulator scale of ``sw`` / ``sp3`` (2^-e)
     sp3: torch.Tensor | None = None    # fp32 RGB stems: split-fp16 packed-row weights (pack_split_weight_p3)
     fs: torch.Tensor | None = None     # fp32 ResNet 7x7/2 stem: fused split stem weights (pack_stem_split)
+    fs_bias: torch.Tensor | None = None  # ... its bias (with the normalisation shift folded in)
+    fs_psum: torch.Tensor | None = None  # ... its border-correction prefix sums [8, 8, 64]
+    fs_scale: float = 1.0              # ... its accumulator scale 2^-e
 
     def to(self, device):
         return Conv(self.w.to(device), self.b.to(device), self.cin, self.cout, self.kh, self.kw,
@@ -60,7 +63,9 @@ class Conv:
                     None if self.p3 is None else self.p3.to(device),
                     None if self.sw is None else self.sw.to(device), self.s_scale,
                     None if self.sp3 is None else self.sp3.to(device),
-                    None if self.fs is None else self.fs.to(device))
+                    None if self.fs is None else self.fs.to(device),
+                    None if self.fs_bias is None else self.fs_bias.to(device),
+                    None if self.fs_psum is None else self.fs_psum.to(device), self.fs_scale)
 
     @property
     def flops_per_out_pixel(self) -> int:
@@ -284,20 +289,39 @@ def pack_split_weight_p3(w: torch.Tensor) -> tuple[torch.Tensor, float]:
     return packed.contiguous(), 2.0 ** -e
 
 
-def pack_stem_split(w: torch.Tensor) -> tuple[torch.Tensor, float]:
-    """ResNet stem [64, 3, 7, 7] -> fused split stem weights [2, 64, 7*32] half
-    (hi, lo) for stem_split_kernel: per kernel row 8 taps x 4 channels (tap 7
-    and channel 3 zero), scaled by 2^e like pack_split_weight."""
+def pack_stem_split(w: torch.Tensor, b: torch.Tensor | None = None):
+    """ResNet stem [64, 3, 7, 7] (+ bias [64]) -> operands of the fused split stem
+    (stem_fused.hip stem_split_kernel, exact-u8 form):
+
+      fs     [2, 64, 7*32] half: hi and lo of w' = w * s_c, s_c = 1/(255 std_c),
+             per kernel row 8 taps x 4 channels (tap 7, channel 3 zero), scaled
+             by 2^e like pack_split_weight;
+      scale  2^-e;
+      bias   [64] f32: b + sum over all taps of w * c_c, c_c = -mean_c / std_c
+             (the normalisation's shift for a pixel whose taps are all inside);
+      psum   [8, 8, 64] f32: 2D prefix sums over (kh, kw) of sum_c w * c_c, from
+             which the kernel corrects border pixels (zero padding in x, not u).
+
+    conv(normalise(u)) = conv(w', u) + sum_{valid taps} w * c: u <= 255 is
+    exact in fp16, so the B operand needs no lo part."""
     cout, cin, kh, kw = w.shape
     if (cout, cin, kh, kw) != (64, 3, 7, 7):
         raise ValueError("the fused split stem takes a [64, 3, 7, 7] conv")
+    w = w.double()
+    mean = torch.tensor(ref.IMAGENET_MEAN, dtype=torch.float64)
+    std = torch.tensor(ref.IMAGENET_STD, dtype=torch.float64)
+    ws = w * (1.0 / (255.0 * std)).view(1, 3, 1, 1)
     p = torch.zeros(cout, kh, 8, 4, dtype=torch.float64)
-    p[:, :, :kw, :cin] = w.double().permute(0, 2, 3, 1)
-    e = _split_scale(w)
+    p[:, :, :kw, :cin] = ws.permute(0, 2, 3, 1)
+    e = _split_scale(ws)
     p = p.reshape(cout, kh * 32) * (2.0 ** e)
     hi = p.half()
     lo = (p - hi.double()).half()
-    return torch.stack([hi, lo]).contiguous(), 2.0 ** -e
+    corr = (w * (-mean / std).view(1, 3, 1, 1)).sum(dim=1)            # [64, 7, 7]
+    ps = torch.zeros(8, 8, cout, dtype=torch.float64)
+    ps[1:, 1:] = corr.permute(1, 2, 0).cumsum(0).cumsum(1)
+    bias = (torch.zeros(cout, dtype=torch.float64) if b is None else b.double()) + ps[7, 7]
+    return torch.stack([hi, lo]).contiguous(), 2.0 ** -e, bias.float().contiguous(), ps.float().contiguous()
 
 
 def unpack_split_weight(c: "Conv") -> torch.Tensor:
@@ -339,11 +363,11 @@ def make_conv(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, relu: bool, dtype: str
     if dtype == "fp32" and pack3_eligible(conv.in_channels, conv.kernel_size[1], conv.stride[0], "fp16") \
             and conv.out_channels % 64 == 0:
         sp3, s_scale = pack_split_weight_p3(fold_bn_f64(conv.weight, conv.bias, bn)[0])
-    fs = None
+    c = Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, conv.kernel_size[0],
+             conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small, None, p3, sw, s_scale, sp3)
     if dtype == "fp32" and tuple(conv.weight.shape) == (64, 3, 7, 7) and conv.stride[0] == 2 and conv.padding[0] == 3:
-        fs, _ = pack_stem_split(fold_bn_f64(conv.weight, conv.bias, bn)[0])   # same 2^-e as sp3
-    return Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, conv.kernel_size[0],
-                conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small, None, p3, sw, s_scale, sp3, fs)
+        c.fs, c.fs_scale, c.fs_bias, c.fs_psum = pack_stem_split(*fold_bn_f64(conv.weight, conv.bias, bn))
+    return c
 
 
 def make_fc(lin: nn.Linear, relu: bool, perm: torch.Tensor | None = None, dtype: str = "fp16") -> Conv:
@@ -582,7 +606,8 @@ class HipRunner:
             if nfront:
                 x = self._split_front_split(img_u8, start, batch, start_offset, nfront, parts)
             elif fused:
-                x = o.stem_split(img_u8, first.fs, first.b, first.s_scale, start, batch, start_offset)
+                x = o.stem_split(img_u8, first.fs, first.fs_bias, first.fs_psum, first.fs_scale, start, batch,
+                                 start_offset)
             else:
                 x = o.maxpool2d_split(self._stem_f32(first, img_u8, start, batch, start_offset), 3, 2, 1)
             for i, blk in enumerate(p.blocks[nfront:], nfront):
@@ -730,9 +755,10 @@ class HipRunner:
         """Whole split ResNet forward of images [sub, sub + nb) of the window."""
         o, p, s = self.ops, self.p, self.p.stem
         if start is not None:
-            x = o.stem_split(img_u8, s.fs, s.b, s.s_scale, start, nb, start_offset, window=window, sub=sub)
+            x = o.stem_split(img_u8, s.fs, s.fs_bias, s.fs_psum, s.fs_scale, start, nb, start_offset,
+                             window=window, sub=sub)
         else:
-            x = o.stem_split(img_u8[sub:sub + nb], s.fs, s.b, s.s_scale)
+            x = o.stem_split(img_u8[sub:sub + nb], s.fs, s.fs_bias, s.fs_psum, s.fs_scale)
         for i, blk in enumerate(p.blocks):
             x = self._block_split(blk, x, last=i == len(p.blocks) - 1)
         x = o.global_avgpool(x)
@@ -769,9 +795,10 @@ class HipRunner:
         for sub in range(0, B, n):
             nb = min(n, B - sub)
             if start is not None:
-                x = o.stem_split(img_u8, s.fs, s.b, s.s_scale, start, nb, start_offset, window=B, sub=sub)
+                x = o.stem_split(img_u8, s.fs, s.fs_bias, s.fs_psum, s.fs_scale, start, nb, start_offset, window=B,
+                                 sub=sub)
             else:
-                x = o.stem_split(img_u8[sub:sub + nb], s.fs, s.b, s.s_scale)
+                x = o.stem_split(img_u8[sub:sub + nb], s.fs, s.fs_bias, s.fs_psum, s.fs_scale)
             for bi in range(nfront):
                 blk = self.p.blocks[bi]
                 if bi < nfront - 1:

@@ -39,12 +39,12 @@ def conv2d_pack3_split(x3, w, bias, acc_scale: float, width: int, kh: int, kw: i
     return load().conv2d_pack3_split(x3, w, bias, width, kh, kw, stride, pad, relu, acc_scale, tile)
 
 
-def stem_split(img_u8, w, bias, acc_scale: float, start=None, batch: int = -1, start_offset: int = 0,
+def stem_split(img_u8, w, bias, psum, acc_scale: float, start=None, batch: int = -1, start_offset: int = 0,
                window: int = -1, sub: int = 0):
     """fp32-accurate fused ResNet stem on split fp16: uint8 [B,224,224,3] ->
     split [B,56,56,128] (normalise, conv 7x7/2 + bias, ReLU, max pool 3x3/2);
-    ``w``, ``acc_scale`` = models.packed.pack_stem_split(w)."""
-    return load().stem_split(img_u8, w, bias, acc_scale, start, batch, start_offset, window, sub)
+    ``w, acc_scale, bias, psum`` = models.packed.pack_stem_split(w, b)."""
+    return load().stem_split(img_u8, w, bias, psum, acc_scale, start, batch, start_offset, window, sub)
 
 
 def split_linear_splits(m: int, k: int, n: int) -> int:

@@ -81,6 +81,32 @@ def test_pack_split_weight_p3_cpu(kh, kw):
     assert p.stem.sp3 is not None
     assert P.build_program("alexnet", dtype="fp32").features[0][1].sp3 is not None
     assert p.stem.fs is not None and p.stem.fs.shape == (2, 64, 224)
+    assert p.stem.fs_psum.shape == (8, 8, 64) and p.stem.fs_bias.shape == (64,)
+
+
+def test_pack_stem_split_exact_u8_cpu():
+    """conv(normalise(u)) == conv(w * s, u) + border-corrected sum of w * c (fp64)."""
+    from idunno.models import reference as ref
+
+    torch.manual_seed(3)
+    w = torch.randn(64, 3, 7, 7) * 0.05
+    b = torch.randn(64) * 0.1
+    fs, scale, bias, psum = P.pack_stem_split(w, b)
+    u = torch.randint(0, 256, (2, 30, 26, 3), dtype=torch.uint8)
+    want = F.conv2d(ref.preprocess_u8(u).double(), w.double(), b.double(), 2, 3)
+    v = fs.double().reshape(2, 64, 7, 8, 4)
+    ws = ((v[0] + v[1]) * scale)[:, :, :7, :3].permute(0, 3, 1, 2)            # w * s_c [64, 3, 7, 7]
+    got = F.conv2d(u.permute(0, 3, 1, 2).double(), ws, bias.double(), 2, 3)
+    H, W = 30, 26
+    for oy in range(got.shape[2]):
+        hlo, hhi = max(0, 3 - 2 * oy), min(7, H + 3 - 2 * oy)
+        for ox in range(got.shape[3]):
+            wlo, whi = max(0, 3 - 2 * ox), min(7, W + 3 - 2 * ox)
+            ps = psum.double()
+            d = ps[hhi, whi] - ps[hlo, whi] - ps[hhi, wlo] + ps[hlo, wlo] - ps[7, 7]
+            got[:, :, oy, ox] += d
+    err = ((got - want).abs().max() / want.abs().max()).item()
+    assert err < 1e-6, err
 
 
 def _emu_split_conv(x, sw, scale, cout, cin, k, stride, pad):
@@ -268,7 +294,8 @@ def test_stem_pack3_split(ops, kh, stride, pad, B, tile):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,hw", [(3, 224), (2, 100), (1, 37)])
-def test_stem_split_fused(ops, B, hw):
+@pytest.mark.parametrize("niw", [2, 1])
+def test_stem_split_fused(ops, B, hw, niw):
     """uint8 -> normalise -> conv7x7/2 -> +bias -> ReLU -> maxpool3x3/2, split out."""
     from idunno.models import reference as ref
 
@@ -276,8 +303,12 @@ def test_stem_split_fused(ops, B, hw):
     img = torch.randint(0, 256, (B, hw, hw, 3), dtype=torch.uint8, device=DEV)
     w = torch.randn(64, 3, 7, 7) / (3 * 49) ** 0.5
     b = torch.randn(64) * 0.1
-    fs, scale = P.pack_stem_split(w)
-    y = ops.stem_split(img, fs.to(DEV), b.to(DEV), scale)
+    fs, scale, bias, psum = P.pack_stem_split(w, b)
+    ops.load().set_stem_split_niw(niw)
+    try:
+        y = ops.stem_split(img, fs.to(DEV), bias.to(DEV), psum.to(DEV), scale)
+    finally:
+        ops.load().set_stem_split_niw(1)
     x = ref.preprocess_u8(img).permute(0, 2, 3, 1)
     want = _ref64(x, w, b, 2, 3, True).permute(0, 3, 1, 2)
     want = F.max_pool2d(want, 3, 2, 1).permute(0, 2, 3, 1)

@@ -36,10 +36,13 @@ def main():
             print(f"| {name} split | {t} | {us:.0f} | {pre:.0f} |", flush=True)
         if kh == 7:
             from idunno.models.packed import pack_stem_split
-            fs, fsc = pack_stem_split(w)
-            fs = fs.to(dev)
-            us = timeit(lambda: ops.stem_split(img, fs, b, fsc))
-            print(f"| {name} fused split stem (+relu+maxpool, no preprocess) | - | {us:.0f} | 0 |", flush=True)
+            fs, fsc, fsb, fsp = (t.to(dev) if torch.is_tensor(t) else t for t in pack_stem_split(w))
+            for niw in (2, 1):
+                ops.load().set_stem_split_niw(niw)
+                us = timeit(lambda: ops.stem_split(img, fs, fsb, fsp, fsc))
+                print(f"| {name} fused split stem (+relu+maxpool, no preprocess), {niw} cout fragments/wave | - |"
+                      f" {us:.0f} | 0 |", flush=True)
+            ops.load().set_stem_split_niw(1)
             x = torch.empty(a.batch, 112, 112, 64, device=dev)
             us = timeit(lambda: ops.maxpool2d_split(x, 3, 2, 1))
             print(f"| maxpool f32 -> split (unfused path) | - | {us:.0f} | - |", flush=True)
