@@ -1158,6 +1158,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "A/B: route split 3x3/s1 convs (Cout % 128 == 0) to the halo-patch kernel (tile 60)");
   m.def("set_stem_split_niw", [](int64_t n) { set_stem_split_niw((int)n); },
         "A/B: fused split stem, 16-cout A fragments per wave (1 default: 3 workgroups/CU; 2)");
+  m.def("set_split_wide_tile", &set_split_wide_tile, "A/B: 128x160 split tiles for M < 50000 (layer4; default on)");
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");
   m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),

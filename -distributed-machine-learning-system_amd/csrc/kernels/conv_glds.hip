@@ -60,7 +60,8 @@ __device__ __forceinline__ void wait_stages(int pending_stages) {
 // out in the same split layout (or fp32 with OUT_F32).
 template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false,
           bool SPLIT = false>
-__global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs a) {
+__global__ void __launch_bounds__(64 * WN * WM, (BM % 64 != 0 && WN * WM == 8) ? 4 : 1)   // 2nd: min waves per SIMD
+conv_glds_kernel(const ConvArgs a) {
   static_assert(!SPLIT || BK == 64, "split stages are 32 channels x (hi, lo)");
   constexpr int NW = WN * WM;
   constexpr int NT = 64 * NW;
@@ -69,10 +70,13 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
   constexpr int CPR = BK / 8;                 // 16-byte chunks per row
   constexpr int RB = BK * 2;                  // bytes per row
   constexpr int RPI = 64 / CPR;               // rows per DMA instruction (1 KiB)
-  constexpr int A_INS = BN / RPI, B_INS = BM / RPI;
+  // B rows staged per stage: BM rounded up to whole DMA instructions per wave
+  // (rows BM.. BMD-1 load zeros and are never read; e.g. BM 160 on 8 waves)
+  constexpr int BMD = (BM + RPI * NW - 1) / (RPI * NW) * (RPI * NW);
+  constexpr int A_INS = BN / RPI, B_INS = BMD / RPI;
   static_assert(A_INS % NW == 0 && B_INS % NW == 0, "DMA instructions must split evenly over waves");
   constexpr int GA = A_INS / NW, GB = B_INS / NW, G = GA + GB;
-  constexpr int A_BYTES = BN * RB, STAGE = (BN + BM) * RB;
+  constexpr int A_BYTES = BN * RB, STAGE = (BN + BMD) * RB;
   static_assert(NS >= 2 && NS <= 4, "ring depth");
   static_assert(G * (NS - 2) < 64, "vmcnt immediate");
 
@@ -116,7 +120,7 @@ __global__ void __launch_bounds__(64 * WN * WM) conv_glds_kernel(const ConvArgs 
     const int row = (wave + NW * j) * RPI + lrow;
     const int m = m0 + row;
     b_ch[j] = (lslot ^ swz_r(row, CPR)) * 8;
-    if (m < a.M) {
+    if (row < BM && m < a.M) {
       const int hw = a.Ho * a.Wo;
       const int b = m / hw, r = m - b * hw;
       const int oh = r / a.Wo, ow = r - oh * a.Wo;
@@ -392,7 +396,9 @@ static void glds_cfg(ConvArgs a, hipStream_t st) {
     a.nK = a.KH * a.KW * a.cblk;
   }
   const int grid = a.tiles_n * a.tiles_m * (a.ksplit > 1 ? a.ksplit : 1);
-  const size_t lds = (size_t)NS * (BN + BM) * BK * 2;
+  constexpr int RPI_ = 64 / (BK / 8), NW_ = WN * WM;
+  constexpr int BMD = (BM + RPI_ * NW_ - 1) / (RPI_ * NW_) * (RPI_ * NW_);
+  const size_t lds = (size_t)NS * (BN + BMD) * BK * 2;
   auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32, P3, SPLIT>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), (int)lds);   // per (kernel, device), launch_util.h
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WN * WM), lds, st, a);
@@ -468,6 +474,11 @@ static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
     case 15: glds_cfg<64, 128, 64, 1, 4, 3, R, F, false, true>(a, st); return true;    // 72 KiB, 2 stages ahead
     case 16: glds_cfg<128, 64, 64, 2, 2, 3, R, F, false, true>(a, st); return true;    // 72 KiB, 2 stages ahead
     case 41: glds_cfg<128, 64, 64, 2, 4, 3, R, F, false, true>(a, st); return true;    // 8 waves, 72 KiB, 2 ahead
+    // 128 x 160 (B staged as 192 rows): 1.91 / 0.96 waves of
+    // blocks on ResNet layer3 / layer4 at B = 400 where 128-pixel tiles make
+    // 2.4 / 1.6 (the partial last wave idles most of the chip)
+    case 42: glds_cfg<128, 160, 64, 4, 2, 2, R, F, false, true>(a, st); return true;    // 8 waves, 32 x 80 wave tiles, 80 KiB
+    case 43: glds_cfg<128, 96, 64, 2, 2, 2, R, F, false, true>(a, st); return true;     // 4 waves, 56 KiB
     case 17: glds_cfg<256, 128, 64, 4, 2, 3, R, F, false, true>(a, st); return true;
     case 24: glds_cfg<128, 128, 64, 2, 4, 3, R, F, false, true>(a, st); return true;
     case 25: glds_cfg<256, 128, 64, 4, 2, 2, R, F, false, true>(a, st); return true;
@@ -492,8 +503,15 @@ bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) 
 
 // Default split tile: same shape logic as the fp16 pick (a stage is 32 channels
 // instead of 64, so a tile does 3x the MFMAs per byte staged).
+static bool g_split_wide = true;
+void set_split_wide_tile(bool on) { g_split_wide = on; }
 int conv_glds_split_pick(int M, int Cout) {
-  if (Cout % 128 == 0) return M >= 50000 ? 36 : 34;
+  if (Cout % 128 == 0) {
+    if (M >= 50000) return 36;
+    // layer4-sized GEMMs: 128 x 160 tiles make ~1 full wave of blocks where
+    // 128 x 64 made 1.6 (whole-graph A/B: profiles/r2_v29_split_wide_tile.md)
+    return g_split_wide ? 42 : 34;
+  }
   return 27;
 }
 

@@ -204,7 +204,7 @@ def test_conv_split_default_tile(ops, B, H, Cin, Cout, k, s, p):
     _check(P.from_split(y), ref)
 
 
-SPLIT_TILES = [14, 15, 16, 17, 24, 25, 26, 27, 30, 33, 34, 35, 36, 37, 38, 41]
+SPLIT_TILES = [14, 15, 16, 17, 24, 25, 26, 27, 30, 33, 34, 35, 36, 37, 38, 41, 42, 43]
 
 
 @pytest.mark.gpu
