@@ -129,6 +129,7 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 int conv_glds_split_pick(int M, int Cout);
 void set_split_wide_tile(bool on);   // A/B: 128x160 tiles for small-M split convs (default on)
+void set_split_wide_l3(bool on);     // A/B: ... also for 50000 <= M < 100000 (layer3)
 // split 3x3/s1/p1 conv with the B operand from a halo patch per 32-channel block (Cout % 128 == 0)
 bool conv3x3_patch_split_supported(int B, int H, int W, int C, int Cout);
 void conv3x3_patch_split_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, void* y,

@@ -505,8 +505,11 @@ bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) 
 // instead of 64, so a tile does 3x the MFMAs per byte staged).
 static bool g_split_wide = true;
 void set_split_wide_tile(bool on) { g_split_wide = on; }
+static bool g_split_wide_l3 = false;
+void set_split_wide_l3(bool on) { g_split_wide_l3 = on; }
 int conv_glds_split_pick(int M, int Cout) {
   if (Cout % 128 == 0) {
+    if (g_split_wide && g_split_wide_l3 && M >= 50000 && M < 100000) return 42;   // layer3: 1.91 vs 2.39 waves
     if (M >= 50000) return 36;
     // layer4-sized GEMMs: 128 x 160 tiles make ~1 full wave of blocks where
     // 128 x 64 made 1.6 (whole-graph A/B: profiles/r2_v29_split_wide_tile.md)
