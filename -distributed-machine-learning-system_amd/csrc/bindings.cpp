@@ -281,10 +281,12 @@ static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
 // row-streaming register-weight kernel (tile 50 of conv2d_split, conv3x3_split.hip).
 static bool g_split_c64_default = true;
 void set_split_c64_default(bool on) { g_split_c64_default = on; }
+#ifdef IDUNNO_EXPERIMENTAL
 // Whether auto selection routes split 3x3/s1 convs with Cout % 128 == 0 to the
-// halo-patch kernel (tile 60, conv3x3_patch_split.hip).
+// halo-patch kernel (tiles 60-62, experimental/conv3x3_patch_split.hip).
 static bool g_split_patch_default = false;
 void set_split_patch_default(bool on) { g_split_patch_default = on; }
+#endif
 // split convs: tile order (0 m-major, 1 n-major, -1 auto heuristic)
 static int g_split_norder = -1;
 void set_split_norder(int64_t mode) { g_split_norder = (int)mode; }
@@ -372,6 +374,7 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     check_launch("conv3x3_split_c64");
     return y;
   }
+#ifdef IDUNNO_EXPERIMENTAL
   const bool patch_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && Cout % 128 == 0 &&
                         conv3x3_patch_split_supported(B, H, W, C2 / 2, Cout);
   if ((tile >= 60 && tile <= 62) || (tile < 0 && patch_ok && g_split_patch_default)) {
@@ -381,6 +384,7 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     check_launch("conv3x3_patch_split");
     return y;
   }
+#endif
   const int t = tile >= 0 ? (int)tile : conv_glds_split_pick(a.M, Cout);
   a.norder = split_norder((Cout + 127) / 128, Kpad);
   TORCH_CHECK(conv_glds_split_launch(a, out_f32, t, cur_stream()), "unknown split conv tile id ", t);
@@ -1154,8 +1158,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_split_c64_default", &set_split_c64_default,
         "A/B: route split 3x3 64->64 convs to the row-streaming kernel (tile 50; default on)");
   m.def("set_split_norder", &set_split_norder, "A/B: split conv tile order (0 m-major, 1 n-major, -1 auto)");
+#ifdef IDUNNO_EXPERIMENTAL
   m.def("set_split_patch_default", &set_split_patch_default,
         "A/B: route split 3x3/s1 convs (Cout % 128 == 0) to the halo-patch kernel (tile 60)");
+#endif
   m.def("set_stem_split_niw", [](int64_t n) { set_stem_split_niw((int)n); },
         "A/B: fused split stem, 16-cout A fragments per wave (1 default: 3 workgroups/CU; 2)");
   m.def("set_split_wide_tile", &set_split_wide_tile, "A/B: 128x160 split tiles for M < 50000 (layer4; default on)");

@@ -130,11 +130,13 @@ bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 int conv_glds_split_pick(int M, int Cout);
 void set_split_wide_tile(bool on);   // A/B: 128x160 tiles for small-M split convs (default on)
 void set_split_wide_l3(bool on);     // A/B: ... also for 50000 <= M < 100000 (layer3)
+#ifdef IDUNNO_EXPERIMENTAL
 // split 3x3/s1/p1 conv with the B operand from a halo patch per 32-channel block (Cout % 128 == 0)
 bool conv3x3_patch_split_supported(int B, int H, int W, int C, int Cout);
 void conv3x3_patch_split_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, void* y,
                                 bool out_f32, const void* zero, int B, int H, int W, int C, int Cout, int relu,
                                 float acc_scale, int nsa, hipStream_t st);
+#endif
 // split 3x3/s1/p1 64 -> 64 conv, weights in registers, input rows streamed through an LDS ring
 bool conv3x3_split_c64_supported(int H, int W, int C, int Cout);
 void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,

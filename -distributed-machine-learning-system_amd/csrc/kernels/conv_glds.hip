@@ -467,30 +467,21 @@ static bool glds_dispatch_p3(ConvArgs a, int tile, hipStream_t st) {
 }
 
 // split fp16 (fp32-accurate) tiles: the BK = 64 shapes of the fp16 table
+// The tiles below are the measured-useful ones: 36 / 42 / 27 are the defaults
+// (conv_glds_split_pick), 26 / 34 / 38 near-equal alternatives kept for A/B.
+// Measured and dropped (profiles/r2_v24..v29): 14/17/25/30 (256-wide), 15/16/41
+// (3-stage rings), 24, 33, 35, 37, 43 -- 5-45 % slower on every ResNet layer.
 template <bool R, bool F>
 static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
   switch (tile) {
-    case 14: glds_cfg<128, 256, 64, 2, 4, 3, R, F, false, true>(a, st); return true;
-    case 15: glds_cfg<64, 128, 64, 1, 4, 3, R, F, false, true>(a, st); return true;    // 72 KiB, 2 stages ahead
-    case 16: glds_cfg<128, 64, 64, 2, 2, 3, R, F, false, true>(a, st); return true;    // 72 KiB, 2 stages ahead
-    case 41: glds_cfg<128, 64, 64, 2, 4, 3, R, F, false, true>(a, st); return true;    // 8 waves, 72 KiB, 2 ahead
-    // 128 x 160 (B staged as 192 rows): 1.91 / 0.96 waves of
-    // blocks on ResNet layer3 / layer4 at B = 400 where 128-pixel tiles make
-    // 2.4 / 1.6 (the partial last wave idles most of the chip)
-    case 42: glds_cfg<128, 160, 64, 4, 2, 2, R, F, false, true>(a, st); return true;    // 8 waves, 32 x 80 wave tiles, 80 KiB
-    case 43: glds_cfg<128, 96, 64, 2, 2, 2, R, F, false, true>(a, st); return true;     // 4 waves, 56 KiB
-    case 17: glds_cfg<256, 128, 64, 4, 2, 3, R, F, false, true>(a, st); return true;
-    case 24: glds_cfg<128, 128, 64, 2, 4, 3, R, F, false, true>(a, st); return true;
-    case 25: glds_cfg<256, 128, 64, 4, 2, 2, R, F, false, true>(a, st); return true;
-    case 30: glds_cfg<128, 256, 64, 2, 4, 2, R, F, false, true>(a, st); return true;
     case 26: glds_cfg<128, 128, 64, 2, 2, 2, R, F, false, true>(a, st); return true;
     case 27: glds_cfg<64, 128, 64, 1, 4, 2, R, F, false, true>(a, st); return true;
-    case 33: glds_cfg<64, 256, 64, 1, 4, 2, R, F, false, true>(a, st); return true;
     case 34: glds_cfg<128, 64, 64, 2, 2, 2, R, F, false, true>(a, st); return true;
-    case 35: glds_cfg<64, 64, 64, 2, 2, 2, R, F, false, true>(a, st); return true;
     case 36: glds_cfg<128, 128, 64, 2, 4, 2, R, F, false, true>(a, st); return true;
-    case 37: glds_cfg<64, 128, 64, 1, 8, 2, R, F, false, true>(a, st); return true;
     case 38: glds_cfg<128, 64, 64, 2, 4, 2, R, F, false, true>(a, st); return true;
+    // 128 x 160 (B staged as 192 rows): 0.96 waves of blocks on ResNet layer4
+    // at B = 400 where 128 x 64 tiles make 1.6 (the partial last wave idles)
+    case 42: glds_cfg<128, 160, 64, 4, 2, 2, R, F, false, true>(a, st); return true;    // 8 waves, 80 KiB
     default: return false;
   }
 }

@@ -1,3 +1,5 @@
+// EXPERIMENTAL (built only with IDUNNO_EXPERIMENTAL=1): measured -0.9 % in the
+// whole graph, profiles/r2_v26_split_patch_c64_ab.md.
 // 3x3 / stride-1 / pad-1 conv on split fp16 (fp32-accurate, conv_glds.hip SPLIT)
 // with the B operand from a halo PATCH: ResNet layers 2-4 (C >= 128, 28x28 .. 7x7).
 //
@@ -17,8 +19,8 @@
 // Pixel rows are 128 B (32 channels x (hi, lo)); chunk c of patch pixel pp sits
 // in 16-byte slot c ^ (pp & 6): conflict-free for 16 consecutive pixels (a row
 // wrap inside a fragment costs an occasional 2-way conflict).
-#include "../kernels.h"
-#include "../launch_util.h"
+#include "../../kernels.h"
+#include "../../launch_util.h"
 
 namespace idunno {
 

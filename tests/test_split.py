@@ -204,7 +204,7 @@ def test_conv_split_default_tile(ops, B, H, Cin, Cout, k, s, p):
     _check(P.from_split(y), ref)
 
 
-SPLIT_TILES = [14, 15, 16, 17, 24, 25, 26, 27, 30, 33, 34, 35, 36, 37, 38, 41, 42, 43]
+SPLIT_TILES = [26, 27, 34, 36, 38, 42]
 
 
 @pytest.mark.gpu
@@ -229,7 +229,9 @@ def test_conv_split_c64_rows(ops, B, H, W, res):
 @pytest.mark.parametrize("res,out_f32", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("tile", [60, 61, 62])
 def test_conv_split_patch(ops, B, H, C, Cout, res, out_f32, tile):
-    """Halo-patch 3x3 split conv (tile 60): tiles spanning images (virtual rows)."""
+    """Halo-patch 3x3 split conv (tiles 60-62, experimental build): tiles spanning images (virtual rows)."""
+    if not ops.load().has_experimental():
+        pytest.skip("experimental kernels not built (IDUNNO_EXPERIMENTAL=1)")
     torch.manual_seed(B * H + C + res + out_f32)
     x = torch.randn(B, H, H, C, device=DEV)
     w = torch.randn(Cout, C, 3, 3) / (9 * C) ** 0.5

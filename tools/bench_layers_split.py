@@ -24,7 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=400)
     ap.add_argument("--model", default="resnet18")
-    ap.add_argument("--tiles", default="14,15,16,17,24,25,26,27,30,33,34,35,36,37,38,41")
+    ap.add_argument("--tiles", default="26,27,34,36,38,42")
     ap.add_argument("--json", default=None)
     ap.add_argument("--norder", type=int, default=-1, help="split conv tile order: 0 m-major, 1 n-major, -1 auto")
     a = ap.parse_args()
