@@ -470,7 +470,8 @@ static bool glds_dispatch_p3(ConvArgs a, int tile, hipStream_t st) {
 // The tiles below are the measured-useful ones: 36 / 42 / 27 are the defaults
 // (conv_glds_split_pick), 26 / 34 / 38 near-equal alternatives kept for A/B.
 // Measured and dropped (profiles/r2_v24..v29): 14/17/25/30 (256-wide), 15/16/41
-// (3-stage rings), 24, 33, 35, 37, 43 -- 5-45 % slower on every ResNet layer.
+// (3-stage rings), 24, 33, 35, 37, 43 -- 5-45 % slower on every ResNet layer;
+// 192 x 128 for AlexNet conv2 (Cout 192): 8 % slower than 64 x 128.
 template <bool R, bool F>
 static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
   switch (tile) {

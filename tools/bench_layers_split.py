@@ -37,7 +37,14 @@ def main():
     tiles = [int(t) for t in a.tiles.split(",")]
     rows = []
     tot = {"def": 0.0, "best": 0.0, "f32": 0.0}
-    for name, B, h, c in layer_shapes(a.model, a.batch):
+    if a.model == "alexnet":
+        from types import SimpleNamespace as NS
+        shapes = [(f"conv{i}", a.batch, h, NS(cin=ci, cout=co, kh=k, kw=k, stride=1, pad=k // 2))
+                  for i, h, ci, co, k in ((2, 27, 64, 192, 5), (3, 13, 192, 384, 3), (4, 13, 384, 256, 3),
+                                          (5, 13, 256, 256, 3))]
+    else:
+        shapes = layer_shapes(a.model, a.batch)
+    for name, B, h, c in shapes:
         if not split_eligible(c.cin, c.cout):
             continue
         w = torch.randn(c.cout, c.cin, c.kh, c.kw) / (c.cin * c.kh * c.kw) ** 0.5
