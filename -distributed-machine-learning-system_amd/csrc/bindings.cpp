@@ -1166,6 +1166,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "A/B: fused split stem, 16-cout A fragments per wave (1 default: 3 workgroups/CU; 2)");
   m.def("set_split_wide_tile", &set_split_wide_tile, "A/B: 128x160 split tiles for M < 50000 (layer4; default on)");
   m.def("set_split_wide_l3", &set_split_wide_l3, "A/B: 128x160 split tiles also for 50000 <= M < 100000 (layer3)");
+  m.def("set_f16_wide_tile", &set_f16_wide_tile, "A/B: fp16 128x160 tiles for M < 50000 (layer4)");
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");
   m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),

@@ -449,6 +449,7 @@ static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
     case 37: glds_cfg<64, 128, 64, 1, 8, 2, R, F>(a, st); return true;    // 8 waves, 48 KiB dbuf
     case 38: glds_cfg<128, 64, 64, 2, 4, 2, R, F>(a, st); return true;    // 8 waves (32x16 wave tile)
     case 39: glds_cfg<128, 128, 32, 2, 4, 4, R, F>(a, st); return true;   // 8 waves, 64 KiB, 3 stages in flight
+    case 42: glds_cfg<128, 160, 64, 4, 2, 2, R, F>(a, st); return true;   // 8 waves, B as 192 rows, 80 KiB (small M)
     default: return false;
   }
 }
@@ -535,10 +536,12 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
 // Default tile per shape, from the per-layer sweep on MI355X (tools/bench_layers.py,
 // profiles/r1_layer_sweep.md): 2 blocks/CU with a 4-deep BK=32 ring wins where
 // M is large; 128x64 tiles keep >= 2 waves of blocks when M is small (layer4).
+static bool g_f16_wide = false;
+void set_f16_wide_tile(bool on) { g_f16_wide = on; }
 int conv_glds_pick(int M, int Cout) {
   // sweeps r1 #3/#4: BK=64 double buffering with 2-3 workgroups/CU beats deeper
   // rings; 8 waves per 128x128 tile (4 waves/SIMD) best where M is large
-  if (Cout % 128 == 0) return M >= 50000 ? 36 : 34;   // 128x128 8-wave | 128x64
+  if (Cout % 128 == 0) return M >= 50000 ? 36 : (g_f16_wide ? 42 : 34);   // 128x128 8-wave | 128x64
   return 27;                                           // 64x128, 48 KiB
 }
 
