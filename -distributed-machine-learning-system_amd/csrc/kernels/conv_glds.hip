@@ -205,9 +205,13 @@ conv_glds_kernel(const ConvArgs a) {
   // SPLIT loads its residual (hi and lo: twice the registers) only after the
   // main loop instead: held across the loop it took the 128x128 8-wave tile
   // from 112 to 140 VGPRs, one block per CU instead of two, +25-50 % time.
+  // The padded-B tiles (BMD > BM, e.g. 128 x 160) load it late too: their
+  // register budget (>= 4 waves/SIMD) would spill the untracked preload, and a
+  // spill of an asm load's destination before the load lands corrupts it.
+  constexpr bool LATE_RES = SPLIT || BMD != BM;
   half4v rv[HAS_RES ? FN : 1][HAS_RES ? FM : 1];
   half4v rl[HAS_RES && SPLIT ? FN : 1][HAS_RES && SPLIT ? FM : 1];   // SPLIT: residual lo parts
-  if constexpr (HAS_RES && !SPLIT) {
+  if constexpr (HAS_RES && !LATE_RES) {
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
       const int n = n0 + wn * TN + i * 16 + (lane >> 4) * 4;
@@ -302,15 +306,18 @@ conv_glds_kernel(const ConvArgs a) {
   }
 
   // ---- epilogue: bias (+residual) (+ReLU), NHWC store --------------------
-  if constexpr (HAS_RES && SPLIT) {
-    // the ring is drained (last wait was vmcnt(0)): ordinary tracked loads
+  // late residual: the ring is drained (last wait was vmcnt(0)), so ordinary
+  // tracked loads; all at once, or per cout fragment for the padded-B tiles
+  // (whose epilogue would otherwise spill at their <= 128-VGPR budget)
+  constexpr bool RES_PER_I = LATE_RES && BMD != BM;
+  auto load_res = [&](int i) {
+    const int n = n0 + wn * TN + i * 16 + (lane >> 4) * 4;
 #pragma unroll
-    for (int i = 0; i < FN; ++i) {
-      const int n = n0 + wn * TN + i * 16 + (lane >> 4) * 4;
-#pragma unroll
-      for (int j = 0; j < FM; ++j) {
-        const int m = m0 + wm * TM + j * 16 + (lane & 15);
-        const size_t off = (m < a.M && n < a.Cout) ? (size_t)m * 2 * a.Cout + split_off(n) : 0;
+    for (int j = 0; j < FM; ++j) {
+      const int m = m0 + wm * TM + j * 16 + (lane & 15);
+      const bool ok = m < a.M && n < a.Cout;
+      if constexpr (SPLIT) {
+        const size_t off = ok ? (size_t)m * 2 * a.Cout + split_off(n) : 0;
         if (a.ablate & 2) {
           rv[i][j] = half4v{0, 0, 0, 0};
           rl[i][j] = half4v{0, 0, 0, 0};
@@ -318,9 +325,16 @@ conv_glds_kernel(const ConvArgs a) {
           rv[i][j] = *reinterpret_cast<const half4v*>(a.res + off);
           rl[i][j] = *reinterpret_cast<const half4v*>(a.res + off + 32);
         }
+      } else {
+        const size_t off = ok ? (size_t)m * a.Cout + n : 0;
+        rv[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : *reinterpret_cast<const half4v*>(a.res + off);
       }
     }
-  } else if constexpr (HAS_RES) {
+  };
+  if constexpr (HAS_RES && LATE_RES && !RES_PER_I) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i) load_res(i);
+  } else if constexpr (HAS_RES && !LATE_RES) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (already retired by the ring's last wait)
 #pragma unroll
     for (int i = 0; i < FN; ++i)
@@ -331,6 +345,7 @@ conv_glds_kernel(const ConvArgs a) {
   for (int i = 0; i < FN; ++i) {
     const int n = n0 + wn * TN + i * 16 + (lane >> 4) * 4;
     if (n >= a.Cout) continue;
+    if constexpr (HAS_RES && RES_PER_I) load_res(i);
     const float4v bv = *reinterpret_cast<const float4v*>(a.bias + n);
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
