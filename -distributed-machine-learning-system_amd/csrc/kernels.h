@@ -128,7 +128,7 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 // ([hi x32][lo x32] per 32 channels), y fp32 with out_f32
 bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 int conv_glds_split_pick(int M, int Cout);
-void set_f16_wide_tile(bool on);     // A/B: fp16 128x160 tiles for M < 50000 (default off)
+void set_f16_wide_tile(bool on);     // A/B: fp16 128x160 tiles for M < 50000 (default on)
 void set_split_wide_tile(bool on);   // A/B: 128x160 tiles for small-M split convs (default on)
 void set_split_wide_l3(bool on);     // A/B: ... also for 50000 <= M < 100000 (layer3)
 #ifdef IDUNNO_EXPERIMENTAL

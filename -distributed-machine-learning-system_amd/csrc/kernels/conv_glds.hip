@@ -551,7 +551,7 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
 // Default tile per shape, from the per-layer sweep on MI355X (tools/bench_layers.py,
 // profiles/r1_layer_sweep.md): 2 blocks/CU with a 4-deep BK=32 ring wins where
 // M is large; 128x64 tiles keep >= 2 waves of blocks when M is small (layer4).
-static bool g_f16_wide = false;
+static bool g_f16_wide = true;   // whole fp16 graph +3.6 % (profiles/r2_v31_wide_tiles.md)
 void set_f16_wide_tile(bool on) { g_f16_wide = on; }
 int conv_glds_pick(int M, int Cout) {
   // sweeps r1 #3/#4: BK=64 double buffering with 2-3 workgroups/CU beats deeper
