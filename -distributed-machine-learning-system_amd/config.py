@@ -61,6 +61,10 @@ class ClusterConfig:
     collective_rounds: bool | None = None
     collective_port_offset: int = 500        # TCPStore port = base_port + offset + epoch % 100
     collective_timeout_s: float = 30.0       # rendezvous timeout; a round's liveness comes from membership
+    collective_op_timeout_s: float = 120.0   # backstop for one pending collective (process-group timeout)
+    abort_join_s: float = 5.0                # how long a stopping node waits for a background epoch abort
+    round_depth: int = 2                     # rounds in flight (double-buffered send / gather / host)
+    job_window: int = 3                      # coordinator-side job: queries in flight before the next is cut
 
     # -- checkpoint / resume ----------------------------------------------------
     checkpoint_period_s: float = 0.0         # coordinator writes state to disk (0 = off)

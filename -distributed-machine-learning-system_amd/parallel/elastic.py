@@ -1,33 +1,41 @@
 """Epoch-versioned collective group for the fault-tolerant node runtime
 (SURVEY.md §5.8 "RCCL fault tolerance", §7.3 hard part 2).
 
-The steady-state query path of a healthy cluster runs in *rounds* on a
-torch.distributed group ("nccl" == RCCL over xGMI on MI355X, "gloo" on CPU):
-the coordinator (rank 0) broadcasts one descriptor row per member and gathers
-the packed top-1 results — the same ``QueryPlane`` bench.py uses.  Membership
-changes are handled by re-forming the group under a new *epoch*:
+The steady-state query path of a healthy cluster runs in *rounds* (see
+``idunno.runtime.rounds``): the coordinator sends every member its work
+descriptor over the TCP control plane (SURVEY.md M9 "control: a per-rank work
+descriptor"), each member writes its packed top-1 pairs into a device send
+buffer, and ONE collective gathers them to the coordinator (M11, RCCL over
+xGMI on MI355X, gloo on CPU).  The reference has no collective at all (every
+RESULT is a TCP message to all 10 hosts, mp4_machinelearning.py:603-613).
 
-  * the coordinator announces GROUP_FORM {epoch, members, port} over the TCP
-    control plane; every member tears down its previous process group
-    (destroying it aborts RCCL communicators, so a collective blocked on a dead
-    peer returns) and rendezvous on a fresh TCPStore hosted by the coordinator
-    under the prefix ``epoch<N>``;
-  * a round whose collectives fail (peer died mid-round) is abandoned; its
-    chunks fall back to the TCP JOB path (idempotent results), and the
-    coordinator re-forms the group over the survivors once the failure
-    detector has removed the dead node.
+Design points:
 
-Liveness is bounded by the failure detector, not by a collective timeout:
-every collective is issued with ``async_op=True`` and polled in short slices
-against a caller check (membership of the round's ranks, a newer epoch, node
-shutdown).  A round whose check fails raises ``RoundAbandoned`` at once and
-the communicator is aborted in the background (``_abort_process_group``:
-ncclCommAbort on RCCL), so a dead rank costs ``failure_timeout_s`` plus the
-re-form, never the process-group timeout -- which is therefore set long
-(idle members may wait for the next round indefinitely).
+  * **No default process group.**  Each epoch is its own backend object
+    (``ProcessGroupNCCL`` / ``ProcessGroupGloo``) built on a ``PrefixStore``
+    of a TCPStore hosted by the coordinator.  An old epoch can still be
+    aborting on a background thread while the next one forms, so a stuck
+    ``ncclCommAbort`` never delays the re-form, and no
+    private ``torch.distributed`` API is needed: ``Backend.abort()`` /
+    ``shutdown()`` are public, and the process-group timeout is given at
+    construction.
+  * **Double-buffered rounds.**  Send, gather and host buffers come in
+    ``depth`` slots (round ``seq`` uses slot ``seq % depth``) so round k+1
+    computes while round k's gather and ingest run.
+  * **Results stay on the device until one copy.**  A member's forward writes
+    (class, prob bits) straight into ``send_buffer(seq)``; the coordinator
+    copies the whole gathered round to pinned host memory once, on a side
+    stream that does not wait for the compute queued behind it.
+  * **Liveness from the failure detector.**  Every wait polls ``work`` in
+    short slices against a caller check (membership of the members, a newer
+    epoch, node shutdown) that raises ``RoundAbandoned``; the process-group
+    timeout (``op_timeout_s``) is only a backstop.  Members idle between
+    queries wait on the TCP control plane, never inside a posted collective.
 
-Only one process group exists per process at a time (torch's default group);
-a new epoch waits for the previous epoch's abort to finish.
+Each send buffer ends with ``HDR_ROWS`` header rows the member fills with the
+measured compute time of one of its earlier chunks (``(us, model_id),
+(n_images, tag)``), so the coordinator's fair-time scheduler learns each
+model's own compute time rather than the round's wall time.
 """
 from __future__ import annotations
 
@@ -37,116 +45,113 @@ import threading
 import time
 from datetime import timedelta
 
+import numpy as np
 import torch
 import torch.distributed as dist
-
-from .dataplane import NO_WORK, Env, QueryPlane
 
 log = logging.getLogger("idunno.elastic")
 
 MODEL_IDS = {"alexnet": 0, "resnet18": 1, "resnet50": 2, "resnet34": 3}
 MODEL_NAMES = {v: k for k, v in MODEL_IDS.items()}
-STOP = -2          # descriptor start value telling members to leave the round loop
-IDLE_TIMEOUT = timedelta(hours=24)   # process-group timeout: liveness comes from the caller's check
+HDR_ROWS = 2        # (compute_us, model_id), (n_images, tag) at the end of every send buffer
 
 
 class RoundAbandoned(RuntimeError):
     """A round's liveness check failed (dead rank, newer epoch, shutdown)."""
 
 
+def _shutdown_backend(pg, abort: bool) -> None:
+    """End a backend object: ``abort()`` when collectives may still be
+    pending on a dead peer (RCCL: ncclCommAbort, pending kernels return),
+    else ``shutdown()`` where the backend has it."""
+    fn = None
+    if not abort:
+        fn = getattr(pg, "shutdown", None)
+    if fn is None:
+        fn = getattr(pg, "abort", None)
+    if fn is not None:
+        fn()
+
+
 class ElasticGroup:
     def __init__(self, device: torch.device, backend: str | None = None, timeout_s: float = 30.0,
-                 max_chunk: int = 1024):
+                 max_chunk: int = 1024, op_timeout_s: float = 120.0, abort_join_s: float = 5.0,
+                 depth: int = 2):
         self.device = torch.device(device)
         self.backend = backend or ("nccl" if self.device.type == "cuda" else "gloo")
-        self.timeout_s = timeout_s
+        self.timeout_s = timeout_s            # rendezvous (store + backend construction)
+        self.op_timeout_s = op_timeout_s      # backstop for one collective; liveness comes from check()
+        self.abort_join_s = abort_join_s      # how long teardown waits for a background abort
         self.max_chunk = max_chunk
+        self.depth = depth
         self.epoch = -1
         self.members: list[str] = []
         self.rank = -1
-        self.plane: QueryPlane | None = None
+        self.pg = None
         self.lock = threading.RLock()
         self._store = None
-        self._aborter: threading.Thread | None = None
+        self._aborters: list[threading.Thread] = []
         self.poll_s = 0.0005
+        self._send = self._gathered = self._host = None
+        self._d2h = None
 
     @property
     def formed(self) -> bool:
-        return self.plane is not None
+        return self.pg is not None
+
+    @property
+    def world(self) -> int:
+        return len(self.members)
+
+    # -- lifecycle ---------------------------------------------------------------
+    def _detach(self):
+        pg, self.pg = self.pg, None
+        self._store = None
+        self._send = self._gathered = self._host = None
+        return pg
 
     def teardown(self) -> None:
         """Clean teardown of a healthy group (no collective in flight)."""
         with self.lock:
-            self._join_aborter()
-            self.plane = None
-            if dist.is_initialized():
-                try:
-                    dist.destroy_process_group()
-                except Exception:  # noqa: BLE001  (a broken group can fail to clean up)
-                    log.exception("destroy_process_group failed")
-            self._store = None
+            pg = self._detach()
+        if pg is not None:
+            try:
+                _shutdown_backend(pg, abort=False)
+            except Exception:  # noqa: BLE001  (a broken group can fail to clean up)
+                log.exception("backend shutdown failed")
 
     def abort_async(self) -> None:
         """Abandon the current epoch with collectives possibly still pending:
-        abort the communicator on a background thread (RCCL: ncclCommAbort
-        returns at once; gloo returns once the peers' sockets close) so the
-        caller never blocks on a dead peer."""
+        abort its backend on a background thread so the caller never blocks
+        on a dead peer.  The next epoch does not wait for it (own backend)."""
         with self.lock:
-            if self.plane is None and not dist.is_initialized():
+            pg = self._detach()
+            if pg is None:
                 return
-            self.plane = None
-            self._store = None
 
             def run():
                 try:
-                    if dist.is_initialized():
-                        dist.distributed_c10d._abort_process_group()
+                    _shutdown_backend(pg, abort=True)
                 except Exception:  # noqa: BLE001
                     log.exception("abort of the old epoch failed")
-                try:
-                    if dist.is_initialized():
-                        dist.destroy_process_group()
-                except Exception:  # noqa: BLE001
-                    pass
 
-            self._join_aborter()
-            self._aborter = threading.Thread(target=run, name="epoch-abort", daemon=True)
-            self._aborter.start()
+            th = threading.Thread(target=run, name="epoch-abort", daemon=True)
+            th.start()
+            self._aborters = [t for t in self._aborters if t.is_alive()] + [th]
 
-    def _join_aborter(self, timeout: float | None = None) -> bool:
-        th = self._aborter
-        if th is None:
-            return True
-        th.join(self.timeout_s if timeout is None else timeout)
-        if th.is_alive():
-            return False
-        self._aborter = None
-        return True
-
-    def _wait(self, work, check) -> None:
-        """Poll ``work`` until it completes; ``check()`` raises RoundAbandoned
-        (liveness) between polls.  Spins ~1 ms, then sleeps ``poll_s``, backing
-        off to 4x after 10 ms and 20x after 1 s of waiting (a member idling
-        between queries wakes 100 times a second, not 2000; a round that
-        follows a long idle gap pays at most ~10 ms more latency)."""
-        if work is None:
-            return
-        t0 = time.perf_counter()
-        while not work.is_completed():
-            if check is not None:
-                check()
-            waited = time.perf_counter() - t0
-            if waited > 0.001:
-                time.sleep(self.poll_s * (1 if waited < 0.01 else 4 if waited < 1.0 else 20))
-        work.wait()
+    def join_aborters(self, timeout: float | None = None) -> bool:
+        """Wait (bounded by ``abort_join_s``) for background aborts to end;
+        True if none is left running.  Used before a process exits."""
+        end = time.monotonic() + (self.abort_join_s if timeout is None else timeout)
+        for th in list(self._aborters):
+            th.join(max(0.0, end - time.monotonic()))
+        self._aborters = [t for t in self._aborters if t.is_alive()]
+        return not self._aborters
 
     def form(self, me: str, members: list[str], epoch: int, host: str, port: int) -> bool:
-        """Join epoch ``epoch`` of the group (blocking rendezvous).  Rank 0 is
-        members[0], which hosts the TCPStore.  Returns False on failure."""
+        """Join epoch ``epoch`` (blocking rendezvous of all ``members``; rank 0
+        = members[0] hosts the TCPStore).  Returns False on failure."""
         with self.lock:
-            if not self._join_aborter():
-                log.warning("%s: previous epoch still aborting; cannot form epoch %d", me, epoch)
-                return False
             self.teardown()
             if me not in members:
                 return False
@@ -157,61 +162,113 @@ class ElasticGroup:
                                       timeout=timedelta(seconds=self.timeout_s), wait_for_workers=False,
                                       use_libuv=False)
                 pstore = dist.PrefixStore(f"epoch{epoch}", store)
-                kw = {}
+                op_to = timedelta(seconds=self.op_timeout_s)
                 if self.backend == "nccl":
+                    # on a collective timeout abort the communicator, never the process
                     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
-                    kw["device_id"] = self.device
-                # rendezvous / connection setup bounded by timeout_s; afterwards the
-                # group's collectives may stay pending for an idle gap of any length
-                dist.init_process_group(self.backend, store=pstore, rank=rank, world_size=world,
-                                        timeout=timedelta(seconds=self.timeout_s), **kw)
-                dist.distributed_c10d._set_pg_timeout(IDLE_TIMEOUT, None)
+                    torch.cuda.set_device(self.device)
+                    pg = dist.ProcessGroupNCCL(pstore, rank, world, op_to)
+                    # communicator set-up now, while every member is in form()
+                    eager = getattr(pg, "eager_connect_single_device", None)
+                    if eager is not None:
+                        eager(self.device)
+                else:
+                    pg = dist.ProcessGroupGloo(pstore, rank, world, op_to)
             except Exception:  # noqa: BLE001
                 log.exception("%s: forming epoch %d failed", me, epoch)
-                self._store = None
                 return False
             self._store = store
+            self.pg = pg
             self.epoch, self.members, self.rank = epoch, list(members), rank
-            env = Env(rank, world, self.device.index or 0, self.device, self.backend)
-            self.plane = QueryPlane(env, coordinator=0, max_chunk=self.max_chunk)
+            self._alloc(world)
             return True
 
-    # -- one round ------------------------------------------------------------------
-    def round(self, table: list[tuple[int, int, int, int]] | None, run_chunk, check=None):
-        """Run one collective round.
+    def _alloc(self, world: int) -> None:
+        dev, rows, D = self.device, self.max_chunk + HDR_ROWS, self.depth
+        self._send = [torch.zeros(rows, 2, dtype=torch.int32, device=dev) for _ in range(D)]
+        if self.rank == 0:
+            self._gathered = [torch.zeros(world, rows, 2, dtype=torch.int32, device=dev) for _ in range(D)]
+            gpu = dev.type == "cuda"
+            self._host = [torch.zeros(world, rows, 2, dtype=torch.int32, pin_memory=gpu) for _ in range(D)]
+            if gpu and self._d2h is None:
+                self._d2h = torch.cuda.Stream(device=dev)
 
-        Rank 0 passes ``table`` (one (model_id, qnum, start, end) row per member,
-        end = NO_WORK for idle members, start = STOP to end the round loop).
-        Every member runs ``run_chunk(model, start, end, packed)`` on its row:
-        it either writes (class, prob bits) pairs into the device send buffer
-        ``packed`` itself and returns None (device-resident results), or returns
-        (cls, prob) host arrays that are packed here.  The results are gathered
-        to rank 0, which gets back ``[(row, cls np, prob np), ...]`` from ONE
-        device->host copy; other ranks get None.  ``check()`` is polled while a
-        collective is pending and raises RoundAbandoned to give up (the caller
-        then calls ``abort_async``); any collective error also raises."""
-        from .dataplane import unpack
+    # -- buffers -----------------------------------------------------------------
+    def send_buffer(self, seq: int) -> torch.Tensor:
+        """[max_chunk, 2] int32 (class, prob bits) of round ``seq``."""
+        return self._send[seq % self.depth][: self.max_chunk]
 
-        plane = self.plane
-        if plane is None:
-            raise RuntimeError("group not formed")
-        self._wait(plane.dispatch_async(table), check)
-        mid, qnum, s, e = plane.my_row()
-        if s == STOP:
-            return "stop"
-        if e != NO_WORK:
-            r = run_chunk(MODEL_NAMES[mid], s, e, plane.send_buffer)
-            if r is not None:
-                cls, prob = r
-                plane.pack(torch.as_tensor(cls).to(self.device), torch.as_tensor(prob).to(self.device))
-        self._wait(plane.gather_async(), check)
-        if plane.env.rank != 0:
-            return None
-        allres = plane.gathered_all.cpu()
-        out = []
-        for r, row in enumerate(table):
-            if row[3] == NO_WORK or row[2] == STOP:
-                continue
-            c, p = unpack(allres[r], row[3] - row[2] + 1)
-            out.append((row, c.numpy(), p.numpy()))
-        return out
+    def header(self, seq: int) -> torch.Tensor:
+        return self._send[seq % self.depth][self.max_chunk:]
+
+    # -- collectives -----------------------------------------------------------------
+    def post_gather(self, seq: int):
+        """Start the gather of round ``seq``'s send buffer to rank 0 (Work)."""
+        pg = self.pg
+        if pg is None:
+            raise RoundAbandoned("group not formed")
+        opts = dist.GatherOptions()
+        opts.rootRank = 0
+        slot = seq % self.depth
+        outs = [list(self._gathered[slot].unbind(0))] if self.rank == 0 else []
+        return pg.gather(outs, [self._send[slot]], opts)
+
+    def wait(self, work, check=None) -> None:
+        """Poll ``work`` until it completes; ``check()`` raises RoundAbandoned
+        (liveness) between polls.  Spins ~1 ms, then sleeps ``poll_s``,
+        backing off to 4x after 10 ms and 20x after 1 s."""
+        if work is None:
+            return
+        t0 = time.perf_counter()
+        while not work.is_completed():
+            if check is not None:
+                check()
+            if self.pg is None:
+                raise RoundAbandoned("epoch torn down")
+            waited = time.perf_counter() - t0
+            if waited > 0.001:
+                time.sleep(self.poll_s * (1 if waited < 0.01 else 4 if waited < 1.0 else 20))
+        work.wait()
+
+    def release(self, work, check=None) -> None:
+        """Member: the slot of a finished round may be rewritten once its
+        gather is done.  On the GPU this is a stream dependency (the next
+        forward on the current stream waits for the gather, the host does
+        not); on the CPU the gather is polled to completion."""
+        if work is None:
+            return
+        if self.device.type == "cuda":
+            work.wait()
+        else:
+            self.wait(work, check)
+
+    def collect(self, seq: int, work, check=None) -> np.ndarray:
+        """Rank 0: wait for round ``seq``'s gather and return the whole round
+        as host int32 [world, max_chunk + HDR_ROWS, 2] (one device->host copy
+        on a side stream: compute queued on the current stream is not waited
+        for)."""
+        self.wait(work, check)
+        slot = seq % self.depth
+        host = self._host[slot]
+        if self.device.type == "cuda":
+            with torch.cuda.stream(self._d2h):
+                host.copy_(self._gathered[slot], non_blocking=True)
+            self._d2h.synchronize()
+        else:
+            host.copy_(self._gathered[slot])
+        return host.numpy()
+
+
+def pack_into(send: torch.Tensor, cls, prob) -> None:
+    """Write host (cls int32 [n], prob fp32 [n]) into a send buffer slot."""
+    c = torch.as_tensor(np.ascontiguousarray(cls, np.int32))
+    p = torch.as_tensor(np.ascontiguousarray(prob, np.float32)).view(torch.int32)
+    n = c.numel()
+    send[:n, 0].copy_(c.to(send.device))
+    send[:n, 1].copy_(p.to(send.device))
+
+
+def unpack_row(row: np.ndarray, n: int) -> tuple[np.ndarray, np.ndarray]:
+    """(cls int32 [n], prob fp32 [n]) from one gathered host row."""
+    r = row[:n]
+    return np.ascontiguousarray(r[:, 0]), np.ascontiguousarray(r[:, 1]).view(np.float32)

@@ -124,6 +124,7 @@ class HipExecutor(Executor):
         self.device = torch.device(device)
         self.seed = seed
         self.dtype = dtype
+        self.asynchronous = True        # run_packed returns before the GPU finishes
         if fp32_impl not in ("split", "f32mfma"):
             raise ValueError(f"fp32_impl must be 'split' or 'f32mfma', got {fp32_impl!r}")
         self.fp32_impl = fp32_impl      # fp32 programs: split-fp16 kernels or the all-f32-MFMA kernels
@@ -216,16 +217,20 @@ class HipExecutor(Executor):
     def run(self, model, images, start, end):
         return self.submit(model, images, start, end).result()
 
-    def run_packed(self, model, images, packed) -> None:
+    def run_packed(self, model, images, packed):
         """Device-resident result path (collective rounds): write (class, prob
         bits) pairs of ``images`` into the int32 [>= n, 2] device tensor
         ``packed`` (the RCCL gather's send buffer) on the current stream's
-        order; nothing comes back to the host."""
+        order; nothing comes back to the host and the host does not wait.
+        Returns (start, end) events around the forward on the private stream:
+        the chunk's own GPU time, read later once ``end`` has completed."""
         r = self.runner(model)
         n = images.shape[0]
         with torch.cuda.device(self.device), self.run_lock:
             s = self._enter(images)
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             with torch.cuda.stream(s):
+                ev0.record(s)
                 if not self.closed and ((self.use_graphs and len(r._graphs) < self.max_graphs)
                                         or r.has_graph(n, packed=packed)):
                     sin, replay = r.capture(n, packed=packed)
@@ -233,7 +238,9 @@ class HipExecutor(Executor):
                     replay()
                 else:
                     r.forward(images.contiguous(), packed=packed)
+                ev1.record(s)
             torch.cuda.current_stream(self.device).wait_stream(s)
+        return ev0, ev1
 
 
     def close(self) -> None:

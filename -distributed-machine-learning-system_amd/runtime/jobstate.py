@@ -221,6 +221,9 @@ class JobState:
             self._reassign_locked(failed, new_worker, tuple(chunk), now, emit=False)
         elif op == "reopen":
             self._reopen_locked(emit=False)
+        elif op == "replan":
+            model, qnum, old, new, now = args
+            self._replan_locked(model, qnum, old, new, now, emit=False)
         # "noop" (a duplicate result) changes nothing
 
     # -- coordinator-side jobs (C28 variant), replicated to the standby ----------
@@ -365,6 +368,39 @@ class JobState:
             self._bump("reopen")
         return n
 
+    def replan(self, model: str, qnum, old, new, now: float | None = None) -> bool:
+        """Replace a queued query's chunk plan (not started anywhere yet) by
+        ``new`` [(worker, s, e)]: the coordinator re-splits queries that wait
+        in the round queue when a second job changes the fair-time partition.
+        False (nothing changed) unless every old chunk is still 'w' as given."""
+        now = self.clock() if now is None else now
+        with self.lock:
+            return self._replan_locked(model, qnum, old, new, now, emit=True)
+
+    def _replan_locked(self, model, qnum, old, new, now, emit: bool) -> bool:
+        key = (model, qnum)
+        ents = self.worker_set.get(key, [])
+        old = {(w, int(s), int(e)) for w, s, e in old}
+        have = {(x[0], x[1], x[2]) for x in ents if x[3] == "w"}
+        if not old or not old <= have:
+            return False
+        self.worker_set[key] = [x for x in ents if not (x[3] == "w" and (x[0], x[1], x[2]) in old)]
+        for w, s, e in old:
+            try:
+                self.working_vm_set[w].remove((model, qnum, s, e))
+            except ValueError:
+                pass
+            if not self.working_vm_set.get(w):
+                self.working_vm_set.pop(w, None)
+        self._open_add(key, -len(old))
+        for w, s, e in new:
+            self.worker_set[key].append((w, int(s), int(e), "w", now, now))
+            self.working_vm_set[w].append((model, qnum, int(s), int(e)))
+            self._open_add(key, 1)
+        if emit:
+            self._bump("replan", model, qnum, [list(c) for c in sorted(old)], [list(c) for c in new], now)
+        return True
+
     def chunks_of(self, worker: str) -> list[tuple]:
         with self.lock:
             return list(self.working_vm_set.get(worker, []))
@@ -410,6 +446,12 @@ class JobState:
     def pending_count(self) -> int:
         with self.lock:
             return sum(self._open.values())
+
+    def open_queries(self, model: str, qlo: int, qhi: int) -> int:
+        """Queries of ``model`` numbered in [qlo, qhi] that still have chunks
+        running (a coordinator-side job's window, O(open queries))."""
+        with self.lock:
+            return sum(1 for (m, q) in self._open if m == model and isinstance(q, int) and qlo <= q <= qhi)
 
     # -- metrics ------------------------------------------------------------------
     def _expire(self, model: str, now: float) -> None:

@@ -40,6 +40,8 @@ class Type:
     REPLY = "REPLY"                  # response to a request (carries "rid")
     KILL = "KILL"                    # fault injection
     GROUP_FORM = "GROUP_FORM"        # coordinator -> members: join collective-group epoch N
+    ROUND = "ROUND"                  # coordinator -> member: its descriptor row of round k (or STOP)
+    RESULTS = "RESULTS"              # coordinator -> standby: every chunk of one finished round
 
 
 Status_RUNNING = "RUNNING"

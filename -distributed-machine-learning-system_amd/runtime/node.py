@@ -79,6 +79,8 @@ class Node:
         self._rerep_pending: list = []
         self._last_chunk_done: float | None = None   # worker: completion time of the previous chunk
         self.tracer = Tracer(name)
+        self._progress = threading.Condition()     # notified on every ingested result (job windows)
+        self._meta_lock = threading.Lock()          # one standby push at a time
         self.device = getattr(executor, "device", None)  # GPU of this node (None = CPU)
         self.rounds = None                          # collective round plane (cfg.collective_rounds)
         self.transport.dead_check = self._peer_dead
@@ -190,6 +192,14 @@ class Node:
             return {"ok": True}
         if t == Type.RESULT:
             self._ingest_result(msg)
+            return None
+        if t == Type.RESULTS:                   # one finished round, mirrored to the standby
+            for r in msg.get("results", []):
+                self._ingest_result(dict(r, src=msg.get("src")))
+            return None
+        if t == Type.ROUND:
+            if self.rounds is not None:
+                self.rounds.on_round(msg)
             return None
         if t == Type.METADATA:
             return self._apply_metadata(msg)
@@ -343,6 +353,16 @@ class Node:
                 s = job["next"]
                 if s > job["end"]:
                     return
+                # flow control: at most job_window of this job's queries open, so every
+                # query is planned (fair-time split, worker subset) against the jobs that
+                # are active NOW -- a burst would plan a whole job on one split and make
+                # a second job queue behind it instead of sharing the GPUs
+                qlo = job["qbase"]
+                qhi = qlo + (job["end"] - job["start"]) // job["bs"]
+                with self._progress:
+                    while not self._stop.is_set() and self.is_coordinator and \
+                            self.state.open_queries(job["model"], qlo, qhi) >= max(1, self.cfg.job_window):
+                        self._progress.wait(0.05)
                 e = min(s + self.cfg.batch_for(job["model"]) - 1, job["end"])
                 q = self.state.job_query_number(jid, s)
                 # skip a query the old coordinator already dispatched (known from the
@@ -378,9 +398,15 @@ class Node:
                                        cls, prob)
         self.tracer.instant("result.ingest", model=msg["model"], q=msg["qnum"], start=msg["start"],
                             worker=msg["worker"], new=new)
-        if new and self.is_coordinator:
+        cs = msg.get("compute_s")
+        if new and cs is not None and self.is_coordinator:
+            # (round results carry no compute_s: the members report their own GPU
+            # time in the gather header instead, see rounds.RoundPlane._finalize)
             n = msg["end"] - msg["start"] + 1
-            self.sched.observe(msg["model"], msg.get("compute_s", 0.0) / n * self.cfg.batch_for(msg["model"]))
+            self.sched.observe(msg["model"], cs / n * self.cfg.batch_for(msg["model"]))
+        if new:
+            with self._progress:
+                self._progress.notify_all()
 
     MAX_CHUNK_RETRIES = 3
 
@@ -501,6 +527,12 @@ class Node:
         mp4_machinelearning.py:971-987)."""
         import msgpack
 
+        if not self.membership.is_alive(self.standby):
+            return False                  # a dead standby must not stall submission / checkpoints
+        with self._meta_lock:             # one push at a time: acks never race backwards
+            return self._push_metadata(msgpack)
+
+    def _push_metadata(self, msgpack) -> bool:
         epoch = self.membership.epoch
         ack = self._standby_ack
         deltas = None
@@ -769,6 +801,10 @@ class Node:
             return {"ok": True, "path": self.save_checkpoint()}
         if v == "summary":
             return self.state.summary()
+        if v == "rounds":
+            return self.rounds.stats() if self.rounds is not None else {"ok": False, "error": "no rounds"}
+        if v == "sched":
+            return {"ok": True, "avg_time": dict(self.sched.avg_time)}
         return {"ok": False, "error": f"unknown view {view}"}
 
     def local_grep(self, pattern: str) -> list[str]:

@@ -1,146 +1,215 @@
 """Collective query rounds inside the fault-tolerant node runtime.
 
-When ``cfg.collective_rounds`` is on (one node per process, e.g. one per GPU
-via ``idunno.launch``), a query whose plan puts at most one chunk on each
-group member runs as ONE collective round on the ``ElasticGroup`` (RCCL
-broadcast of the descriptor table + gather of packed top-1 results, the same
-``QueryPlane`` bench.py drives) instead of per-chunk TCP JOB/RESULT messages.
-The reference has no equivalent (every chunk is a TCP message,
-mp4_machinelearning.py:560-613); the TCP path stays as the fallback:
+When ``cfg.collective_rounds`` is on (one node per process and per GPU, e.g.
+via ``idunno.launch``), queries whose plan puts at most one chunk on each
+group member run as *rounds* on the ``ElasticGroup`` instead of per-chunk TCP
+JOB/RESULT messages (the reference sends every chunk and every RESULT as a TCP
+message, mp4_machinelearning.py:560-613, 796-806).
 
-  * a round whose collectives fail is abandoned and its chunks are re-sent as
-    TCP JOBs (results are idempotent by chunk key);
-  * every membership change (failure, join, standby promotion) makes the
-    coordinator re-form the group under a new epoch over the live members.
+One round:
+  1. the coordinator sends each member its descriptor row ``(model_id, qnum,
+     start, end)`` or ``None`` as a small ROUND message on the TCP control
+     plane (SURVEY.md M9 "control: a per-rank work descriptor");
+  2. every member stages its images, launches the HIP forward, which writes
+     packed (class, prob) pairs straight into the round's device send buffer,
+     and posts the gather without waiting for the GPU;
+  3. ONE collective gathers the round to the coordinator (RCCL over xGMI /
+     gloo), which copies it to the host once and ingests every chunk.
 
-Each node runs ONE driver thread that owns the process group, so forming,
-rounds and teardown never race: as coordinator it forms epochs and serves the
-round queue, as a member it follows the latest GROUP_FORM it was sent.
+Space sharing.  The round table is *packed*: queued
+queries whose worker sets are disjoint go into the same round, oldest first,
+and a query that does not fit reserves its workers so a younger query cannot
+starve it.  The scheduler gives concurrent jobs disjoint, fair-time-sized
+worker subsets (``scheduler.partition``), so an AlexNet job and a ResNet18
+job share every round -- on 8 GPUs they run side by side, as the reference's
+jobs do on disjoint VM subsets (report Fig 2), not in turns.
 
-Liveness: collectives are polled against the failure
-detector, never waited on blindly.  The coordinator abandons a round as soon
-as membership marks one of its members dead (``failure_timeout_s``), falls
-back to TCP for the live members' chunks and aborts the epoch in the
-background; a member abandons its wait when a newer epoch is announced or
-the coordinator is dead.  Idle gaps are free (the process-group timeout is
-long), so no keepalive rounds are needed.
+Pipelining.  Send/gather/host buffers are double-buffered: the coordinator
+keeps ``round_depth`` (2) rounds in flight, so a member's GPU runs round k+1
+while round k is gathered and ingested, and members stage round k+1's images
+while round k computes.  A member's forward does not block its host thread;
+only the coordinator waits, for the oldest round's gather.
 
-Results stay on the device: a member's forward writes its packed top-1 pairs
-straight into the gather's send buffer (``HipExecutor.run_packed``), and the
-coordinator copies the whole round to the host once.
+Scheduler feedback.  Each member writes the measured GPU time of one of its
+earlier chunks (CUDA events around the forward) into two header rows of its
+send buffer; the coordinator feeds those to the fair-time EMA, so averages
+are each model's own compute time, not the round's wall time.
+
+Liveness.  Every wait polls against the failure detector: the
+coordinator abandons the in-flight rounds as soon as membership marks ANY
+member dead (not only members already dead when the round began), re-sends
+their chunks as TCP JOBs (results are idempotent by chunk key), aborts the
+epoch's backend in the background and re-forms over the survivors.  A member
+abandons when a newer epoch is announced or the coordinator is dead.  Idle
+members wait for the next ROUND message on the control plane with no
+collective posted, so no RCCL kernel spins on an idle GPU.
 """
 from __future__ import annotations
 
 import logging
-import queue
 import threading
 import time
+from collections import deque
 
-import numpy as np
+import torch
 
-from ..parallel.dataplane import NO_WORK
-from ..parallel.elastic import MODEL_IDS, STOP, ElasticGroup, RoundAbandoned
+from ..parallel.elastic import HDR_ROWS, MODEL_IDS, MODEL_NAMES, ElasticGroup, RoundAbandoned, pack_into, \
+    unpack_row
 from .messages import Type
+from .scheduler import split_range
 
 log = logging.getLogger("idunno.rounds")
 
 
+class _Query:
+    __slots__ = ("model", "qnum", "rows", "members")
+
+    def __init__(self, model, qnum, rows, members):
+        self.model, self.qnum, self.rows, self.members = model, qnum, rows, members
+
+
+class _Round:
+    __slots__ = ("seq", "queries", "table", "work")
+
+    def __init__(self, seq, queries, table):
+        self.seq, self.queries, self.table, self.work = seq, queries, table, None
+
+
 class RoundPlane:
+    HDR_RING = 4        # pinned header buffers (> depth: a slot is rewritten only after its gather)
+
     def __init__(self, node, device):
         self.node = node
-        self.cfg = node.cfg
-        self.group = ElasticGroup(device, timeout_s=self.cfg.collective_timeout_s, max_chunk=self.cfg.max_chunk)
-        self.q: queue.Queue = queue.Queue()
+        self.cfg = cfg = node.cfg
+        self.group = ElasticGroup(device, timeout_s=cfg.collective_timeout_s, max_chunk=cfg.max_chunk,
+                                  op_timeout_s=cfg.collective_op_timeout_s, abort_join_s=cfg.abort_join_s,
+                                  depth=cfg.round_depth)
         self.lock = threading.Lock()
-        self.epoch = 0                      # last epoch formed or announced
+        self.cv = threading.Condition(self.lock)
+        self._queue: deque = deque()          # coordinator: queued _Query, FIFO
+        self._round_msgs: dict = {}           # member: (epoch, seq) -> ROUND message
+        self.epoch = 0                        # last epoch formed or announced
         self.members: list[str] = []
-        self.healthy = False                # coordinator: rounds may be queued
+        self.healthy = False                  # coordinator: rounds may be queued
         self.rounds_done = 0
         self.rounds_failed = 0
+        self.mixed_rounds = 0                 # rounds that carried more than one model
+        self.max_queries_per_round = 0
+        self.parked = True                    # member: waiting on the control plane, nothing posted
+        self._inflight: deque = deque()       # this node's posted, unfinished gathers
         self._reform_at: float | None = None
         self._pending_form: dict | None = None
         self._released = False
+        self._release_done = threading.Event()
         self._wake = threading.Event()
         self._thread: threading.Thread | None = None
+        self._timings: deque = deque(maxlen=64)   # (model_id, n, (ev0, ev1) | seconds)
+        self._hdr = None
+        self._tag = 0
+        self._next_seq = 0                    # coordinator: seq of the next round of this epoch
 
+    # -- lifecycle -------------------------------------------------------------------
     def start(self) -> None:
         self._thread = threading.Thread(target=self._driver, name=f"{self.node.name}-rounds", daemon=True)
         self._thread.start()
 
     def stop(self) -> None:
         self._wake.set()
+        with self.cv:
+            self.cv.notify_all()
 
     def join(self, timeout: float = 5.0) -> None:
-        """Wait for the driver thread and any background epoch abort to end
+        """Wait for the driver thread and (bounded) for background epoch aborts
         (a process must not exit while a communicator is being torn down)."""
         th = self._thread
         if th is not None and th is not threading.current_thread():
             th.join(timeout)
-        self.group._join_aborter(timeout)
+        self.group.join_aborters()
 
     def release(self, timeout: float = 10.0) -> bool:
-        """Coordinator: end the epoch cleanly (a STOP round lets every member
-        leave its round loop and destroy the group) and form no new one.
-        Used before a planned shutdown of the whole cluster."""
-        done = threading.Event()
-        with self.lock:
-            self.healthy = False
+        """Coordinator: finish the queued rounds, end the epoch cleanly (STOP)
+        and form no new one.  Used before a planned shutdown of the cluster."""
+        with self.cv:
             self._released = True
-        self.q.put(("__release__", done))
+            self.cv.notify_all()
         self._wake.set()
-        return done.wait(timeout)
+        return self._release_done.wait(timeout)
 
     # -- triggers (any thread) ----------------------------------------------------------
     def schedule_reform(self, reason: str, delay: float = 0.2) -> None:
         """Coordinator: re-form the group over the live members after ``delay``
         (several triggers inside the window collapse into one re-form)."""
-        with self.lock:
+        with self.cv:
             self.healthy = False
             at = time.monotonic() + delay
             self._reform_at = at if self._reform_at is None else min(self._reform_at, at)
+            self.cv.notify_all()
         log.info("%s: re-form scheduled (%s)", self.node.name, reason)
         self._wake.set()
 
     def on_group_form(self, msg: dict) -> None:
-        with self.lock:
+        with self.cv:
             if int(msg["epoch"]) <= self.epoch:
                 return
             self._pending_form = dict(msg)
+            self.cv.notify_all()
         self._wake.set()
 
+    def on_round(self, msg: dict) -> None:
+        """Member: a ROUND descriptor (or STOP) from the coordinator."""
+        with self.cv:
+            ep = int(msg["epoch"])
+            if ep < self.epoch:
+                return
+            self._round_msgs[(ep, int(msg["seq"]))] = msg
+            self.cv.notify_all()
+
     def try_enqueue(self, model: str, qnum, plan) -> bool:
-        """Coordinator: queue a query as one collective round if the group covers
-        its plan (one chunk per member at most)."""
-        with self.lock:
-            if not self.healthy:
+        """Coordinator: queue a query for the round path if the group covers its
+        plan (one chunk per member at most)."""
+        with self.cv:
+            if not self.healthy or self._released:
                 return False
-            members = list(self.members)
+            members = tuple(self.members)
         workers = [w for w, _, _ in plan]
-        if len(set(workers)) != len(workers) or not set(workers) <= set(members):
+        if not workers or len(set(workers)) != len(workers) or not set(workers) <= set(members):
             return False
         if any(e - s + 1 > self.cfg.max_chunk for _, s, e in plan):
             return False
-        mid = MODEL_IDS.get(model)
-        if mid is None:
+        if model not in MODEL_IDS:
             return False
-        by = {w: (s, e) for w, s, e in plan}
-        table = [(mid, int(qnum), by[m][0], by[m][1]) if m in by else (mid, int(qnum), 0, NO_WORK)
-                 for m in members]
-        self.q.put((model, qnum, table, members))
+        q = _Query(model, qnum, {w: (int(s), int(e)) for w, s, e in plan}, members)
+        with self.cv:
+            self._queue.append(q)
+            self.cv.notify_all()
         self._wake.set()
         return True
 
-    # -- liveness checks (polled while a collective is pending) ---------------------------
+    def stats(self) -> dict:
+        g = self.group
+        return {"ok": True, "epoch": g.epoch, "formed": g.formed, "members": list(g.members),
+                "rounds_done": self.rounds_done, "rounds_failed": self.rounds_failed,
+                "mixed_rounds": self.mixed_rounds, "max_queries_per_round": self.max_queries_per_round,
+                "parked": self.parked, "pending_collectives": self.pending_collectives(),
+                "queued": len(self._queue)}
+
+    def pending_collectives(self) -> int:
+        """Posted gathers of this node that have not completed."""
+        works = [x.work if isinstance(x, _Round) else x[1] for x in list(self._inflight)]
+        return sum(1 for w in works if w is not None and not w.is_completed())
+
+    # -- liveness checks (polled while a collective or a descriptor is pending) -------------
     def _check_coordinator(self, members: list[str]):
         n = self.node
-        alive = set(n.membership.alive())
 
         def check():
             if not n.alive_flag:
                 raise RoundAbandoned("node stopping")
             if not n.is_coordinator:
                 raise RoundAbandoned("no longer coordinator")
-            dead = [m for m in members if m not in alive and not n.membership.is_alive(m)]
+            # ANY member the detector now marks dead (a member that dies
+            # during the round must count, not only one already dead at its start)
+            dead = [m for m in members if m != n.name and not n.membership.is_alive(m)]
             if dead:
                 raise RoundAbandoned(f"member(s) {dead} failed")
         return check
@@ -157,32 +226,64 @@ class RoundPlane:
                 raise RoundAbandoned(f"coordinator {coordinator} failed")
         return check
 
-    # -- driver thread ---------------------------------------------------------------------
-    def _run_chunk(self, model: str, s: int, e: int, packed=None):
-        """This member's chunk of a round.  On a GPU executor the packed top-1
-        pairs go straight into ``packed`` (the gather's send buffer) and None
-        is returned; otherwise (cls, prob) host arrays."""
+    # -- the work of one member in one round ------------------------------------------------
+    def _run_chunk(self, row, seq: int) -> None:
+        """Stage and launch this member's chunk of round ``seq`` into its send
+        buffer.  A GPU executor returns at once (timing events are kept for a
+        later header); a host executor is timed here."""
         n = self.node
+        mid, qnum, s, e = (int(v) for v in row)
+        model = MODEL_NAMES[mid]
         delay = self.cfg.worker_start_delay_s + n.extra_delay_s
         if delay:
             time.sleep(delay)
-        t0 = time.perf_counter()
-        tags = dict(model=model, start=s, end=e, epoch=self.group.epoch)
+        cnt = e - s + 1
+        send = self.group.send_buffer(seq)
+        tags = dict(model=model, q=qnum, start=s, end=e, epoch=self.group.epoch, seq=seq)
         with n.tracer.span("round.stage", **tags):
             imgs = n.source.get(s, e) if n.source is not None else None
-        with n.tracer.span("round.compute", **tags):
-            run_packed = getattr(n.executor, "run_packed", None)
-            if run_packed is not None and packed is not None and imgs is not None and \
-                    imgs.device.type == "cuda" and packed.device == imgs.device:
-                run_packed(model, imgs, packed[:e - s + 1])
-                out = None
+        run_packed = getattr(n.executor, "run_packed", None)
+        with n.tracer.span("round.launch", **tags):
+            if run_packed is not None and imgs is not None and imgs.device.type == "cuda" and \
+                    send.device == imgs.device:
+                evs = run_packed(model, imgs, send[:cnt])
+                if evs is not None:
+                    self._timings.append((mid, cnt, evs))
             else:
+                t0 = time.perf_counter()
                 cls, prob = n.executor.run(model, imgs, s, e)
-                out = np.ascontiguousarray(cls, np.int32), np.ascontiguousarray(prob, np.float32)
+                self._timings.append((mid, cnt, time.perf_counter() - t0))
+                pack_into(send, cls, prob)
         n.chunks_done += 1
-        self._last_compute = time.perf_counter() - t0
-        return out
 
+    def _write_header(self, seq: int) -> None:
+        """Report one finished chunk's own compute time in round ``seq``'s
+        header rows: (us, model_id), (n_images, tag); zeros if none finished."""
+        us = mid = cnt = 0
+        if self._timings:
+            m, c, t = self._timings[0]
+            if isinstance(t, tuple):
+                ev0, ev1 = t
+                if ev1.query():
+                    us, mid, cnt = int(ev0.elapsed_time(ev1) * 1000.0), m, c
+                    self._timings.popleft()
+            else:
+                us, mid, cnt = int(t * 1e6), m, c
+                self._timings.popleft()
+        self._tag += 1
+        vals = torch.tensor([us, mid, cnt, self._tag], dtype=torch.int32).view(HDR_ROWS, 2)
+        hdr = self.group.header(seq)
+        if hdr.device.type == "cuda":
+            if self._hdr is None:
+                self._hdr = [torch.zeros(HDR_ROWS, 2, dtype=torch.int32, pin_memory=True)
+                             for _ in range(self.HDR_RING)]
+            p = self._hdr[seq % self.HDR_RING]
+            p.copy_(vals)
+            hdr.copy_(p, non_blocking=True)
+        else:
+            hdr.copy_(vals)
+
+    # -- driver thread ---------------------------------------------------------------------
     def _driver(self) -> None:
         n = self.node
         while n.alive_flag:
@@ -197,90 +298,243 @@ class RoundPlane:
                     self._member_step()
             except Exception:  # noqa: BLE001
                 log.exception("%s: round driver error", n.name)
-                self._drop_group()
-        self._drop_group()
+                self._drop_group(abandoned=True)
+        self._drop_group(abandoned=self.group.formed)
 
     def _drop_group(self, abandoned: bool = False) -> None:
-        with self.lock:
+        with self.cv:
             self.healthy = False
+        self._inflight.clear()
         if abandoned:
             self.group.abort_async()          # collectives may still be pending on dead peers
         else:
             self.group.teardown()
 
     # coordinator -------------------------------------------------------------------------
+    def _reform_due(self) -> bool:
+        with self.cv:
+            return self._reform_at is not None
+
     def _coordinator_step(self) -> None:
-        n = self.node
-        with self.lock:
+        with self.cv:
             due = self._reform_at is not None and time.monotonic() >= self._reform_at and not self._released
             if due:
                 self._reform_at = None
+            pending = self._reform_at is not None
         if due:
             self._reform()
             return
-        if self._reform_at is not None:
+        if pending:
             self._wake.set()                       # keep polling until it is due
+            time.sleep(0.01)
+            return
         if not self.group.formed:
             self._flush_queue_to_tcp()
+            if self._released:
+                self._release_done.set()
             return
-        while n.alive_flag and self._reform_at is None:
-            try:
-                item = self.q.get(timeout=0.05)
-            except queue.Empty:
-                return
-            if item[0] == "__release__":
-                self._stop_epoch()
-                item[1].set()
-                return
-            model, qnum, table, members = item
-            if members != self.group.members:
-                self._fallback(model, qnum, table, members)
+        self._serve()
+
+    def _build(self, members: tuple):
+        """Pack the next round from the queue: oldest first, every query whose
+        workers are all still free joins; a query that does not fit reserves
+        its workers (no starvation).  Queued queries are first re-split onto
+        the current fair-time partition (``_replan``).  Returns (queries,
+        stale) where stale queries were planned for another member set (-> TCP)."""
+        with self.cv:
+            qs, self._queue = list(self._queue), deque()
+        if not qs:
+            return [], []
+        take, stale, keep = [], [], []
+        live = [q for q in qs if q.members == members]
+        stale = [q for q in qs if q.members != members]
+        self._replan(live, members)
+        used, reserved = set(), set()
+        for q in live:
+            ws = set(q.rows)
+            if ws & used or ws & reserved or len(used) >= len(members):
+                reserved |= ws
+                keep.append(q)
+            else:
+                used |= ws
+                take.append(q)
+        with self.cv:
+            keep.extend(self._queue)               # queued while we were packing
+            self._queue = deque(keep)
+        return take, stale
+
+    def _replan(self, qs: list, members: tuple) -> None:
+        """Move queued (not yet posted) queries onto the current partition.
+        A query planned while its job ran alone holds every GPU; once a second
+        job is active it is re-split onto its own fair-time subset, so the two
+        jobs share the very next round instead of after the first job's backlog
+        drains.  The change is a replicated job-state op (the standby sees it)."""
+        n = self.node
+        if not qs:
+            return
+        active = {m for (m, *_r) in n.state.pending()}
+        if len(active) < 2:
+            return
+        alive = set(n.membership.alive())
+        part = n.sched.subsets(active, [w for w in sorted(members) if w in alive])
+        for q in qs:
+            tgt = part.get(q.model)
+            if not tgt or set(tgt) == set(q.rows):
                 continue
-            t0 = time.perf_counter()
-            try:
-                out = self.group.round(table, self._run_chunk, check=self._check_coordinator(members))
-            except Exception as e:  # noqa: BLE001
-                self.rounds_failed += 1
-                log.warning("%s: round failed in epoch %d (%s); falling back to TCP", n.name, self.group.epoch, e)
-                n.tracer.instant("round.failed", epoch=self.group.epoch, q=qnum)
-                self._drop_group(abandoned=True)
-                self._fallback(model, qnum, table, members)
-                self._flush_queue_to_tcp()
-                # the failure detector re-forms on a death; re-form anyway in case it was
-                # transient -- after the detector had time to drop a dead member
-                self.schedule_reform("round failure", delay=self.cfg.failure_timeout_s * 1.2)
+            s0 = min(s for s, _ in q.rows.values())
+            e0 = max(e for _, e in q.rows.values())
+            new = [(w, s, e) for w, (s, e) in zip(tgt, split_range(s0, e0, len(tgt)))]
+            if any(e - s + 1 > self.cfg.max_chunk for _, s, e in new):
+                continue
+            old = [(w, s, e) for w, (s, e) in q.rows.items()]
+            if n.state.replan(q.model, q.qnum, old, new):
+                q.rows = {w: (s, e) for w, s, e in new}
+
+    def _serve(self) -> None:
+        """Run rounds of the current epoch until the queue is drained and a
+        re-form / release / role change asks to stop (coordinator)."""
+        n, g = self.node, self.group
+        members = tuple(g.members)
+        check = self._check_coordinator(list(members))
+        inflight = self._inflight
+        idle_since = time.monotonic()
+        try:
+            while n.alive_flag and n.is_coordinator and not self._reform_due():
+                # at most depth-1 rounds in flight when the next is posted: a slot (and the
+                # members' pinned header ring) is rewritten only after its gather finished
+                while len(inflight) >= g.depth:
+                    self._finalize_oldest(members, check)
+                while inflight and inflight[0].work.is_completed():
+                    self._finalize_oldest(members, check)
+                qs, stale = self._build(members)
+                for q in stale:
+                    self._fallback_query(q)
+                if not qs:
+                    if inflight:
+                        # the next query (a job's window refills on ingest) may arrive
+                        # while the oldest round still computes: post it as soon as it
+                        # does instead of blocking on the gather
+                        self._wait_queue_or(inflight[0].work, check)
+                        continue
+                    if self._released:
+                        break
+                    with self.cv:
+                        if not self._queue and not self._released and self._reform_at is None:
+                            self.cv.wait(0.05)
+                    if time.monotonic() - idle_since > 0.5:
+                        return        # hand back to the driver loop now and then (cheap)
+                    continue
+                idle_since = time.monotonic()
+                r = _Round(self._next_seq, qs, self._table(members, qs))
+                self._next_seq += 1
+                inflight.append(r)
+                self._post(r, members)
+            while inflight:
+                self._finalize_oldest(members, check)
+            self._stop_epoch()
+            if self._released:
+                self._release_done.set()
+        except Exception as e:  # noqa: BLE001
+            self.rounds_failed += 1
+            log.warning("%s: round failed in epoch %d (%s); falling back to TCP", n.name, g.epoch, e)
+            n.tracer.instant("round.failed", epoch=g.epoch)
+            lost = list(inflight)
+            self._drop_group(abandoned=True)
+            for r in lost:
+                for q in r.queries:
+                    self._fallback_query(q)
+            self._flush_queue_to_tcp()
+            if self._released:
+                self._release_done.set()
                 return
-            round_s = time.perf_counter() - t0
-            self.rounds_done += 1
-            now = time.time()
-            for row, cls, prob in out:
-                w = members[table.index(row)]
-                # the members run in parallel: the round's wall time is each chunk's
-                # (stage + compute) time as the fair-time scheduler measures it
-                res = {"t": Type.RESULT, "model": model, "qnum": qnum, "start": row[2], "end": row[3],
-                       "worker": w, "cls": cls.tobytes(), "prob": prob.tobytes(), "compute_s": round_s,
-                       "epoch": n.membership.epoch, "t_done": now}
-                n._ingest_result(dict(res, src=n.name))
-                if n.standby != n.name and n.membership.is_alive(n.standby):
-                    n.transport.send(n.standby, res)
+            # the failure detector re-forms on a death; re-form anyway in case it was
+            # transient -- after the detector had time to drop a dead member
+            self.schedule_reform("round failure", delay=self.cfg.failure_timeout_s * 1.2)
+
+    def _wait_queue_or(self, work, check) -> None:
+        t0 = time.perf_counter()
+        while not work.is_completed():
+            with self.cv:
+                if self._queue or self._released or self._reform_at is not None:
+                    return
+                self.cv.wait(0.0002 if time.perf_counter() - t0 < 0.01 else 0.002)
+            check()
+
+    @staticmethod
+    def _table(members: tuple, qs: list) -> list:
+        table = [None] * len(members)
+        idx = {m: i for i, m in enumerate(members)}
+        for q in qs:
+            mid = MODEL_IDS[q.model]
+            for w, (s, e) in q.rows.items():
+                table[idx[w]] = (mid, int(q.qnum), s, e)
+        return table
+
+    def _post(self, r: _Round, members: tuple) -> None:
+        n, g = self.node, self.group
+        for i, m in enumerate(members[1:], 1):
+            row = r.table[i]
+            msg = {"t": Type.ROUND, "epoch": g.epoch, "seq": r.seq, "row": list(row) if row else None}
+            if not n.transport.send(m, msg):
+                raise RoundAbandoned(f"ROUND {r.seq} to {m} not delivered")
+        if r.table[0] is not None:
+            self._run_chunk(r.table[0], r.seq)
+        self._write_header(r.seq)
+        r.work = g.post_gather(r.seq)
+        models = {q.model for q in r.queries}
+        if len(models) > 1:
+            self.mixed_rounds += 1
+        self.max_queries_per_round = max(self.max_queries_per_round, len(r.queries))
+
+    def _finalize_oldest(self, members: tuple, check) -> None:
+        # popped only once ingested: a round that fails here stays in flight and
+        # its queries go back to the TCP path with the others
+        self._finalize(self._inflight[0], members, check)
+        self._inflight.popleft()
+
+    def _finalize(self, r: _Round, members: tuple, check) -> None:
+        """Wait for round ``r``'s gather, ingest every chunk, feed the members'
+        measured compute times to the scheduler, mirror the results to the
+        standby in one message."""
+        n, g = self.node, self.group
+        arr = g.collect(r.seq, r.work, check)
+        mc = g.max_chunk
+        now = time.time()
+        batch = []
+        for i, row in enumerate(r.table):
+            us, hmid, cnt = int(arr[i, mc, 0]), int(arr[i, mc, 1]), int(arr[i, mc + 1, 0])
+            if cnt > 0 and hmid in MODEL_NAMES:
+                model = MODEL_NAMES[hmid]
+                n.sched.observe(model, us * 1e-6 / cnt * self.cfg.batch_for(model))
+            if row is None:
+                continue
+            mid, qnum, s, e = row
+            cls, prob = unpack_row(arr[i], e - s + 1)
+            res = {"t": Type.RESULT, "model": MODEL_NAMES[mid], "qnum": qnum, "start": s, "end": e,
+                   "worker": members[i], "cls": cls.tobytes(), "prob": prob.tobytes(),
+                   "epoch": n.membership.epoch, "t_done": now}
+            n._ingest_result(dict(res, src=n.name))
+            batch.append(res)
+        self.rounds_done += 1
+        if batch and n.standby != n.name and n.membership.is_alive(n.standby):
+            n.transport.send(n.standby, {"t": Type.RESULTS, "results": batch})
 
     def _stop_epoch(self) -> None:
-        """Let members leave the current epoch cleanly (STOP round), then drop it."""
-        abandoned = False
-        if self.group.formed:
-            try:
-                self.group.round([(0, 0, STOP, NO_WORK)] * len(self.group.members), self._run_chunk,
-                                 check=self._check_coordinator(self.group.members))
-            except Exception:  # noqa: BLE001
-                abandoned = True
-        self._drop_group(abandoned=abandoned)
+        """End an idle epoch cleanly: every member gets STOP as its next round
+        (it drains its gathers and shuts its backend down), then ours."""
+        if not self.group.formed:
+            return
+        for m in self.group.members[1:]:
+            self.node.transport.send(m, {"t": Type.ROUND, "epoch": self.group.epoch, "seq": self._next_seq,
+                                         "stop": True})
+        self._drop_group(abandoned=False)
 
     def _reform(self) -> None:
         n = self.node
-        self._stop_epoch()
+        self._stop_epoch()                         # idle epoch (the serve loop drained it)
         self._flush_queue_to_tcp()
         members = [n.name] + [m for m in n.membership.alive() if m != n.name]
-        with self.lock:
+        with self.cv:
             self.epoch = max(self.epoch + 1, n.membership.epoch * 1000 + 1)
             epoch = self.epoch
             self.members = members
@@ -292,60 +546,85 @@ class RoundPlane:
         for m in members[1:]:
             n.transport.send(m, {"t": Type.GROUP_FORM, "epoch": epoch, "members": members, "port": port})
         ok = self.group.form(n.name, members, epoch, self.cfg.host, port)
-        with self.lock:
+        self._next_seq = 0
+        with self.cv:
             self.healthy = ok and self._reform_at is None and epoch == self.epoch
         if not ok:
             log.warning("%s: epoch %d rendezvous failed; TCP path until the next re-form", n.name, epoch)
             self.schedule_reform("rendezvous failed", delay=self.cfg.failure_timeout_s * 1.5)
 
     def _flush_queue_to_tcp(self) -> None:
-        while True:
-            try:
-                item = self.q.get_nowait()
-            except queue.Empty:
-                return
-            if item[0] == "__release__":
-                self._stop_epoch()
-                item[1].set()
-                continue
-            model, qnum, table, members = item
-            self._fallback(model, qnum, table, members)
+        with self.cv:
+            qs, self._queue = list(self._queue), deque()
+        for q in qs:
+            self._fallback_query(q)
 
-    def _fallback(self, model, qnum, table, members) -> None:
-        """Re-send a round's chunks as TCP JOBs.  Chunks of dead members are
-        re-dispatched by the failure handler (it owns the reassignment)."""
+    def _fallback_query(self, q: _Query) -> None:
+        """Re-send a query's chunks as TCP JOBs.  Chunks of dead members are
+        re-dispatched by the failure handler (it owns the reassignment); a
+        chunk whose result is already held is dropped by the idempotent ingest."""
         n = self.node
         alive = set(n.membership.alive())
-        for m, row in zip(members, table):
-            if row[3] != NO_WORK and m in alive:
-                n._send_job(m, model, qnum, row[2], row[3])
+        for w, (s, e) in q.rows.items():
+            if w in alive and not n.state.images_held(q.model, q.qnum, s, e):
+                n._send_job(w, q.model, q.qnum, s, e)
 
     # member ---------------------------------------------------------------------------------
     def _member_step(self) -> None:
         n = self.node
-        with self.lock:
+        with self.cv:
             msg, self._pending_form = self._pending_form, None
-        if msg is None:
-            return
-        epoch, members, port = int(msg["epoch"]), list(msg["members"]), int(msg["port"])
-        with self.lock:
+            if msg is None:
+                return
+            epoch, members, port = int(msg["epoch"]), list(msg["members"]), int(msg["port"])
             if epoch < self.epoch:
                 return
             self.epoch, self.members = epoch, members
+            self._round_msgs = {k: v for k, v in self._round_msgs.items() if k[0] >= epoch}
         if not self.group.form(n.name, members, epoch, self.cfg.host, port):
             return
-        check = self._check_member(members[0])
-        abandoned = False
-        while n.alive_flag:
-            try:
-                r = self.group.round(None, self._run_chunk, check=check)
-            except Exception as e:  # noqa: BLE001
-                log.info("%s: left epoch %d (%s)", n.name, epoch, e)
-                abandoned = True
-                break
-            if r == "stop":
-                break
-            self.rounds_done += 1
-        self._drop_group(abandoned=abandoned)
+        self._follow(epoch, members)
         if self._pending_form is not None:
             self._wake.set()
+
+    def _await_round(self, epoch: int, seq: int, check) -> dict:
+        """Member: wait on the control plane (nothing posted on the GPU) for
+        the coordinator's descriptor of round ``seq``."""
+        while True:
+            with self.cv:
+                msg = self._round_msgs.pop((epoch, seq), None)
+                if msg is None:
+                    self.parked = True
+                    self.cv.wait(0.05)
+                    msg = self._round_msgs.pop((epoch, seq), None)
+                if msg is not None:
+                    self.parked = False
+                    return msg
+            check()
+
+    def _follow(self, epoch: int, members: list[str]) -> None:
+        g = self.group
+        check = self._check_member(members[0])
+        inflight = self._inflight
+        abandoned = False
+        seq = 0
+        try:
+            while True:
+                msg = self._await_round(epoch, seq, check)
+                if msg.get("stop"):
+                    while inflight:
+                        g.wait(inflight.popleft()[1], check)
+                    break
+                while inflight and inflight[0][0] <= seq - g.depth:
+                    g.release(inflight.popleft()[1], check)
+                row = msg.get("row")
+                if row is not None:
+                    self._run_chunk(row, seq)
+                self._write_header(seq)
+                inflight.append((seq, g.post_gather(seq)))
+                self.rounds_done += 1
+                seq += 1
+        except Exception as e:  # noqa: BLE001
+            log.info("%s: left epoch %d (%s)", self.node.name, epoch, e)
+            abandoned = True
+        self._drop_group(abandoned=abandoned)

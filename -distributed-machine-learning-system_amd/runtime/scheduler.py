@@ -45,17 +45,61 @@ def split_range(start: int, end: int, n_workers: int) -> list[tuple[int, int]]:
     return out
 
 
-def fair_share(avg_time: dict[str, float], model: str, budget: int, alive: int) -> int:
-    """Workers for ``model`` under the two-job fair-time rule."""
-    ta = max(avg_time.get("alexnet", 1.0), 1e-9)
-    tr = max(avg_time.get("resnet18", 1.0), 1e-9)
-    ratio = ta / tr
-    if model == "alexnet":
-        n = round(ratio / (ratio + 1) * budget)
-    else:
-        inv = 1.0 / ratio
-        n = round(inv / (inv + 1) * budget)
+def time_shares(avg_time: dict[str, float], models) -> dict[str, float]:
+    """Each active model's share of the worker budget: t_i / sum(t) over the
+    active models (the slower model gets more workers).  For the reference's
+    two models this is its formula: ratio = t_a / t_r, share_a = ratio /
+    (ratio + 1) = t_a / (t_a + t_r) (mp4_machinelearning.py:504-514).  Every
+    model reads ITS OWN average (the reference only knew alexnet/resnet18)."""
+    models = sorted(set(models))
+    t = {m: max(float(avg_time.get(m, 1.0)), 1e-9) for m in models}
+    tot = sum(t.values())
+    return {m: t[m] / tot for m in models}
+
+
+def fair_share(avg_time: dict[str, float], model: str, budget: int, alive: int,
+               active=("alexnet", "resnet18")) -> int:
+    """Workers for ``model`` under the fair-time rule over the ``active``
+    models (default: the reference's pair), rounded half-even and clamped to
+    the alive count like the reference."""
+    active = set(active) | {model}
+    n = round(time_shares(avg_time, active)[model] * budget)
     return int(max(0, min(n, alive)))
+
+
+def partition(avg_time: dict[str, float], models, workers: list, budget: int) -> dict[str, list]:
+    """Disjoint worker subsets for concurrently active models (space sharing).
+
+    Sizes follow ``fair_share`` (at least one worker each), then are adjusted
+    by largest remainder so they add up to min(budget, len(workers)) -- the
+    reference's independent rounding can leave a worker idle or over-commit
+    one.  Subsets are contiguous slices of ``workers`` in model-name order, so
+    consecutive queries of one job land on the same GPUs and two jobs'
+    queries never share one (they can run in the same collective round).
+    With more models than workers, workers are shared round-robin."""
+    models = sorted(set(models))
+    workers = list(workers)
+    if not models or not workers:
+        return {m: [] for m in models}
+    if len(models) > len(workers):
+        return {m: [workers[i % len(workers)]] for i, m in enumerate(models)}
+    eff = min(budget, len(workers))
+    if len(models) == 1:
+        return {models[0]: workers[:eff]}
+    sh = time_shares(avg_time, models)
+    exact = {m: sh[m] * eff for m in models}
+    n = {m: max(1, round(exact[m])) for m in models}
+    while sum(n.values()) > eff:
+        m = max((m for m in models if n[m] > 1), key=lambda m: (n[m] - exact[m], m))
+        n[m] -= 1
+    while sum(n.values()) < eff:
+        m = max(models, key=lambda m: (exact[m] - n[m], m))
+        n[m] += 1
+    out, i = {}, 0
+    for m in models:
+        out[m] = workers[i:i + n[m]]
+        i += n[m]
+    return out
 
 
 @dataclass
@@ -76,6 +120,24 @@ class FairTimeScheduler:
     def __post_init__(self):
         self._rng = random.Random(self.seed)
         self._seen: set = set()
+        self._part: dict = {}
+
+    def subsets(self, active, workers: list) -> dict[str, list]:
+        """``partition`` of ``workers`` over the ``active`` models, sticky: the
+        previous split is kept while every model's size is within one worker
+        of its exact fair-time share, so EMA jitter does not move a job's GPUs
+        from query to query (a moved subset would collide with the other
+        job's in-flight queries and cost a round of packing)."""
+        key = (frozenset(active), tuple(workers))
+        cur = self._part.get(key)
+        if cur is not None:
+            eff = min(self.budget, len(workers))
+            sh = time_shares(self.avg_time, active)
+            if all(abs(len(cur[m]) - sh[m] * eff) < 1.0 for m in cur):
+                return cur
+        cur = partition(self.avg_time, active, list(workers), self.budget)
+        self._part = {key: cur}
+        return cur
 
     def observe(self, model: str, normalized_query_time: float) -> None:
         """Feed a measured full-query-equivalent time for ``model`` (EMA)."""
@@ -90,14 +152,24 @@ class FairTimeScheduler:
         if len(self.active_jobs - {model}) == 0:
             # a single job owns the whole budget
             return max(1, min(self.budget, len(alive)))
-        return max(1, fair_share(self.avg_time, model, self.budget, len(alive)))
+        return max(1, fair_share(self.avg_time, model, self.budget, len(alive), self.active_jobs))
 
     def assign(self, model: str, start: int, end: int, alive: list,
                n: int | None = None, shuffle: bool = True) -> list[tuple]:
-        """Returns [(worker, s, e), ...] for the inclusive query range."""
+        """Returns [(worker, s, e), ...] for the inclusive query range.
+
+        A single active job gets the whole budget (a random sample of the
+        alive workers when the budget is smaller, as the reference samples,
+        :520-521).  With several active jobs each gets its own disjoint,
+        fair-time-sized subset (``partition``), so concurrent jobs share the
+        node in space instead of queueing on the same GPUs."""
         if not alive:
             return []
-        n = self.n_workers(model, alive) if n is None else max(1, min(n, len(alive)))
-        workers = self._rng.sample(list(alive), n) if shuffle else list(alive)[:n]
-        chunks = split_range(start, end, n)
+        active = set(self.active_jobs) | {model}
+        if n is None and len(active) > 1:
+            workers = self.subsets(active, list(alive))[model]
+        else:
+            n = self.n_workers(model, alive) if n is None else max(1, min(n, len(alive)))
+            workers = self._rng.sample(list(alive), n) if shuffle else list(alive)[:n]
+        chunks = split_range(start, end, len(workers))
         return [(w, s, e) for w, (s, e) in zip(workers, chunks)]

@@ -20,52 +20,68 @@ torch fp32 itself (``max_rel_logit_err_vs_fp64``,
 The other fp32 implementation and the fp16 path (f16 MFMA, f32 accumulate,
 fp16 activations) are reported as extra keys.
 
-One *step* is one round of the cluster's query path, end to end:
-  1. the coordinator (rank 0) splits the round's image range over the ranks
-     with the scheduler's split rule (reference mp4_machinelearning.py:523-536)
-     and dispatches the chunk descriptors (RCCL broadcast);
-  2. every rank takes its chunk from its HBM-resident replica of the dataset
-     and runs preprocess + the HIP forward + fused softmax-top1 (one hipGraph
-     replay of hand-written gfx950 kernels, window start read on the device);
-  3. top-1 (class, prob) pairs are gathered to the coordinator over RCCL,
-     copied to host and recorded in the job-state tables.
-Headline = weak scaling (400 images per GPU per step).  Strong scaling (ONE
-400-image query split over the N ranks, as the reference splits a query over
-its workers) is reported as ``*_strong`` keys.
+The process the driver starts is a pure LAUNCHER: it never touches a GPU and
+runs three phases of child processes (one per GPU), then prints ONE JSON line.
+
+  1. headline ("raw round loop"): one *step* is one round of the cluster's
+     query path, end to end -- the coordinator (rank 0) splits the round's
+     image range over the ranks with the scheduler's split rule (reference
+     mp4_machinelearning.py:523-536) and broadcasts the chunk descriptors
+     (RCCL); every rank runs preprocess + the HIP forward + fused
+     softmax-top1 on its chunk of its HBM-resident dataset replica (one
+     hipGraph replay of hand-written gfx950 kernels, window start read on the
+     device); top-1 (class, prob) pairs are gathered to the coordinator (RCCL),
+     copied to host and recorded in the job-state tables.  Weak scaling (400
+     images per GPU per step); strong scaling (ONE 400-image query split over
+     the N ranks) as ``*_strong`` keys.
+  2. system (``value_system``, ``p50_system_s``, ``two_job_*``,
+     ``workers_per_query_*``): N node processes of the fault-tolerant runtime
+     (membership + failure detector, coordinator on rank 0, hot standby on the
+     last rank, RCCL rounds for N > 1).  The coordinator's client submits
+     ResNet18 queries (same shape as the headline), then an AlexNet job and a
+     ResNet18 job at the same time: the fair-time scheduler splits the GPUs
+     between them and the round path runs both side by side (report Fig 2).
+  3. coordinator failover (``coord_failover_*``): max(N, 2) node processes;
+     mid-job the launcher SIGKILLs the coordinator process, the standby
+     promotes itself, re-forms the collective group over the survivors and
+     finishes the job (report Fig 5).
+Phases 2-3 are bounded (``--extras-timeout``); if one fails its keys are null
+and ``extras_error`` says why -- the headline is never lost to them.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-  --gpus N > 1 without torchrun env vars: bench.py starts N rank processes
-  itself (one per GPU, RCCL over 127.0.0.1 rendezvous) and exits non-zero if
-  any rank fails.  Under torchrun (RANK set) it is one rank of the job.
-  --dry-run: gloo on the CPU with a fake forward (tests the launcher, the
-  collectives and the JSON contract without a GPU).
-  --system: the same metric through the fault-tolerant cluster runtime: every
-  rank runs a Node (membership + failure detector, coordinator on rank 0, hot
-  standby on the last rank), rank 0's client submits the queries to the
-  coordinator, which schedules them (fair-time split) as RCCL rounds over the
-  ranks (N > 1; TCP control plane for N = 1) and ingests the results into the
-  job-state tables.  Prints one JSON line with "mode": "system".
+  Without torchrun env vars the launcher starts the N ranks itself (RCCL over
+  127.0.0.1 rendezvous); under torchrun (RANK set) each torchrun process
+  starts its own rank child, and rank 0's launcher runs phases 2-3 on all N
+  GPUs after the headline.  Exits non-zero if a headline rank fails.
+  --dry-run: gloo on the CPU with a fake forward (launcher / collectives /
+  JSON contract without a GPU).  --system: phase 2 only (its own JSON line).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
+import signal
 import socket
 import statistics
 import subprocess
 import sys
+import tempfile
 import time
 
 BASELINE_IMG_PER_S = 41.0          # BASELINE.md: 400 img / 9.749 s (ResNet18, 5 workers)
 BASELINE_P50_S = 9.749             # BASELINE.md: p50 ResNet18 400-image query latency
+BASELINE_COORD_RECOVERY_S = 6.999  # BASELINE.md: coordinator failure, 1 undone query (report Fig 5)
 METRIC = "images/sec (whole node) + p50 query latency, ResNet18 bs=400 at 1/2/4/8 GPU"
 QUERY = 400                        # images per query (reference report p.1, ResNet18)
+QUERY_ALEXNET = 500                # AlexNet query size (report p.1)
 COMPUTE_F32 = ("f32-input MFMA (v_mfma_f32_16x16x4_f32), fp32 activations/weights, fp32 accumulate; "
                "3x3/s1 convs by fused fp32 Winograd F(2x2,3x3)")
 COMPUTE_SPLIT = ("fp32-accurate: every conv (fused stem, residual stages) on split fp16 (each fp32 value as "
                  "hi+lo halfs, 22-bit significand, 4 bytes; hi*hi+hi*lo+lo*hi on v_mfma_f32_16x16x32_f16, "
                  "fp32 accumulate), FC on the f32-input MFMA; logits checked against fp64 next to torch fp32")
+ROLE = "IDUNNO_BENCH_ROLE"
 
 
 def parse(argv=None):
@@ -83,18 +99,24 @@ def parse(argv=None):
                     help="synthetic images replicated in every rank's HBM (grown to fit a round)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--no-extras", action="store_true", help="skip the strong-scaling / fp16 / numerics extras")
+    ap.add_argument("--no-system", action="store_true", help="skip phases 2-3 (system + failover)")
+    ap.add_argument("--extras-timeout", type=float, default=240.0, help="seconds per system / failover phase")
+    ap.add_argument("--two-job-queries", type=int, default=10, help="queries per job in the two-job run")
+    ap.add_argument("--failover-queries", type=int, default=12, help="queries of the job the failover kills into")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--dry-run", action="store_true", help="CPU + gloo + fake forward (launcher/contract test)")
     ap.add_argument("--fail-rank", type=int, default=-1, help="testing: this rank exits 3 after warmup")
-    ap.add_argument("--launch-timeout", type=float, default=1500.0, help="self-launch: seconds before ranks are killed")
-    ap.add_argument("--system", action="store_true", help="measure through the node runtime (see docstring)")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0, help="seconds before headline ranks are killed")
+    ap.add_argument("--system", action="store_true", help="phase 2 only (see docstring)")
+    ap.add_argument("--phase", default="system", choices=["system", "failover"], help=argparse.SUPPRESS)
+    ap.add_argument("--work-dir", default=None, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
 # ---------------------------------------------------------------------------
-# self-launch (no torchrun): one child process per GPU, started before any
-# HIP call in this process
+# launcher (never initialises a GPU: children are started with subprocess,
+# nothing is ever exec'd in place)
 # ---------------------------------------------------------------------------
 
 def _free_port() -> int:
@@ -103,17 +125,39 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def launch_local(a, argv) -> int:
-    n = a.gpus
-    port = _free_port()
-    procs = []
-    for r in range(n):
-        env = dict(os.environ)
-        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
-    deadline = time.time() + a.launch_timeout
+def _child_env(role: str, rank: int, world: int, port: int, local: int | None = None) -> dict:
+    env = dict(os.environ)
+    for k in ("TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_RUN_ID", "GROUP_RANK", "ROLE_RANK"):
+        env.pop(k, None)
+    env.update({ROLE: role, "RANK": str(rank), "LOCAL_RANK": str(rank if local is None else local),
+                "WORLD_SIZE": str(world), "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(port)})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def _spawn(argv, env) -> subprocess.Popen:
+    return subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                            stdin=subprocess.DEVNULL)
+
+
+def _stop_all(procs, grace: float = 20.0) -> None:
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    end = time.time() + grace
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, end - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+
+
+def _wait_all(procs, timeout: float, what: str, on_poll=None) -> int:
+    """Wait for every child; the first non-zero exit (or the timeout) stops
+    the others.  Returns 0, the failing code, or 124."""
+    deadline = time.time() + timeout
     rc = 0
     try:
         while True:
@@ -121,30 +165,176 @@ def launch_local(a, argv) -> int:
             bad = [c for c in codes if c not in (None, 0)]
             if bad:
                 rc = bad[0]
-                print(f"bench: a rank exited with {rc}; stopping the others", file=sys.stderr, flush=True)
+                print(f"bench: a {what} process exited with {rc}; stopping the others", file=sys.stderr, flush=True)
                 break
             if all(c == 0 for c in codes):
                 return 0
             if time.time() > deadline:
-                print("bench: ranks timed out", file=sys.stderr, flush=True)
+                print(f"bench: {what} processes timed out", file=sys.stderr, flush=True)
                 rc = 124
                 break
-            time.sleep(0.2)
+            if on_poll is not None:
+                on_poll()
+            time.sleep(0.1)
     finally:
-        for p in procs:
-            if p.poll() is None:
-                p.terminate()
-        for p in procs:
-            try:
-                p.wait(timeout=20)
-            except subprocess.TimeoutExpired:
-                p.kill()
-                p.wait()
-    return rc if rc else 1
+        _stop_all(procs)
+    return rc
+
+
+def _read_json(path: str):
+    try:
+        with open(path) as f:
+            return json.loads(f.read().strip().splitlines()[-1])
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+def _headline(a, argv, work: str) -> tuple[int, dict | None]:
+    """Phase 1.  Self-launch: N rank children.  Under torchrun: this
+    process's own rank child (the others are started by their torchrun peers)."""
+    out = os.path.join(work, "headline.json")
+    child = [x for x in argv]
+    child += ["--json-out", out]
+    if "RANK" in os.environ:
+        rank, world = int(os.environ["RANK"]), int(os.environ.get("WORLD_SIZE", "1"))
+        if world != a.gpus:
+            print(json.dumps({"error": f"--gpus {a.gpus} but WORLD_SIZE={world}"}), flush=True)
+            return 2, None
+        # a port of its own (the torchrun agent store keeps MASTER_PORT)
+        port = int(os.environ.get("MASTER_PORT", "29500")) + 11
+        local = int(os.environ.get("LOCAL_RANK", str(rank)))
+        procs = [_spawn(child, _child_env("rank", rank, world, port, local))]
+    else:
+        port = _free_port()
+        procs = [_spawn(child, _child_env("rank", r, a.gpus, port)) for r in range(a.gpus)]
+    rc = _wait_all(procs, a.launch_timeout, "rank")
+    if rc:
+        return (rc if rc else 1), None
+    return 0, _read_json(out) if ("RANK" not in os.environ or int(os.environ["RANK"]) == 0) else None
+
+
+def _system_phase(a, work: str) -> dict:
+    """Phase 2: the runtime with N node processes (single job + two jobs)."""
+    out = os.path.join(work, "system.json")
+    port = _free_port()
+    argv = _phase_argv(a, "system", out, work)
+    procs = [_spawn(argv, _child_env("node", r, a.gpus, port)) for r in range(a.gpus)]
+    rc = _wait_all(procs, a.extras_timeout, "system-node")
+    d = _read_json(out)
+    if d is None:
+        return {"extras_error": f"system phase failed (rc={rc})"}
+    return d
+
+
+def _failover_phase(a, work: str) -> dict:
+    """Phase 3: SIGKILL the coordinator process mid-job (the standby times it)."""
+    out = os.path.join(work, "failover.json")
+    n = max(a.gpus, 2)
+    port = _free_port()
+    argv = _phase_argv(a, "failover", out, work)
+    procs = [_spawn(argv, _child_env("node", r, n, port, local=r % a.gpus)) for r in range(n)]
+    marker, killed = os.path.join(work, "kill_now"), os.path.join(work, "killed_at")
+    state = {"done": False}
+
+    def poll():
+        if not state["done"] and os.path.exists(marker):
+            procs[0].send_signal(signal.SIGKILL)          # the coordinator, mid-job
+            t = time.time()
+            with open(killed + ".tmp", "w") as f:
+                f.write(repr(t))
+            os.replace(killed + ".tmp", killed)
+            state["done"] = True
+
+    deadline = time.time() + a.extras_timeout
+    try:
+        while time.time() < deadline:
+            poll()
+            if procs[-1].poll() is not None:               # the standby wrote its result and left
+                break
+            if any(p.poll() not in (None, 0) for p in procs[1:]):
+                break
+            time.sleep(0.02)
+    finally:
+        _stop_all(procs)
+    d = _read_json(out)
+    if d is None:
+        return {"extras_error": f"failover phase failed (standby rc={procs[-1].returncode})"}
+    return d
+
+
+def _phase_argv(a, phase: str, out: str, work: str) -> list:
+    argv = ["--gpus", str(a.gpus), "--steps", str(a.steps), "--warmup", str(a.warmup), "--model", a.model,
+            "--dtype", a.dtype, "--fp32-impl", a.fp32_impl, "--batch", str(a.batch), "--seed", str(a.seed),
+            "--two-job-queries", str(a.two_job_queries), "--failover-queries", str(a.failover_queries),
+            "--phase", phase, "--json-out", out, "--work-dir", work, "--launch-timeout", str(a.extras_timeout)]
+    if a.dry_run:
+        argv.append("--dry-run")
+    return argv
+
+
+def launcher(a, argv) -> int:
+    work = tempfile.mkdtemp(prefix="idunno_bench_")
+    try:
+        if a.system:                                      # phase 2 only
+            d = _system_phase(a, work)
+            line = json.dumps(d)
+            print(line, flush=True)
+            if a.json_out:
+                with open(a.json_out, "w") as f:
+                    f.write(line + "\n")
+            return 0 if "extras_error" not in d else 1
+        rc, head = _headline(a, [x for x in argv if x not in ("--json-out",)], work)
+        if rc:
+            return rc
+        if head is None:                                  # a torchrun rank other than 0
+            return 0
+        if not a.no_system:
+            t0 = time.time()
+            for name, fn in (("system", _system_phase), ("failover", _failover_phase)):
+                try:
+                    d = fn(a, work)
+                except Exception as e:  # noqa: BLE001
+                    d = {"extras_error": f"{name}: {type(e).__name__}: {e}"}
+                err = d.pop("extras_error", None)
+                if err:
+                    head["extras_error"] = (head.get("extras_error", "") + "; " + err).lstrip("; ")
+                head.update(d)
+            head["extras_wall_s"] = round(time.time() - t0, 1)
+        line = json.dumps(head)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+        return 0
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    role = os.environ.get(ROLE)
+    if role == "rank":
+        return run_rank(a)
+    if role == "node":
+        return run_node(a)
+    # strip a --json-out the caller gave: the launcher writes the merged line there
+    clean, skip = [], False
+    for x in argv:
+        if skip:
+            skip = False
+            continue
+        if x == "--json-out":
+            skip = True
+            continue
+        if x.startswith("--json-out="):
+            continue
+        clean.append(x)
+    return launcher(a, clean)
 
 
 # ---------------------------------------------------------------------------
-# one rank
+# phase 1: one headline rank
 # ---------------------------------------------------------------------------
 
 class FakeRunner:
@@ -164,15 +354,7 @@ class FakeRunner:
         return run
 
 
-def main(argv=None) -> int:
-    argv = sys.argv[1:] if argv is None else argv
-    a = parse(argv)
-    if "RANK" not in os.environ and a.gpus > 1:
-        return launch_local(a, argv)
-
-    if a.system:
-        return run_system(a)
-
+def run_rank(a) -> int:
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -368,7 +550,6 @@ def main(argv=None) -> int:
         if runner is not None:
             out["model_tflops"] = round(program_flops(runner.p) * ips / 1e12, 2)
         line = json.dumps(out)
-        print(line, flush=True)
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
@@ -378,123 +559,228 @@ def main(argv=None) -> int:
     return 0
 
 
-def run_system(a) -> int:
-    """One rank of the --system measurement (see the module docstring)."""
-    import tempfile
 
+
+# ---------------------------------------------------------------------------
+# phases 2-3: one node process of the fault-tolerant runtime
+# ---------------------------------------------------------------------------
+
+def run_node(a) -> int:
+    """One node of the --system / failover measurement (see the docstring)."""
     import torch
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from idunno.config import ClusterConfig
-    from idunno.runtime.client import Client
     from idunno.runtime.data import SyntheticSource
     from idunno.runtime.executor import FakeExecutor, HipExecutor
-    from idunno.runtime.messages import Type
     from idunno.runtime.node import Node
-    from idunno.runtime.transport import TcpTransport, wait_for
+    from idunno.runtime.transport import TcpTransport
 
     rank = int(os.environ.get("RANK", "0"))
-    W = int(os.environ.get("WORLD_SIZE", "1"))
+    n = int(os.environ.get("WORLD_SIZE", "1"))           # node processes (failover: >= 2)
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    if W != a.gpus:
-        print(json.dumps({"error": f"--gpus {a.gpus} but WORLD_SIZE={W}"}), flush=True)
-        return 2
     gpu = not a.dry_run and torch.cuda.is_available()
     if not a.dry_run and not gpu:
-        print(json.dumps({"error": "bench.py --system needs a GPU (MI355X); use --dry-run on CPU"}), flush=True)
+        print(json.dumps({"error": "bench.py phases 2-3 need a GPU (MI355X); use --dry-run on CPU"}), flush=True)
         return 2
     dev = torch.device("cuda", local) if gpu else torch.device("cpu")
     if gpu:
         torch.cuda.set_device(dev)
+    W = a.gpus
     B = a.batch
     base = int(os.environ.get("MASTER_PORT", "29500")) + 200
     tmp = tempfile.mkdtemp(prefix=f"idunno_bench_r{rank}_")
-    cfg = ClusterConfig(num_nodes=W, base_port=base, store_root=tmp, collective_rounds=W > 1, dtype=a.dtype,
-                        max_chunk=B, rpc_timeout_s=60.0, worker_budget=W, dataset_size=10 ** 9,
-                        batch_size={a.model: W * B}, collective_port_offset=100)
+    # RCCL rounds need one GPU per node process; the 1-GPU failover shares GPU 0 (TCP path)
+    rounds = n > 1 and n <= W
+    cfg = ClusterConfig(num_nodes=n, base_port=base, store_root=tmp, collective_rounds=rounds, dtype=a.dtype,
+                        fp32_impl=a.fp32_impl, max_chunk=max(2048, B), rpc_timeout_s=60.0, worker_budget=W,
+                        dataset_size=10 ** 9, collective_port_offset=100,
+                        batch_size={"resnet18": QUERY * W, "alexnet": QUERY_ALEXNET * W, a.model: B * W})
+    if a.phase == "failover":
+        cfg.update(heartbeat_period_s=0.1, failure_timeout_s=1.0, metadata_period_s=0.2)
     name = cfg.node_name(rank)
-    ex = FakeExecutor() if a.dry_run else HipExecutor(dev, seed=a.seed, dtype=a.dtype)
+    ex = FakeExecutor() if a.dry_run else HipExecutor(dev, seed=a.seed, dtype=a.dtype, fp32_impl=a.fp32_impl)
     node = Node(cfg, name, TcpTransport(name, cfg.address, cfg.address(name)), ex)
     node.source = None if a.dry_run else SyntheticSource(cfg.data_seed, dev)
     if not a.dry_run:
-        ex.warmup(a.model, B)                       # capture before the clock starts
+        ex.warmup(a.model, B)                           # capture before any clock starts
     if rank != 0:
-        time.sleep(1.0)                             # the coordinator listens first
+        _wait_port(cfg.address(cfg.coordinator_name), 120)   # the coordinator listens first
     node.start(join=True)
-    if rank != 0:
+    driver = (rank == 0) if a.phase == "system" else (rank == n - 1)
+    if not driver:
         t_end = time.time() + a.launch_timeout
         while node.alive_flag and time.time() < t_end:
             time.sleep(0.2)
         node.stop()
         return 0
-    cl = Client(node)
     try:
-        assert wait_for(lambda: len(node.membership.alive()) == W, 60), node.membership.table()
-        if W > 1:
-            assert wait_for(lambda: node.rounds.group.formed and len(node.rounds.group.members) == W, 60)
-        per_q = W * B
-        nxt = [0]
-
-        def submit(k):
-            for _ in range(k):
-                s0 = nxt[0]
-                nxt[0] += per_q
-                cl.submit(a.model, s0, s0 + per_q - 1)
-
-        def done():
-            return node.state.images_done(a.model)
-
-        def wait_done(target, timeout=600):
-            return wait_for(lambda: done() >= target and node.state.pending_count() == 0, timeout, 0.001)
-
-        submit(a.warmup)
-        assert wait_done(nxt[0]), node.state.summary()
-        lat0 = len(node.state.query_latency[a.model])
-        t0 = time.perf_counter()
-        submit(a.steps)
-        assert wait_done(nxt[0]), node.state.summary()
-        elapsed = time.perf_counter() - t0
-        loaded = sorted(node.state.query_latency[a.model][lat0:])
-        lat1 = len(node.state.query_latency[a.model])
-        for _ in range(max(5, min(a.steps, 20))):   # unloaded: one query at a time
-            submit(1)
-            assert wait_done(nxt[0])
-        unloaded = sorted(node.state.query_latency[a.model][lat1:])
-        rounds = node.rounds.rounds_done if node.rounds is not None else 0
-        ips = per_q * a.steps / elapsed
-        p50 = unloaded[len(unloaded) // 2]
-        out = {
-            "metric": METRIC if (a.model == "resnet18" and B == QUERY) else
-            f"images/sec (whole node) + p50 query latency, {a.model} bs={B} at {W} GPU",
-            "value": round(ips, 2), "unit": "images/sec", "n_gpus": W, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(1000 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": round(ips / BASELINE_IMG_PER_S, 2) if a.model == "resnet18" and B == QUERY else None,
-            "dtype": "fp32" if a.dry_run else a.dtype, "mode": "system",
-            "data": "synthetic uint8 224x224x3 images (SyntheticSource on each GPU), random-init weights",
-            "config": {"model": a.model, "global_batch": per_q, "seq_len": None, "image_hw": 224,
-                       "batch_per_gpu": B, "parallelism": f"dp{W}",
-                       "path": ("client -> coordinator Node (membership, standby) -> fair-time split -> "
-                                + ("RCCL rounds" if W > 1 else "local JOB queue") + " -> job-state ingest"),
-                       "dry_run": a.dry_run},
-            "p50_query_latency_s": round(p50, 6),
-            "p50_query_latency_loaded_s": round(loaded[len(loaded) // 2], 6) if loaded else None,
-            "p50_vs_baseline_speedup": round(BASELINE_P50_S / p50, 1),
-            "results_recorded": done(), "collective_rounds": rounds,
-        }
-        line = json.dumps(out)
-        print(line, flush=True)
-        if a.json_out:
-            with open(a.json_out, "w") as f:
-                f.write(line + "\n")
+        res = _drive_system(a, node, W, B) if a.phase == "system" else _drive_failover(a, node, n)
+        with open(a.json_out + ".tmp", "w") as f:
+            f.write(json.dumps(res) + "\n")
+        os.replace(a.json_out + ".tmp", a.json_out)
         return 0
     finally:
-        if node.rounds is not None:
-            node.rounds.release()                   # members leave the epoch cleanly
+        from idunno.runtime.messages import Type
+
+        if node.rounds is not None and node.is_coordinator:
+            node.rounds.release()                       # members leave the epoch cleanly
         for m in node.membership.alive():
             if m != node.name:
                 node.transport.send(m, {"t": Type.KILL})
         time.sleep(0.2)
         node.stop()
+
+
+def _wait_port(addr, timeout: float) -> None:
+    end = time.time() + timeout
+    while time.time() < end:
+        try:
+            socket.create_connection(addr, timeout=0.2).close()
+            return
+        except OSError:
+            time.sleep(0.05)
+
+
+def _cluster_ready(node, n: int, timeout: float = 120.0) -> None:
+    from idunno.runtime.transport import wait_for
+
+    assert wait_for(lambda: len(node.membership.alive()) == n, timeout), node.membership.table()
+    if node.cfg.collective_rounds and node.is_coordinator:
+        assert wait_for(lambda: node.rounds.group.formed and len(node.rounds.group.members) == n, timeout)
+
+
+def _drive_system(a, node, W: int, B: int) -> dict:
+    """Coordinator (rank 0): single-job throughput + p50, then two concurrent
+    jobs under the fair-time split."""
+    from idunno.runtime.client import Client
+    from idunno.runtime.transport import wait_for
+
+    _cluster_ready(node, W)
+    cl = Client(node)
+    st = node.state
+    per_q = W * B
+    nxt = [0]
+
+    def submit(k):
+        for _ in range(k):
+            s0 = nxt[0]
+            nxt[0] += per_q
+            cl.submit(a.model, s0, s0 + per_q - 1)
+
+    def wait_done(target, timeout=300):
+        return wait_for(lambda: st.images_done(a.model) >= target and st.pending_count() == 0, timeout, 0.001)
+
+    submit(a.warmup)
+    assert wait_done(nxt[0]), st.summary()
+    lat0 = len(st.query_latency[a.model])
+    t0 = time.perf_counter()
+    submit(a.steps)
+    assert wait_done(nxt[0]), st.summary()
+    elapsed = time.perf_counter() - t0
+    loaded = sorted(st.query_latency[a.model][lat0:])
+    lat1 = len(st.query_latency[a.model])
+    for _ in range(max(5, min(a.steps, 20))):   # unloaded: one query at a time
+        submit(1)
+        assert wait_done(nxt[0])
+    unloaded = sorted(st.query_latency[a.model][lat1:])
+    ips = per_q * a.steps / elapsed
+    p50 = unloaded[len(unloaded) // 2]
+    out = {"value_system": round(ips, 2), "ms_per_step_system": round(1000 * elapsed / a.steps, 4),
+           "p50_system_s": round(p50, 6),
+           "p50_system_loaded_s": round(loaded[len(loaded) // 2], 6) if loaded else None,
+           "system_path": ("client -> coordinator Node (membership, hot standby) -> fair-time split -> "
+                           + ("RCCL rounds" if node.rounds is not None else "local JOB queue")
+                           + " -> job-state ingest"),
+           "system_results_recorded": st.images_done(a.model)}
+
+    # two concurrent jobs: AlexNet + ResNet18 (report Fig 2), coordinator-side jobs
+    bs = {"alexnet": QUERY_ALEXNET * W, "resnet18": QUERY * W}
+    done = {m: st.images_done(m) for m in bs}
+    base_img = [10 ** 7]
+
+    def two_jobs(q: int):
+        qn0 = {m: st.next_qnum[m] for m in bs}
+        t = time.perf_counter()
+        for m in ("alexnet", "resnet18"):
+            cl.submit_job(base_img[0], base_img[0] + q * bs[m] - 1, m)
+            done[m] += q * bs[m]
+        base_img[0] += 10 ** 6
+        ok = wait_for(lambda: all(st.images_done(m) >= done[m] for m in bs) and st.pending_count() == 0,
+                      300, 0.002)
+        assert ok, st.summary()
+        return time.perf_counter() - t, qn0
+
+    two_jobs(2)                                  # warm: graphs for the split sizes, EMAs settle
+    r0 = node.rounds.stats() if node.rounds is not None else {}
+    wall, qn0 = two_jobs(a.two_job_queries)
+    r1 = node.rounds.stats() if node.rounds is not None else {}
+    imgs = a.two_job_queries * sum(bs.values())
+    per = {}
+    with st.lock:
+        for m in bs:
+            ws = []
+            for q in range(qn0[m] + 1, st.next_qnum[m] + 1):
+                ents = st.worker_set.get((m, q), [])
+                if ents:
+                    ws.append(len({e[0] for e in ents}))
+            per[m] = ws
+            lat = st.query_latency[m][-a.two_job_queries:]
+            out[f"two_job_p50_{m}_s"] = round(statistics.median(lat), 6) if lat else None
+    out.update({"two_job_images_per_s": round(imgs / wall, 2), "two_job_wall_s": round(wall, 4),
+                "two_job_queries_per_job": a.two_job_queries,
+                "two_job_query_images": bs,
+                "workers_per_query_alexnet": per["alexnet"], "workers_per_query_resnet18": per["resnet18"],
+                "two_job_mixed_rounds": (r1.get("mixed_rounds", 0) - r0.get("mixed_rounds", 0)) if r1 else None,
+                "sched_avg_time_s": {m: round(v, 6) for m, v in node.sched.avg_time.items()}})
+    return out
+
+
+def _drive_failover(a, node, n: int) -> dict:
+    """Standby (last node): submit a job, let the launcher SIGKILL the
+    coordinator mid-job, time the promotion and the restored service."""
+    from idunno.runtime.client import Client
+    from idunno.runtime.transport import wait_for
+
+    _cluster_ready(node, n)
+    if node.cfg.collective_rounds:
+        wait_for(lambda: False, 1.0)             # let the coordinator's epoch settle
+    cl = Client(node)
+    st = node.state
+    model = "resnet18"
+    bs = node.cfg.batch_for(model)
+    Q = a.failover_queries
+    total = Q * bs
+    promoted = {}
+    node.membership.on_master_change.append(
+        lambda new, ep: promoted.setdefault("t", time.time()) if new == node.name else None)
+    cl.submit_job(0, total - 1, model)
+    # kill once a few queries have finished at the standby (mirrored results)
+    assert wait_for(lambda: st.images_done(model) >= min(2, Q - 1) * bs, 120, 0.002), st.summary()
+    done_at_kill = st.images_done(model)
+    work = a.work_dir or tempfile.gettempdir()
+    with open(os.path.join(work, "kill_now"), "w") as f:
+        f.write("1")
+    killed = os.path.join(work, "killed_at")
+    assert wait_for(lambda: os.path.exists(killed), 30, 0.001), "launcher did not kill the coordinator"
+    with open(killed) as f:
+        t_kill = float(f.read())
+    assert wait_for(lambda: "t" in promoted and node.is_coordinator, 60, 0.001), "standby did not promote"
+    base_done = st.images_done(model)
+    t_prom = promoted["t"]
+    wait_for(lambda: st.images_done(model) > base_done or st.images_done(model) >= total, 60, 0.001)
+    t_restored = time.time()
+    ok = wait_for(lambda: st.images_done(model) >= total and st.pending_count() == 0, 120, 0.002)
+    t_all = time.time()
+    rec = max(0.0, t_restored - t_kill)
+    return {"coord_failover_recovery_s": round(rec, 4),
+            "coord_failover_detect_s": round(t_prom - t_kill, 4),
+            "coord_failover_all_done_s": round(t_all - t_kill, 4),
+            "coord_failover_undone_queries": Q - done_at_kill // bs,
+            "coord_failover_images_exact": bool(ok and st.images_done(model) == total),
+            "coord_failover_nodes": n, "coord_failover_failure_timeout_s": node.cfg.failure_timeout_s,
+            "coord_failover_vs_baseline_speedup": round(BASELINE_COORD_RECOVERY_S / rec, 1) if rec > 0 else None,
+            "coord_failover_rounds": bool(node.cfg.collective_rounds)}
 
 
 def numerics_check(runner, a, device, n: int = 8) -> dict:

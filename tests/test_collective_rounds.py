@@ -10,6 +10,7 @@ Liveness comes from the failure detector, not the collective timeout: the
 killed member's round must be recovered within failure_timeout_s + 1 s, and an
 idle gap longer than collective_timeout_s (now only the rendezvous timeout)
 must not break the epoch."""
+import ast
 import os
 import signal
 import subprocess
@@ -25,14 +26,14 @@ from idunno.runtime.executor import FakeExecutor
 from idunno.runtime.node import Node
 from idunno.runtime.transport import TcpTransport, wait_for
 
-from test_multiprocess import ROOT, _base_port
+from test_multiprocess import ROOT, _base_port, wait_listening
 
 
 def _indices(cl):
     idx = set()
     for _k, chunks in cl.view("c4")["results"].items():
         for ch in chunks:
-            idx |= {int(t[0][5:-5]) for t in eval(ch)}
+            idx |= {int(t[0][5:-5]) for t in ast.literal_eval(ch)}
     return idx
 
 
@@ -55,7 +56,7 @@ def test_collective_rounds_with_failures():
     assert cfg.collective_rounds
     me = Node(cfg, "node03", TcpTransport("node03", cfg.address, cfg.address("node03")), FakeExecutor())
     try:
-        time.sleep(1.0)
+        wait_listening([base + i for i in range(n - 1)], procs=list(procs.values()))
         me.start(join=True)
         assert wait_for(lambda: len(me.membership.alive()) == n, 15), me.membership.table()
         # the coordinator forms the group over all 4 nodes; this node is a member

@@ -42,6 +42,27 @@ def _base_port(n):
     raise RuntimeError("no port range")
 
 
+def wait_listening(ports, timeout: float = 60.0, procs=None) -> None:
+    """Block until every port accepts a TCP connection (a started node's
+    control plane is up) instead of sleeping a fixed time: a loaded machine
+    can take seconds to import torch in each child."""
+    end = time.monotonic() + timeout
+    left = set(ports)
+    while left:
+        for p in list(left):
+            try:
+                socket.create_connection(("127.0.0.1", p), timeout=0.2).close()
+                left.discard(p)
+            except OSError:
+                pass
+        if left:
+            if procs and any(pr.poll() is not None for pr in procs):
+                raise RuntimeError("a node process exited during start-up")
+            if time.monotonic() > end:
+                raise TimeoutError(f"ports {sorted(left)} not listening after {timeout}s")
+            time.sleep(0.05)
+
+
 @pytest.mark.slow
 def test_multiprocess_cluster_failures():
     n = 4
@@ -59,7 +80,7 @@ def test_multiprocess_cluster_failures():
                         failure_timeout_s=1.2, metadata_period_s=0.1, rpc_timeout_s=3.0)
     me = Node(cfg, "node03", TcpTransport("node03", cfg.address, cfg.address("node03")), FakeExecutor())
     try:
-        time.sleep(1.0)
+        wait_listening([base + i for i in range(n - 1)], procs=list(procs.values()))
         me.start(join=True)
         assert wait_for(lambda: len(me.membership.alive()) == n, 15), me.membership.table()
         cl = Client(me)
