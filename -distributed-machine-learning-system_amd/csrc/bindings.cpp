@@ -287,6 +287,31 @@ void set_split_c64_default(bool on) { g_split_c64_default = on; }
 static bool g_split_patch_default = false;
 void set_split_patch_default(bool on) { g_split_patch_default = on; }
 #endif
+// Split range guard (common.h split_guard): the int32 flag
+// that this thread's split launches write to when a value leaves fp16's range;
+// HipRunner sets it around a split forward (a captured graph keeps the pointer).
+static thread_local int* g_split_guard = nullptr;
+static thread_local int g_split_guard_dev = -1;
+void set_split_guard(c10::optional<torch::Tensor> flag) {
+  if (!flag.has_value() || !flag->defined()) {
+    g_split_guard = nullptr;
+    g_split_guard_dev = -1;
+    return;
+  }
+  auto& f = *flag;
+  CHECK_DEV(f);
+  CHECK_CONTIG(f);
+  CHECK_DT(f, torch::kInt);
+  TORCH_CHECK(f.numel() >= 1, "split guard flag must hold one int32");
+  g_split_guard = f.data_ptr<int>();
+  g_split_guard_dev = f.device().index();
+}
+static int* split_guard_for(const torch::Device& dev) {
+  if (g_split_guard == nullptr) return nullptr;
+  TORCH_CHECK(dev.index() == g_split_guard_dev, "split guard flag lives on another device");
+  return g_split_guard;
+}
+
 // split convs: tile order (0 m-major, 1 n-major, -1 auto heuristic)
 static int g_split_norder = -1;
 void set_split_norder(int64_t mode) { g_split_norder = (int)mode; }
@@ -363,6 +388,7 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   a.relu = relu ? 1 : 0;
   a.acc_scale = (float)acc_scale;
   a.ablate = g_conv_ablate;
+  a.ovf = out_f32 ? nullptr : split_guard_for(x.device());
   if (M == 0) return y;
   a.zero = zero_buffer(x.device()).data_ptr();
   const bool c64_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 &&
@@ -370,7 +396,7 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   if (tile == 50 || (tile < 0 && c64_ok && g_split_c64_default)) {
     TORCH_CHECK(c64_ok, "tile 50 (row-streaming split 3x3 64->64 conv) does not support this shape");
     conv3x3_split_c64_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W, a.relu,
-                             a.acc_scale, cur_stream());
+                             a.acc_scale, a.ovf, cur_stream());
     check_launch("conv3x3_split_c64");
     return y;
   }
@@ -445,7 +471,8 @@ torch::Tensor linear_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
                          relu ? 1 : 0, y.data_ptr(), true, cur_stream());
   else
     splitk_reduce_split_launch(part.data_ptr<float>(), (int)splits, (long)(M * N), (int)N, bias.data_ptr<float>(),
-                               relu ? 1 : 0, reinterpret_cast<half_t*>(y.data_ptr()), cur_stream());
+                               relu ? 1 : 0, reinterpret_cast<half_t*>(y.data_ptr()), split_guard_for(x.device()),
+                               cur_stream());
   check_launch("splitk_reduce");
   return y;
 }
@@ -462,7 +489,8 @@ torch::Tensor split_from_f32(torch::Tensor x) {
   auto y = torch::empty(sz, x.options().dtype(torch::kHalf));
   const long npix = C ? x.numel() / C : 0;
   if (npix == 0) return y;
-  split_from_f32_launch(x.data_ptr<float>(), reinterpret_cast<half_t*>(y.data_ptr()), npix, C, cur_stream());
+  split_from_f32_launch(x.data_ptr<float>(), reinterpret_cast<half_t*>(y.data_ptr()), npix, C,
+                        split_guard_for(x.device()), cur_stream());
   check_launch("split_from_f32");
   return y;
 }
@@ -509,7 +537,7 @@ torch::Tensor maxpool2d_split(torch::Tensor x, int64_t k, int64_t s, int64_t pad
   }
   if ((long)B * Ho * Wo == 0) return y;
   maxpool_split_launch(x.data_ptr(), in_split, reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, C, Ho, Wo, k, s, pad,
-                       cur_stream());
+                       split_guard_for(x.device()), cur_stream());
   check_launch("maxpool_split");
   return y;
 }
@@ -942,7 +970,7 @@ torch::Tensor stem_split(torch::Tensor img, torch::Tensor w, torch::Tensor bias,
   if (B) {
     stem_split_launch(img.data_ptr<uint8_t>(), reinterpret_cast<const half_t*>(w.data_ptr()), bias.data_ptr<float>(),
                       psum.data_ptr<float>(), (float)acc_scale, reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp,
-                      start_offset, max_start, sp ? sub : 0, cur_stream());
+                      start_offset, max_start, sp ? sub : 0, split_guard_for(img.device()), cur_stream());
     check_launch("stem_split");
   }
   return y;
@@ -1100,7 +1128,8 @@ torch::Tensor global_avgpool_nhwc(torch::Tensor x) {
 
 // Optional `packed` [>= rows, 2] int32: also write (class, prob bits) pairs there
 // (the data plane's gather send buffer, so no repack kernel runs afterwards).
-std::vector<torch::Tensor> softmax_top1(torch::Tensor logits, c10::optional<torch::Tensor> packed) {
+std::vector<torch::Tensor> softmax_top1(torch::Tensor logits, c10::optional<torch::Tensor> packed,
+                                        c10::optional<torch::Tensor> ovf) {
   CHECK_DEV(logits);
   CHECK_DT(logits, torch::kFloat);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [rows, N] with unit column stride");
@@ -1117,8 +1146,16 @@ std::vector<torch::Tensor> softmax_top1(torch::Tensor logits, c10::optional<torc
     TORCH_CHECK(p.dim() == 2 && p.size(1) == 2 && p.size(0) >= rows, "packed must be [>= rows, 2] int32");
     pk = p.data_ptr<int>();
   }
+  const int* of = nullptr;
+  if (ovf.has_value() && ovf->defined()) {
+    auto& f = *ovf;
+    CHECK_DEV(f);
+    CHECK_DT(f, torch::kInt);
+    TORCH_CHECK(f.device() == logits.device() && f.numel() >= 1, "ovf must be an int32 flag on the logits device");
+    of = f.data_ptr<int>();
+  }
   if (rows) softmax_top1_launch(logits.data_ptr<float>(), ld, N, rows, cls.data_ptr<int>(), prob.data_ptr<float>(),
-                                pk, cur_stream()); check_launch("softmax_top1");
+                                pk, of, cur_stream()); check_launch("softmax_top1");
   return {cls, prob};
 }
 
@@ -1203,8 +1240,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool2d_nhwc", &maxpool2d_nhwc, "NHWC max pool (into ``out`` when given)", py::arg("x"), py::arg("k"),
         py::arg("s"), py::arg("pad"), py::arg("out") = py::none());
   m.def("global_avgpool_nhwc", &global_avgpool_nhwc, "NHWC global average pool");
-  m.def("softmax_top1", &softmax_top1, "fused row softmax + argmax", py::arg("logits"),
-        py::arg("packed") = py::none());
+  m.def("softmax_top1", &softmax_top1, "fused row softmax + argmax; a set ``ovf`` flag marks every row -2",
+        py::arg("logits"), py::arg("packed") = py::none(), py::arg("ovf") = py::none());
+  m.def("set_split_guard", &set_split_guard,
+        "split range guard flag (int32 device tensor) for this thread's split launches; None = off",
+        py::arg("flag") = py::none());
   m.def("synth_images", &synth_images, "deterministic synthetic uint8 images [n,hw,hw,3]");
   m.def("pick_tile", &pick_tile, "tile id the conv heuristic picks for (M, Cout)");
   m.def("set_stem_workgroups_per_cu", &set_stem_workgroups_per_cu,

@@ -107,6 +107,18 @@ __device__ __forceinline__ void split_f16x4(const float4v v, half4v& h, half4v& 
   }
 }
 
+// Split range guard: a value with |v| >= 65504 has no
+// finite hi half, so a split epilogue that meets one flags the forward.  The
+// flag is an int in device memory owned by the runner (nullptr: unguarded);
+// every lane that sees an out-of-range value stores 1 with a plain vector
+// store (racing writers store the same value).  softmax_top1 then marks the
+// batch, and the host reruns it on the all-f32 path, which has fp32's range.
+__device__ __forceinline__ void split_guard(int* ovf, const float4v v) {
+  constexpr float kMax = 65504.f;
+  if (ovf != nullptr && !(fabsf(v[0]) < kMax && fabsf(v[1]) < kMax && fabsf(v[2]) < kMax && fabsf(v[3]) < kMax))
+    *ovf = 1;
+}
+
 __device__ __forceinline__ void reg_tie(half4v& r) { asm volatile("" : "+v"(r)); }
 __device__ __forceinline__ void reg_tie(float4v& r) { asm volatile("" : "+v"(r)); }
 

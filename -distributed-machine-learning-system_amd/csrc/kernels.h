@@ -32,6 +32,16 @@ struct ConvArgs {
   long ysplit;
   float acc_scale;   // conv_glds SPLIT: accumulator multiplier (2^-e of the pre-scaled split weights)
   int norder;        // conv_glds: 1 = n-major tile order (tn = lid / tiles_m), 0 = m-major
+  int* ovf;          // conv_glds SPLIT: split range guard flag (common.h split_guard) or nullptr
+  // conv_glds SPLIT dual conv (two convs of one input in one launch, outputs side
+  // by side in y): output channels >= nsplit_n are the second conv -- its own
+  // accumulator scale acc_scale2, no ReLU, and with center_only its K loop runs
+  // over the centre tap only (a 1x1/s stride-s conv is the centre tap of the
+  // 3x3/s pad-1 conv on the same input: ResNet downsample + first 3x3)
+  int nsplit_n;
+  int center_only;
+  float acc_scale2;
+  int ldr;           // residual pixel stride in halfs (0: the output width, 2*Cout split / Cout fp16)
 };
 
 // fp32 (reference-precision) conv: same geometry fields as ConvArgs, f32 tensors.
@@ -116,10 +126,10 @@ void maxpool_f32_launch(const float* x, float* y, int B, int H, int W, int C, in
                         int pad, hipStream_t st);
 void avgpool_f32_launch(const float* x, float* y, int B, int HW, int C, hipStream_t st);
 // split-fp16 layout conversions and pooling (elementwise_split.hip)
-void split_from_f32_launch(const float* x, half_t* y, long npix, int C, hipStream_t st);
+void split_from_f32_launch(const float* x, half_t* y, long npix, int C, int* ovf, hipStream_t st);
 void f32_from_split_launch(const half_t* x, float* y, long npix, int C, hipStream_t st);
 void maxpool_split_launch(const void* x, bool in_split, half_t* y, int B, int H, int W, int C, int Ho, int Wo, int k,
-                          int s, int pad, hipStream_t st);
+                          int s, int pad, int* ovf, hipStream_t st);
 
 void conv_igemm_launch(ConvArgs a, bool small, bool out_f32, int tile, hipStream_t st);
 int conv_pick_tile(int M, int Cout);
@@ -141,7 +151,8 @@ void conv3x3_patch_split_launch(const half_t* x, const half_t* w, const float* b
 // split 3x3/s1/p1 64 -> 64 conv, weights in registers, input rows streamed through an LDS ring
 bool conv3x3_split_c64_supported(int H, int W, int C, int Cout);
 void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
-                              const void* zero, int B, int H, int W, int relu, float acc_scale, hipStream_t st);
+                              const void* zero, int B, int H, int W, int relu, float acc_scale, int* ovf,
+                              hipStream_t st);
 // split-fp16 RGB stem on packed rows (a.cpk > 0, x from preprocess_pack3_split): fp32 output
 bool conv_glds_split_p3_launch(ConvArgs a, int tile, hipStream_t st);   // a.cpk > 0: pack3 stem
 bool conv_big_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
@@ -161,7 +172,7 @@ int conv_glds_pick(int M, int Cout);
 void set_stem_split_niw(int n);   // A/B: 16-cout fragments per wave (1 default, 2)
 void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
                        half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,
-                       long long max_start, long long sub, hipStream_t st);
+                       long long max_start, long long sub, int* ovf, hipStream_t st);
 void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, half_t* y, int B, int H, int W,
                        const long long* start_idx, long long start_off, long long max_start, long long sub,
                        hipStream_t st);
@@ -176,10 +187,11 @@ void synth_images_launch(uint8_t* out, uint64_t seed, long start, long n, long b
                          hipStream_t st);
 // split-K combine into the split-fp16 layout [M][2N] (N % 32 == 0)
 void splitk_reduce_split_launch(const float* part, int S, long MN, int N, const float* bias, int relu, half_t* y,
-                                hipStream_t st);
+                                int* ovf, hipStream_t st);
 void splitk_reduce_launch(const float* part, int S, long MN, int N, const float* bias, int relu, void* y,
                           bool out_f32, hipStream_t st);
+// ovf (or nullptr): a set split range guard marks every row class -2, prob 0 (rerun on the f32 path)
 void softmax_top1_launch(const float* logits, int ld, int N, int rows, int* cls, float* prob, int* packed,
-                         hipStream_t st);
+                         const int* ovf, hipStream_t st);
 
 }  // namespace idunno

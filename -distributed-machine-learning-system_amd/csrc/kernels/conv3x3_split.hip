@@ -47,6 +47,7 @@ struct C64sArgs {
   const void* zero;     // >= 16 zero bytes
   int B, H, W, relu, band, nbands, ntasks;
   float acc_scale;
+  int* ovf;             // split range guard flag or nullptr (common.h split_guard)
 };
 
 __device__ __forceinline__ int c64s_slot(int chunk, int col) { return chunk ^ ((2 * col) & 15); }
@@ -218,6 +219,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
         }
+        split_guard(a.ovf, v);
         half4v h, l;
         split_f16x4(v, h, l);
         *reinterpret_cast<half4v*>(a.y + off) = h;
@@ -235,9 +237,11 @@ bool conv3x3_split_c64_supported(int H, int W, int C, int Cout) {
 }
 
 void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
-                              const void* zero, int B, int H, int W, int relu, float acc_scale, hipStream_t st) {
+                              const void* zero, int B, int H, int W, int relu, float acc_scale, int* ovf,
+                              hipStream_t st) {
   using namespace c64s;
   C64sArgs a;
+  a.ovf = ovf;
   a.x = x;
   a.w = w;
   a.bias = bias;

@@ -94,6 +94,8 @@ conv_glds_kernel(const ConvArgs a) {
   const int tm = a.norder ? lid % a.tiles_m : lid / a.tiles_n;
   const int tn = a.norder ? lid / a.tiles_m : lid % a.tiles_n;
   const int n0 = tn * BN, m0 = tm * BM;
+  // dual conv: this tile belongs to the second conv (see ConvArgs::nsplit_n)
+  const bool second = a.nsplit_n > 0 && n0 >= a.nsplit_n;
   const half_t* const xin = a.x + (size_t)split * a.kslice;        // split-K: this block's K slice
   const half_t* const win = a.w + (size_t)split * a.kslice;
 
@@ -140,8 +142,16 @@ conv_glds_kernel(const ConvArgs a) {
     }
   }
 
-  // issue-side K coordinates (run NS-1 stages ahead of compute)
+  // issue-side K coordinates (run NS-1 stages ahead of compute); the second
+  // conv of a centre-only dual launch covers the centre tap's cblk stages
   int i_s = 0, i_cb = 0, i_kw = 0, i_kh = 0;
+  int nK = a.nK;
+  if (second && a.center_only) {
+    i_kh = a.KH / 2;
+    i_kw = a.KW / 2;
+    i_s = (i_kh * a.KW + i_kw) * a.cblk;
+    nK = a.cblk;
+  }
   auto issue = [&](int buf) {
     char* base = smem + buf * STAGE;
     const int koff = i_s * BK;
@@ -218,13 +228,12 @@ conv_glds_kernel(const ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
         const int m = m0 + wm * TM + j * 16 + (lane & 15);
-        const size_t off = (m < a.M && n < a.Cout) ? (size_t)m * a.Cout + n : 0;
+        const size_t off = (m < a.M && n < a.Cout) ? (size_t)m * (a.ldr ? a.ldr : a.Cout) + n : 0;
         rv[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : gload_b64_untracked(a.res + off);
       }
     }
   }
 
-  const int nK = a.nK;
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < nK) issue(p);
@@ -317,7 +326,7 @@ conv_glds_kernel(const ConvArgs a) {
       const int m = m0 + wm * TM + j * 16 + (lane & 15);
       const bool ok = m < a.M && n < a.Cout;
       if constexpr (SPLIT) {
-        const size_t off = ok ? (size_t)m * 2 * a.Cout + split_off(n) : 0;
+        const size_t off = ok ? (size_t)m * (a.ldr ? a.ldr : 2 * a.Cout) + split_off(n) : 0;
         if (a.ablate & 2) {
           rv[i][j] = half4v{0, 0, 0, 0};
           rl[i][j] = half4v{0, 0, 0, 0};
@@ -326,11 +335,13 @@ conv_glds_kernel(const ConvArgs a) {
           rl[i][j] = *reinterpret_cast<const half4v*>(a.res + off + 32);
         }
       } else {
-        const size_t off = ok ? (size_t)m * a.Cout + n : 0;
+        const size_t off = ok ? (size_t)m * (a.ldr ? a.ldr : a.Cout) + n : 0;
         rv[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : *reinterpret_cast<const half4v*>(a.res + off);
       }
     }
   };
+  const float acc_scale = second ? a.acc_scale2 : a.acc_scale;
+  const bool relu = a.relu && !second;
   if constexpr (HAS_RES && LATE_RES && !RES_PER_I) {
 #pragma unroll
     for (int i = 0; i < FN; ++i) load_res(i);
@@ -352,7 +363,7 @@ conv_glds_kernel(const ConvArgs a) {
       const int m = m0 + wm * TM + j * 16 + (lane & 15);
       if (m >= a.M) continue;
       float4v v;
-      if constexpr (SPLIT) v = acc[i][j] * a.acc_scale + bv;
+      if constexpr (SPLIT) v = acc[i][j] * acc_scale + bv;
       else v = acc[i][j] + bv;
       if constexpr (HAS_RES) {
         const half4v r = rv[i][j];
@@ -369,7 +380,7 @@ conv_glds_kernel(const ConvArgs a) {
           v[3] += (float)r[3];
         }
       }
-      if (a.relu) {
+      if (relu) {
         v[0] = fmaxf(v[0], 0.f);
         v[1] = fmaxf(v[1], 0.f);
         v[2] = fmaxf(v[2], 0.f);
@@ -380,6 +391,7 @@ conv_glds_kernel(const ConvArgs a) {
       } else if constexpr (OUT_F32) {
         *reinterpret_cast<float4v*>(static_cast<float*>(a.y) + (size_t)split * a.ysplit + (size_t)m * a.ldy + n) = v;
       } else if constexpr (SPLIT) {
+        split_guard(a.ovf, v);
         half4v h, l;
         split_f16x4(v, h, l);
         half_t* yp = static_cast<half_t*>(a.y) + (size_t)m * a.ldy + split_off(n);

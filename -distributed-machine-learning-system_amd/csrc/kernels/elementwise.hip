@@ -214,7 +214,8 @@ void avgpool_launch(const half_t* x, half_t* y, int B, int HW, int C, hipStream_
 // Split-K combine: y[m][n] = act(sum_s part[s][m][n] + bias[n]), 4 outputs per
 // thread (16-byte partial loads), fp16 or fp32 out.
 __global__ void splitk_reduce_kernel(const float* __restrict__ part, int S, long MN, int N,
-                                     const float* __restrict__ bias, int relu, void* __restrict__ y, int out_f32) {
+                                     const float* __restrict__ bias, int relu, void* __restrict__ y, int out_f32,
+                                     int* ovf) {
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= MN) return;
   float4v v = *reinterpret_cast<const float4v*>(part + i);
@@ -228,6 +229,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, int S, long
     v[3] = fmaxf(v[3], 0.f);
   }
   if (out_f32 == 2) {                     // split-fp16 layout [M][2N] (N % 32 == 0)
+    split_guard(ovf, v);
     half4v h, l;
     split_f16x4(v, h, l);
     half_t* yp = static_cast<half_t*>(y) + (i / N) * 2 * N + split_off(n);
@@ -246,10 +248,10 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, int S, long
 }
 
 void splitk_reduce_split_launch(const float* part, int S, long MN, int N, const float* bias, int relu, half_t* y,
-                                hipStream_t st) {
+                                int* ovf, hipStream_t st) {
   const long threads = (MN + 3) / 4;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, part, S, MN, N,
-                     bias, relu, (void*)y, 2);
+                     bias, relu, (void*)y, 2, ovf);
 }
 
 void splitk_reduce_launch(const float* part, int S, long MN, int N, const float* bias, int relu, void* y,
@@ -257,17 +259,29 @@ void splitk_reduce_launch(const float* part, int S, long MN, int N, const float*
   const int bs = 256;
   const long threads = (MN + 3) / 4;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((threads + bs - 1) / bs)), dim3(bs), 0, st, part, S, MN, N,
-                     bias, relu, y, out_f32 ? 1 : 0);
+                     bias, relu, y, out_f32 ? 1 : 0, (int*)nullptr);
 }
 
 // Row softmax + top-1: one 64-lane wave per row of fp32 logits.
 // prob(top1) = 1 / sum_j exp(x_j - x_max).  Ties resolve to the lowest index
 // (torch.topk semantics on CPU).
 __global__ void softmax_top1_kernel(const float* __restrict__ logits, int ld, int N, int rows,
-                                    int* __restrict__ cls, float* __restrict__ prob, int* __restrict__ packed) {
+                                    int* __restrict__ cls, float* __restrict__ prob, int* __restrict__ packed,
+                                    const int* __restrict__ ovf) {
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (wave >= rows) return;
+  if (ovf != nullptr && *ovf != 0) {        // split range exceeded somewhere in this forward
+    if (lane == 0) {
+      cls[wave] = -2;
+      prob[wave] = 0.f;
+      if (packed != nullptr) {
+        packed[2 * wave] = -2;
+        packed[2 * wave + 1] = 0;
+      }
+    }
+    return;
+  }
   const float* r = logits + (size_t)wave * ld;
   float best = -INFINITY;
   int bidx = 0x7fffffff;
@@ -302,11 +316,11 @@ __global__ void softmax_top1_kernel(const float* __restrict__ logits, int ld, in
 }
 
 void softmax_top1_launch(const float* logits, int ld, int N, int rows, int* cls, float* prob, int* packed,
-                         hipStream_t st) {
+                         const int* ovf, hipStream_t st) {
   const int bs = 256;  // 4 rows per block
   const int grid = (rows + 3) / 4;
   hipLaunchKernelGGL(softmax_top1_kernel, dim3(grid), dim3(bs), 0, st, logits, ld, N, rows, cls,
-                     prob, packed);
+                     prob, packed, ovf);
 }
 
 // Deterministic synthetic images: byte group g (8 bytes) of image `idx` is the

@@ -21,7 +21,8 @@ __device__ __forceinline__ float4v load_split4(const half_t* p) {
                  (float)h[3] + (float)l[3]};
 }
 
-__device__ __forceinline__ void store_split4(half_t* p, const float4v v) {
+__device__ __forceinline__ void store_split4(half_t* p, const float4v v, int* ovf = nullptr) {
+  split_guard(ovf, v);
   half4v h, l;
   split_f16x4(v, h, l);
   *reinterpret_cast<half4v*>(p) = h;
@@ -29,13 +30,14 @@ __device__ __forceinline__ void store_split4(half_t* p, const float4v v) {
 }
 
 // one thread = 4 channels of one pixel
-__global__ void split_from_f32_kernel(const float* __restrict__ x, half_t* __restrict__ y, long npix, int C) {
+__global__ void split_from_f32_kernel(const float* __restrict__ x, half_t* __restrict__ y, long npix, int C,
+                                      int* ovf) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int cv = C / 4;
   if (t >= npix * cv) return;
   const long pix = t / cv;
   const int c = (int)(t - pix * cv) * 4;
-  store_split4(y + pix * 2 * C + split_off(c), *reinterpret_cast<const float4v*>(x + pix * C + c));
+  store_split4(y + pix * 2 * C + split_off(c), *reinterpret_cast<const float4v*>(x + pix * C + c), ovf);
 }
 
 __global__ void f32_from_split_kernel(const half_t* __restrict__ x, float* __restrict__ y, long npix, int C) {
@@ -47,9 +49,10 @@ __global__ void f32_from_split_kernel(const half_t* __restrict__ x, float* __res
   *reinterpret_cast<float4v*>(y + pix * C + c) = load_split4(x + pix * 2 * C + split_off(c));
 }
 
-void split_from_f32_launch(const float* x, half_t* y, long npix, int C, hipStream_t st) {
+void split_from_f32_launch(const float* x, half_t* y, long npix, int C, int* ovf, hipStream_t st) {
   const long total = npix * (C / 4);
-  hipLaunchKernelGGL(split_from_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, y, npix, C);
+  hipLaunchKernelGGL(split_from_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, y, npix, C,
+                     ovf);
 }
 
 void f32_from_split_launch(const half_t* x, float* y, long npix, int C, hipStream_t st) {
@@ -62,7 +65,7 @@ void f32_from_split_launch(const half_t* x, float* y, long npix, int C, hipStrea
 // so a wave reads whole 256-byte (f32) pixel rows.
 template <bool IN_SPLIT>
 __global__ void maxpool_split_kernel(const void* __restrict__ xv, half_t* __restrict__ y, int B, int H, int W,
-                                     int C, int Ho, int Wo, int k, int s, int pad) {
+                                     int C, int Ho, int Wo, int k, int s, int pad, int* ovf) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int cv = C / 4;
   const long total = (long)B * Ho * Wo * cv;
@@ -94,17 +97,18 @@ __global__ void maxpool_split_kernel(const void* __restrict__ xv, half_t* __rest
       m[3] = fmaxf(m[3], v[3]);
     }
   }
-  store_split4(y + (size_t)opix * 2 * C + split_off(c), m);
+  // (a split input is already in range: only an fp32 input can leave it)
+  store_split4(y + (size_t)opix * 2 * C + split_off(c), m, IN_SPLIT ? nullptr : ovf);
 }
 
 void maxpool_split_launch(const void* x, bool in_split, half_t* y, int B, int H, int W, int C, int Ho, int Wo, int k,
-                          int s, int pad, hipStream_t st) {
+                          int s, int pad, int* ovf, hipStream_t st) {
   const long total = (long)B * Ho * Wo * (C / 4);
   const dim3 grid((unsigned)((total + 255) / 256));
   if (in_split)
-    hipLaunchKernelGGL(maxpool_split_kernel<true>, grid, dim3(256), 0, st, x, y, B, H, W, C, Ho, Wo, k, s, pad);
+    hipLaunchKernelGGL(maxpool_split_kernel<true>, grid, dim3(256), 0, st, x, y, B, H, W, C, Ho, Wo, k, s, pad, ovf);
   else
-    hipLaunchKernelGGL(maxpool_split_kernel<false>, grid, dim3(256), 0, st, x, y, B, H, W, C, Ho, Wo, k, s, pad);
+    hipLaunchKernelGGL(maxpool_split_kernel<false>, grid, dim3(256), 0, st, x, y, B, H, W, C, Ho, Wo, k, s, pad, ovf);
 }
 
 }  // namespace idunno

@@ -75,6 +75,7 @@ __device__ __forceinline__ int hp_off(int r, int px, int c) { return (r * stem::
 struct StemGeom {
   int B, H, W, Hc, Wc, Hp, Wp, tiles_x, tiles_y, ntiles;
   int ablate;   // profiling only (set_stem_ablation): skip 1 pool, 2 MFMAs, 4 patch normalise, 8 conv epilogue, 16 patch loads
+  int* ovf;     // stem_split: split range guard flag or nullptr (common.h split_guard)
 };
 
 static int g_stem_ablate = 0;
@@ -319,7 +320,7 @@ void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, h
                        const long long* start_idx, long long start_off, long long max_start, long long sub,
                        hipStream_t st) {
   using namespace stem;
-  StemGeom g;
+  StemGeom g{};
   g.B = B;
   g.H = H;
   g.W = W;
@@ -552,6 +553,8 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
             m0[e] = fmaxf(m0[e] * acc_scale + pb0[e], 0.f);
             m1[e] = fmaxf(m1[e] * acc_scale + pb1[e], 0.f);
           }
+          split_guard(g.ovf, m0);
+          split_guard(g.ovf, m1);
           half4v h0, l0, h1, l1;
           split_f16x4(m0, h0, l0);
           split_f16x4(m1, h1, l1);
@@ -569,9 +572,10 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
 
 void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
                        half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,
-                       long long max_start, long long sub, hipStream_t st) {
+                       long long max_start, long long sub, int* ovf, hipStream_t st) {
   using namespace stem;
   StemGeom g;
+  g.ovf = ovf;
   g.B = B;
   g.H = H;
   g.W = W;

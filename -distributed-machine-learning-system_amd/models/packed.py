@@ -527,21 +527,73 @@ class HipRunner:
         # None = measured default (tools/bench_split.py, profiles/r1_v8_front_split.log):
         # 2 parts for ResNet18/34 at >= 256 images (+1.3 %), else 1 (ResNet50: -0.6 %)
         self.front_split = front_split
+        # >1: the WHOLE ResNet forward on this many batch parts, each part's
+        # activations small enough to stay in the 256 MiB Infinity Cache from
+        # producer to consumer (the memory-bound ResNet50 bottlenecks read every
+        # 4x-wide tensor twice: next block's 1x1 reduce and its residual add).
+        # None = measured default (_auto_batch_parts)
+        self.batch_parts: int | None = None
         self.device = torch.device(device or "cuda")
         self.p = program.to(self.device)
         self._graphs: dict[int, tuple] = {}
+        # split range guard: the split kernels set this flag
+        # when an activation leaves fp16's range (|v| >= 65504 has no finite hi
+        # half); softmax_top1 then marks the batch (class -2) and the eager
+        # paths rerun it on the all-f32 kernels, which have fp32's range
+        self._ovf = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.overflow_fallback = True
+        self.overflow_reruns = 0
+        self._capturing = False
 
     # -- eager forward ------------------------------------------------------
+    def _guarded(self) -> bool:
+        return self.p.dtype == "fp32" and self.split and self._split_ok()
+
     def logits(self, img_u8: torch.Tensor, start: torch.Tensor | None = None, batch: int = -1,
                start_offset: int = 0) -> torch.Tensor:
         """fp32 logits.  With ``start`` (int64 GPU scalar) and ``batch``,
         ``img_u8`` is a whole HBM-resident shard and the images
-        [*start - start_offset, ... + batch) are classified (device-side window)."""
+        [*start - start_offset, ... + batch) are classified (device-side window).
+
+        On the split path the range guard is armed; outside a graph capture a
+        forward that tripped it is recomputed on the all-f32 kernels (one host
+        read of the flag per eager call)."""
+        if not self._guarded():
+            return self._logits(img_u8, start, batch, start_offset)
+        self._ovf.zero_()
+        self.ops.set_split_guard(self._ovf)
+        try:
+            out = self._logits(img_u8, start, batch, start_offset)
+        finally:
+            self.ops.set_split_guard(None)
+        if self.overflow_fallback and not self._capturing and int(self._ovf.item()):
+            out = self.logits_f32_exact(img_u8, start, batch, start_offset)
+        return out
+
+    def logits_f32_exact(self, img_u8, start=None, batch: int = -1, start_offset: int = 0):
+        """The same forward on the all-f32-MFMA kernels (fp32 range)."""
+        self.overflow_reruns += 1
+        was = self.split
+        self.split = False
+        try:
+            return self._logits(img_u8, start, batch, start_offset)
+        finally:
+            self.split = was
+
+    def _auto_batch_parts(self, nb: int) -> int:
+        return 1
+
+    def _logits(self, img_u8: torch.Tensor, start: torch.Tensor | None = None, batch: int = -1,
+                start_offset: int = 0) -> torch.Tensor:
         o = self.ops
         p = self.p
         native = tuple(img_u8.shape[1:3]) == (224, 224)
         if start is not None and not native:
             raise ValueError("device-side windows need 224x224 shards")
+        nb = batch if start is not None else img_u8.shape[0]
+        parts = self.batch_parts if self.batch_parts is not None else self._auto_batch_parts(nb)
+        if p.kind == "resnet" and native and parts > 1 and nb >= 2 * parts:
+            return self._logits_in_parts(img_u8, start, nb, start_offset, parts)
         if p.dtype == "fp32":
             return self._logits_f32(img_u8, start, batch, start_offset, native)
         s = p.stem
@@ -655,6 +707,24 @@ class HipRunner:
             x = o.linear(x, fc.w, fc.b, relu=fc.relu)
         return x
 
+    def _logits_in_parts(self, img_u8, start, nb: int, start_offset: int, parts: int):
+        """The whole forward on ``parts`` consecutive batch parts (same
+        numbers as one pass: every op is per image)."""
+        n = -(-nb // parts)
+        outs = []
+        keep = self.batch_parts
+        self.batch_parts = 1
+        try:
+            for sub in range(0, nb, n):
+                m = min(n, nb - sub)
+                if start is None:
+                    outs.append(self._logits(img_u8[sub:sub + m]))
+                else:
+                    outs.append(self._logits(img_u8, start + sub, m, start_offset))
+        finally:
+            self.batch_parts = keep
+        return torch.cat(outs, 0)
+
     def _stem_f32(self, first, img_u8, start, batch, start_offset, window: int = -1, sub: int = 0):
         """fp32 RGB stem conv (+ReLU) of a window / part of the images."""
         o = self.ops
@@ -716,8 +786,8 @@ class HipRunner:
 
     def _variant(self) -> tuple:
         """Kernel-choice switches a captured graph depends on (part of its cache key)."""
-        return (self.split, self.split_front, self.split_streams, self.winograd, self.wino_variant, self.pack3, self.pack3_f16, self.side_down,
-                self.stem_parts, self.front_split, self.fuse_stem)
+        return (self.split, self.split_front, self.split_streams, self.winograd, self.wino_variant, self.pack3,
+                self.pack3_f16, self.side_down, self.stem_parts, self.front_split, self.fuse_stem, self.batch_parts)
 
     def _split_ok(self) -> bool:
         p = self.p
@@ -853,7 +923,8 @@ class HipRunner:
                 start_offset: int = 0, packed: torch.Tensor | None = None):
         """(class int32 [B], prob fp32 [B]); with ``packed`` the fused
         softmax-top1 also writes (class, prob bits) pairs into it."""
-        return self.ops.softmax_top1(self.logits(img_u8, start, batch, start_offset), packed)
+        z = self.logits(img_u8, start, batch, start_offset)
+        return self.ops.softmax_top1(z, packed, self._ovf if self._guarded() else None)
 
     __call__ = forward
 
@@ -881,12 +952,20 @@ class HipRunner:
             st = torch.cuda.Stream(device=self.device)
             st.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(st):
-                for _ in range(2):
-                    self.forward(shard, start, batch, start_offset, packed)
+                self._capturing = True        # warm-up launches: no flag reads (a capture follows)
+                try:
+                    for _ in range(2):
+                        self.forward(shard, start, batch, start_offset, packed)
+                finally:
+                    self._capturing = False
             torch.cuda.current_stream(self.device).wait_stream(st)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                sout = self.forward(shard, start, batch, start_offset, packed)
+            self._capturing = True
+            try:
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    sout = self.forward(shard, start, batch, start_offset, packed)
+            finally:
+                self._capturing = False
         self._graphs[key] = (g, start, sout)
         return start, self._replayer(g, sout, shard, packed)
 
@@ -931,12 +1010,20 @@ class HipRunner:
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):
-                for _ in range(2):
-                    self.forward(sin, packed=packed)
+                self._capturing = True
+                try:
+                    for _ in range(2):
+                        self.forward(sin, packed=packed)
+                finally:
+                    self._capturing = False
             torch.cuda.current_stream(self.device).wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                sout = self.forward(sin, packed=packed)
+            self._capturing = True
+            try:
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    sout = self.forward(sin, packed=packed)
+            finally:
+                self._capturing = False
         self._graphs[key] = (g, sin, sout)
         return sin, self._replayer(g, sout, packed)
 

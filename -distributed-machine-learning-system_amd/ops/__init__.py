@@ -207,11 +207,21 @@ def global_avgpool(x):
     return load().global_avgpool_nhwc(x)
 
 
-def softmax_top1(logits, packed=None):
+def softmax_top1(logits, packed=None, ovf=None):
     """Returns (class int32 [B], probability fp32 [B]); with ``packed`` (int32
-    [>= B, 2]) also writes (class, prob bits) pairs into it."""
-    cls, prob = load().softmax_top1(logits, packed)
+    [>= B, 2]) also writes (class, prob bits) pairs into it.  A set split
+    range-guard flag ``ovf`` marks every row class -2 (OVERFLOW_CLASS)."""
+    cls, prob = load().softmax_top1(logits, packed, ovf)
     return cls, prob
+
+
+OVERFLOW_CLASS = -2      # softmax_top1's mark: a split activation left fp16's range
+
+
+def set_split_guard(flag=None):
+    """Split launches of this thread write their range-guard flag (int32
+    device tensor) here; None turns the guard off."""
+    load().set_split_guard(flag)
 
 
 def pick_tile(m: int, cout: int) -> int:

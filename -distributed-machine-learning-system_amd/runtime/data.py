@@ -129,6 +129,7 @@ class SdfsSource:
         self.S = int(shard_images)
         self.stager = HbmStager(self.device)
         self.cache: OrderedDict[int, torch.Tensor] = OrderedDict()
+        self.ver: dict[int, int] = {}             # SDFS version of each cached shard
         self.cache_bytes = cache_bytes
         self.lock = threading.Lock()
         self.fetches = 0
@@ -142,12 +143,16 @@ class SdfsSource:
         with self.lock:
             return all(k in self.cache for k in range(start // self.S, end // self.S + 1))
 
-    def export_shard(self, name: str, consumer_pid: int | None = None):
-        """IPC export of a cached shard (SDFS FETCH_HBM), or None."""
+    def export_shard(self, name: str, consumer_pid: int | None = None, ver: int | None = None):
+        """IPC export of a cached shard (SDFS FETCH_HBM), or None -- also when
+        the cached copy is not of the requested version ``ver``."""
         from .ipc import export_tensor
 
         with self.lock:
-            t = next((v for k, v in self.cache.items() if shard_name(k) == name), None)
+            k = next((k for k in self.cache if shard_name(k) == name), None)
+            t = self.cache.get(k) if k is not None else None
+            if t is not None and ver is not None and self.ver.get(k) != int(ver):
+                t = None
         if t is None:
             return None
         torch.cuda.current_stream(self.device).synchronize()     # staged bytes have landed
@@ -160,26 +165,30 @@ class SdfsSource:
                 self.cache.move_to_end(k)
                 return t
         name = shard_name(k)
-        t = self.sdfs.fetch_hbm(name, self.device) if self.peer_copy else None
-        if t is not None:
+        got = self.sdfs.fetch_hbm(name, self.device) if self.peer_copy else None
+        if got is not None:
+            t, ver = got
             self.peer_fetches += 1
         else:
-            data = self.sdfs.get_bytes(name)
-            if data is None:
+            got = self.sdfs.get_bytes_ver(name)
+            if got is None:
                 raise KeyError(f"missing SDFS shard {name}")
+            data, ver = got
             n = len(data) // IMG_BYTES
             t = self.stager.stage(data, (n, HW, HW, 3))
         dropped = []
         with self.lock:
             self.fetches += 1
             self.cache[k] = t
+            self.ver[k] = ver
             tot = sum(v.numel() for v in self.cache.values())
             while tot > self.cache_bytes and len(self.cache) > 1:
                 ko, old = self.cache.popitem(last=False)
+                self.ver.pop(ko, None)
                 tot -= old.numel()
                 dropped.append(ko)
         if self.device.type == "cuda":
-            self.sdfs.announce_hbm(name)
+            self.sdfs.announce_hbm(name, ver=ver)
             for ko in dropped:
                 self.sdfs.announce_hbm(shard_name(ko), held=False)
         return t

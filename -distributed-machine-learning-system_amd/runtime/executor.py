@@ -90,8 +90,9 @@ class TorchExecutor(Executor):
 
 
 class _HipPending:
-    def __init__(self, ex, slot, ev, out):
+    def __init__(self, ex, slot, ev, out, model=None, images=None):
         self.ex, self.slot, self.ev, self.out = ex, slot, ev, out
+        self.model, self.images = model, images
         self._res = None
 
     def result(self):
@@ -102,6 +103,11 @@ class _HipPending:
                 self._res = (out[:, 0].numpy().copy(), out[:, 1].contiguous().view(torch.float32).numpy().copy())
             finally:
                 self.ex._release(self.slot)
+            if self.images is not None and (self._res[0] < 0).any():
+                # the split range guard tripped (class -2): this chunk again on the
+                # all-f32 kernels, which have fp32's range
+                self._res = self.ex.rerun_exact(self.model, self.images)
+            self.images = None
         return self._res
 
 
@@ -207,7 +213,19 @@ class HipExecutor(Executor):
         except BaseException:
             self._release(slot)
             raise
-        return _HipPending(self, slot, ev, out)
+        return _HipPending(self, slot, ev, out, model, images)
+
+    def rerun_exact(self, model, images):
+        """(cls, prob) of ``images`` on the all-f32-MFMA kernels: the fallback
+        for a chunk whose split forward left fp16's range."""
+        r = self.runner(model)
+        with torch.cuda.device(self.device), self.run_lock:
+            s = self._enter(images)
+            with torch.cuda.stream(s):
+                z = r.logits_f32_exact(images.contiguous())
+                cls, prob = r.ops.softmax_top1(z)
+                res = (cls.cpu().numpy().astype(np.int32), prob.cpu().numpy().astype(np.float32))
+        return res
 
     def _release(self, slot: int) -> None:
         with self._slot_cv:

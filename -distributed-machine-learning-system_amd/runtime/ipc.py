@@ -19,6 +19,7 @@ from __future__ import annotations
 import itertools
 import os
 import threading
+import time
 
 import torch
 
@@ -27,9 +28,20 @@ _DTYPES = {"uint8": torch.uint8, "float32": torch.float32, "float16": torch.floa
 
 # same-process hand-offs (nodes of an in-process cluster share one address
 # space, and a process cannot open its own IPC handle): the tensor itself
-_LOCAL: dict[int, torch.Tensor] = {}
+_LOCAL: dict[int, tuple[float, torch.Tensor]] = {}
 _LOCAL_LOCK = threading.Lock()
 _KEYS = itertools.count(1)
+# a parked tensor whose consumer never came (lost FETCH_HBM reply, timed-out
+# request) is released after this long (it pinned tens of MB of HBM)
+LOCAL_TTL_S = 30.0
+LOCAL_MAX = 64
+
+
+def _prune_locked(now: float) -> None:
+    for k in [k for k, (t0, _) in _LOCAL.items() if now - t0 > LOCAL_TTL_S]:
+        del _LOCAL[k]
+    while len(_LOCAL) > LOCAL_MAX:
+        del _LOCAL[min(_LOCAL)]
 
 
 def export_tensor(t: torch.Tensor, consumer_pid: int | None = None) -> dict:
@@ -40,8 +52,10 @@ def export_tensor(t: torch.Tensor, consumer_pid: int | None = None) -> dict:
         raise ValueError("export_tensor takes a contiguous CUDA tensor")
     if consumer_pid is not None and consumer_pid == os.getpid():
         key = next(_KEYS)
+        now = time.monotonic()
         with _LOCAL_LOCK:
-            _LOCAL[key] = t
+            _prune_locked(now)
+            _LOCAL[key] = (now, t)
         return {"pid": os.getpid(), "local": key, "shape": list(t.shape)}
     dt = next((k for k, v in _DTYPES.items() if v == t.dtype), None)
     if dt is None:
@@ -62,7 +76,10 @@ def import_copy(meta: dict, device: torch.device | int | str, out: torch.Tensor 
         raise ValueError("import_copy needs a CUDA device")
     if "local" in meta:
         with _LOCAL_LOCK:
-            src = _LOCAL.pop(meta["local"])
+            ent = _LOCAL.pop(meta["local"], None)
+        if ent is None:
+            raise KeyError("parked tensor expired before it was fetched")
+        src = ent[1]
         dst = out if out is not None else torch.empty_like(src, device=dev)
         dst.copy_(src, non_blocking=True)
         torch.cuda.current_stream(dev).synchronize()

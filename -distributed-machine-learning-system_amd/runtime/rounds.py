@@ -510,6 +510,14 @@ class RoundPlane:
                 continue
             mid, qnum, s, e = row
             cls, prob = unpack_row(arr[i], e - s + 1)
+            if (cls < 0).any():
+                # the member's split forward left fp16's range (class -2): the chunk
+                # goes to it again as a TCP JOB, whose executor path reruns it on
+                # the all-f32 kernels
+                log.warning("%s: chunk %s %s [%d,%d] on %s exceeded the split range; rerun in fp32",
+                            n.name, MODEL_NAMES[mid], qnum, s, e, members[i])
+                n._send_job(members[i], MODEL_NAMES[mid], qnum, s, e)
+                continue
             res = {"t": Type.RESULT, "model": MODEL_NAMES[mid], "qnum": qnum, "start": s, "end": e,
                    "worker": members[i], "cls": cls.tobytes(), "prob": prob.tobytes(),
                    "epoch": n.membership.epoch, "t_done": now}

@@ -137,7 +137,7 @@ class Sdfs:
         # master metadata (reference sdfs_file_version / sdfs_file_process / sdfs_store_dict)
         self.file_version: dict[str, int] = {}
         self.file_replicas: dict[str, list[str]] = {}
-        self.hbm_holders: dict[str, list[str]] = {}   # master: nodes holding a file in HBM
+        self.hbm_holders: dict[str, dict[str, int]] = {}   # master: file -> {node: version it holds in HBM}
         self.hbm_provider = None                      # this node: name -> IPC export dict or None
         self.peer_copies = 0
         racecheck.instrument(self, ("file_version", "file_replicas", "hbm_holders"), f"Sdfs[{node.name}]")
@@ -197,7 +197,10 @@ class Sdfs:
                 return {"ok": False, "exists": False}
             alive = set(self._ring())
             reps = [r for r in self.file_replicas.get(name, []) if r in alive]
-            hbm = [h for h in self.hbm_holders.get(name, []) if h in alive]
+            ver = self.file_version[name]
+            # only holders of the CURRENT version (a late HBM_HAS of an
+            # older version must not re-publish a stale copy to peers)
+            hbm = [h for h, v in self.hbm_holders.get(name, {}).items() if h in alive and v == ver]
             return {"ok": True, "exists": True, "ver": self.file_version[name], "replicas": reps, "hbm": hbm}
 
     def _master_delete(self, name: str) -> dict:
@@ -272,12 +275,16 @@ class Sdfs:
             return self._master_delete(msg["name"])
         if t == Type.HBM_HAS:
             with self.lock:
-                if msg["name"] in self.file_version:
-                    hs = [h for h in self.hbm_holders.get(msg["name"], []) if h != msg["node"]]
-                    self.hbm_holders[msg["name"]] = hs + [msg["node"]] if msg.get("held", True) else hs
+                name = msg["name"]
+                if name in self.file_version:
+                    hs = self.hbm_holders.setdefault(name, {})
+                    hs.pop(msg["node"], None)
+                    if msg.get("held", True):
+                        hs[msg["node"]] = int(msg.get("ver", self.file_version[name]))
             return {"ok": True}
         if t == Type.FETCH_HBM:
-            meta = self.hbm_provider(msg["name"], msg.get("pid")) if self.hbm_provider is not None else None
+            meta = self.hbm_provider(msg["name"], msg.get("pid"), msg.get("ver")) \
+                if self.hbm_provider is not None else None
             return {"ok": meta is not None, "meta": meta}
         return None
 
@@ -294,17 +301,22 @@ class Sdfs:
         return self._req(self._master(), {"t": Type.PUT, "name": name, "data": data}, 60.0)
 
     def _fetch(self, name: str, ver: int | None) -> bytes | None:
+        got = self._fetch_ver(name, ver)
+        return None if got is None else got[0]
+
+    def _fetch_ver(self, name: str, ver: int | None):
         loc = self._req(self._master(), {"t": Type.GET, "name": name})
         if not loc.get("exists"):
             return None
+        want = ver if ver is not None else loc["ver"]
         reps = loc["replicas"]
         if self.node.name in reps:          # local replica: no transfer
             reps = [self.node.name] + [r for r in reps if r != self.node.name]
         for r in reps:
             try:
-                rep = self._req(r, {"t": Type.FETCH, "name": name, "ver": ver if ver is not None else loc["ver"]}, 60.0)
+                rep = self._req(r, {"t": Type.FETCH, "name": name, "ver": want}, 60.0)
                 if rep.get("ok"):
-                    return rep["data"]
+                    return rep["data"], int(want)
             except Exception:  # noqa: BLE001
                 continue
         return None
@@ -312,9 +324,16 @@ class Sdfs:
     def get_bytes(self, name: str, ver: int | None = None) -> bytes | None:
         return self._fetch(name, ver)
 
-    def announce_hbm(self, name: str, held: bool = True) -> None:
-        """Tell the master this node holds (or dropped) ``name`` in HBM."""
+    def get_bytes_ver(self, name: str) -> tuple[bytes, int] | None:
+        """(bytes, version) of the current version of ``name``."""
+        return self._fetch_ver(name, None)
+
+    def announce_hbm(self, name: str, held: bool = True, ver: int | None = None) -> None:
+        """Tell the master this node holds (or dropped) version ``ver`` of
+        ``name`` in HBM."""
         msg = {"t": Type.HBM_HAS, "name": name, "node": self.node.name, "held": held}
+        if ver is not None:
+            msg["ver"] = int(ver)
         master = self._master()
         try:
             if master == self.node.name:
@@ -325,22 +344,27 @@ class Sdfs:
             pass
 
     def fetch_hbm(self, name: str, device):
-        """GPU-to-GPU copy of ``name`` from a node holding it in HBM, or None."""
+        """(tensor, version): GPU-to-GPU copy of the current version of
+        ``name`` from a node holding it in HBM, or None.  The holder exports
+        its copy only if it is of the version the master just located."""
         from .ipc import import_copy
 
         try:
             loc = self._req(self._master(), {"t": Type.GET, "name": name})
         except Exception:  # noqa: BLE001
             return None
+        if not loc.get("exists"):
+            return None
+        ver = int(loc["ver"])
         for h in loc.get("hbm", []):
             if h == self.node.name:
                 continue
             try:
-                rep = self._req(h, {"t": Type.FETCH_HBM, "name": name, "pid": os.getpid()})
+                rep = self._req(h, {"t": Type.FETCH_HBM, "name": name, "pid": os.getpid(), "ver": ver})
                 if rep.get("ok") and rep.get("meta"):
                     t = import_copy(rep["meta"], device)
                     self.peer_copies += 1
-                    return t
+                    return t, ver
             except Exception as e:  # noqa: BLE001
                 log.warning("hbm copy of %s from %s failed: %s", name, h, e)
         return None

@@ -234,3 +234,53 @@ def test_standby_mirrors_by_deltas(cluster):
     assert coord.meta_bytes < 8000, coord.meta_bytes
     assert sorted(q for q in sb.state.worker_set) == sorted(q for q in coord.state.worker_set)
     assert big >= 0
+
+
+def test_sdfs_hbm_holders_are_version_checked(cluster):
+    """a late HBM_HAS for an older version must not re-publish a
+    stale HBM copy; peers are offered only holders of the current version."""
+    from idunno.runtime.messages import Type
+
+    n = cluster.nodes["node02"]
+    master = cluster.coordinator()
+    assert n.sdfs.put_bytes(b"x" * 64, "images/shard_0")["ver"] == 1
+    n.sdfs.announce_hbm("images/shard_0", ver=1)
+    assert wait_for(lambda: master.sdfs._master_locate("images/shard_0")["hbm"] == ["node02"], 2)
+    assert n.sdfs.put_bytes(b"y" * 64, "images/shard_0")["ver"] == 2      # re-put clears holders
+    assert master.sdfs._master_locate("images/shard_0")["hbm"] == []
+    # the old announcement arrives late: recorded as version 1, never offered
+    master.sdfs.handle({"t": Type.HBM_HAS, "name": "images/shard_0", "node": "node03", "held": True, "ver": 1,
+                        "src": "node03"})
+    assert master.sdfs._master_locate("images/shard_0")["hbm"] == []
+    master.sdfs.handle({"t": Type.HBM_HAS, "name": "images/shard_0", "node": "node04", "held": True, "ver": 2,
+                        "src": "node04"})
+    assert master.sdfs._master_locate("images/shard_0")["hbm"] == ["node04"]
+    # a holder asked for another version than it caches exports nothing
+    calls = []
+    n.sdfs.hbm_provider = lambda name, pid, ver: calls.append(ver)
+    n.sdfs.handle({"t": Type.FETCH_HBM, "name": "images/shard_0", "pid": 1, "ver": 2, "src": "node05"})
+    assert calls == [2]
+
+
+def test_ipc_local_parking_expires(monkeypatch):
+    """a same-process hand-off whose consumer never came is dropped
+    after LOCAL_TTL_S instead of pinning the tensor forever."""
+    from idunno.runtime import ipc
+
+    class T:
+        is_cuda = True
+        shape = (2, 3)
+
+        def is_contiguous(self):
+            return True
+
+    monkeypatch.setattr(ipc, "LOCAL_TTL_S", 0.05)
+    import os
+
+    meta = ipc.export_tensor(T(), consumer_pid=os.getpid())
+    assert meta["local"] in ipc._LOCAL
+    time.sleep(0.1)
+    ipc.export_tensor(T(), consumer_pid=os.getpid())     # any export prunes expired entries
+    assert meta["local"] not in ipc._LOCAL
+    with pytest.raises(KeyError):
+        ipc.import_copy(meta, "cuda:0")

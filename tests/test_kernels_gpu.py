@@ -97,6 +97,7 @@ def _need_experimental(ops):
         pytest.skip("experimental conv loops not built (IDUNNO_EXPERIMENTAL=1)")
 
 
+@pytest.mark.experimental
 @pytest.mark.parametrize("tile", BIG_TILES)
 @pytest.mark.parametrize("B,H,Cin,Cout,k,s,res", [
     (3, 28, 128, 128, 3, 1, True),    # layer2 3x3 + residual, M = 2352 (not a tile multiple)
@@ -124,6 +125,7 @@ def test_conv_big_tiles(ops, tile, B, H, Cin, Cout, k, s, res):
     _check(y, ref)
 
 
+@pytest.mark.experimental
 @pytest.mark.parametrize("tile", [70, 71, 72, 73])
 @pytest.mark.parametrize("res", [False, True])
 def test_conv_persistent_many_tiles_per_workgroup(ops, tile, res):

@@ -224,6 +224,7 @@ def test_conv_split_c64_rows(ops, B, H, W, res):
 
 
 @pytest.mark.gpu
+@pytest.mark.experimental
 @pytest.mark.parametrize("B,H,C,Cout", [(3, 28, 128, 128), (2, 14, 256, 256), (3, 7, 512, 512), (2, 13, 96, 128),
                                         (1, 9, 128, 256)])
 @pytest.mark.parametrize("res,out_f32", [(False, False), (True, False), (True, True)])
@@ -382,3 +383,74 @@ def test_model_split_vs_fp64_oracle(ops, name, B):
     err = (got[:n] - want).abs().max().item() / scale
     assert err <= 1e-5, f"{name}: rel logit err {err:.2e}"
     assert torch.equal(got[:n].argmax(1), want.argmax(1))
+
+
+# ---------------------------------------------------------------------------
+# fp32 range on the split path: a value past 65504 has no
+# finite fp16 hi half.  The split kernels flag it, softmax_top1 marks the batch
+# class -2 and the runner / executor rerun it on the all-f32 kernels.
+# ---------------------------------------------------------------------------
+
+@pytest.mark.gpu
+def test_split_guard_flags_residual_sum_past_fp16_range(ops):
+    torch.manual_seed(5)
+    x = P.to_split(torch.rand(2, 7, 7, 128, device=DEV) * 0.1)
+    sw, scale = P.pack_split_weight(torch.randn(128, 128, 3, 3) * 0.01)
+    sw = sw.to(DEV)
+    flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+
+    def run(bias, res):
+        flag.zero_()
+        ops.set_split_guard(flag)
+        try:
+            y = ops.conv2d_split(x, sw, torch.full((128,), bias, device=DEV), scale, 3, 3, 1, 1, False,
+                                 residual=P.to_split(torch.full((2, 7, 7, 128), res, device=DEV)))
+        finally:
+            ops.set_split_guard(None)
+        torch.cuda.synchronize()
+        return int(flag.item()), y
+
+    f, y = run(20000.0, 40000.0)               # every part and the sum < 65504
+    assert f == 0 and bool(torch.isfinite(P.from_split(y)).all())
+    f, _ = run(10000.0, 60000.0)               # each part fits, the sum does not
+    assert f == 1
+    f, _ = run(10000.0, 40000.0)               # the flag was reset: clean again
+    assert f == 0
+
+
+@pytest.mark.gpu
+def test_split_activations_past_fp16_range_match_fp64(ops):
+    """Stem weights x 1e5: activations ~1e5-1e6 and residual sums far past
+    65504.  The split forward trips the guard and is recomputed on the f32
+    kernels: logits match the fp64 oracle at the fp32 tolerance."""
+    from idunno.models import reference as ref
+    from idunno.runtime.executor import HipExecutor
+
+    m = ref.build("resnet18", seed=3)
+    with torch.no_grad():
+        m.conv1.weight *= 1e5
+    prog = P.compile_model(m, "resnet18", "fp32")
+    r = P.HipRunner(prog)
+    assert r.split and r._split_ok()
+    img = ops.synth_images(4, 0, 4, DEV)
+    with torch.no_grad():
+        want = m.double()(ref.preprocess_u8(img.cpu()).double())
+        act = torch.relu(m.bn1(m.conv1(ref.preprocess_u8(img.cpu()).double())))
+    assert act.abs().max().item() > 1e5                               # the regime under test
+    got = r.logits(img).double().cpu()
+    assert r.overflow_reruns == 1
+    scale = want.abs().max().item()
+    err = (got - want).abs().max().item() / scale
+    assert err <= 2e-5, f"rel logit err {err:.2e}"
+    assert torch.equal(got.argmax(1), want.argmax(1))
+    # a captured graph marks the batch instead (no host read inside the graph) ...
+    sin, replay = r.capture(4)
+    sin.copy_(img)
+    cls, _ = replay()
+    assert bool((cls == ops.OVERFLOW_CLASS).all())
+    # ... and the executor reruns such a chunk on the f32 kernels
+    ex = HipExecutor(DEV, seed=3)
+    ex.runners["resnet18"] = r
+    c2, p2 = ex.run("resnet18", img, 0, 3)
+    assert (c2 == want.argmax(1).numpy()).all()
+    assert abs(float(p2[0]) - torch.softmax(want, 1).max(1).values[0].item()) < 1e-4
