@@ -324,13 +324,27 @@ static int split_norder(int tiles_n, long kpad) {
 //   x   : [B, H, W, 2C] half, split layout ([hi x32][lo x32] per 32 channels), C % 32 == 0
 //   w   : [Cout, KH*KW*2C] half, same layout per tap, pre-scaled by 1/acc_scale
 //   res : optional [B, Ho, Wo, 2Cout] half (split);  y: split half, or fp32 [B, Ho, Wo, Cout]
-torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias, c10::optional<torch::Tensor> res,
-                           int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool relu, double acc_scale,
-                           bool out_f32, int64_t tile, c10::optional<torch::Tensor> out) {
+// Pixel stride (halfs) of an NHWC view whose channels are contiguous and whose
+// pixels are equally spaced: a channel slice of a wider tensor (the two halves
+// of a dual conv's output) is read in place.
+static int64_t nhwc_pixel_stride(const torch::Tensor& t, const char* what) {
+  TORCH_CHECK(t.dim() == 4, what, " must be 4-D NHWC");
+  const int64_t P = t.stride(2);
+  TORCH_CHECK(t.stride(3) == 1 && P >= t.size(3) && t.stride(1) == t.size(2) * P && t.stride(0) == t.size(1) * t.stride(1),
+              what, " must be NHWC with contiguous channels and equally strided pixels");
+  TORCH_CHECK(P % 8 == 0 && t.storage_offset() % 8 == 0, what, " pixel stride / offset must be 16-byte aligned");
+  return P;
+}
+
+static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
+                                       c10::optional<torch::Tensor> res, int64_t KH, int64_t KW, int64_t stride,
+                                       int64_t pad, bool relu, double acc_scale, bool out_f32, int64_t tile,
+                                       c10::optional<torch::Tensor> out, int64_t nsplit, bool center_only,
+                                       double acc_scale2) {
   CHECK_DEV(x);
   CHECK_DEV(w);
   CHECK_DEV(bias);
-  CHECK_CONTIG(x);
+  const int64_t xP = nhwc_pixel_stride(x, "x");
   CHECK_CONTIG(w);
   CHECK_CONTIG(bias);
   CHECK_DT(x, torch::kHalf);
@@ -348,7 +362,7 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   TORCH_CHECK(Ho > 0 && Wo > 0, "empty output");
   const long M = (long)B * Ho * Wo;
-  TORCH_CHECK(M < (1L << 31) && (long)B * H * W * C2 < (1L << 31) && M * 2 * Cout < (1L << 31),
+  TORCH_CHECK(M < (1L << 31) && (long)B * H * W * xP < (1L << 31) && M * 2 * Cout < (1L << 31),
               "tensor too large for int32 indexing");
   const int64_t ych = out_f32 ? Cout : 2 * Cout;
   torch::Tensor y;
@@ -364,10 +378,11 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     y = torch::empty({B, Ho, Wo, ych}, x.options().dtype(out_f32 ? torch::kFloat : torch::kHalf));
   }
   const half_t* rp = nullptr;
+  int64_t rP = 2 * Cout;
   if (res.has_value() && res->defined()) {
     auto& r = *res;
     CHECK_DEV(r);
-    CHECK_CONTIG(r);
+    rP = nhwc_pixel_stride(r, "residual");
     CHECK_DT(r, torch::kHalf);
     TORCH_CHECK(r.device() == x.device(), "residual on a different device");
     TORCH_CHECK(r.dim() == 4 && r.size(0) == B && r.size(1) == Ho && r.size(2) == Wo && r.size(3) == 2 * Cout,
@@ -389,9 +404,19 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   a.acc_scale = (float)acc_scale;
   a.ablate = g_conv_ablate;
   a.ovf = out_f32 ? nullptr : split_guard_for(x.device());
+  // strided views (a dual conv's halves): conv_glds reads them in place
+  const bool strided = xP != C2 || rP != 2 * Cout;
+  a.ldx = xP != C2 ? (int)xP : 0;
+  a.ldr = rP != 2 * Cout ? (int)rP : 0;
+  TORCH_CHECK(nsplit >= 0 && nsplit < Cout && nsplit % 32 == 0, "dual conv split must be a multiple of 32 below Cout");
+  a.nsplit_n = (int)nsplit;
+  a.center_only = center_only ? 1 : 0;
+  a.acc_scale2 = (float)acc_scale2;
+  TORCH_CHECK(!center_only || (nsplit > 0 && KH % 2 == 1 && KW % 2 == 1 && pad == KH / 2 && pad == KW / 2),
+              "centre-only dual conv needs an odd, 'same'-padded kernel");
   if (M == 0) return y;
   a.zero = zero_buffer(x.device()).data_ptr();
-  const bool c64_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 &&
+  const bool c64_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 && !strided && nsplit == 0 &&
                       conv3x3_split_c64_supported(H, W, C2 / 2, Cout);
   if (tile == 50 || (tile < 0 && c64_ok && g_split_c64_default)) {
     TORCH_CHECK(c64_ok, "tile 50 (row-streaming split 3x3 64->64 conv) does not support this shape");
@@ -401,8 +426,8 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     return y;
   }
 #ifdef IDUNNO_EXPERIMENTAL
-  const bool patch_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && Cout % 128 == 0 &&
-                        conv3x3_patch_split_supported(B, H, W, C2 / 2, Cout);
+  const bool patch_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && Cout % 128 == 0 && !strided &&
+                        nsplit == 0 && conv3x3_patch_split_supported(B, H, W, C2 / 2, Cout);
   if ((tile >= 60 && tile <= 62) || (tile < 0 && patch_ok && g_split_patch_default)) {
     TORCH_CHECK(patch_ok, "tiles 60-62 (split 3x3 patch conv) do not support this shape");
     conv3x3_patch_split_launch(a.x, a.w, a.bias, a.res, a.y, out_f32, a.zero, B, H, W, C2 / 2, Cout, a.relu,
@@ -416,6 +441,27 @@ torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   TORCH_CHECK(conv_glds_split_launch(a, out_f32, t, cur_stream()), "unknown split conv tile id ", t);
   check_launch("conv_glds_split");
   return y;
+}
+
+torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias, c10::optional<torch::Tensor> res,
+                           int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool relu, double acc_scale,
+                           bool out_f32, int64_t tile, c10::optional<torch::Tensor> out) {
+  return conv2d_split_impl(x, w, bias, res, KH, KW, stride, pad, relu, acc_scale, out_f32, tile, out, 0, false, 1.0);
+}
+
+// Two split convs of one input in ONE launch (the ResNet stride-2
+// block's 1x1/2 downsample is the centre tap of its 3x3/2 conv): w / bias are
+// [Cout1 + Cout2, ...] with the second conv's weights in the centre-tap K block
+// (zeros elsewhere, never read); output channels [0, nsplit) = conv 1 (ReLU if
+// relu, scale acc_scale), [nsplit, Cout) = conv 2 (no ReLU, scale acc_scale2,
+// K loop over the centre tap only when center_only).  y = [B, Ho, Wo, 2*Cout]
+// split; its channel halves are read in place by the next convs (pixel stride).
+torch::Tensor conv2d_split_dual(torch::Tensor x, torch::Tensor w, torch::Tensor bias, int64_t KH, int64_t KW,
+                                int64_t stride, int64_t pad, bool relu, double acc_scale, double acc_scale2,
+                                int64_t nsplit, bool center_only, int64_t tile) {
+  TORCH_CHECK(nsplit > 0, "dual conv needs nsplit > 0");
+  return conv2d_split_impl(x, w, bias, c10::nullopt, KH, KW, stride, pad, relu, acc_scale, false, tile,
+                           c10::nullopt, nsplit, center_only, acc_scale2);
 }
 
 // fp32-accurate FC on split fp16: y = act(acc_scale * x @ w.T + bias)
@@ -1180,6 +1226,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("acc_scale"), py::arg("out_f32") = false, py::arg("tile") = -1,
         py::arg("out") = py::none());
+  m.def("conv2d_split_dual", &conv2d_split_dual,
+        "two split convs of one input in one launch (downsample as the centre tap of the 3x3/s conv)",
+        py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
+        py::arg("relu"), py::arg("acc_scale"), py::arg("acc_scale2"), py::arg("nsplit"), py::arg("center_only"),
+        py::arg("tile") = -1);
   m.def("conv2d_pack3_split", &conv2d_pack3_split, "split-fp16 RGB stem conv on packed rows, fp32 out",
         py::arg("x3"), py::arg("w"), py::arg("bias"), py::arg("W"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("acc_scale"), py::arg("tile") = -1);

@@ -92,7 +92,14 @@ __device__ __forceinline__ void c64s_load_row(const C64sArgs& a, char* ring, int
   }
 }
 
-template <bool HAS_RES>
+// D groups of B reads in the register ring: D - 1 groups in flight behind the
+// group whose MFMAs issue
+template <int N>
+__device__ __forceinline__ void c64s_wait_groups() {
+  lds_waitcnt<2 * N>();
+}
+
+template <bool HAS_RES, int D>
 __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArgs a) {
   using namespace c64s;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -160,9 +167,9 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
 #pragma unroll
       for (int f = 0; f < NF; ++f) acc[f] = float4v{0.f, 0.f, 0.f, 0.f};
       // 72 groups g = (tap t, block cb, pixel fragment F): 2 B reads (hi, lo),
-      // 3 MFMAs; a 3-deep register ring keeps the reads of groups g+1, g+2 in
-      // flight behind group g's MFMAs (counted lgkmcnt)
-      half8v bf[3][2];
+      // 3 MFMAs; a D-deep register ring keeps the reads of groups g+1 .. g+D-1
+      // in flight behind group g's MFMAs (counted lgkmcnt)
+      half8v bf[D][2];
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) asm volatile("" : "+v"(loff[kw]));
       uint32_t rowb[3];
@@ -175,18 +182,22 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
         for (int p = 0; p < 2; ++p)
           bf[buf][p] = lds_read_frag(rowb[kh] + (loff[kw] ^ (uint32_t)((2 * cb + p) << 6)), F);
       };
-      issue(0, 0);
-      issue(1, 1);
+#pragma unroll
+      for (int p = 0; p < D - 1; ++p) issue(p, p);
 #pragma unroll
       for (int g = 0; g < 72; ++g) {
-        const int buf = g % 3;
-        if (g + 2 < 72) {
-          issue(g + 2, (g + 2) % 3);
-          lds_waitcnt<4>();
-        } else if (g + 1 < 72) {
-          lds_waitcnt<2>();
+        const int buf = g % D;
+        if (g + D - 1 < 72) {
+          issue(g + D - 1, (g + D - 1) % D);
+          c64s_wait_groups<D - 1>();
+        } else if (g == 72 - 4) {
+          c64s_wait_groups<3>();
+        } else if (g == 72 - 3) {
+          c64s_wait_groups<2>();
+        } else if (g == 72 - 2) {
+          c64s_wait_groups<1>();
         } else {
-          lds_waitcnt<0>();
+          c64s_wait_groups<0>();
         }
         lds_tie(bf[buf][0]);
         lds_tie(bf[buf][1]);
@@ -232,6 +243,18 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
 
 // W in [49, 62]: every one of the 4 pixel fragments has a valid column, so
 // each wave issues exactly NST epilogue stores per row (counted vmcnt above)
+template <int D>
+static void c64s_launch(const C64sArgs& a, bool res, int grid, hipStream_t st) {
+  using namespace c64s;
+  if (res) {
+    ensure_lds_attr(reinterpret_cast<const void*>(conv3x3_split_c64_kernel<true, D>), LDS);
+    hipLaunchKernelGGL((conv3x3_split_c64_kernel<true, D>), dim3(grid), dim3(256), LDS, st, a);
+  } else {
+    ensure_lds_attr(reinterpret_cast<const void*>(conv3x3_split_c64_kernel<false, D>), LDS);
+    hipLaunchKernelGGL((conv3x3_split_c64_kernel<false, D>), dim3(grid), dim3(256), LDS, st, a);
+  }
+}
+
 bool conv3x3_split_c64_supported(int H, int W, int C, int Cout) {
   return C == 64 && Cout == 64 && W >= 49 && W <= 62 && H >= 1;
 }
@@ -262,13 +285,10 @@ void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bia
   a.nbands = (H + band - 1) / band;
   a.ntasks = B * a.nbands;
   const int grid = a.ntasks < per ? a.ntasks : per;
-  if (res) {
-    ensure_lds_attr(reinterpret_cast<const void*>(conv3x3_split_c64_kernel<true>), LDS);
-    hipLaunchKernelGGL(conv3x3_split_c64_kernel<true>, dim3(grid), dim3(256), LDS, st, a);
-  } else {
-    ensure_lds_attr(reinterpret_cast<const void*>(conv3x3_split_c64_kernel<false>), LDS);
-    hipLaunchKernelGGL(conv3x3_split_c64_kernel<false>, dim3(grid), dim3(256), LDS, st, a);
-  }
+  // depth 4 only without the residual: with it the kernel spills (256 VGPRs at depth 3 already)
+  // ring depth 3: a 4th group of reads spills the residual variant (256 VGPRs at
+  // depth 3), and without a residual it measured +0.09 % (profiles/r3_ab_c64_depth.log)
+  c64s_launch<3>(a, res != nullptr, grid, st);
 }
 
 }  // namespace idunno

@@ -56,7 +56,7 @@ def run_node(a) -> int:
         # one node per process and per GPU: queries run as RCCL rounds by default
         # (RCCL needs a distinct GPU per rank; nodes sharing a GPU use the TCP path)
         cfg.collective_rounds = dev.type == "cuda" and a.executor in ("auto", "hip") and \
-            torch.cuda.device_count() >= cfg.num_nodes
+            torch.cuda.device_count() >= cfg.num_nodes      # (a single node: one-member rounds)
     tr = TcpTransport(name, cfg.address, cfg.address(name))
     node = Node(cfg, name, tr, ex)
     node.source = (SdfsSource(node.sdfs, dev, peer_copy=cfg.sdfs_peer_copy) if a.source == "sdfs"

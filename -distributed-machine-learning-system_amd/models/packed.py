@@ -533,6 +533,12 @@ class HipRunner:
         # 4x-wide tensor twice: next block's 1x1 reduce and its residual add).
         # None = measured default (_auto_batch_parts)
         self.batch_parts: int | None = None
+        # split path: a stride-2 block's 1x1/2 downsample in the same launch as
+        # its 3x3/2 conv (the downsample is that conv's centre tap; one input
+        # read, one launch).  Measured slower (-2.1 / -3.1 % whole forward,
+        # profiles/r3_dual_downsample.md), so off by default
+        self.fuse_down = False
+        self._dual: dict = {}
         self.device = torch.device(device or "cuda")
         self.p = program.to(self.device)
         self._graphs: dict[int, tuple] = {}
@@ -787,7 +793,8 @@ class HipRunner:
     def _variant(self) -> tuple:
         """Kernel-choice switches a captured graph depends on (part of its cache key)."""
         return (self.split, self.split_front, self.split_streams, self.winograd, self.wino_variant, self.pack3,
-                self.pack3_f16, self.side_down, self.stem_parts, self.front_split, self.fuse_stem, self.batch_parts)
+                self.pack3_f16, self.side_down, self.stem_parts, self.front_split, self.fuse_stem, self.batch_parts,
+                self.fuse_down)
 
     def _split_ok(self) -> bool:
         p = self.p
@@ -812,9 +819,36 @@ class HipRunner:
         return self.ops.conv2d_split(x, c.sw, c.b, c.s_scale, c.kh, c.kw, c.stride, c.pad, c.relu, residual,
                                      out_f32, out=out)
 
+    def _dual_ok(self, blk) -> bool:
+        d, c0 = blk.down, blk.convs[0] if blk.convs else None
+        return (self.fuse_down and d is not None and len(blk.convs) == 2 and c0.kh == 3 and c0.kw == 3
+                and c0.pad == 1 and d.kh == 1 and d.kw == 1 and d.pad == 0 and d.stride == c0.stride
+                and d.cin == c0.cin and d.cout == c0.cout and c0.relu and not d.relu
+                and c0.sw is not None and d.sw is not None and c0.cout % 32 == 0)
+
+    def _dual_weights(self, blk):
+        """[2 Cout, 9*2C] split weights: the 3x3 conv's rows, then the 1x1
+        downsample's rows in the centre-tap K block (zeros elsewhere)."""
+        key = id(blk)
+        got = self._dual.get(key)
+        if got is None:
+            c0, d = blk.convs[0], blk.down
+            c2 = c0.sw.shape[1] // 9
+            w = torch.zeros((2 * c0.cout, c0.sw.shape[1]), dtype=c0.sw.dtype, device=c0.sw.device)
+            w[:c0.cout] = c0.sw
+            w[c0.cout:, 4 * c2:5 * c2] = d.sw
+            got = self._dual[key] = (w, torch.cat([c0.b, d.b]).contiguous())
+        return got
+
     def _block_split(self, blk, x, last: bool = False, out=None):
         """Residual block on split-fp16 activations; with ``last`` the block's
         output is fp32 (for the avgpool / FC head); into ``out`` when given."""
+        if self._dual_ok(blk):
+            c0, d = blk.convs[0], blk.down
+            w, b = self._dual_weights(blk)
+            both = self.ops.conv2d_split_dual(x, w, b, c0.s_scale, d.s_scale, c0.cout, 3, 3, c0.stride, 1, True)
+            y, idt = both[..., :2 * c0.cout], both[..., 2 * c0.cout:]
+            return self._conv_split(blk.convs[1], y, residual=idt, out_f32=last, out=out)
         idt = x if blk.down is None else self._conv_split(blk.down, x)
         y = x
         for c in blk.convs[:-1]:

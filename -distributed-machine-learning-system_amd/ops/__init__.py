@@ -26,6 +26,19 @@ def conv2d_split(x, w, bias, acc_scale: float, kh: int, kw: int, stride: int, pa
     return load().conv2d_split(x, w, bias, residual, kh, kw, stride, pad, relu, acc_scale, out_f32, tile, out)
 
 
+def conv2d_split_dual(x, w, bias, acc_scale: float, acc_scale2: float, nsplit: int, kh: int, kw: int,
+                      stride: int, pad: int, relu: bool, center_only: bool = True, tile: int = -1):
+    """Two split convs of one input in one launch: output channels [0, nsplit)
+    are conv 1 (``relu``, ``acc_scale``), the rest conv 2 (no ReLU,
+    ``acc_scale2``; K over the centre tap only with ``center_only`` -- a 1x1
+    stride-s conv is the centre tap of the 3x3 stride-s pad-1 conv).  Returns
+    the [B, Ho, Wo, 2*Cout] split tensor; ``y[..., :2*nsplit]`` and
+    ``y[..., 2*nsplit:]`` are the two convs' outputs (strided views that the
+    split convs read in place)."""
+    return load().conv2d_split_dual(x, w, bias, kh, kw, stride, pad, relu, acc_scale, acc_scale2, nsplit,
+                                    center_only, tile)
+
+
 def preprocess_pack3_split(img_u8, kw: int, stride: int, pad: int, start=None, batch: int = -1,
                            start_offset: int = 0, window: int = -1, sub: int = 0):
     """uint8 [B,H,W,3] -> split-fp16 packed-row stem input [B, H, 2*nc, wp]."""

@@ -60,6 +60,33 @@ class RoundAbandoned(RuntimeError):
     """A round's liveness check failed (dead rank, newer epoch, shutdown)."""
 
 
+class _Solo:
+    """The backend of a one-member group: nothing to talk to.  A single-GPU
+    node still runs its queries as pipelined rounds (device-resident results,
+    one device->host copy per round, two rounds in flight), just without a
+    collective."""
+
+    def abort(self):
+        pass
+
+    def shutdown(self):
+        pass
+
+
+class _EventWork:
+    """Work-like handle of a solo round: complete once the round's kernels
+    (recorded event) have finished; nothing to wait for on the CPU."""
+
+    def __init__(self, ev=None):
+        self.ev = ev
+
+    def is_completed(self) -> bool:
+        return self.ev is None or self.ev.query()
+
+    def wait(self):
+        return True
+
+
 def _shutdown_backend(pg, abort: bool) -> None:
     """End a backend object: ``abort()`` when collectives may still be
     pending on a dead peer (RCCL: ncclCommAbort, pending kernels return),
@@ -157,6 +184,11 @@ class ElasticGroup:
                 return False
             rank = members.index(me)
             world = len(members)
+            if world == 1:
+                self.pg = _Solo()
+                self.epoch, self.members, self.rank = epoch, list(members), 0
+                self._alloc(1)
+                return True
             try:
                 store = dist.TCPStore(host, port, world_size=world, is_master=(rank == 0),
                                       timeout=timedelta(seconds=self.timeout_s), wait_for_workers=False,
@@ -186,8 +218,11 @@ class ElasticGroup:
     def _alloc(self, world: int) -> None:
         dev, rows, D = self.device, self.max_chunk + HDR_ROWS, self.depth
         self._send = [torch.zeros(rows, 2, dtype=torch.int32, device=dev) for _ in range(D)]
-        if self.rank == 0:
+        if self.rank == 0 and world == 1:
+            self._gathered = [s.unsqueeze(0) for s in self._send]       # the send buffer IS the round
+        elif self.rank == 0:
             self._gathered = [torch.zeros(world, rows, 2, dtype=torch.int32, device=dev) for _ in range(D)]
+        if self.rank == 0:
             gpu = dev.type == "cuda"
             self._host = [torch.zeros(world, rows, 2, dtype=torch.int32, pin_memory=gpu) for _ in range(D)]
             if gpu and self._d2h is None:
@@ -207,6 +242,12 @@ class ElasticGroup:
         pg = self.pg
         if pg is None:
             raise RoundAbandoned("group not formed")
+        if isinstance(pg, _Solo):
+            ev = None
+            if self.device.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.device))
+            return _EventWork(ev)
         opts = dist.GatherOptions()
         opts.rootRank = 0
         slot = seq % self.depth

@@ -135,6 +135,9 @@ class Node:
             self._threads.append(th)
         if join:
             self.join_with_retry()
+        if self.rounds is not None and self.is_coordinator:
+            # the first epoch (joins re-form it; a lone node forms a one-member group)
+            self.rounds.schedule_reform("start", delay=0.3)
         if self.cfg.resume and self.is_coordinator:
             def resume():   # let the workers join first
                 time.sleep(self.cfg.failure_timeout_s)

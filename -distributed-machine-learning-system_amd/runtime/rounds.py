@@ -546,8 +546,8 @@ class RoundPlane:
             self.epoch = max(self.epoch + 1, n.membership.epoch * 1000 + 1)
             epoch = self.epoch
             self.members = members
-        if len(members) < 2:
-            return                                 # nothing to collect from; TCP path only
+        # a lone node forms a one-member group: no collective, the same pipelined
+        # rounds (device-resident results, one copy per round, two in flight)
         port = self.cfg.base_port + self.cfg.collective_port_offset + epoch % 100
         log.warning("%s: forming collective epoch %d over %s", n.name, epoch, members)
         n.tracer.instant("round.form", epoch=epoch, members=len(members))

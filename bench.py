@@ -590,8 +590,9 @@ def run_node(a) -> int:
     B = a.batch
     base = int(os.environ.get("MASTER_PORT", "29500")) + 200
     tmp = tempfile.mkdtemp(prefix=f"idunno_bench_r{rank}_")
-    # RCCL rounds need one GPU per node process; the 1-GPU failover shares GPU 0 (TCP path)
-    rounds = n > 1 and n <= W
+    # rounds need one GPU per node process (RCCL for n > 1, a one-member group at n = 1);
+    # the 1-GPU failover puts 2 nodes on GPU 0 (TCP path)
+    rounds = n <= W
     cfg = ClusterConfig(num_nodes=n, base_port=base, store_root=tmp, collective_rounds=rounds, dtype=a.dtype,
                         fp32_impl=a.fp32_impl, max_chunk=max(2048, B), rpc_timeout_s=60.0, worker_budget=W,
                         dataset_size=10 ** 9, collective_port_offset=100,
@@ -690,7 +691,8 @@ def _drive_system(a, node, W: int, B: int) -> dict:
            "p50_system_s": round(p50, 6),
            "p50_system_loaded_s": round(loaded[len(loaded) // 2], 6) if loaded else None,
            "system_path": ("client -> coordinator Node (membership, hot standby) -> fair-time split -> "
-                           + ("RCCL rounds" if node.rounds is not None else "local JOB queue")
+                           + (("RCCL rounds" if W > 1 else "pipelined rounds (one-member group)")
+                              if node.rounds is not None else "local JOB queue")
                            + " -> job-state ingest"),
            "system_results_recorded": st.images_done(a.model)}
 

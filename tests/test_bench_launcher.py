@@ -86,4 +86,5 @@ def test_bench_system_mode_dry_run(n):
     d = _line(r.stdout)
     assert d["system_results_recorded"] == (1 + 4 + 5) * 400 * n
     assert ("RCCL rounds" in d["system_path"]) == (n > 1)
+    assert "rounds" in d["system_path"]
     assert d["p50_system_s"] > 0 and d["value_system"] > 0

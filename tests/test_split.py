@@ -454,3 +454,57 @@ def test_split_activations_past_fp16_range_match_fp64(ops):
     c2, p2 = ex.run("resnet18", img, 0, 3)
     assert (c2 == want.argmax(1).numpy()).all()
     assert abs(float(p2[0]) - torch.softmax(want, 1).max(1).values[0].item()) < 1e-4
+
+
+# ---------------------------------------------------------------------------
+# dual conv: a stride-2 block's 1x1/2 downsample in the launch of its 3x3/2
+# conv (the downsample is the centre tap), halves read in place downstream
+# ---------------------------------------------------------------------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,C,Cout,tile", [(2, 56, 64, 128, -1), (3, 28, 128, 256, -1), (2, 14, 256, 512, -1),
+                                             (3, 13, 64, 128, 36), (2, 9, 128, 256, 42), (1, 15, 64, 128, 34)])
+def test_conv_split_dual_downsample(ops, B, H, C, Cout, tile):
+    torch.manual_seed(B + H + C)
+    x = torch.randn(B, H, H, C, device=DEV)
+    w3 = torch.randn(Cout, C, 3, 3) / (9 * C) ** 0.5
+    w1 = torch.randn(Cout, C, 1, 1) / C ** 0.5 * 3.0          # a different weight scale (own acc_scale2)
+    b3, b1 = torch.randn(Cout) * 0.1, torch.randn(Cout) * 0.1
+    s3, sc3 = P.pack_split_weight(w3)
+    s1, sc1 = P.pack_split_weight(w1)
+    c2 = s3.shape[1] // 9
+    wd = torch.zeros(2 * Cout, s3.shape[1], dtype=s3.dtype)
+    wd[:Cout] = s3
+    wd[Cout:, 4 * c2:5 * c2] = s1
+    xs = ops.split_from_f32(x)
+    both = ops.conv2d_split_dual(xs, wd.to(DEV), torch.cat([b3, b1]).to(DEV), sc3, sc1, Cout, 3, 3, 2, 1, True,
+                                 tile=tile)
+    main, down = both[..., :2 * Cout], both[..., 2 * Cout:]
+    _check(P.from_split(main.contiguous()), _ref64(x, w3, b3, 2, 1, True))
+    _check(P.from_split(down.contiguous()), _ref64(x, w1, b1, 2, 0, False))
+    # the next conv reads the halves in place: x with a 2x pixel stride, residual likewise
+    w2 = torch.randn(Cout, Cout, 3, 3) / (9 * Cout) ** 0.5
+    b2 = torch.randn(Cout) * 0.1
+    s2, sc2 = P.pack_split_weight(w2)
+    y = ops.conv2d_split(main, s2.to(DEV), b2.to(DEV), sc2, 3, 3, 1, 1, True, residual=down)
+    y_ref = ops.conv2d_split(main.contiguous(), s2.to(DEV), b2.to(DEV), sc2, 3, 3, 1, 1, True,
+                             residual=down.contiguous())
+    assert torch.equal(y, y_ref)
+    mid = P.from_split(main.contiguous()).double()
+    _check(P.from_split(y), _ref64(mid, w2, b2, 1, 1, True, P.from_split(down.contiguous())))
+
+
+@pytest.mark.gpu
+def test_resnet18_fused_downsample_same_logits(ops):
+    from idunno.models import reference as ref
+
+    m = ref.build("resnet18", seed=2, randomize_bn=True)
+    r = P.HipRunner(P.compile_model(m, "resnet18", "fp32"))
+    img = ops.synth_images(7, 0, 24, DEV)
+    r.fuse_down = True
+    assert all(r._dual_ok(b) for b in r.p.blocks if b.down is not None)
+    fused = r.logits(img).double()
+    r.fuse_down = False
+    plain = r.logits(img).double()
+    scale = plain.abs().max().item()
+    assert (fused - plain).abs().max().item() <= 1e-6 * scale
