@@ -88,3 +88,26 @@ def test_bench_system_mode_dry_run(n):
     assert ("RCCL rounds" in d["system_path"]) == (n > 1)
     assert "rounds" in d["system_path"]
     assert d["p50_system_s"] > 0 and d["value_system"] > 0
+
+
+def test_bench_under_torchrun_dry_run():
+    """The driver's N > 1 form: torchrun starts N launcher processes (RANK set);
+    each starts its own rank child, rank 0's launcher then runs phases 2-3 on
+    all N GPUs and prints the ONE merged line."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--dry-run"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["results_recorded"] == (1 + 3 + 5) * 800
+    assert "extras_error" not in d and d["two_job_mixed_rounds"] >= 1
+    assert d["coord_failover_images_exact"] is True
