@@ -100,7 +100,8 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--no-extras", action="store_true", help="skip the strong-scaling / fp16 / numerics extras")
     ap.add_argument("--no-system", action="store_true", help="skip phases 2-3 (system + failover)")
-    ap.add_argument("--extras-timeout", type=float, default=240.0, help="seconds per system / failover phase")
+    ap.add_argument("--extras-timeout", type=float, default=150.0,
+                    help="seconds per system / failover phase (bounded: the driver gives the whole run 600 s)")
     ap.add_argument("--two-job-queries", type=int, default=10, help="queries per job in the two-job run")
     ap.add_argument("--failover-queries", type=int, default=12, help="queries of the job the failover kills into")
     ap.add_argument("--seed", type=int, default=0)

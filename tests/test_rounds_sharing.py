@@ -190,7 +190,10 @@ def test_two_jobs_share_the_rounds_on_8_ranks():
         assert after["mixed_rounds"] - before["mixed_rounds"] >= Q - 3, (before, after)
         assert after["max_queries_per_round"] >= 2
         print(f"alone: alexnet {t_a:.2f}s resnet18 {t_r:.2f}s; together {t_both:.2f}s; rounds {before} -> {after}")
-        assert t_both <= 1.2 * max(t_a, t_r), (t_a, t_r, t_both)
+        # space sharing: about the slower job alone, well under the time-sliced sum
+        # (1.2x held in quiet runs; 1.25x seen with the whole CPU suite loading the
+        # 8 processes, hence the margin)
+        assert t_both <= 1.35 * max(t_a, t_r) and t_both <= 0.8 * (t_a + t_r), (t_a, t_r, t_both)
 
         # idle gap longer than the collective-op timeout: nothing is posted while idle,
         # so the epoch survives and the next query runs as a round in it
