@@ -78,7 +78,9 @@ def _compile_cmd(src: Path, obj: Path, incs, abi) -> list[str]:
     return cmd
 
 
-FLAGS = BUILD / "flags.txt"
+# next to the .so (not under build/, which never ships to the GPU box): a box
+# that receives a prebuilt _C.so must not rebuild it for want of this file
+FLAGS = PKG_DIR / "_C.so.flags"
 
 
 def _flags() -> str:

@@ -1253,6 +1253,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_stem_split_niw", [](int64_t n) { set_stem_split_niw((int)n); },
         "A/B: fused split stem, 16-cout A fragments per wave (1 default: 3 workgroups/CU; 2)");
   m.def("set_split_wide_tile", &set_split_wide_tile, "A/B: 128x160 split tiles for M < 50000 (layer4; default on)");
+  m.def("set_c64_split_variant", &set_c64_split_variant,
+        "layer1 split 3x3 64->64 kernel: 0 = 16 couts per wave (2 workgroups/CU), 2 / 3 = 32 couts per wave");
+  m.def("c64_split_variant", &c64_split_variant, "current layer1 split kernel variant");
   m.def("set_split_wide_l3", &set_split_wide_l3, "A/B: 128x160 split tiles also for 50000 <= M < 100000 (layer3)");
   m.def("set_f16_wide_tile", &set_f16_wide_tile, "A/B: fp16 128x160 tiles for M < 50000 (layer4)");
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");

@@ -141,6 +141,8 @@ int conv_glds_split_pick(int M, int Cout);
 void set_f16_wide_tile(bool on);     // A/B: fp16 128x160 tiles for M < 50000 (default on)
 void set_split_wide_tile(bool on);   // A/B: 128x160 tiles for small-M split convs (default on)
 void set_split_wide_l3(bool on);     // A/B: ... also for 50000 <= M < 100000 (layer3)
+void set_c64_split_variant(int v);  // layer1 split kernel: 0 = 16 couts/wave, 2/3 = 32 couts/wave (read ring depth)
+int c64_split_variant();
 #ifdef IDUNNO_EXPERIMENTAL
 // split 3x3/s1/p1 conv with the B operand from a halo patch per 32-channel block (Cout % 128 == 0)
 bool conv3x3_patch_split_supported(int B, int H, int W, int C, int Cout);

@@ -20,7 +20,7 @@
 // Workgroup = 4 waves (2 x 2): each wave 32 channels (2 A frags) x 7 pixel
 // fragments (112 px) -> 14 MFMAs per 32-wide K step.  LDS <= ~68 KiB -> 2
 // workgroups per CU.
-#include "../kernels.h"
+#include "../../kernels.h"
 
 namespace idunno {
 

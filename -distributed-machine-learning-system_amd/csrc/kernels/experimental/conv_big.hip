@@ -21,7 +21,7 @@
 //     and has NS-1 stages of MFMA time to land.
 // Operand staging, swizzle and epilogue follow conv_glds.hip (weights = MFMA A,
 // pixels = MFMA B, NHWC 8-byte epilogue stores).
-#include "../kernels.h"
+#include "../../kernels.h"
 
 namespace idunno {
 

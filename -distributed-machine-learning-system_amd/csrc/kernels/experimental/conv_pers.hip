@@ -20,7 +20,7 @@
 //     no store or load latency is waited for in front of the MFMAs.
 // Loop body per stage (BK = 64, two K32 chunks, two fragment register sets)
 // as conv_big.hip; tiles and swizzles as conv_glds.hip.
-#include "../kernels.h"
+#include "../../kernels.h"
 
 namespace idunno {
 

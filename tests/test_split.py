@@ -210,8 +210,20 @@ SPLIT_TILES = [26, 27, 34, 36, 38, 42]
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,H,W", [(2, 56, 56), (3, 13, 49), (1, 9, 62)])
 @pytest.mark.parametrize("res", [False, True])
-def test_conv_split_c64_rows(ops, B, H, W, res):
-    """Row-streaming register-weight 3x3 64->64 kernel (tile 50)."""
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5])
+def test_conv_split_c64_rows(ops, B, H, W, res, variant):
+    """Row-streaming register-weight 3x3 64->64 kernel (tile 50): 16 couts per
+    wave (variant 0) and 32 couts per wave with a 2- / 3-deep read ring."""
+    ext = ops.load()
+    keep = ext.c64_split_variant()
+    ext.set_c64_split_variant(variant)
+    try:
+        _c64_rows_case(ops, B, H, W, res)
+    finally:
+        ext.set_c64_split_variant(keep)
+
+
+def _c64_rows_case(ops, B, H, W, res):
     torch.manual_seed(B * H + W + res)
     x = torch.randn(B, H, W, 64, device=DEV)
     w = torch.randn(64, 64, 3, 3) / 24
