@@ -173,6 +173,14 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
                        cur_stream()); check_launch("conv3x3_c64");
     return y;
   }
+  const bool c1s_ok = KH == 1 && KW == 1 && (stride == 1 || stride == 2) && pad == 0 && !out_f32 &&
+                      a.ablate == 0 && conv1x1_stream_supported(C, Cout, M);
+  if (tile == 80 || (tile < 0 && c1s_ok && conv1x1_stream_default(C, stride))) {
+    TORCH_CHECK(c1s_ok, "tile 80 (streaming 1x1 conv) does not support this shape");
+    conv1x1_stream_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, a.M, C, Cout, a.relu,
+                          H, W, Wo, Ho * Wo, stride, cur_stream()); check_launch("conv1x1_stream");
+    return y;
+  }
   const int t = tile >= 10 ? (int)tile : conv_glds_pick(a.M, Cout);
 #ifdef IDUNNO_EXPERIMENTAL
   if (t >= 70 && t < 80) {             // persistent loop (conv_pers.hip); 1-stage convs fall back to tile 65
@@ -1253,6 +1261,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_stem_split_niw", [](int64_t n) { set_stem_split_niw((int)n); },
         "A/B: fused split stem, 16-cout A fragments per wave (1 default: 3 workgroups/CU; 2)");
   m.def("set_split_wide_tile", &set_split_wide_tile, "A/B: 128x160 split tiles for M < 50000 (layer4; default on)");
+  m.def("set_conv1x1_stream", &set_conv1x1_stream,
+        "A/B: persistent streaming kernel (tile 80) as the default for eligible fp16 1x1/s1 convs");
+  m.def("set_conv1x1_stream_mask", &set_conv1x1_stream_mask,
+        "A/B: shapes that take the streaming 1x1 kernel by default (1 Cin<=128, 2 Cin 256, 4 Cin 512, 8 stride 2)");
   m.def("set_c64_split_variant", &set_c64_split_variant,
         "layer1 split 3x3 64->64 kernel: 0 = 16 couts per wave (2 workgroups/CU), 2 / 3 = 32 couts per wave");
   m.def("c64_split_variant", &c64_split_variant, "current layer1 split kernel variant");

@@ -141,6 +141,14 @@ int conv_glds_split_pick(int M, int Cout);
 void set_f16_wide_tile(bool on);     // A/B: fp16 128x160 tiles for M < 50000 (default on)
 void set_split_wide_tile(bool on);   // A/B: 128x160 tiles for small-M split convs (default on)
 void set_split_wide_l3(bool on);     // A/B: ... also for 50000 <= M < 100000 (layer3)
+// persistent streaming 1x1 fp16 conv, stride 1 or 2 (conv1x1_stream.hip): shapes in conv1x1_stream_supported
+bool conv1x1_stream_supported(int C, int Cout, long M);
+bool conv1x1_stream_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
+                           const void* zero, int M, int C, int Cout, int relu, int H, int W, int Wo, int HWo,
+                           int stride, hipStream_t st);
+void set_conv1x1_stream(bool on);   // default choice for eligible fp16 1x1 convs (A/B)
+void set_conv1x1_stream_mask(int mask);  // default shapes: 1 Cin<=128, 2 Cin 256, 4 Cin 512, 8 stride 2
+bool conv1x1_stream_default(int C, int stride);
 void set_c64_split_variant(int v);  // layer1 split kernel: 0 = 16 couts/wave, 2/3 = 32 couts/wave (read ring depth)
 int c64_split_variant();
 #ifdef IDUNNO_EXPERIMENTAL

@@ -1,0 +1,322 @@
+// Persistent streaming 1x1 / stride-1 convolution (fp16 NHWC) for the
+// memory-bound ResNet50 bottleneck layers (K = Cin 64 or 128).
+//
+// Why: at B = 1024 the 1x1 expansion convs (64 -> 256 with the residual, and
+// the layer1 downsample) run at 47-60 % of HBM on the implicit-GEMM tiles
+// (profiles/r3_resnet50_b1024_fp16_layer_roofline.md).  Their K loop is one or
+// two stages, so each 128 x 128 block is a single memory round trip -- load,
+// a few MFMAs, residual, store -- and with its epilogue traffic ablated the
+// layer still takes 448 us for a 0.4 GB read (profiles/
+// r3_resnet50_1x1_epilogue_ablation.log): the blocks are latency-bound.
+// Here each workgroup stays resident and streams pixel tiles:
+//   * its 4 waves each own 64 output channels and keep their weights in
+//     REGISTERS for the whole launch (K = 64: 32 VGPRs);
+//   * the 64-pixel input tile of the NEXT item is DMA'd (global_load_lds) into
+//     the other half of a 2-tile LDS ring, and its residual is loaded into the
+//     other half of a register double buffer, while the current item computes
+//     and stores: every wait is a counted `s_waitcnt vmcnt(N)` that leaves the
+//     younger loads and the previous item's stores in flight;
+//   * epilogue stores are buffer stores issued by every lane (masked lanes
+//     write past the descriptor's size and are dropped), so each wave issues
+//     the same number of memory operations per item and the counts hold.
+// Workgroup g takes cout slab g % nslab (256 channels) and every (G/nslab)-th
+// pixel tile; the slabs of one tile are adjacent ids, placed on one XCD by
+// xcd_remap so the second read of the tile hits that XCD's L2.
+#include <type_traits>
+
+#include "../kernels.h"
+#include "../launch_util.h"
+
+namespace idunno {
+
+typedef __attribute__((address_space(3))) void lds_void_c1;
+typedef __attribute__((address_space(1))) void glb_void_c1;
+typedef unsigned int u32x2_c1 __attribute__((ext_vector_type(2)));
+
+struct C1sArgs {
+  const half_t* x;      // [M][K]
+  const half_t* w;      // [N][K]
+  const float* bias;    // [N]
+  const half_t* res;    // [M][N] or nullptr
+  half_t* y;            // [M][N]
+  const void* zero;     // >= 16 zero bytes
+  int M, N, relu;
+  int nslab;            // cout slabs of NW * 64 channels
+  int ntiles;           // ceil(M / BM)
+  int G;                // workgroups (a multiple of nslab)
+  int H, W, Wo, HWo, stride;   // stride 2: output pixel m reads input pixel (b, 2 oh, 2 ow)
+};
+
+typedef int int4s __attribute__((ext_vector_type(4)));
+
+// 8-byte buffer load (offen + SGPR soffset + immediate) that the wait-count pass
+// does not track: the caller counts it in its own vmcnt waits and reg_tie()s
+// the result after them
+template <int IMM>
+__device__ __forceinline__ half4v bload_b64_untracked(int4s rsrc, uint32_t voff, uint32_t soff) {
+  half4v v;
+  asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen offset:%4"
+               : "=v"(v) : "v"(voff), "s"(rsrc), "s"(soff), "n"(IMM) : "memory");
+  return v;
+}
+
+template <int N_>
+__device__ __forceinline__ void c1_vmcnt() {
+  static_assert(N_ >= 0 && N_ < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
+}
+
+template <int K, int NW, int BM, int CW, bool HAS_RES>
+__global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: min waves per SIMD
+(const C1sArgs a) {
+  // BM pixels per tile: 64, or 32 for K = 128 (whose 64 A-fragment registers
+  // plus a 64-pixel tile's accumulators and residual double buffer spill)
+  // CW output channels per wave: 64, or 32 for K = 256 / 512 (A fragments: CW*K/128 VGPRs)
+  constexpr int FN = CW / 16, FM = BM / 16;
+  constexpr int KK = K / 32;             // MFMA K chunks
+  constexpr int KC = K / 64;             // 128-byte sub-rows per pixel (one LDS sub-tile each)
+  constexpr int SUB = BM * 128;          // bytes per sub-tile
+  constexpr int IPS = BM / 8;            // DMA instructions per sub-tile (8 rows of 128 B each)
+  constexpr int TILE = KC * SUB;
+  constexpr int NINS = TILE / 1024;      // DMA instructions per tile
+  static_assert(NINS % NW == 0, "DMA instructions split evenly over the waves");
+  constexpr int GX = NINS / NW;          // per wave
+  constexpr int GS = FN * FM;            // epilogue stores per wave and item
+  constexpr int GR = HAS_RES ? FN * FM : 0;
+  static_assert(GS + GX + GR < 64, "vmcnt immediate");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lid = xcd_remap((int)blockIdx.x, a.G);
+  const int slab = lid % a.nslab;
+  const int tstride = a.G / a.nslab;
+  int t = lid / a.nslab;
+  if (t >= a.ntiles) return;             // uniform
+  const int frow = lane & 15, fch = lane >> 4;
+  const int nw0 = slab * (NW * CW) + wave * CW;
+
+  // ---- this wave's weights, resident: A fragments [cout frag][K chunk] ----
+  half8v fa[FN][KK];
+  float4v bv[FN];
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int row = nw0 + i * 16 + frow;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+      fa[i][kk] = row < a.N ? *reinterpret_cast<const half8v*>(a.w + (size_t)row * K + kk * 32 + fch * 8)
+                            : half8v{0, 0, 0, 0, 0, 0, 0, 0};
+    const int n = nw0 + i * 16 + fch * 4;
+    bv[i] = n < a.N ? *reinterpret_cast<const float4v*>(a.bias + n) : float4v{0.f, 0.f, 0.f, 0.f};
+  }
+  const half_t* zero = static_cast<const half_t*>(a.zero);
+  const unsigned out_bytes = (unsigned)a.M * (unsigned)a.N * 2u;
+  const auto out_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)out_bytes, 0x00020000);
+
+  // DMA of tile tt into ring buffer buf: instruction ins covers rows 8*(ins%IPS).. of sub-tile ins/IPS;
+  // lane l lands in row (l >> 3), slot (l & 7), and fetches chunk slot ^ swz_r(row)
+  auto issue_x = [&](int tt, int buf) {   // buf: a constant at every call
+#pragma unroll
+    for (int j = 0; j < GX; ++j) {
+      const int ins = wave + NW * j;
+      const int sub = ins / IPS, r = (ins % IPS) * 8 + (lane >> 3);
+      const int m = tt * BM + r;
+      const int ch = (lane & 7) ^ swz_r(r, 8);
+      int pin = m;                            // input pixel of output pixel m
+      if (a.stride != 1) {
+        const int b = m / a.HWo, rr = m - b * a.HWo;
+        const int oh = rr / a.Wo, ow = rr - oh * a.Wo;
+        pin = (b * a.H + oh * a.stride) * a.W + ow * a.stride;
+      }
+      const half_t* src = m < a.M ? a.x + (size_t)pin * K + sub * 64 + ch * 8 : zero;
+      __builtin_amdgcn_global_load_lds((glb_void_c1*)src, (lds_void_c1*)(smem + buf * TILE + ins * 1024), 16, 0, 0);
+    }
+  };
+  // residual and output addressing: byte offset of element (pixel m, cout n) =
+  // lane part (frow*N + nw0 + 4*fch)*2 [VGPR] + tile / fragment-row part
+  // (tt*BM + 16j)*N*2 [SGPR] + 32i [immediate]; rows past M fall outside the
+  // descriptors (num_records = M*N*2): loads return 0, stores are dropped
+  const uint32_t lane_off = (uint32_t)((frow * a.N + nw0 + 4 * fch) * 2);
+  int4s res_rsrc = {0, 0, 0, 0};
+  if constexpr (HAS_RES) {
+    const unsigned long long rp = reinterpret_cast<unsigned long long>(a.res);
+    res_rsrc = int4s{(int)(rp & 0xffffffffu), (int)(rp >> 32), (int)out_bytes, 0x00020000};
+  }
+  // residual of tile tt (C/D layout: 4 consecutive couts of one pixel per
+  // fragment): buffer loads the wait-count pass does not track (counted here)
+  half4v rv[2][HAS_RES ? FN : 1][HAS_RES ? FM : 1];
+  auto load_res = [&](int tt, auto rb_c) {
+    if constexpr (HAS_RES) {
+      constexpr int rb = decltype(rb_c)::value;
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const uint32_t soff = (uint32_t)((tt * BM + j * 16) * a.N * 2);
+        rv[rb][0][j] = bload_b64_untracked<0>(res_rsrc, lane_off, soff);
+        if constexpr (FN > 1) rv[rb][1][j] = bload_b64_untracked<32>(res_rsrc, lane_off, soff);
+        if constexpr (FN > 2) rv[rb][2][j] = bload_b64_untracked<64>(res_rsrc, lane_off, soff);
+        if constexpr (FN > 3) rv[rb][3][j] = bload_b64_untracked<96>(res_rsrc, lane_off, soff);
+      }
+    }
+  };
+
+  issue_x(t, 0);
+  load_res(t, std::integral_constant<int, 0>{});
+  const uint32_t lds0 = lds_addr(smem);
+  bool first = true;
+  // one item; BUF (the ring half and residual register set of tile t) is a
+  // template constant so rv never needs runtime indexing (it went to scratch)
+  auto item = [&](auto buf_c) -> bool {
+    constexpr int buf = decltype(buf_c)::value;
+    const int tn = t + tstride;
+    const bool more = tn < a.ntiles;      // wave-uniform
+    // tile t's DMA landed: younger are its residual loads and the previous item's stores
+    if (first) c1_vmcnt<GR>(); else c1_vmcnt<GR + GS>();
+    __builtin_amdgcn_s_barrier();         // everyone's DMA landed; the other buffer's reads are done
+    if (more) {
+      issue_x(tn, buf ^ 1);
+      load_res(tn, std::integral_constant<int, buf ^ 1>{});
+    }
+    float4v acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+    const uint32_t base = lds0 + buf * TILE;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      half8v fb[FM];
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int r = j * 16 + frow;
+        const int c = 4 * (kk & 1) + fch;
+        fb[j] = lds_read_b128(base + (kk >> 1) * SUB + r * 128 + ((c ^ swz_r(r, 8)) << 4));
+      }
+      lds_waitcnt<0>();
+#pragma unroll
+      for (int j = 0; j < FM; ++j) lds_tie(fb[j]);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][kk], fb[j], acc[i][j], 0, 0, 0);
+    }
+    // ---- epilogue: bias (+ residual) (+ ReLU), fp16, buffer stores ----
+    if constexpr (HAS_RES) {
+      // this item's residual landed: younger are the previous stores and, with a
+      // next item, its DMA and residual loads
+      if (first) {
+        if (more) c1_vmcnt<GX + GR>(); else c1_vmcnt<0>();
+      } else {
+        if (more) c1_vmcnt<GS + GX + GR>(); else c1_vmcnt<GS>();
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) reg_tie(rv[buf][i][j]);
+    }
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int soff = (t * BM + j * 16) * a.N * 2;
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        float4v v = acc[i][j] + bv[i];
+        if constexpr (HAS_RES) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)rv[buf][i][j][e];
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        half4v o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (half_t)v[e];
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_c1, o), out_rsrc, (int)lane_off + 32 * i,
+                                              soff, 0);
+      }
+    }
+    t = tn;
+    first = false;
+    return more;
+  };
+  while (item(std::integral_constant<int, 0>{}) && item(std::integral_constant<int, 1>{})) {
+  }
+  c1_vmcnt<0>();
+}
+
+template <int K, int NW, int BM, int CW, bool R>
+static void c1s_cfg(C1sArgs a, hipStream_t st) {
+  a.nslab = a.N / (NW * CW);
+  constexpr int TILE = (K / 64) * BM * 128;
+  a.ntiles = (a.M + BM - 1) / BM;
+  const int per_cu = 8 / NW;                        // two waves per SIMD
+  int G = per_cu * device_cu_count();
+  G -= G % a.nslab;
+  const long items = (long)a.ntiles * a.nslab;
+  if (G > items) G = (int)items;
+  a.G = G;
+  auto kern = conv1x1_stream_kernel<K, NW, BM, CW, R>;
+  ensure_lds_attr(reinterpret_cast<const void*>(kern), 2 * TILE);
+  hipLaunchKernelGGL(kern, dim3(G), dim3(64 * NW), 2 * TILE, st, a);
+}
+
+bool conv1x1_stream_supported(int C, int Cout, long M) {
+  // Cout 64 at C 64: one-wave workgroups, 8 per CU; C 256 / 512: 32 couts per
+  // wave, slabs of 64 (two waves, C 256) or 128 channels
+  const bool shape = (C == 64 && (Cout == 64 || Cout % 256 == 0)) || (C == 128 && Cout % 256 == 0) ||
+                     (C == 256 && (Cout == 64 || Cout % 128 == 0)) || (C == 512 && Cout % 128 == 0);
+  return shape && M > 0 && M * Cout * 2 < (1L << 31);
+}
+
+// default on: ResNet50 b1024 fp16 whole forward 19.21 -> 17.80 ms (+7.9 %),
+// profiles/r3_conv1x1_stream.md
+static bool g_c1s_default = true;
+// which eligible shapes take it by default: bit 0 Cin <= 128, bit 1 Cin 256
+// (+3.7 % whole forward on top of bit 0), bit 2 Cin 512 (+1.7 %), bit 3 stride 2
+// (+1.0 %): profiles/r3_conv1x1_stream.md
+static int g_c1s_mask = 15;
+void set_conv1x1_stream(bool on) { g_c1s_default = on; }
+void set_conv1x1_stream_mask(int mask) { g_c1s_mask = mask; }
+bool conv1x1_stream_default(int C, int stride) {
+  if (!g_c1s_default || (stride != 1 && !(g_c1s_mask & 8))) return false;
+  const int bit = C <= 128 ? 1 : C == 256 ? 2 : C == 512 ? 4 : 0;
+  return (g_c1s_mask & bit) != 0;
+}
+
+bool conv1x1_stream_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
+                           const void* zero, int M, int C, int Cout, int relu, int H, int W, int Wo, int HWo,
+                           int stride, hipStream_t st) {
+  if (!conv1x1_stream_supported(C, Cout, M)) return false;
+  C1sArgs a;
+  a.H = H;
+  a.W = W;
+  a.Wo = Wo;
+  a.HWo = HWo;
+  a.stride = stride;
+  a.x = x;
+  a.w = w;
+  a.bias = bias;
+  a.res = res;
+  a.y = y;
+  a.zero = zero;
+  a.M = M;
+  a.N = Cout;
+  a.relu = relu;
+  const bool r = res != nullptr;
+  if (C == 64 && Cout == 64) {
+    r ? c1s_cfg<64, 1, 64, 64, true>(a, st) : c1s_cfg<64, 1, 64, 64, false>(a, st);
+  } else if (C == 64) {
+    r ? c1s_cfg<64, 4, 64, 64, true>(a, st) : c1s_cfg<64, 4, 64, 64, false>(a, st);
+  } else if (C == 128) {
+    r ? c1s_cfg<128, 4, 32, 64, true>(a, st) : c1s_cfg<128, 4, 32, 64, false>(a, st);
+  } else if (C == 256 && Cout == 64) {
+    r ? c1s_cfg<256, 2, 32, 32, true>(a, st) : c1s_cfg<256, 2, 32, 32, false>(a, st);
+  } else if (C == 256) {
+    r ? c1s_cfg<256, 4, 32, 32, true>(a, st) : c1s_cfg<256, 4, 32, 32, false>(a, st);
+  } else {
+    r ? c1s_cfg<512, 4, 32, 32, true>(a, st) : c1s_cfg<512, 4, 32, 32, false>(a, st);
+  }
+  return true;
+}
+
+}  // namespace idunno

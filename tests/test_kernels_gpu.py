@@ -87,6 +87,34 @@ def test_conv_all_tiles_with_residual(ops, tile, H):
     _check(y, ref)
 
 
+# streaming 1x1 conv (tile 80, conv1x1_stream.hip): the ResNet50 bottleneck 1x1
+# shapes; M values that leave a partial last tile and give some workgroups one
+# item, others several (B*H*H vs the 2-per-CU resident grid)
+@pytest.mark.parametrize("stride", [1, 2])
+@pytest.mark.parametrize("B,H,Cin,Cout,res", [
+    (3, 56, 64, 256, True), (3, 56, 64, 256, False), (2, 56, 64, 64, False), (5, 28, 128, 512, True),
+    (1, 9, 64, 256, True), (1, 7, 128, 512, False), (2, 13, 64, 512, True), (40, 56, 64, 256, True),
+    (2, 56, 256, 64, False), (3, 14, 256, 1024, True), (2, 20, 256, 128, False), (1, 11, 256, 384, True),
+    (2, 28, 512, 128, False), (3, 7, 512, 2048, True)])
+def test_conv1x1_stream(ops, B, H, Cin, Cout, res, stride):
+    from idunno.models.packed import pack_conv_weight
+
+    torch.manual_seed(B * 7 + H + Cin + Cout + res + stride)
+    x = torch.randn(B, H, H, Cin, device=DEV).half()
+    w = torch.randn(Cout, Cin, 1, 1) / Cin ** 0.5
+    b = torch.randn(Cout) * 0.1
+    ho = (H - 1) // stride + 1
+    r = torch.randn(B, ho, ho, Cout, device=DEV).half() if res else None
+    pw, _ = pack_conv_weight(w)
+    for relu in (True, False):
+        y = ops.conv2d(x, pw.to(DEV), b.to(DEV), 1, 1, stride, 0, relu, residual=r, tile=80)
+        ref = _ref_conv(x, w.half().float().to(DEV), b.to(DEV), stride, 0, relu, r)
+        _check(y, ref)
+        # same rounding as the implicit-GEMM tile: identical fp16 outputs
+        y36 = ops.conv2d(x, pw.to(DEV), b.to(DEV), 1, 1, stride, 0, relu, residual=r, tile=36)
+        assert (y.float() - y36.float()).abs().max().item() <= 2e-3 * (y36.float().abs().max().item() + 1)
+
+
 BIG_TILES = [60, 61, 62, 63, 65, 66, 67, 68, 69, 70, 71, 72, 73]
 
 
