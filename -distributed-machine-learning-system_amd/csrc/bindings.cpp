@@ -175,7 +175,7 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   }
   const bool c1s_ok = KH == 1 && KW == 1 && (stride == 1 || stride == 2) && pad == 0 && !out_f32 &&
                       a.ablate == 0 && conv1x1_stream_supported(C, Cout, M);
-  if (tile == 80 || (tile < 0 && c1s_ok && conv1x1_stream_default(C, stride))) {
+  if (tile == 80 || (tile < 0 && c1s_ok && conv1x1_stream_default(C, stride, M))) {
     TORCH_CHECK(c1s_ok, "tile 80 (streaming 1x1 conv) does not support this shape");
     conv1x1_stream_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, a.M, C, Cout, a.relu,
                           H, W, Wo, Ho * Wo, stride, cur_stream()); check_launch("conv1x1_stream");
@@ -444,6 +444,15 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
     return y;
   }
 #endif
+  const bool c1s_ok = KH == 1 && KW == 1 && (stride == 1 || stride == 2) && pad == 0 && !out_f32 && !strided &&
+                      nsplit == 0 && a.ablate == 0 && conv1x1_stream_split_supported(C2 / 2, Cout, M);
+  if (tile == 80 || (tile < 0 && c1s_ok && conv1x1_stream_split_default(C2 / 2, stride))) {
+    TORCH_CHECK(c1s_ok, "tile 80 (streaming split 1x1 conv) does not support this shape");
+    conv1x1_stream_split_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, a.M, C2 / 2, Cout,
+                                a.relu, a.acc_scale, a.ovf, H, W, Wo, Ho * Wo, stride, cur_stream());
+    check_launch("conv1x1_stream_split");
+    return y;
+  }
   const int t = tile >= 0 ? (int)tile : conv_glds_split_pick(a.M, Cout);
   a.norder = split_norder((Cout + 127) / 128, Kpad);
   TORCH_CHECK(conv_glds_split_launch(a, out_f32, t, cur_stream()), "unknown split conv tile id ", t);
@@ -1265,6 +1274,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "A/B: persistent streaming kernel (tile 80) as the default for eligible fp16 1x1/s1 convs");
   m.def("set_conv1x1_stream_mask", &set_conv1x1_stream_mask,
         "A/B: shapes that take the streaming 1x1 kernel by default (1 Cin<=128, 2 Cin 256, 4 Cin 512, 8 stride 2)");
+  m.def("set_conv1x1_stream_split_mask", &set_conv1x1_stream_split_mask,
+        "A/B: split-path shapes that take the streaming 1x1 kernel by default (bits as set_conv1x1_stream_mask)");
   m.def("set_c64_split_variant", &set_c64_split_variant,
         "layer1 split 3x3 64->64 kernel: 0 = 16 couts per wave (2 workgroups/CU), 2 / 3 = 32 couts per wave");
   m.def("c64_split_variant", &c64_split_variant, "current layer1 split kernel variant");

@@ -148,7 +148,13 @@ bool conv1x1_stream_launch(const half_t* x, const half_t* w, const float* bias, 
                            int stride, hipStream_t st);
 void set_conv1x1_stream(bool on);   // default choice for eligible fp16 1x1 convs (A/B)
 void set_conv1x1_stream_mask(int mask);  // default shapes: 1 Cin<=128, 2 Cin 256, 4 Cin 512, 8 stride 2
-bool conv1x1_stream_default(int C, int stride);
+bool conv1x1_stream_default(int C, int stride, long M);
+bool conv1x1_stream_split_supported(int C, int Cout, long M);    // split fp16 (fp32-accurate) 1x1 convs
+bool conv1x1_stream_split_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
+                                 const void* zero, int M, int C, int Cout, int relu, float acc_scale, int* ovf, int H,
+                                 int W, int Wo, int HWo, int stride, hipStream_t st);
+void set_conv1x1_stream_split_mask(int mask);   // default shapes of the split path (bits as the fp16 mask)
+bool conv1x1_stream_split_default(int C, int stride);
 void set_c64_split_variant(int v);  // layer1 split kernel: 0 = 16 couts/wave, 2/3 = 32 couts/wave (read ring depth)
 int c64_split_variant();
 #ifdef IDUNNO_EXPERIMENTAL

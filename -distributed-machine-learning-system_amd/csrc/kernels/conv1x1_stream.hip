@@ -45,6 +45,8 @@ struct C1sArgs {
   int ntiles;           // ceil(M / BM)
   int G;                // workgroups (a multiple of nslab)
   int H, W, Wo, HWo, stride;   // stride 2: output pixel m reads input pixel (b, 2 oh, 2 ow)
+  float acc_scale;      // SPLIT: accumulator multiplier 2^-e of the pre-scaled split weights
+  int* ovf;             // SPLIT: range guard flag (common.h split_guard) or nullptr
 };
 
 typedef int int4s __attribute__((ext_vector_type(4)));
@@ -60,13 +62,23 @@ __device__ __forceinline__ half4v bload_b64_untracked(int4s rsrc, uint32_t voff,
   return v;
 }
 
+// byte offset of cout fragment i (16 channels) from the wave's first channel:
+// plain 32 i; split (pixel = [hi x32][lo x32] per 32 channels, the wave starting
+// on a 32-channel boundary) 2 * (64 (i / 2) + 16 (i % 2)), lo 64 bytes further
+template <bool SPLIT>
+__host__ __device__ constexpr int c1_frag_off(int i) { return SPLIT ? 2 * (64 * (i >> 1) + 16 * (i & 1)) : 32 * i; }
+
 template <int N_>
 __device__ __forceinline__ void c1_vmcnt() {
   static_assert(N_ >= 0 && N_ < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
 }
 
-template <int K, int NW, int BM, int CW, bool HAS_RES>
+// SPLIT: fp32-accurate split-fp16 operands (conv_glds.hip SPLIT): a pixel is 2K
+// halfs, [hi x32][lo x32] per 32 channels, so one 128-byte LDS sub-row holds a
+// channel chunk's hi and lo parts; 3 MFMAs per chunk (hi*hi + hi*lo + lo*hi);
+// residual and output in the same layout, scaled by acc_scale, range-guarded.
+template <int K, int NW, int BM, int CW, bool HAS_RES, bool SPLIT = false>
 __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: min waves per SIMD
 (const C1sArgs a) {
   // BM pixels per tile: 64, or 32 for K = 128 (whose 64 A-fragment registers
@@ -74,15 +86,17 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   // CW output channels per wave: 64, or 32 for K = 256 / 512 (A fragments: CW*K/128 VGPRs)
   constexpr int FN = CW / 16, FM = BM / 16;
   constexpr int KK = K / 32;             // MFMA K chunks
-  constexpr int KC = K / 64;             // 128-byte sub-rows per pixel (one LDS sub-tile each)
+  constexpr int PXH = SPLIT ? 2 * K : K;  // halfs per input pixel
+  constexpr int SP = SPLIT ? 2 : 1;       // (hi, lo) parts
+  constexpr int KC = PXH / 64;            // 128-byte sub-rows per pixel (one LDS sub-tile each)
   constexpr int SUB = BM * 128;          // bytes per sub-tile
   constexpr int IPS = BM / 8;            // DMA instructions per sub-tile (8 rows of 128 B each)
   constexpr int TILE = KC * SUB;
   constexpr int NINS = TILE / 1024;      // DMA instructions per tile
   static_assert(NINS % NW == 0, "DMA instructions split evenly over the waves");
   constexpr int GX = NINS / NW;          // per wave
-  constexpr int GS = FN * FM;            // epilogue stores per wave and item
-  constexpr int GR = HAS_RES ? FN * FM : 0;
+  constexpr int GS = FN * FM * SP;       // epilogue stores per wave and item
+  constexpr int GR = HAS_RES ? FN * FM * SP : 0;
   static_assert(GS + GX + GR < 64, "vmcnt immediate");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -97,20 +111,24 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   const int nw0 = slab * (NW * CW) + wave * CW;
 
   // ---- this wave's weights, resident: A fragments [cout frag][K chunk] ----
-  half8v fa[FN][KK];
+  half8v fa[FN][KK][SP];
   float4v bv[FN];
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
     const int row = nw0 + i * 16 + frow;
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk)
-      fa[i][kk] = row < a.N ? *reinterpret_cast<const half8v*>(a.w + (size_t)row * K + kk * 32 + fch * 8)
-                            : half8v{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int p = 0; p < SP; ++p)
+        fa[i][kk][p] = row < a.N ? *reinterpret_cast<const half8v*>(a.w + (size_t)row * PXH + kk * (32 * SP) +
+                                                                    p * 32 + fch * 8)
+                                 : half8v{0, 0, 0, 0, 0, 0, 0, 0};
     const int n = nw0 + i * 16 + fch * 4;
     bv[i] = n < a.N ? *reinterpret_cast<const float4v*>(a.bias + n) : float4v{0.f, 0.f, 0.f, 0.f};
   }
   const half_t* zero = static_cast<const half_t*>(a.zero);
-  const unsigned out_bytes = (unsigned)a.M * (unsigned)a.N * 2u;
+  constexpr int OPX = SPLIT ? 2 : 1;     // output / residual halfs per channel
+  const unsigned out_bytes = (unsigned)a.M * (unsigned)a.N * (unsigned)(2 * OPX);
   const auto out_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)out_bytes, 0x00020000);
 
   // DMA of tile tt into ring buffer buf: instruction ins covers rows 8*(ins%IPS).. of sub-tile ins/IPS;
@@ -128,7 +146,7 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
         const int oh = rr / a.Wo, ow = rr - oh * a.Wo;
         pin = (b * a.H + oh * a.stride) * a.W + ow * a.stride;
       }
-      const half_t* src = m < a.M ? a.x + (size_t)pin * K + sub * 64 + ch * 8 : zero;
+      const half_t* src = m < a.M ? a.x + (size_t)pin * PXH + sub * 64 + ch * 8 : zero;
       __builtin_amdgcn_global_load_lds((glb_void_c1*)src, (lds_void_c1*)(smem + buf * TILE + ins * 1024), 16, 0, 0);
     }
   };
@@ -136,7 +154,9 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   // lane part (frow*N + nw0 + 4*fch)*2 [VGPR] + tile / fragment-row part
   // (tt*BM + 16j)*N*2 [SGPR] + 32i [immediate]; rows past M fall outside the
   // descriptors (num_records = M*N*2): loads return 0, stores are dropped
-  const uint32_t lane_off = (uint32_t)((frow * a.N + nw0 + 4 * fch) * 2);
+  // (SPLIT: channel n sits at split_off(n) of a 2N-half pixel; nw0 % 32 == 0 or FN == 1,
+  // so fragment i's offset from the lane part is the constant c1_frag_off(i))
+  const uint32_t lane_off = (uint32_t)((frow * a.N * OPX + (SPLIT ? split_off(nw0) : nw0) + 4 * fch) * 2);
   int4s res_rsrc = {0, 0, 0, 0};
   if constexpr (HAS_RES) {
     const unsigned long long rp = reinterpret_cast<unsigned long long>(a.res);
@@ -144,17 +164,23 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   }
   // residual of tile tt (C/D layout: 4 consecutive couts of one pixel per
   // fragment): buffer loads the wait-count pass does not track (counted here)
-  half4v rv[2][HAS_RES ? FN : 1][HAS_RES ? FM : 1];
+  half4v rv[2][HAS_RES ? FN : 1][HAS_RES ? FM : 1][SP];
   auto load_res = [&](int tt, auto rb_c) {
     if constexpr (HAS_RES) {
       constexpr int rb = decltype(rb_c)::value;
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
-        const uint32_t soff = (uint32_t)((tt * BM + j * 16) * a.N * 2);
-        rv[rb][0][j] = bload_b64_untracked<0>(res_rsrc, lane_off, soff);
-        if constexpr (FN > 1) rv[rb][1][j] = bload_b64_untracked<32>(res_rsrc, lane_off, soff);
-        if constexpr (FN > 2) rv[rb][2][j] = bload_b64_untracked<64>(res_rsrc, lane_off, soff);
-        if constexpr (FN > 3) rv[rb][3][j] = bload_b64_untracked<96>(res_rsrc, lane_off, soff);
+        const uint32_t soff = (uint32_t)(tt * BM + j * 16) * (uint32_t)a.N * (uint32_t)(2 * OPX);
+        rv[rb][0][j][0] = bload_b64_untracked<c1_frag_off<SPLIT>(0)>(res_rsrc, lane_off, soff);
+        if constexpr (FN > 1) rv[rb][1][j][0] = bload_b64_untracked<c1_frag_off<SPLIT>(1)>(res_rsrc, lane_off, soff);
+        if constexpr (FN > 2) rv[rb][2][j][0] = bload_b64_untracked<c1_frag_off<SPLIT>(2)>(res_rsrc, lane_off, soff);
+        if constexpr (FN > 3) rv[rb][3][j][0] = bload_b64_untracked<c1_frag_off<SPLIT>(3)>(res_rsrc, lane_off, soff);
+        if constexpr (SPLIT) {
+          rv[rb][0][j][1] = bload_b64_untracked<c1_frag_off<SPLIT>(0) + 64>(res_rsrc, lane_off, soff);
+          if constexpr (FN > 1) rv[rb][1][j][1] = bload_b64_untracked<c1_frag_off<SPLIT>(1) + 64>(res_rsrc, lane_off, soff);
+          if constexpr (FN > 2) rv[rb][2][j][1] = bload_b64_untracked<c1_frag_off<SPLIT>(2) + 64>(res_rsrc, lane_off, soff);
+          if constexpr (FN > 3) rv[rb][3][j][1] = bload_b64_untracked<c1_frag_off<SPLIT>(3) + 64>(res_rsrc, lane_off, soff);
+        }
       }
     }
   };
@@ -184,21 +210,37 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
     const uint32_t base = lds0 + buf * TILE;
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
-      half8v fb[FM];
+      // chunk kk: plain -- sub-row kk/2, chunks 4(kk&1)+fch; SPLIT -- sub-row kk,
+      // hi in chunks 0-3, lo in 4-7
+      half8v fb[FM][SP];
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
         const int r = j * 16 + frow;
-        const int c = 4 * (kk & 1) + fch;
-        fb[j] = lds_read_b128(base + (kk >> 1) * SUB + r * 128 + ((c ^ swz_r(r, 8)) << 4));
+#pragma unroll
+        for (int p = 0; p < SP; ++p) {
+          const int c = SPLIT ? 4 * p + fch : 4 * (kk & 1) + fch;
+          fb[j][p] = lds_read_b128(base + (SPLIT ? kk : kk >> 1) * SUB + r * 128 + ((c ^ swz_r(r, 8)) << 4));
+        }
       }
       lds_waitcnt<0>();
 #pragma unroll
-      for (int j = 0; j < FM; ++j) lds_tie(fb[j]);
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int p = 0; p < SP; ++p) lds_tie(fb[j][p]);
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int j = 0; j < FM; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][kk], fb[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][kk][0], fb[j][0], acc[i][j], 0, 0, 0);
+      if constexpr (SPLIT) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][kk][0], fb[j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][kk][1], fb[j][0], acc[i][j], 0, 0, 0);
+          }
+      }
     }
     // ---- epilogue: bias (+ residual) (+ ReLU), fp16, buffer stores ----
     if constexpr (HAS_RES) {
@@ -212,27 +254,40 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
-        for (int j = 0; j < FM; ++j) reg_tie(rv[buf][i][j]);
+        for (int j = 0; j < FM; ++j)
+#pragma unroll
+          for (int p = 0; p < SP; ++p) reg_tie(rv[buf][i][j][p]);
     }
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
-      const int soff = (t * BM + j * 16) * a.N * 2;
+      const uint32_t soff = (uint32_t)(t * BM + j * 16) * (uint32_t)a.N * (uint32_t)(2 * OPX);
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
-        float4v v = acc[i][j] + bv[i];
+        float4v v = SPLIT ? acc[i][j] * a.acc_scale + bv[i] : acc[i][j] + bv[i];
         if constexpr (HAS_RES) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (float)rv[buf][i][j][e];
+          for (int e = 0; e < 4; ++e) {
+            v[e] += (float)rv[buf][i][j][0][e];
+            if constexpr (SPLIT) v[e] += (float)rv[buf][i][j][SP - 1][e];
+          }
         }
         if (a.relu) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
         }
-        half4v o;
+        const int voff = (int)lane_off + c1_frag_off<SPLIT>(i);
+        if constexpr (SPLIT) {
+          split_guard(a.ovf, v);
+          half4v h, l;
+          split_f16x4(v, h, l);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_c1, h), out_rsrc, voff, (int)soff, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_c1, l), out_rsrc, voff + 64, (int)soff, 0);
+        } else {
+          half4v o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (half_t)v[e];
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_c1, o), out_rsrc, (int)lane_off + 32 * i,
-                                              soff, 0);
+          for (int e = 0; e < 4; ++e) o[e] = (half_t)v[e];
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_c1, o), out_rsrc, voff, (int)soff, 0);
+        }
       }
     }
     t = tn;
@@ -244,10 +299,10 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   c1_vmcnt<0>();
 }
 
-template <int K, int NW, int BM, int CW, bool R>
+template <int K, int NW, int BM, int CW, bool R, bool SPLIT = false>
 static void c1s_cfg(C1sArgs a, hipStream_t st) {
   a.nslab = a.N / (NW * CW);
-  constexpr int TILE = (K / 64) * BM * 128;
+  constexpr int TILE = (SPLIT ? 2 : 1) * (K / 64) * BM * 128;
   a.ntiles = (a.M + BM - 1) / BM;
   const int per_cu = 8 / NW;                        // two waves per SIMD
   int G = per_cu * device_cu_count();
@@ -255,7 +310,7 @@ static void c1s_cfg(C1sArgs a, hipStream_t st) {
   const long items = (long)a.ntiles * a.nslab;
   if (G > items) G = (int)items;
   a.G = G;
-  auto kern = conv1x1_stream_kernel<K, NW, BM, CW, R>;
+  auto kern = conv1x1_stream_kernel<K, NW, BM, CW, R, SPLIT>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), 2 * TILE);
   hipLaunchKernelGGL(kern, dim3(G), dim3(64 * NW), 2 * TILE, st, a);
 }
@@ -277,8 +332,11 @@ static bool g_c1s_default = true;
 static int g_c1s_mask = 15;
 void set_conv1x1_stream(bool on) { g_c1s_default = on; }
 void set_conv1x1_stream_mask(int mask) { g_c1s_mask = mask; }
-bool conv1x1_stream_default(int C, int stride) {
+bool conv1x1_stream_default(int C, int stride, long M) {
   if (!g_c1s_default || (stride != 1 && !(g_c1s_mask & 8))) return false;
+  // fp16 stride 2 below ~100k output pixels (ResNet18's downsamples at B = 400):
+  // -0.4 % whole forward, so those stay on the implicit-GEMM tiles
+  if (stride != 1 && M < 100000) return false;
   const int bit = C <= 128 ? 1 : C == 256 ? 2 : C == 512 ? 4 : 0;
   return (g_c1s_mask & bit) != 0;
 }
@@ -287,7 +345,7 @@ bool conv1x1_stream_launch(const half_t* x, const half_t* w, const float* bias, 
                            const void* zero, int M, int C, int Cout, int relu, int H, int W, int Wo, int HWo,
                            int stride, hipStream_t st) {
   if (!conv1x1_stream_supported(C, Cout, M)) return false;
-  C1sArgs a;
+  C1sArgs a{};
   a.H = H;
   a.W = W;
   a.Wo = Wo;
@@ -315,6 +373,66 @@ bool conv1x1_stream_launch(const half_t* x, const half_t* w, const float* bias, 
     r ? c1s_cfg<256, 4, 32, 32, true>(a, st) : c1s_cfg<256, 4, 32, 32, false>(a, st);
   } else {
     r ? c1s_cfg<512, 4, 32, 32, true>(a, st) : c1s_cfg<512, 4, 32, 32, false>(a, st);
+  }
+  return true;
+}
+
+// split fp16 (fp32-accurate) 1x1 convs: 32-pixel tiles (16 where the A
+// fragments, CW x K / 64 registers, leave no room for 32); 32 couts per wave,
+// 16 for Cin 512 or Cout 64
+bool conv1x1_stream_split_supported(int C, int Cout, long M) {
+  const bool shape = ((C == 64 || C == 128 || C == 256) && (Cout % 128 == 0 || (Cout == 64 && C != 128))) ||
+                     (C == 512 && Cout % 64 == 0);
+  return shape && M > 0 && (M + 64) * Cout * 4 < (1L << 32);
+}
+
+// default shapes of the split path: bit 0 Cin <= 128, bit 1 Cin 256, bit 2 Cin 512, bit 3 stride 2
+// (all on: ResNet50 b1024 split +9.4 %, ResNet18 b400 split +0.5 %, profiles/r3_conv1x1_stream.md)
+static int g_c1s_split_mask = 15;
+void set_conv1x1_stream_split_mask(int mask) { g_c1s_split_mask = mask; }
+bool conv1x1_stream_split_default(int C, int stride) {
+  if (stride != 1 && !(g_c1s_split_mask & 8)) return false;
+  const int bit = C <= 128 ? 1 : C == 256 ? 2 : C == 512 ? 4 : 0;
+  return (g_c1s_split_mask & bit) != 0;
+}
+
+bool conv1x1_stream_split_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
+                                 const void* zero, int M, int C, int Cout, int relu, float acc_scale, int* ovf, int H,
+                                 int W, int Wo, int HWo, int stride, hipStream_t st) {
+  if (!conv1x1_stream_split_supported(C, Cout, M)) return false;
+  C1sArgs a{};
+  a.x = x;
+  a.w = w;
+  a.bias = bias;
+  a.res = res;
+  a.y = y;
+  a.zero = zero;
+  a.M = M;
+  a.N = Cout;
+  a.relu = relu;
+  a.H = H;
+  a.W = W;
+  a.Wo = Wo;
+  a.HWo = HWo;
+  a.stride = stride;
+  a.acc_scale = acc_scale;
+  a.ovf = ovf;
+  const bool r = res != nullptr;
+  const bool narrow = C == 512 || Cout == 64;
+  switch (C) {
+    case 64:
+      if (narrow) r ? c1s_cfg<64, 4, 32, 16, true, true>(a, st) : c1s_cfg<64, 4, 32, 16, false, true>(a, st);
+      else r ? c1s_cfg<64, 4, 32, 32, true, true>(a, st) : c1s_cfg<64, 4, 32, 32, false, true>(a, st);
+      break;
+    case 128:
+      r ? c1s_cfg<128, 4, 32, 32, true, true>(a, st) : c1s_cfg<128, 4, 32, 32, false, true>(a, st);
+      break;
+    case 256:
+      if (narrow) r ? c1s_cfg<256, 4, 32, 16, true, true>(a, st) : c1s_cfg<256, 4, 32, 16, false, true>(a, st);
+      else r ? c1s_cfg<256, 4, 16, 32, true, true>(a, st) : c1s_cfg<256, 4, 16, 32, false, true>(a, st);
+      break;
+    default:
+      r ? c1s_cfg<512, 4, 16, 16, true, true>(a, st) : c1s_cfg<512, 4, 16, 16, false, true>(a, st);
   }
   return true;
 }

@@ -204,6 +204,28 @@ def test_conv_split_default_tile(ops, B, H, Cin, Cout, k, s, p):
     _check(P.from_split(y), ref)
 
 
+# streaming split 1x1 conv (tile 80, conv1x1_stream.hip SPLIT): ResNet50 bottleneck
+# and downsample shapes, partial last tiles, multi-slab Cout
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,Cin,Cout,s,res", [
+    (2, 56, 64, 256, 1, True), (2, 56, 64, 64, 1, False), (3, 28, 128, 512, 1, True), (2, 14, 256, 1024, 1, True),
+    (2, 56, 256, 64, 1, False), (1, 13, 256, 384, 1, False), (2, 28, 512, 128, 1, False), (2, 7, 512, 2048, 1, True),
+    (2, 56, 64, 128, 2, False), (2, 28, 256, 512, 2, False), (3, 14, 512, 1024, 2, False), (1, 9, 128, 256, 2, True)])
+def test_conv_split_1x1_stream(ops, B, H, Cin, Cout, s, res):
+    torch.manual_seed(B * 100 + H + Cin + Cout + s + res)
+    x = torch.randn(B, H, H, Cin, device=DEV)
+    w = torch.randn(Cout, Cin, 1, 1) / Cin ** 0.5
+    b = torch.randn(Cout) * 0.1
+    ho = (H - 1) // s + 1
+    r = torch.randn(B, ho, ho, Cout, device=DEV) if res else None
+    sw, scale = P.pack_split_weight(w)
+    for relu in (True, False):
+        y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, 1, 1, s, 0, relu,
+                             residual=None if r is None else ops.split_from_f32(r), tile=80)
+        assert y.shape == (B, ho, ho, 2 * Cout)
+        _check(P.from_split(y), _ref64(x, w, b, s, 0, relu, r))
+
+
 SPLIT_TILES = [26, 27, 34, 36, 38, 42]
 
 
