@@ -34,7 +34,8 @@ typedef __attribute__((address_space(1))) void glb_void_c1;
 typedef unsigned int u32x2_c1 __attribute__((ext_vector_type(2)));
 
 struct C1sArgs {
-  const half_t* x;      // [M][K]
+  const half_t* x;      // [M][K] (dual input: [M][K1])
+  const half_t* x2;     // dual input: [B][H][W][K - K1] at stride `stride`, or nullptr
   const half_t* w;      // [N][K]
   const float* bias;    // [N]
   const half_t* res;    // [M][N] or nullptr
@@ -78,7 +79,11 @@ __device__ __forceinline__ void c1_vmcnt() {
 // halfs, [hi x32][lo x32] per 32 channels, so one 128-byte LDS sub-row holds a
 // channel chunk's hi and lo parts; 3 MFMAs per chunk (hi*hi + hi*lo + lo*hi);
 // residual and output in the same layout, scaled by acc_scale, range-guarded.
-template <int K, int NW, int BM, int CW, bool HAS_RES, bool SPLIT = false>
+// K1 > 0: TWO inputs concatenated along K -- channels [0, K1) from x (at the
+// output resolution, stride 1) and [K1, K) from x2 (stride `stride`): a
+// ResNet bottleneck's expansion 1x1 and its 1x1 downsample as one GEMM
+// (W3 | Wds) . (y | x) + (b3 + bds): the downsample's output never reaches HBM.
+template <int K, int NW, int BM, int CW, bool HAS_RES, bool SPLIT = false, int K1 = 0>
 __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: min waves per SIMD
 (const C1sArgs a) {
   // BM pixels per tile: 64, or 32 for K = 128 (whose 64 A-fragment registers
@@ -140,13 +145,20 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
       const int sub = ins / IPS, r = (ins % IPS) * 8 + (lane >> 3);
       const int m = tt * BM + r;
       const int ch = (lane & 7) ^ swz_r(r, 8);
-      int pin = m;                            // input pixel of output pixel m
-      if (a.stride != 1) {
-        const int b = m / a.HWo, rr = m - b * a.HWo;
-        const int oh = rr / a.Wo, ow = rr - oh * a.Wo;
-        pin = (b * a.H + oh * a.stride) * a.W + ow * a.stride;
+      constexpr int KC1 = K1 * SP / 64;       // sub-rows of the first input (0: single input)
+      const half_t* src = zero;
+      if (K1 > 0 && sub < KC1) {              // first input: output resolution, stride 1
+        if (m < a.M) src = a.x + (size_t)m * (K1 * SP) + sub * 64 + ch * 8;
+      } else {
+        int pin = m;                          // input pixel of output pixel m
+        if (a.stride != 1) {
+          const int b = m / a.HWo, rr = m - b * a.HWo;
+          const int oh = rr / a.Wo, ow = rr - oh * a.Wo;
+          pin = (b * a.H + oh * a.stride) * a.W + ow * a.stride;
+        }
+        const half_t* xs = K1 > 0 ? a.x2 : a.x;
+        if (m < a.M) src = xs + (size_t)pin * ((K - K1) * SP) + (sub - KC1) * 64 + ch * 8;
       }
-      const half_t* src = m < a.M ? a.x + (size_t)pin * PXH + sub * 64 + ch * 8 : zero;
       __builtin_amdgcn_global_load_lds((glb_void_c1*)src, (lds_void_c1*)(smem + buf * TILE + ins * 1024), 16, 0, 0);
     }
   };
@@ -299,7 +311,7 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   c1_vmcnt<0>();
 }
 
-template <int K, int NW, int BM, int CW, bool R, bool SPLIT = false>
+template <int K, int NW, int BM, int CW, bool R, bool SPLIT = false, int K1 = 0>
 static void c1s_cfg(C1sArgs a, hipStream_t st) {
   a.nslab = a.N / (NW * CW);
   constexpr int TILE = (SPLIT ? 2 : 1) * (K / 64) * BM * 128;
@@ -310,7 +322,7 @@ static void c1s_cfg(C1sArgs a, hipStream_t st) {
   const long items = (long)a.ntiles * a.nslab;
   if (G > items) G = (int)items;
   a.G = G;
-  auto kern = conv1x1_stream_kernel<K, NW, BM, CW, R, SPLIT>;
+  auto kern = conv1x1_stream_kernel<K, NW, BM, CW, R, SPLIT, K1>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), 2 * TILE);
   hipLaunchKernelGGL(kern, dim3(G), dim3(64 * NW), 2 * TILE, st, a);
 }
@@ -434,6 +446,37 @@ bool conv1x1_stream_split_launch(const half_t* x, const half_t* w, const float* 
     default:
       r ? c1s_cfg<512, 4, 16, 16, true, true>(a, st) : c1s_cfg<512, 4, 16, 16, false, true>(a, st);
   }
+  return true;
+}
+
+// dual input (ResNet bottleneck expansion + 1x1 downsample as one GEMM):
+// (K1, K2) = (64, 64) [layer1] or (128, 256) [layer2, downsample stride 2]
+bool conv1x1_dual_supported(int K1, int K2, int Cout, long M) {
+  const bool shape = (K1 == 64 && K2 == 64 && Cout % 256 == 0) || (K1 == 128 && K2 == 256 && Cout % 128 == 0);
+  return shape && M > 0 && (M + 64) * Cout * 2 < (1L << 31);
+}
+
+bool conv1x1_dual_launch(const half_t* x1, const half_t* x2, const half_t* w, const float* bias, half_t* y,
+                         const void* zero, int M, int K1, int K2, int Cout, int relu, int H, int W, int Wo, int HWo,
+                         int stride, hipStream_t st) {
+  if (!conv1x1_dual_supported(K1, K2, Cout, M)) return false;
+  C1sArgs a{};
+  a.x = x1;
+  a.x2 = x2;
+  a.w = w;
+  a.bias = bias;
+  a.y = y;
+  a.zero = zero;
+  a.M = M;
+  a.N = Cout;
+  a.relu = relu;
+  a.H = H;
+  a.W = W;
+  a.Wo = Wo;
+  a.HWo = HWo;
+  a.stride = stride;
+  if (K1 == 64) c1s_cfg<128, 4, 32, 64, false, false, 64>(a, st);
+  else c1s_cfg<384, 4, 32, 32, false, false, 128>(a, st);
   return true;
 }
 

@@ -539,6 +539,11 @@ class HipRunner:
         # profiles/r3_dual_downsample.md), so off by default
         self.fuse_down = False
         self._dual: dict = {}
+        # fp16 bottleneck blocks with a 1x1 downsample: the expansion 1x1 and the
+        # downsample as ONE GEMM over [y | x] (ops.conv1x1_dual), so the
+        # downsample's output (the residual) never reaches HBM
+        self.fuse_down_1x1 = True
+        self._dual1: dict = {}
         self.device = torch.device(device or "cuda")
         self.p = program.to(self.device)
         self._graphs: dict[int, tuple] = {}
@@ -756,11 +761,34 @@ class HipRunner:
             return self.ops.conv2d_wino(x, c.wino, c.b, c.relu, residual, var)
         return self.ops.conv2d(x, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu, residual=residual, out=out)
 
+    def _dual1_ok(self, blk, x, out) -> bool:
+        d, last = blk.down, blk.convs[-1]
+        if not (self.fuse_down_1x1 and out is None and d is not None and x.dtype == torch.float16 and x.is_cuda):
+            return False
+        if not (last.kh == last.kw == 1 and last.stride == 1 and last.pad == 0 and d.kh == d.kw == 1 and d.pad == 0
+                and not last.small and not d.small):
+            return False
+        ho = (x.shape[1] - 1) // d.stride + 1
+        return bool(self.ops.load().conv1x1_dual_ok(last.cin, d.cin, last.cout, x.shape[0] * ho * ho))
+
+    def _dual1_weights(self, blk):
+        key = id(blk)
+        if key not in self._dual1:
+            last, d = blk.convs[-1], blk.down
+            self._dual1[key] = (torch.cat([last.w, d.w], 1).contiguous(), (last.b + d.b).contiguous())
+        return self._dual1[key]
+
     def _block(self, blk, x, out=None):
         """One residual block; the last conv fuses +identity and ReLU (into ``out``).
         With ``side_down`` the 1x1 downsample conv runs on a second stream,
         concurrently with the block's first conv (a fork/join that hipGraph
         capture keeps as two parallel branches)."""
+        if self._dual1_ok(blk, x, out):
+            y = x
+            for c in blk.convs[:-1]:
+                y = self._conv(c, y)
+            w, b = self._dual1_weights(blk)
+            return self.ops.conv1x1_dual(y, x, w, b, blk.down.stride, blk.convs[-1].relu)
         idt = x
         join = None
         if blk.down is not None:
@@ -794,7 +822,7 @@ class HipRunner:
         """Kernel-choice switches a captured graph depends on (part of its cache key)."""
         return (self.split, self.split_front, self.split_streams, self.winograd, self.wino_variant, self.pack3,
                 self.pack3_f16, self.side_down, self.stem_parts, self.front_split, self.fuse_stem, self.batch_parts,
-                self.fuse_down)
+                self.fuse_down, self.fuse_down_1x1)
 
     def _split_ok(self) -> bool:
         p = self.p

@@ -13,7 +13,7 @@ __all__ = [
     "available", "load", "so_path", "conv2d", "linear", "preprocess", "resize_crop",
     "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile", "pick_tile_f32", "synth_images", "stem_fused",
     "conv2d_wino", "wino_supported", "preprocess_pack3", "conv2d_pack3",
-    "conv2d_split", "linear_split", "stem_split", "preprocess_pack3_split", "conv2d_pack3_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
+    "conv1x1_dual", "conv2d_split", "linear_split", "stem_split", "preprocess_pack3_split", "conv2d_pack3_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
 ]
 
 
@@ -110,6 +110,13 @@ def conv2d(x, w, bias, kh: int, kw: int, stride: int, pad: int, relu: bool,
     if x.dtype == torch.float32:
         return load().conv2d_nhwc_f32(x, w, bias, residual, kh, kw, stride, pad, relu, tile, out)
     return load().conv2d_nhwc(x, w, bias, residual, kh, kw, stride, pad, relu, out_f32, tile, out)
+
+
+def conv1x1_dual(x1, x2, w, bias, stride: int, relu: bool):
+    """ResNet bottleneck tail as one GEMM (fp16): act([x1 | x2 at stride] . w^T
+    + bias), w = [W_expand | W_downsample] (packed 1x1 weights side by side),
+    bias = b_expand + b_downsample."""
+    return load().conv1x1_dual(x1, x2, w, bias, stride, relu)
 
 
 def conv2d_wino(x, u, bias, relu: bool, residual=None, variant: int = 0):

@@ -115,6 +115,49 @@ def test_conv1x1_stream(ops, B, H, Cin, Cout, res, stride):
         assert (y.float() - y36.float()).abs().max().item() <= 2e-3 * (y36.float().abs().max().item() + 1)
 
 
+@pytest.mark.parametrize("B,Ho,K1,K2,Cout,s", [(2, 56, 64, 64, 256, 1), (3, 28, 128, 256, 512, 2), (1, 9, 64, 64, 512, 1),
+                                               (2, 13, 128, 256, 128, 2)])
+def test_conv1x1_dual(ops, B, Ho, K1, K2, Cout, s):
+    """Bottleneck expansion 1x1 + 1x1 downsample as one GEMM over [y | x]."""
+    from idunno.models.packed import pack_conv_weight
+
+    torch.manual_seed(B + Ho + K1 + K2 + Cout + s)
+    H = (Ho - 1) * s + 1 + (s - 1)
+    y = torch.randn(B, Ho, Ho, K1, device=DEV).half()
+    x = torch.randn(B, H, H, K2, device=DEV).half()
+    w3 = torch.randn(Cout, K1, 1, 1) / K1 ** 0.5
+    wd = torch.randn(Cout, K2, 1, 1) / K2 ** 0.5
+    b3, bd = torch.randn(Cout) * 0.1, torch.randn(Cout) * 0.1
+    p3, _ = pack_conv_weight(w3)
+    pd, _ = pack_conv_weight(wd)
+    w = torch.cat([p3, pd], 1).to(DEV).contiguous()
+    out = ops.conv1x1_dual(y, x, w, (b3 + bd).to(DEV), s, True)
+    ref = F.relu(_ref_conv(y, w3.half().float().to(DEV), b3.to(DEV), 1, 0, False)
+                 + _ref_conv(x, wd.half().float().to(DEV), bd.to(DEV), s, 0, False))
+    assert out.shape == ref.shape
+    _check(out, ref)
+
+
+def test_resnet50_fused_downsample_matches_unfused(ops):
+    from idunno.models import HipRunner, build_program
+
+    torch.manual_seed(0)
+    prog = build_program("resnet50", seed=0, randomize_bn=True)
+    img = ops.synth_images(7, 0, 6, torch.device(DEV))
+    outs = {}
+    for fuse in (False, True):
+        r = HipRunner(prog, DEV)
+        r.fuse_down_1x1 = fuse
+        outs[fuse] = r.logits(img).float()
+    scale = outs[False].abs().max().item()
+    assert (outs[True] - outs[False]).abs().max().item() <= 2e-2 * scale
+    # top-1 agrees wherever the unfused top-2 margin exceeds the fp16 noise (random
+    # init nets have near ties; the fused GEMM rounds the residual sum once, not twice)
+    top2 = outs[False].topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 2e-3 * scale
+    assert torch.equal(outs[True].argmax(1)[clear], outs[False].argmax(1)[clear])
+
+
 BIG_TILES = [60, 61, 62, 63, 65, 66, 67, 68, 69, 70, 71, 72, 73]
 
 
