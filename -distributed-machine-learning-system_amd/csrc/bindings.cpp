@@ -240,6 +240,44 @@ bool conv1x1_dual_ok(int64_t K1, int64_t K2, int64_t Cout, int64_t M) {
   return conv1x1_dual_supported((int)K1, (int)K2, (int)Cout, (long)M);
 }
 
+static int* split_guard_for(const torch::Device& dev);
+
+// split (fp32-accurate) form of conv1x1_dual: x1 [B, Ho, Wo, 2 K1], x2 [B, H, W, 2 K2]
+// split layouts, w [Cout, 2 (K1 + K2)] = pack_split_weight([W3 | Wds]) with one
+// accumulator scale; split output [B, Ho, Wo, 2 Cout] (range-guarded)
+torch::Tensor conv1x1_dual_split(torch::Tensor x1, torch::Tensor x2, torch::Tensor w, torch::Tensor bias,
+                                 double acc_scale, int64_t stride, bool relu) {
+  CHECK_DEV(x1); CHECK_DEV(x2); CHECK_DEV(w); CHECK_DEV(bias);
+  CHECK_CONTIG(x1); CHECK_CONTIG(x2); CHECK_CONTIG(w); CHECK_CONTIG(bias);
+  CHECK_DT(x1, torch::kHalf); CHECK_DT(x2, torch::kHalf); CHECK_DT(w, torch::kHalf); CHECK_DT(bias, torch::kFloat);
+  TORCH_CHECK(x1.dim() == 4 && x2.dim() == 4 && w.dim() == 2 && bias.dim() == 1, "bad ranks");
+  TORCH_CHECK(x2.device() == x1.device() && w.device() == x1.device() && bias.device() == x1.device(),
+              "operands on different devices");
+  TORCH_CHECK(stride >= 1, "bad stride");
+  const int B = x1.size(0), Ho = x1.size(1), Wo = x1.size(2), K1 = x1.size(3) / 2;
+  const int H = x2.size(1), W = x2.size(2), K2 = x2.size(3) / 2;
+  const int Cout = w.size(0);
+  TORCH_CHECK(x1.size(3) % 64 == 0 && x2.size(3) % 64 == 0, "split inputs need 2C halfs with C % 32 == 0");
+  TORCH_CHECK(x2.size(0) == B && (H - 1) / stride + 1 == Ho && (W - 1) / stride + 1 == Wo,
+              "x2 must be the block input at `stride` of x1's resolution");
+  TORCH_CHECK(w.size(1) == 2 * (K1 + K2) && bias.size(0) == Cout, "split weight must be [Cout, 2 (K1 + K2)]");
+  const long M = (long)B * Ho * Wo;
+  TORCH_CHECK(conv1x1_dual_split_supported(K1, K2, Cout, M), "conv1x1_dual_split: unsupported shape (K1 ", K1,
+              ", K2 ", K2, ", Cout ", Cout, ")");
+  auto y = torch::empty({B, Ho, Wo, 2 * Cout}, x1.options());
+  conv1x1_dual_split_launch(reinterpret_cast<const half_t*>(x1.data_ptr()),
+                            reinterpret_cast<const half_t*>(x2.data_ptr()), reinterpret_cast<const half_t*>(w.data_ptr()),
+                            bias.data_ptr<float>(), reinterpret_cast<half_t*>(y.data_ptr()),
+                            zero_buffer(x1.device()).data_ptr(), (int)M, K1, K2, Cout, relu ? 1 : 0, (float)acc_scale,
+                            split_guard_for(x1.device()), H, W, Wo, Ho * Wo, (int)stride, cur_stream());
+  check_launch("conv1x1_dual_split");
+  return y;
+}
+
+bool conv1x1_dual_split_ok(int64_t K1, int64_t K2, int64_t Cout, int64_t M) {
+  return conv1x1_dual_split_supported((int)K1, (int)K2, (int)Cout, (long)M);
+}
+
 // fp32 (reference precision) conv: y = act(conv(x, w) + bias (+ res)), all f32.
 //   x   : [B, H, W, C] f32 NHWC, C == 4 (RGB+0 stem) or C % 16 == 0
 //   w   : [Cout, Kpad] f32: big (kh, kw, c), Kpad = KH*KW*C;
@@ -1274,6 +1312,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_dual", &conv1x1_dual, "bottleneck expansion 1x1 + 1x1 downsample as one GEMM (fp16)",
         py::arg("x1"), py::arg("x2"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("relu"));
   m.def("conv1x1_dual_ok", &conv1x1_dual_ok, "whether conv1x1_dual supports (K1, K2, Cout, M)");
+  m.def("conv1x1_dual_split", &conv1x1_dual_split, "split (fp32-accurate) form of conv1x1_dual", py::arg("x1"),
+        py::arg("x2"), py::arg("w"), py::arg("bias"), py::arg("acc_scale"), py::arg("stride"), py::arg("relu"));
+  m.def("conv1x1_dual_split_ok", &conv1x1_dual_split_ok, "whether conv1x1_dual_split supports (K1, K2, Cout, M)");
   m.def("conv2d_nhwc", &conv2d_nhwc, "implicit-GEMM MFMA conv + bias (+res) (+relu)", py::arg("x"), py::arg("w"),
         py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("relu"), py::arg("out_f32") = false, py::arg("tile") = -1, py::arg("out") = py::none());

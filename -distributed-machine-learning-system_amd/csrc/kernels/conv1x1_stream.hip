@@ -480,4 +480,37 @@ bool conv1x1_dual_launch(const half_t* x1, const half_t* x2, const half_t* w, co
   return true;
 }
 
+// split (fp32-accurate) dual input: x1 [M][2 K1], x2 [..][2 K2] split layouts,
+// w = pack_split_weight([W3 | Wds]) (one scale), split output
+bool conv1x1_dual_split_supported(int K1, int K2, int Cout, long M) {
+  const bool shape = (K1 == 64 && K2 == 64 && Cout % 128 == 0) || (K1 == 128 && K2 == 256 && Cout % 64 == 0);
+  return shape && M > 0 && (M + 64) * Cout * 4 < (1L << 32);
+}
+
+bool conv1x1_dual_split_launch(const half_t* x1, const half_t* x2, const half_t* w, const float* bias, half_t* y,
+                               const void* zero, int M, int K1, int K2, int Cout, int relu, float acc_scale, int* ovf,
+                               int H, int W, int Wo, int HWo, int stride, hipStream_t st) {
+  if (!conv1x1_dual_split_supported(K1, K2, Cout, M)) return false;
+  C1sArgs a{};
+  a.x = x1;
+  a.x2 = x2;
+  a.w = w;
+  a.bias = bias;
+  a.y = y;
+  a.zero = zero;
+  a.M = M;
+  a.N = Cout;
+  a.relu = relu;
+  a.H = H;
+  a.W = W;
+  a.Wo = Wo;
+  a.HWo = HWo;
+  a.stride = stride;
+  a.acc_scale = acc_scale;
+  a.ovf = ovf;
+  if (K1 == 64) c1s_cfg<128, 4, 32, 32, false, true, 64>(a, st);
+  else c1s_cfg<384, 4, 16, 16, false, true, 128>(a, st);
+  return true;
+}
+
 }  // namespace idunno

@@ -877,11 +877,36 @@ class HipRunner:
             both = self.ops.conv2d_split_dual(x, w, b, c0.s_scale, d.s_scale, c0.cout, 3, 3, c0.stride, 1, True)
             y, idt = both[..., :2 * c0.cout], both[..., 2 * c0.cout:]
             return self._conv_split(blk.convs[1], y, residual=idt, out_f32=last, out=out)
+        if not last and out is None and self._dual1_split_ok(blk, x):
+            y = x
+            for c in blk.convs[:-1]:
+                y = self._conv_split(c, y)
+            w, b, scale = self._dual1_split_weights(blk)
+            return self.ops.conv1x1_dual_split(y, x, w, b, scale, blk.down.stride, blk.convs[-1].relu)
         idt = x if blk.down is None else self._conv_split(blk.down, x)
         y = x
         for c in blk.convs[:-1]:
             y = self._conv_split(c, y)
         return self._conv_split(blk.convs[-1], y, residual=idt, out_f32=last, out=out)
+
+    def _dual1_split_ok(self, blk, x) -> bool:
+        d, last = blk.down, blk.convs[-1]
+        if not (self.fuse_down_1x1 and d is not None and x.is_cuda and last.sw is not None and d.sw is not None):
+            return False
+        if not (last.kh == last.kw == 1 and last.stride == 1 and last.pad == 0 and d.kh == d.kw == 1 and d.pad == 0):
+            return False
+        ho = (x.shape[1] - 1) // d.stride + 1
+        return bool(self.ops.load().conv1x1_dual_split_ok(last.cin, d.cin, last.cout, x.shape[0] * ho * ho))
+
+    def _dual1_split_weights(self, blk):
+        """[W3 | Wds] re-packed as ONE split weight (one accumulator scale)."""
+        key = ("split", id(blk))
+        if key not in self._dual1:
+            last, d = blk.convs[-1], blk.down
+            w = torch.cat([unpack_split_weight(last).cpu(), unpack_split_weight(d).cpu()], 1)
+            sw, scale = pack_split_weight(w)
+            self._dual1[key] = (sw.to(self.device), (last.b + d.b).contiguous(), scale)
+        return self._dual1[key]
 
     def _split_part(self, img_u8, start, nb, start_offset, window, sub):
         """Whole split ResNet forward of images [sub, sub + nb) of the window."""

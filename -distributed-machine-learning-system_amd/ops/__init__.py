@@ -13,7 +13,7 @@ __all__ = [
     "available", "load", "so_path", "conv2d", "linear", "preprocess", "resize_crop",
     "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile", "pick_tile_f32", "synth_images", "stem_fused",
     "conv2d_wino", "wino_supported", "preprocess_pack3", "conv2d_pack3",
-    "conv1x1_dual", "conv2d_split", "linear_split", "stem_split", "preprocess_pack3_split", "conv2d_pack3_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
+    "conv1x1_dual", "conv1x1_dual_split", "conv2d_split", "linear_split", "stem_split", "preprocess_pack3_split", "conv2d_pack3_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
 ]
 
 
@@ -117,6 +117,12 @@ def conv1x1_dual(x1, x2, w, bias, stride: int, relu: bool):
     + bias), w = [W_expand | W_downsample] (packed 1x1 weights side by side),
     bias = b_expand + b_downsample."""
     return load().conv1x1_dual(x1, x2, w, bias, stride, relu)
+
+
+def conv1x1_dual_split(x1, x2, w, bias, acc_scale: float, stride: int, relu: bool):
+    """Split-fp16 (fp32-accurate) form of ``conv1x1_dual``: split activations,
+    w = pack_split_weight of [W_expand | W_downsample] (one ``acc_scale``)."""
+    return load().conv1x1_dual_split(x1, x2, w, bias, acc_scale, stride, relu)
 
 
 def conv2d_wino(x, u, bias, relu: bool, residual=None, variant: int = 0):

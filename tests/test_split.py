@@ -226,6 +226,41 @@ def test_conv_split_1x1_stream(ops, B, H, Cin, Cout, s, res):
         _check(P.from_split(y), _ref64(x, w, b, s, 0, relu, r))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,Ho,K1,K2,Cout,s", [(2, 56, 64, 64, 256, 1), (3, 28, 128, 256, 512, 2), (1, 9, 64, 64, 128, 1),
+                                               (2, 13, 128, 256, 64, 2)])
+def test_conv1x1_dual_split(ops, B, Ho, K1, K2, Cout, s):
+    """Split bottleneck tail: expansion 1x1 + (strided) 1x1 downsample as one GEMM, vs fp64."""
+    torch.manual_seed(B + Ho + K1 + K2 + Cout + s)
+    H = (Ho - 1) * s + 1 + (s - 1)
+    y = torch.randn(B, Ho, Ho, K1, device=DEV)
+    x = torch.randn(B, H, H, K2, device=DEV)
+    w3 = torch.randn(Cout, K1, 1, 1) / K1 ** 0.5
+    wd = torch.randn(Cout, K2, 1, 1) / K2 ** 0.5 * 0.1       # different magnitudes: one shared scale
+    b3, bd = torch.randn(Cout) * 0.1, torch.randn(Cout) * 0.1
+    sw, scale = P.pack_split_weight(torch.cat([w3, wd], 1))
+    out = ops.conv1x1_dual_split(ops.split_from_f32(y), ops.split_from_f32(x), sw.to(DEV), (b3 + bd).to(DEV), scale,
+                                 s, True)
+    assert out.shape == (B, Ho, Ho, 2 * Cout)
+    ref = torch.relu(_ref64(y, w3, b3, 1, 0, False) + _ref64(x, wd, bd, s, 0, False))
+    _check(P.from_split(out), ref)
+
+
+@pytest.mark.gpu
+def test_resnet50_split_fused_downsample_matches_unfused(ops):
+    from idunno.models import HipRunner, build_program
+
+    prog = build_program("resnet50", seed=0, randomize_bn=True, dtype="fp32")
+    img = ops.synth_images(11, 0, 4, torch.device(DEV))
+    outs = {}
+    for fuse in (False, True):
+        r = HipRunner(prog, DEV)
+        r.fuse_down_1x1 = fuse
+        outs[fuse] = r.logits(img).double()
+    scale = outs[False].abs().max().item()
+    assert (outs[True] - outs[False]).abs().max().item() <= 2e-5 * scale
+
+
 SPLIT_TILES = [26, 27, 34, 36, 38, 42]
 
 
