@@ -242,6 +242,59 @@ bool conv1x1_dual_ok(int64_t K1, int64_t K2, int64_t Cout, int64_t M) {
 
 static int* split_guard_for(const torch::Device& dev);
 
+// Bottleneck tail + the NEXT block's reduce 1x1 in one pass (fp16, layer1 of
+// ResNet50): y = relu(x1 . W^T + b + res) -- or, with x2, the dual form
+// relu([x1 | x2] . W^T + b) -- and z = relu(y . w2^T + b2) from the output tile
+// on chip.  Returns [y, z].
+std::vector<torch::Tensor> conv1x1_fused_next(torch::Tensor x1, c10::optional<torch::Tensor> x2, torch::Tensor w,
+                                              torch::Tensor bias, c10::optional<torch::Tensor> res, torch::Tensor w2,
+                                              torch::Tensor b2, int64_t stride, bool relu) {
+  CHECK_DEV(x1); CHECK_DEV(w); CHECK_DEV(bias); CHECK_DEV(w2); CHECK_DEV(b2);
+  CHECK_CONTIG(x1); CHECK_CONTIG(w); CHECK_CONTIG(bias); CHECK_CONTIG(w2); CHECK_CONTIG(b2);
+  CHECK_DT(x1, torch::kHalf); CHECK_DT(w, torch::kHalf); CHECK_DT(bias, torch::kFloat);
+  CHECK_DT(w2, torch::kHalf); CHECK_DT(b2, torch::kFloat);
+  TORCH_CHECK(x1.dim() == 4 && w.dim() == 2 && w2.dim() == 2, "bad ranks");
+  const int B = x1.size(0), Ho = x1.size(1), Wo = x1.size(2), K1 = x1.size(3);
+  const int N = w.size(0), N2 = w2.size(0);
+  const half_t* x2p = nullptr;
+  int H = Ho, W = Wo, K2 = 0;
+  if (x2.has_value() && x2->defined()) {
+    auto& t = *x2;
+    CHECK_DEV(t); CHECK_CONTIG(t); CHECK_DT(t, torch::kHalf);
+    TORCH_CHECK(t.dim() == 4 && t.size(0) == B, "x2 must be [B, H, W, K2]");
+    H = t.size(1); W = t.size(2); K2 = t.size(3);
+    TORCH_CHECK((H - 1) / stride + 1 == Ho && (W - 1) / stride + 1 == Wo, "x2 must be at `stride` of x1's resolution");
+    x2p = reinterpret_cast<const half_t*>(t.data_ptr());
+  }
+  TORCH_CHECK(w.size(1) == K1 + K2 && bias.size(0) == N && w2.size(1) == N && b2.size(0) == N2, "weight shapes");
+  const half_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    auto& r = *res;
+    CHECK_DEV(r); CHECK_CONTIG(r); CHECK_DT(r, torch::kHalf);
+    TORCH_CHECK(r.dim() == 4 && r.size(0) == B && r.size(1) == Ho && r.size(2) == Wo && r.size(3) == N,
+                "residual shape mismatch");
+    TORCH_CHECK(x2p == nullptr, "the dual form carries its residual as the second GEMM input");
+    rp = reinterpret_cast<const half_t*>(r.data_ptr());
+  }
+  const long M = (long)B * Ho * Wo;
+  TORCH_CHECK(conv1x1_fused_next_supported(K1, K2, N, N2, M), "conv1x1_fused_next: unsupported shape");
+  auto y = torch::empty({B, Ho, Wo, N}, x1.options());
+  auto z = torch::empty({B, Ho, Wo, N2}, x1.options());
+  conv1x1_fused_next_launch(reinterpret_cast<const half_t*>(x1.data_ptr()), x2p,
+                            reinterpret_cast<const half_t*>(w.data_ptr()), bias.data_ptr<float>(), rp,
+                            reinterpret_cast<half_t*>(y.data_ptr()), reinterpret_cast<const half_t*>(w2.data_ptr()),
+                            b2.data_ptr<float>(), reinterpret_cast<half_t*>(z.data_ptr()),
+                            zero_buffer(x1.device()).data_ptr(), (int)M, K1, K2, N, N2, relu ? 1 : 0, H, W, Wo,
+                            Ho * Wo, (int)stride, cur_stream());
+  check_launch("conv1x1_fused_next");
+  return {y, z};
+}
+
+bool conv1x1_fused_next_ok(int64_t K1, int64_t K2, int64_t N, int64_t N2, int64_t M) {
+  return conv1x1_fused_next_supported((int)K1, (int)K2, (int)N, (int)N2, (long)M);
+}
+
+
 // split (fp32-accurate) form of conv1x1_dual: x1 [B, Ho, Wo, 2 K1], x2 [B, H, W, 2 K2]
 // split layouts, w [Cout, 2 (K1 + K2)] = pack_split_weight([W3 | Wds]) with one
 // accumulator scale; split output [B, Ho, Wo, 2 Cout] (range-guarded)
@@ -1312,6 +1365,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_dual", &conv1x1_dual, "bottleneck expansion 1x1 + 1x1 downsample as one GEMM (fp16)",
         py::arg("x1"), py::arg("x2"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("relu"));
   m.def("conv1x1_dual_ok", &conv1x1_dual_ok, "whether conv1x1_dual supports (K1, K2, Cout, M)");
+  m.def("conv1x1_fused_next", &conv1x1_fused_next, "bottleneck tail + next block's reduce 1x1 in one pass (fp16)",
+        py::arg("x1"), py::arg("x2"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("w2"), py::arg("b2"),
+        py::arg("stride"), py::arg("relu"));
+  m.def("conv1x1_fused_next_ok", &conv1x1_fused_next_ok, "whether conv1x1_fused_next supports (K1, K2, N, N2, M)");
   m.def("conv1x1_dual_split", &conv1x1_dual_split, "split (fp32-accurate) form of conv1x1_dual", py::arg("x1"),
         py::arg("x2"), py::arg("w"), py::arg("bias"), py::arg("acc_scale"), py::arg("stride"), py::arg("relu"));
   m.def("conv1x1_dual_split_ok", &conv1x1_dual_split_ok, "whether conv1x1_dual_split supports (K1, K2, Cout, M)");

@@ -161,6 +161,11 @@ bool conv1x1_dual_split_supported(int K1, int K2, int Cout, long M);
 bool conv1x1_dual_split_launch(const half_t* x1, const half_t* x2, const half_t* w, const float* bias, half_t* y,
                                const void* zero, int M, int K1, int K2, int Cout, int relu, float acc_scale, int* ovf,
                                int H, int W, int Wo, int HWo, int stride, hipStream_t st);
+bool conv1x1_fused_next_supported(int K1, int K2, int N, int N2, long M);   // + next block's reduce 1x1
+bool conv1x1_fused_next_launch(const half_t* x1, const half_t* x2, const half_t* w, const float* bias,
+                               const half_t* res, half_t* y, const half_t* w2, const float* b2, half_t* z,
+                               const void* zero, int M, int K1, int K2, int N, int N2, int relu, int H, int W, int Wo,
+                               int HWo, int stride, hipStream_t st);
 void set_conv1x1_stream_split_mask(int mask);   // default shapes of the split path (bits as the fp16 mask)
 bool conv1x1_stream_split_default(int C, int stride);
 void set_c64_split_variant(int v);  // layer1 split kernel: 0 = 16 couts/wave, 2/3 = 32 couts/wave (read ring depth)

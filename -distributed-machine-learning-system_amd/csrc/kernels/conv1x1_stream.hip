@@ -48,7 +48,17 @@ struct C1sArgs {
   int H, W, Wo, HWo, stride;   // stride 2: output pixel m reads input pixel (b, 2 oh, 2 ow)
   float acc_scale;      // SPLIT: accumulator multiplier 2^-e of the pre-scaled split weights
   int* ovf;             // SPLIT: range guard flag (common.h split_guard) or nullptr
+  // N2 > 0 (fused next 1x1): z = relu(y . w2^T + b2), y the fp16 output tile
+  const half_t* w2;     // [N2][N]
+  const float* b2;      // [N2]
+  half_t* z;            // [M][N2]
 };
+
+// ds_write_b64 outside the wait-count pass (a compiler LDS store after the
+// next tile's LDS-DMA would get a vmcnt(0) in front of it)
+__device__ __forceinline__ void c1_lds_write_b64(uint32_t addr, half4v v) {
+  asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
 
 typedef int int4s __attribute__((ext_vector_type(4)));
 
@@ -83,7 +93,12 @@ __device__ __forceinline__ void c1_vmcnt() {
 // output resolution, stride 1) and [K1, K) from x2 (stride `stride`): a
 // ResNet bottleneck's expansion 1x1 and its 1x1 downsample as one GEMM
 // (W3 | Wds) . (y | x) + (b3 + bds): the downsample's output never reaches HBM.
-template <int K, int NW, int BM, int CW, bool HAS_RES, bool SPLIT = false, int K1 = 0>
+// N2 > 0 (fp16, the whole output row N = NW * CW in one workgroup): the NEXT
+// bottleneck block's reduce 1x1 (N -> N2, ReLU) runs on the output tile while
+// it is on chip -- the tile is also written to LDS (fp16, exactly the values
+// stored), and each wave computes N2 / NW of its channels -- so the next block
+// never re-reads this block's 4x-wide output.
+template <int K, int NW, int BM, int CW, bool HAS_RES, bool SPLIT = false, int K1 = 0, int N2 = 0>
 __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: min waves per SIMD
 (const C1sArgs a) {
   // BM pixels per tile: 64, or 32 for K = 128 (whose 64 A-fragment registers
@@ -100,7 +115,11 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   constexpr int NINS = TILE / 1024;      // DMA instructions per tile
   static_assert(NINS % NW == 0, "DMA instructions split evenly over the waves");
   constexpr int GX = NINS / NW;          // per wave
-  constexpr int GS = FN * FM * SP;       // epilogue stores per wave and item
+  constexpr int NY = NW * CW;             // output channels of a workgroup
+  constexpr int CW2 = N2 / NW, FN2 = N2 ? CW2 / 16 : 1, KK2 = NY / 32;
+  static_assert(N2 == 0 || (!SPLIT && CW2 % 16 == 0), "fused next 1x1: fp16, N2 a multiple of 16 * NW");
+  constexpr int YROW = NY * 2;            // bytes per pixel row of the LDS output tile
+  constexpr int GS = FN * FM * SP + (N2 ? FN2 * FM : 0);   // stores per wave and item (y, z)
   constexpr int GR = HAS_RES ? FN * FM * SP : 0;
   static_assert(GS + GX + GR < 64, "vmcnt immediate");
 
@@ -130,6 +149,18 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
                                  : half8v{0, 0, 0, 0, 0, 0, 0, 0};
     const int n = nw0 + i * 16 + fch * 4;
     bv[i] = n < a.N ? *reinterpret_cast<const float4v*>(a.bias + n) : float4v{0.f, 0.f, 0.f, 0.f};
+  }
+  // fused next 1x1: this wave's N2/NW output channels, weights resident
+  half8v fa2[N2 ? FN2 : 1][N2 ? KK2 : 1];
+  float4v bv2[N2 ? FN2 : 1];
+  if constexpr (N2 > 0) {
+#pragma unroll
+    for (int i = 0; i < FN2; ++i) {
+      const int row = wave * CW2 + i * 16 + frow;
+#pragma unroll
+      for (int kk = 0; kk < KK2; ++kk) fa2[i][kk] = *reinterpret_cast<const half8v*>(a.w2 + (size_t)row * NY + kk * 32 + fch * 8);
+      bv2[i] = *reinterpret_cast<const float4v*>(a.b2 + wave * CW2 + i * 16 + fch * 4);
+    }
   }
   const half_t* zero = static_cast<const half_t*>(a.zero);
   constexpr int OPX = SPLIT ? 2 : 1;     // output / residual halfs per channel
@@ -200,6 +231,9 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   issue_x(t, 0);
   load_res(t, std::integral_constant<int, 0>{});
   const uint32_t lds0 = lds_addr(smem);
+  const uint32_t ytile = lds0 + 2 * TILE;    // fused next 1x1: the output tile (BM x NY fp16)
+  const auto z_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.z, 0, (int)((unsigned)a.M * (unsigned)(N2 * 2)), 0x00020000);
+  const uint32_t lane_off2 = (uint32_t)((frow * N2 + wave * CW2 + 4 * fch) * 2);
   bool first = true;
   // one item; BUF (the ring half and residual register set of tile t) is a
   // template constant so rv never needs runtime indexing (it went to scratch)
@@ -299,6 +333,51 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = (half_t)v[e];
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_c1, o), out_rsrc, voff, (int)soff, 0);
+          if constexpr (N2 > 0) {
+            // output tile -> LDS [pixel][NY] fp16, 16-byte chunk c of pixel row p at c ^ (p & 15)
+            const int p = j * 16 + frow, c = (wave * CW + i * 16 + 4 * fch) >> 3;
+            c1_lds_write_b64(ytile + p * YROW + ((c ^ (p & 15)) << 4) + (fch & 1) * 8, o);
+          }
+        }
+      }
+    }
+    if constexpr (N2 > 0) {
+      // ---- fused next 1x1: z = relu(y_tile . w2^T + b2) ----
+      lds_waitcnt<0>();
+      __builtin_amdgcn_s_barrier();       // the whole output tile is in LDS
+      float4v acc2[FN2][FM];
+#pragma unroll
+      for (int i = 0; i < FN2; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc2[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK2; ++kk) {
+        half8v fb2[FM];
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          const int p = j * 16 + frow, c = 4 * kk + fch;
+          fb2[j] = lds_read_b128(ytile + p * YROW + ((c ^ (p & 15)) << 4));
+        }
+        lds_waitcnt<0>();
+#pragma unroll
+        for (int j = 0; j < FM; ++j) lds_tie(fb2[j]);
+#pragma unroll
+        for (int i = 0; i < FN2; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j)
+            acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa2[i][kk], fb2[j], acc2[i][j], 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const uint32_t soff2 = (uint32_t)(t * BM + j * 16) * (uint32_t)(N2 * 2);
+#pragma unroll
+        for (int i = 0; i < FN2; ++i) {
+          const float4v v = acc2[i][j] + bv2[i];
+          half4v o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (half_t)fmaxf(v[e], 0.f);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_c1, o), z_rsrc, (int)lane_off2 + 32 * i,
+                                                (int)soff2, 0);
         }
       }
     }
@@ -311,10 +390,11 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   c1_vmcnt<0>();
 }
 
-template <int K, int NW, int BM, int CW, bool R, bool SPLIT = false, int K1 = 0>
+template <int K, int NW, int BM, int CW, bool R, bool SPLIT = false, int K1 = 0, int N2 = 0>
 static void c1s_cfg(C1sArgs a, hipStream_t st) {
   a.nslab = a.N / (NW * CW);
   constexpr int TILE = (SPLIT ? 2 : 1) * (K / 64) * BM * 128;
+  constexpr int LDSB = 2 * TILE + (N2 ? BM * NW * CW * 2 : 0);
   a.ntiles = (a.M + BM - 1) / BM;
   const int per_cu = 8 / NW;                        // two waves per SIMD
   int G = per_cu * device_cu_count();
@@ -322,9 +402,9 @@ static void c1s_cfg(C1sArgs a, hipStream_t st) {
   const long items = (long)a.ntiles * a.nslab;
   if (G > items) G = (int)items;
   a.G = G;
-  auto kern = conv1x1_stream_kernel<K, NW, BM, CW, R, SPLIT, K1>;
-  ensure_lds_attr(reinterpret_cast<const void*>(kern), 2 * TILE);
-  hipLaunchKernelGGL(kern, dim3(G), dim3(64 * NW), 2 * TILE, st, a);
+  auto kern = conv1x1_stream_kernel<K, NW, BM, CW, R, SPLIT, K1, N2>;
+  ensure_lds_attr(reinterpret_cast<const void*>(kern), LDSB);
+  hipLaunchKernelGGL(kern, dim3(G), dim3(64 * NW), LDSB, st, a);
 }
 
 bool conv1x1_stream_supported(int C, int Cout, long M) {
@@ -510,6 +590,49 @@ bool conv1x1_dual_split_launch(const half_t* x1, const half_t* x2, const half_t*
   a.ovf = ovf;
   if (K1 == 64) c1s_cfg<128, 4, 32, 32, false, true, 64>(a, st);
   else c1s_cfg<384, 4, 16, 16, false, true, 128>(a, st);
+  return true;
+}
+
+// ResNet50 layer1 bottleneck tail + the NEXT block's reduce 1x1, fp16, one pass:
+//   y = relu(x1 . W^T + b (+ res)), or the dual form relu([x1 | x2 at stride] . W^T + b);
+//   z = relu(y . w2^T + b2)  (N = 256, N2 = 64 or 128)
+bool conv1x1_fused_next_supported(int K1, int K2, int N, int N2, long M) {
+  // (the dual form with N2 = 128 spills and is no ResNet50 shape: layer1 block 0 feeds a 64-channel reduce)
+  return N == 256 && M > 0 && (M + 64) * N * 2 < (1L << 31) && K1 == 64 &&
+         ((K2 == 0 && (N2 == 64 || N2 == 128)) || (K2 == 64 && N2 == 64));
+}
+
+bool conv1x1_fused_next_launch(const half_t* x1, const half_t* x2, const half_t* w, const float* bias,
+                               const half_t* res, half_t* y, const half_t* w2, const float* b2, half_t* z,
+                               const void* zero, int M, int K1, int K2, int N, int N2, int relu, int H, int W, int Wo,
+                               int HWo, int stride, hipStream_t st) {
+  if (!conv1x1_fused_next_supported(K1, K2, N, N2, M)) return false;
+  C1sArgs a{};
+  a.x = x1;
+  a.x2 = x2;
+  a.w = w;
+  a.bias = bias;
+  a.res = res;
+  a.y = y;
+  a.zero = zero;
+  a.M = M;
+  a.N = N;
+  a.relu = relu;
+  a.H = H;
+  a.W = W;
+  a.Wo = Wo;
+  a.HWo = HWo;
+  a.stride = stride;
+  a.w2 = w2;
+  a.b2 = b2;
+  a.z = z;
+  const bool r = res != nullptr;
+  if (K2 == 0) {
+    if (N2 == 64) r ? c1s_cfg<64, 4, 32, 64, true, false, 0, 64>(a, st) : c1s_cfg<64, 4, 32, 64, false, false, 0, 64>(a, st);
+    else r ? c1s_cfg<64, 4, 32, 64, true, false, 0, 128>(a, st) : c1s_cfg<64, 4, 32, 64, false, false, 0, 128>(a, st);
+  } else {
+    c1s_cfg<128, 4, 32, 64, false, false, 64, 64>(a, st);
+  }
   return true;
 }
 

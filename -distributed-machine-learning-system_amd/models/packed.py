@@ -544,6 +544,9 @@ class HipRunner:
         # downsample's output (the residual) never reaches HBM
         self.fuse_down_1x1 = True
         self._dual1: dict = {}
+        # fp16 ResNet50 layer1: a block's tail kernel also computes the next
+        # block's reduce 1x1 from its output tile on chip (ops.conv1x1_fused_next)
+        self.fuse_next_1x1 = True
         self.device = torch.device(device or "cuda")
         self.p = program.to(self.device)
         self._graphs: dict[int, tuple] = {}
@@ -634,8 +637,7 @@ class HipRunner:
             else:
                 x = o.conv2d(x, s.w, s.b, s.kh, s.kw, s.stride, s.pad, s.relu)
                 x = o.maxpool2d(x, 3, 2, 1)
-            for blk in p.blocks[nfront:]:
-                x = self._block(blk, x)
+            x = self._blocks(p.blocks[nfront:], x)
             x = o.global_avgpool(x)
         else:
             for k, v in p.features[1:] if p3 else p.features:
@@ -761,6 +763,57 @@ class HipRunner:
             return self.ops.conv2d_wino(x, c.wino, c.b, c.relu, residual, var)
         return self.ops.conv2d(x, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu, residual=residual, out=out)
 
+    def _blocks(self, blocks, x):
+        """fp16 residual stages; with ``fuse_next_1x1`` a bottleneck block whose
+        successor starts with a 1x1 reduce hands that conv's output over from
+        its own tail kernel (ops.conv1x1_fused_next), and the successor skips it."""
+        pre = None
+        for i, blk in enumerate(blocks):
+            nxt = blocks[i + 1] if i + 1 < len(blocks) else None
+            x, pre = self._block_next(blk, x, pre, nxt)
+        return x
+
+    def _next_ok(self, blk, x, nxt) -> tuple | None:
+        """(K2, stride) of a fusable tail + next reduce, else None."""
+        if not (self.fuse_next_1x1 and nxt is not None and x.dtype == torch.float16 and x.is_cuda):
+            return None
+        last, d, r = blk.convs[-1], blk.down, nxt.convs[0]
+        if not (last.kh == last.kw == 1 and last.stride == 1 and last.pad == 0 and r.kh == r.kw == 1
+                and r.stride == 1 and r.pad == 0 and r.relu and last.relu and r.cin == last.cout):
+            return None
+        k2, stride = 0, 1
+        if d is not None:
+            if not (self.fuse_down_1x1 and d.kh == d.kw == 1 and d.pad == 0):
+                return None
+            k2, stride = d.cin, d.stride
+        ho = (x.shape[1] - 1) // stride + 1
+        ok = self.ops.load().conv1x1_fused_next_ok(last.cin, k2, last.cout, r.cout, x.shape[0] * ho * ho)
+        return (k2, stride) if ok else None
+
+    def _block_next(self, blk, x, pre, nxt):
+        """(block output, the next block's first-conv output or None); ``pre`` =
+        this block's first-conv output, already computed by the previous tail."""
+        fused = self._next_ok(blk, x, nxt)
+        if pre is None and fused is None:
+            return self._block(blk, x), None
+        y = pre if pre is not None else self._conv(blk.convs[0], x)
+        for c in blk.convs[1:-1]:
+            y = self._conv(c, y)
+        if fused is None:
+            last = blk.convs[-1]
+            if self._dual1_ok(blk, x, None):
+                w, b = self._dual1_weights(blk)
+                return self.ops.conv1x1_dual(y, x, w, b, blk.down.stride, last.relu), None
+            idt = x if blk.down is None else self._conv(blk.down, x)
+            return self._conv(last, y, residual=idt), None
+        r = nxt.convs[0]
+        if blk.down is not None:
+            w, b = self._dual1_weights(blk)
+            out, z = self.ops.conv1x1_fused_next(y, w, b, r.w, r.b, x2=x, stride=fused[1])
+        else:
+            out, z = self.ops.conv1x1_fused_next(y, blk.convs[-1].w, blk.convs[-1].b, r.w, r.b, residual=x)
+        return out, z
+
     def _dual1_ok(self, blk, x, out) -> bool:
         d, last = blk.down, blk.convs[-1]
         if not (self.fuse_down_1x1 and out is None and d is not None and x.dtype == torch.float16 and x.is_cuda):
@@ -822,7 +875,7 @@ class HipRunner:
         """Kernel-choice switches a captured graph depends on (part of its cache key)."""
         return (self.split, self.split_front, self.split_streams, self.winograd, self.wino_variant, self.pack3,
                 self.pack3_f16, self.side_down, self.stem_parts, self.front_split, self.fuse_stem, self.batch_parts,
-                self.fuse_down, self.fuse_down_1x1)
+                self.fuse_down, self.fuse_down_1x1, self.fuse_next_1x1)
 
     def _split_ok(self) -> bool:
         p = self.p

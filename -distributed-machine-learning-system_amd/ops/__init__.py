@@ -13,7 +13,7 @@ __all__ = [
     "available", "load", "so_path", "conv2d", "linear", "preprocess", "resize_crop",
     "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile", "pick_tile_f32", "synth_images", "stem_fused",
     "conv2d_wino", "wino_supported", "preprocess_pack3", "conv2d_pack3",
-    "conv1x1_dual", "conv1x1_dual_split", "conv2d_split", "linear_split", "stem_split", "preprocess_pack3_split", "conv2d_pack3_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
+    "conv1x1_dual", "conv1x1_dual_split", "conv1x1_fused_next", "conv2d_split", "linear_split", "stem_split", "preprocess_pack3_split", "conv2d_pack3_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
 ]
 
 
@@ -117,6 +117,15 @@ def conv1x1_dual(x1, x2, w, bias, stride: int, relu: bool):
     + bias), w = [W_expand | W_downsample] (packed 1x1 weights side by side),
     bias = b_expand + b_downsample."""
     return load().conv1x1_dual(x1, x2, w, bias, stride, relu)
+
+
+def conv1x1_fused_next(x1, w, bias, w2, b2, residual=None, x2=None, stride: int = 1, relu: bool = True):
+    """Bottleneck tail and the next block's reduce 1x1 in one pass (fp16):
+    y = act(x1 . w^T + bias + residual) -- or with ``x2`` (block input, at
+    ``stride``) the dual form act([x1 | x2] . w^T + bias) -- and
+    z = relu(y . w2^T + b2).  Returns (y, z)."""
+    y, z = load().conv1x1_fused_next(x1, x2, w, bias, residual, w2, b2, stride, relu)
+    return y, z
 
 
 def conv1x1_dual_split(x1, x2, w, bias, acc_scale: float, stride: int, relu: bool):

@@ -138,6 +138,51 @@ def test_conv1x1_dual(ops, B, Ho, K1, K2, Cout, s):
     _check(out, ref)
 
 
+@pytest.mark.parametrize("B,H,N2,dual", [(2, 56, 64, False), (3, 20, 128, False), (2, 56, 64, True), (1, 9, 64, True)])
+def test_conv1x1_fused_next(ops, B, H, N2, dual):
+    """Bottleneck tail (residual or dual form) + the next block's reduce 1x1 from the on-chip tile."""
+    from idunno.models.packed import pack_conv_weight
+
+    torch.manual_seed(B + H + N2 + dual)
+    y = torch.randn(B, H, H, 64, device=DEV).half()
+    x = torch.randn(B, H, H, 64 if dual else 256, device=DEV).half()
+    w3 = torch.randn(256, 64, 1, 1) / 8
+    b3 = torch.randn(256) * 0.1
+    w2 = torch.randn(N2, 256, 1, 1) / 16
+    b2 = torch.randn(N2) * 0.1
+    p3, _ = pack_conv_weight(w3)
+    p2, _ = pack_conv_weight(w2)
+    if dual:
+        wd = torch.randn(256, 64, 1, 1) / 8
+        bd = torch.randn(256) * 0.1
+        pd, _ = pack_conv_weight(wd)
+        out, z = ops.conv1x1_fused_next(y, torch.cat([p3, pd], 1).to(DEV).contiguous(), (b3 + bd).to(DEV),
+                                        p2.to(DEV), b2.to(DEV), x2=x)
+        ref = F.relu(_ref_conv(y, w3.half().float().to(DEV), b3.to(DEV), 1, 0, False)
+                     + _ref_conv(x, wd.half().float().to(DEV), bd.to(DEV), 1, 0, False))
+    else:
+        out, z = ops.conv1x1_fused_next(y, p3.to(DEV), b3.to(DEV), p2.to(DEV), b2.to(DEV), residual=x)
+        ref = _ref_conv(y, w3.half().float().to(DEV), b3.to(DEV), 1, 0, True, x)
+    _check(out, ref)
+    # z is exactly the reduce conv of the stored (fp16) output
+    z_ref = ops.conv2d(out, p2.to(DEV), b2.to(DEV), 1, 1, 1, 0, True, tile=36)
+    assert (z.float() - z_ref.float()).abs().max().item() <= 2e-3 * (z_ref.float().abs().max().item() + 1)
+
+
+def test_resnet50_fused_next_matches_unfused(ops):
+    from idunno.models import HipRunner, build_program
+
+    prog = build_program("resnet50", seed=0, randomize_bn=True)
+    img = ops.synth_images(5, 0, 6, torch.device(DEV))
+    outs = {}
+    for fuse in (False, True):
+        r = HipRunner(prog, DEV)
+        r.fuse_next_1x1 = fuse
+        outs[fuse] = r.logits(img).float()
+    scale = outs[False].abs().max().item()
+    assert (outs[True] - outs[False]).abs().max().item() <= 1e-2 * scale
+
+
 def test_resnet50_fused_downsample_matches_unfused(ops):
     from idunno.models import HipRunner, build_program
 
