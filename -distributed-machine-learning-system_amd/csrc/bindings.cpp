@@ -1414,6 +1414,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "A/B: shapes that take the streaming 1x1 kernel by default (1 Cin<=128, 2 Cin 256, 4 Cin 512, 8 stride 2)");
   m.def("set_conv1x1_stream_split_mask", &set_conv1x1_stream_split_mask,
         "A/B: split-path shapes that take the streaming 1x1 kernel by default (bits as set_conv1x1_stream_mask)");
+  m.def("set_conv1x1_split_wide", &set_conv1x1_split_wide, "A/B: 64 couts per wave for split Cin 64 / 128 1x1 convs");
   m.def("set_c64_split_variant", &set_c64_split_variant,
         "layer1 split 3x3 64->64 kernel: 0 = 16 couts per wave (2 workgroups/CU), 2 / 3 = 32 couts per wave");
   m.def("c64_split_variant", &c64_split_variant, "current layer1 split kernel variant");

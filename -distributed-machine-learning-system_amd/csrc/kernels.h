@@ -166,7 +166,8 @@ bool conv1x1_fused_next_launch(const half_t* x1, const half_t* x2, const half_t*
                                const half_t* res, half_t* y, const half_t* w2, const float* b2, half_t* z,
                                const void* zero, int M, int K1, int K2, int N, int N2, int relu, int H, int W, int Wo,
                                int HWo, int stride, hipStream_t st);
-void set_conv1x1_stream_split_mask(int mask);   // default shapes of the split path (bits as the fp16 mask)
+void set_conv1x1_stream_split_mask(int mask);
+void set_conv1x1_split_wide(bool on);   // A/B: 64 couts per wave for split Cin 64 / 128, Cout % 256 == 0   // default shapes of the split path (bits as the fp16 mask)
 bool conv1x1_stream_split_default(int C, int stride);
 void set_c64_split_variant(int v);  // layer1 split kernel: 0 = 16 couts/wave, 2/3 = 32 couts/wave (read ring depth)
 int c64_split_variant();

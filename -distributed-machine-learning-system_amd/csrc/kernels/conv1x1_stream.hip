@@ -481,6 +481,9 @@ bool conv1x1_stream_split_supported(int C, int Cout, long M) {
 // default shapes of the split path: bit 0 Cin <= 128, bit 1 Cin 256, bit 2 Cin 512, bit 3 stride 2
 // (all on: ResNet50 b1024 split +9.4 %, ResNet18 b400 split +0.5 %, profiles/r3_conv1x1_stream.md)
 static int g_c1s_split_mask = 15;
+// on: ResNet50 b1024 split +2.5 % (profiles/r3_conv1x1_stream_ab_split.log)
+static bool g_c1s_split_wide = true;
+void set_conv1x1_split_wide(bool on) { g_c1s_split_wide = on; }
 void set_conv1x1_stream_split_mask(int mask) { g_c1s_split_mask = mask; }
 bool conv1x1_stream_split_default(int C, int stride) {
   if (stride != 1 && !(g_c1s_split_mask & 8)) return false;
@@ -511,13 +514,18 @@ bool conv1x1_stream_split_launch(const half_t* x, const half_t* w, const float* 
   a.ovf = ovf;
   const bool r = res != nullptr;
   const bool narrow = C == 512 || Cout == 64;
+  // wide: 64 couts per wave (256-channel slabs: 4x the bytes per item, the input
+  // tile read once per 256 outputs) for Cin 64 / 128
+  const bool wide = g_c1s_split_wide && Cout % 256 == 0;
   switch (C) {
     case 64:
       if (narrow) r ? c1s_cfg<64, 4, 32, 16, true, true>(a, st) : c1s_cfg<64, 4, 32, 16, false, true>(a, st);
+      else if (wide) r ? c1s_cfg<64, 4, 32, 64, true, true>(a, st) : c1s_cfg<64, 4, 32, 64, false, true>(a, st);
       else r ? c1s_cfg<64, 4, 32, 32, true, true>(a, st) : c1s_cfg<64, 4, 32, 32, false, true>(a, st);
       break;
     case 128:
-      r ? c1s_cfg<128, 4, 32, 32, true, true>(a, st) : c1s_cfg<128, 4, 32, 32, false, true>(a, st);
+      if (wide) r ? c1s_cfg<128, 4, 16, 64, true, true>(a, st) : c1s_cfg<128, 4, 16, 64, false, true>(a, st);
+      else r ? c1s_cfg<128, 4, 32, 32, true, true>(a, st) : c1s_cfg<128, 4, 32, 32, false, true>(a, st);
       break;
     case 256:
       if (narrow) r ? c1s_cfg<256, 4, 32, 16, true, true>(a, st) : c1s_cfg<256, 4, 32, 16, false, true>(a, st);
@@ -588,7 +596,8 @@ bool conv1x1_dual_split_launch(const half_t* x1, const half_t* x2, const half_t*
   a.stride = stride;
   a.acc_scale = acc_scale;
   a.ovf = ovf;
-  if (K1 == 64) c1s_cfg<128, 4, 32, 32, false, true, 64>(a, st);
+  if (K1 == 64 && g_c1s_split_wide && Cout % 256 == 0) c1s_cfg<128, 4, 16, 64, false, true, 64>(a, st);
+  else if (K1 == 64) c1s_cfg<128, 4, 32, 32, false, true, 64>(a, st);
   else c1s_cfg<384, 4, 16, 16, false, true, 128>(a, st);
   return true;
 }

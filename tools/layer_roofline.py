@@ -41,20 +41,21 @@ def main():
 
     recs = []
     names = ("conv2d", "conv2d_split", "stem_fused", "stem_split", "linear", "linear_split", "global_avgpool",
-             "conv3x3_c64")
+             "conv3x3_c64", "conv1x1_dual", "conv1x1_dual_split", "conv1x1_fused_next")
     orig = {n: getattr(ops, n) for n in names if hasattr(ops, n)}
 
     def wrap(n, f):
         def g(*args, **kw):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            y = f(*args, **kw)
+            out = f(*args, **kw)
             e1.record()
+            y = out[0] if isinstance(out, tuple) else out    # conv1x1_fused_next: (y, z)
             x = args[0]
             res = kw.get("residual")
             recs.append((n, tuple(x.shape), x.element_size(), tuple(y.shape), y.element_size(),
                          None if res is None else res.numel() * res.element_size(), args, e0, e1))
-            return y
+            return out
         return g
 
     per = collections.defaultdict(list)
