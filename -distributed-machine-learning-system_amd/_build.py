@@ -135,9 +135,21 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     r = subprocess.run(link, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    _check_undefined(Path(str(TARGET) + ".tmp"))
     os.replace(str(TARGET) + ".tmp", TARGET)
     FLAGS.write_text(_flags())
     return TARGET
+
+
+def _check_undefined(so: Path) -> None:
+    """Refuse a library that references one of its own symbols without
+    defining it (e.g. a kernel launch stub the host pass silently dropped)."""
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    r = subprocess.run([nm, "-D", "--undefined-only", str(so)], capture_output=True, text=True)
+    bad = [ln.split()[-1] for ln in r.stdout.splitlines() if "idunno" in ln]
+    if bad:
+        so.unlink(missing_ok=True)
+        raise RuntimeError(f"link left {len(bad)} undefined idunno symbols, e.g. {bad[:3]}")
 
 
 def main(argv=None) -> int:

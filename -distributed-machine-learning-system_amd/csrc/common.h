@@ -61,6 +61,39 @@ __device__ __forceinline__ half8v lds_read_b128(uint32_t addr) {
   return v;
 }
 
+// 16-byte-per-lane LDS-DMA through a buffer resource (buffer_load_dwordx4 ... lds):
+// voff per lane, soff uniform; lanes past num_records land zeros.  A plain
+// __device__ wrapper: called straight from a __global__ template's body, the
+// target builtin made the host pass drop the kernel's launch stub without a
+// diagnostic (every conv_glds instantiation became an undefined symbol).
+__device__ __forceinline__ void dma_buf16(__amdgpu_buffer_rsrc_t rsrc, void* lds, uint32_t voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
+// ds_read_b128 at addr + OFF (OFF an immediate, < 64 KiB)
+template <int OFF>
+__device__ __forceinline__ half8v lds_read_b128_imm(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset range");
+  half8v v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF) : "memory");
+  return v;
+}
+
+// ds_read_b128 at addr + i * STEP for a compile-time-after-unrolling i < 16
+template <int STEP>
+__device__ __forceinline__ half8v lds_read_b128_step(uint32_t addr, int i) {
+  switch (i) {
+    case 0: return lds_read_b128_imm<0>(addr);
+    case 1: return lds_read_b128_imm<STEP>(addr);
+    case 2: return lds_read_b128_imm<2 * STEP>(addr);
+    case 3: return lds_read_b128_imm<3 * STEP>(addr);
+    case 4: return lds_read_b128_imm<4 * STEP>(addr);
+    case 5: return lds_read_b128_imm<5 * STEP>(addr);
+    case 6: return lds_read_b128_imm<6 * STEP>(addr);
+    default: return lds_read_b128_imm<7 * STEP>(addr);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void lds_waitcnt() {
   asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");

@@ -152,7 +152,51 @@ conv_glds_kernel(const ConvArgs a) {
     i_s = (i_kh * a.KW + i_kw) * a.cblk;
     nK = a.cblk;
   }
-  auto issue = [&](int buf) {
+  // Buffer-resource DMA (every non-P3 conv; operands must fit 2 GiB, glds_cfg):
+  // per-lane byte offsets are fixed -- A for the whole launch, B per kernel
+  // tap (recomputed when the channel block wraps) -- and the stage's K offset
+  // is the instruction's SGPR soffset, so a stage's DMA costs no VALU (the
+  // global-pointer form spent ~28 VALU per stage on ih/iw/bounds/64-bit adds,
+  // and the 128x128 split tile is issue-bound: profiles/r3_pmc_split_forward.md).
+  // Padding taps and rows past M / Cout get an offset past num_records: the
+  // hardware returns zeros.
+  constexpr uint32_t OOR = 0x80000000u;
+  const auto w_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)win, 0, 0x7fffffff, 0x00020000);
+  const auto x_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)xin, 0, 0x7fffffff, 0x00020000);
+  uint32_t a_voff[GA], b_voff[GB];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int n = n0 + (wave + NW * j) * RPI + lrow;
+    a_voff[j] = n < a.Cout ? (uint32_t)((n * a.Kpad + a_ch[j]) * 2) : OOR;
+  }
+  auto set_tap = [&]() {
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int ih = b_ih0[j] + i_kh, iw = b_iw0[j] + i_kw;
+      const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      b_voff[j] = ok ? (uint32_t)((b_base[j] + (ih * a.W + iw) * ldx) * 2) : OOR;
+    }
+  };
+  auto issue_buf = [&](int buf) {
+    char* base = smem + buf * STAGE;
+    if (i_cb == 0) set_tap();
+    const int koff = i_s * BK * 2, coff = i_cb * BK * 2;
+#pragma unroll
+    for (int j = 0; j < GA; ++j)
+      dma_buf16(w_rsrc, base + (wave + NW * j) * 1024, a_voff[j], koff);
+#pragma unroll
+    for (int j = 0; j < GB; ++j)
+      dma_buf16(x_rsrc, base + A_BYTES + (wave + NW * j) * 1024, b_voff[j], coff);
+    ++i_s;
+    if (++i_cb == a.cblk) {
+      i_cb = 0;
+      if (++i_kw == a.KW) {
+        i_kw = 0;
+        ++i_kh;
+      }
+    }
+  };
+  auto issue_glb = [&](int buf) {
     char* base = smem + buf * STAGE;
     const int koff = i_s * BK;
 #pragma unroll
@@ -199,6 +243,10 @@ conv_glds_kernel(const ConvArgs a) {
       }
     }
   };
+  auto issue = [&](int buf) {
+    if constexpr (P3) issue_glb(buf);
+    else issue_buf(buf);
+  };
 
   float4v acc[FN][FM];
 #pragma unroll
@@ -239,6 +287,15 @@ conv_glds_kernel(const ConvArgs a) {
     if (p < nK) issue(p);
 
   const int frow = lane & 15, fch = lane >> 4;
+  // per-lane LDS byte offsets (within a stage) of fragment 0 of each K chunk
+  uint32_t frag_a[BK / 32], frag_b[BK / 32];
+#pragma unroll
+  for (int kk = 0; kk < BK / 32; ++kk) {
+    const int ch = fch + 4 * kk;
+    const int ra = wn * TN + frow, rb = wm * TM + frow;
+    frag_a[kk] = (uint32_t)(ra * RB + ((ch ^ swz_r(ra, CPR)) << 4));
+    frag_b[kk] = (uint32_t)(A_BYTES + rb * RB + ((ch ^ swz_r(rb, CPR)) << 4));
+  }
   for (int s = 0; s < nK; ++s) {
     const int ahead = min(NS - 2, nK - 1 - s);
     wait_stages<G, NS>(ahead);
@@ -253,19 +310,18 @@ conv_glds_kernel(const ConvArgs a) {
     const uint32_t base = lds_addr(smem) + (s % NS) * STAGE;
     constexpr int KK = BK / 32, NR = FN + FM;
     half8v fa[KK][FN], fb[KK][FM];
+    // fragment rows 16 apart share the swizzle (swz_r(row) depends on row mod 16
+    // for both row sizes), so fragment i of chunk kk is the lane's chunk-kk
+    // address + i * 16 rows: one VGPR add per (operand, kk) and stage, the rest
+    // immediate offsets (the per-read address adds were 16 VALU per stage)
+    static_assert(16 * RB * (FN > FM ? FN : FM) <= 65536, "fragment offsets must fit the ds immediate");
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
-      const int ch = fch + 4 * kk;
+      const uint32_t abase = base + frag_a[kk], bbase = base + frag_b[kk];
 #pragma unroll
-      for (int i = 0; i < FN; ++i) {
-        const int row = wn * TN + i * 16 + frow;
-        fa[kk][i] = lds_read_b128(base + row * RB + ((ch ^ swz_r(row, CPR)) << 4));
-      }
+      for (int i = 0; i < FN; ++i) fa[kk][i] = lds_read_b128_step<16 * RB>(abase, i);
 #pragma unroll
-      for (int j = 0; j < FM; ++j) {
-        const int row = wm * TM + j * 16 + frow;
-        fb[kk][j] = lds_read_b128(base + A_BYTES + row * RB + ((ch ^ swz_r(row, CPR)) << 4));
-      }
+      for (int j = 0; j < FM; ++j) fb[kk][j] = lds_read_b128_step<16 * RB>(bbase, j);
     }
     auto mfma_chunk = [&](int kk) {
 #pragma unroll
@@ -409,6 +465,12 @@ conv_glds_kernel(const ConvArgs a) {
   }
 }
 
+// the buffer-resource DMA addresses x and w with 32-bit byte offsets
+static bool glds_fits(const ConvArgs& a) {
+  const long xb = (long)a.B * a.H * a.W * (a.ldx ? a.ldx : a.C) * 2, wb = (long)a.Cout * a.Kpad * 2;
+  return xb < (1L << 31) && wb < (1L << 31);
+}
+
 template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false,
           bool SPLIT = false>
 static void glds_cfg(ConvArgs a, hipStream_t st) {
@@ -519,6 +581,7 @@ static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
 }
 
 bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
+  if (!glds_fits(a)) return false;
   const bool res = a.res != nullptr;
   if (res) return out_f32 ? glds_dispatch_split<true, true>(a, tile, st) : glds_dispatch_split<true, false>(a, tile, st);
   return out_f32 ? glds_dispatch_split<false, true>(a, tile, st) : glds_dispatch_split<false, false>(a, tile, st);
@@ -559,6 +622,7 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
     if (res) return false;
     return out_f32 ? glds_dispatch_p3<true>(a, tile, st) : glds_dispatch_p3<false>(a, tile, st);
   }
+  if (!glds_fits(a)) return false;
   if (res) return out_f32 ? glds_dispatch<true, true>(a, tile, st) : glds_dispatch<true, false>(a, tile, st);
   return out_f32 ? glds_dispatch<false, true>(a, tile, st) : glds_dispatch<false, false>(a, tile, st);
 }
