@@ -469,6 +469,22 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
     // conv columns of this lane whose taps leave the image: border delta needed
     int wlo, whi;
     tap_range(ox0 + cx, g.W, wlo, whi);
+    const bool colb = wlo > 0 || whi < KH;
+    // the delta of an interior row (all 7 kh taps valid) depends on the column
+    // only: S(7, whi) - S(7, wlo) - S(7, 7) (S(0, .) = 0), loaded once per tile
+    // instead of 5 dependent global loads in every conv row of an edge tile
+    float4v colcorr[NIW];
+#pragma unroll
+    for (int i = 0; i < NIW; ++i) {
+      colcorr[i] = float4v{0.f, 0.f, 0.f, 0.f};
+      if (colb) {
+        const int co = (ch0 + i) * 16 + fch * 4;
+        const float4v s_h = *reinterpret_cast<const float4v*>(psum + (7 * 8 + whi) * 64 + co);
+        const float4v s_l = *reinterpret_cast<const float4v*>(psum + (7 * 8 + wlo) * 64 + co);
+        const float4v s_f = *reinterpret_cast<const float4v*>(psum + (7 * 8 + 7) * 64 + co);
+        colcorr[i] = (s_h - s_l - s_f) * inv_scale;
+      }
+    }
 
     for (int f = wave / NCH; f < CRY; f += 4 / NCH) {
       const char* pb = patch + ((2 * f) * IPC + 2 * cx + 2 * fch + PCO) * 8;
@@ -488,7 +504,11 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
       const bool rowv = (unsigned)oy < (unsigned)g.Hc;    // wave-uniform
       int hlo, hhi;
       tap_range(oy, g.H, hlo, hhi);
-      if (rowv && (hlo > 0 || hhi < KH || wlo > 0 || whi < KH)) {
+      const bool rowb = hlo > 0 || hhi < KH;              // wave-uniform
+      if (rowv && !rowb && colb) {
+#pragma unroll
+        for (int i = 0; i < NIW; ++i) acc[i] += colcorr[i];
+      } else if (rowv && rowb) {
         // border pixel: add (sum of w*c over its valid taps) - (the full sum in
         // the bias), from the 2D prefix sums psum[kh][kw][64] (kh, kw in 0..7)
 #pragma unroll
