@@ -560,7 +560,8 @@ static bool glds_dispatch_p3(ConvArgs a, int tile, hipStream_t st) {
 // The tiles below are the measured-useful ones: 36 / 42 / 27 are the defaults
 // (conv_glds_split_pick), 26 / 34 / 38 near-equal alternatives kept for A/B.
 // Measured and dropped (profiles/r2_v24..v29): 14/17/25/30 (256-wide), 15/16/41
-// (3-stage rings), 24, 33, 35, 37, 43 -- 5-45 % slower on every ResNet layer;
+// (3-stage rings), 24, 33, 35, 37, 43 -- 5-45 % slower on every ResNet layer (15/16/24
+// re-measured after the round-3 buffer-DMA rewrite: still 5-30 % slower, profiles/r3_split_resweep.log);
 // 192 x 128 for AlexNet conv2 (Cout 192): 8 % slower than 64 x 128.  Round 3
 // (profiles/r3_split_stagger_layers.md): half the waves issuing the next stage's
 // DMA behind their first MFMA chunk (0-13 % slower), 128 x 256 with a 3-stage
