@@ -139,8 +139,10 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 int conv_glds_split_pick(int M, int Cout);
 void set_f16_wide_tile(bool on);     // A/B: fp16 128x160 tiles for M < 50000 (default on)
+void set_f16_wide_all(bool on);      // A/B: ... at every M
 void set_split_wide_tile(bool on);   // A/B: 128x160 tiles for small-M split convs (default on)
 void set_split_wide_l3(bool on);     // A/B: ... also for 50000 <= M < 100000 (layer3)
+void set_split_wide_all(bool on);    // A/B: ... at every M
 // persistent streaming 1x1 fp16 conv, stride 1 or 2 (conv1x1_stream.hip): shapes in conv1x1_stream_supported
 bool conv1x1_stream_supported(int C, int Cout, long M);
 bool conv1x1_stream_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,

@@ -594,8 +594,11 @@ static bool g_split_wide = true;
 void set_split_wide_tile(bool on) { g_split_wide = on; }
 static bool g_split_wide_l3 = false;
 void set_split_wide_l3(bool on) { g_split_wide_l3 = on; }
+static bool g_split_wide_all = false;
+void set_split_wide_all(bool on) { g_split_wide_all = on; }
 int conv_glds_split_pick(int M, int Cout) {
   if (Cout % 128 == 0) {
+    if (g_split_wide && g_split_wide_all) return 42;
     if (g_split_wide && g_split_wide_l3 && M >= 50000 && M < 100000) return 42;   // layer3: 1.91 vs 2.39 waves
     if (M >= 50000) return 36;
     // layer4-sized GEMMs: 128 x 160 tiles make ~1 full wave of blocks where
@@ -633,10 +636,17 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
 // M is large; 128x64 tiles keep >= 2 waves of blocks when M is small (layer4).
 static bool g_f16_wide = true;   // whole fp16 graph +3.6 % (profiles/r2_v31_wide_tiles.md)
 void set_f16_wide_tile(bool on) { g_f16_wide = on; }
+// fp16 A/B after the buffer-DMA rewrite: 42 at every M, ResNet18 b400 +4.2 %, ResNet50 b1024
+// +3.4 % (profiles/r3_ab_f16_wide_all.md; per-layer: profiles/r3_f16_big_tiles.log)
+static bool g_f16_wide_all = true;
+void set_f16_wide_all(bool on) { g_f16_wide_all = on; }
 int conv_glds_pick(int M, int Cout) {
   // sweeps r1 #3/#4: BK=64 double buffering with 2-3 workgroups/CU beats deeper
   // rings; 8 waves per 128x128 tile (4 waves/SIMD) best where M is large
-  if (Cout % 128 == 0) return M >= 50000 ? 36 : (g_f16_wide ? 42 : 34);   // 128x128 8-wave | 128x64
+  if (Cout % 128 == 0) {
+    if (g_f16_wide && g_f16_wide_all) return 42;
+    return M >= 50000 ? 36 : (g_f16_wide ? 42 : 34);   // 128x128 8-wave | 128x64
+  }
   return 27;                                           // 64x128, 48 KiB
 }
 
