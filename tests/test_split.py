@@ -366,9 +366,11 @@ def test_stem_pack3_split(ops, kh, stride, pad, B, tile):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,hw", [(3, 224), (2, 100), (1, 37)])
-@pytest.mark.parametrize("niw", [2, 1])
+@pytest.mark.parametrize("niw", [2, 1, "rp2", "reg3", "reg4"])
 def test_stem_split_fused(ops, B, hw, niw):
-    """uint8 -> normalise -> conv7x7/2 -> +bias -> ReLU -> maxpool3x3/2, split out."""
+    """uint8 -> normalise -> conv7x7/2 -> +bias -> ReLU -> maxpool3x3/2, split out
+    (niw "rp2": one cout fragment per wave, two conv rows per pass; "regN": the
+    register-pooled kernel at N workgroups per CU)."""
     from idunno.models import reference as ref
 
     torch.manual_seed(B + hw)
@@ -376,11 +378,16 @@ def test_stem_split_fused(ops, B, hw, niw):
     w = torch.randn(64, 3, 7, 7) / (3 * 49) ** 0.5
     b = torch.randn(64) * 0.1
     fs, scale, bias, psum = P.pack_stem_split(w, b)
-    ops.load().set_stem_split_niw(niw)
+    ext = ops.load()
+    ext.set_stem_split_niw(2 if niw == 2 else 1)
+    ext.set_stem_split_rp2(niw == "rp2")
+    ext.set_stem_split_reg(int(niw[3:]) if str(niw).startswith("reg") else 0)
     try:
         y = ops.stem_split(img, fs.to(DEV), bias.to(DEV), psum.to(DEV), scale)
     finally:
-        ops.load().set_stem_split_niw(1)
+        ext.set_stem_split_niw(1)
+        ext.set_stem_split_rp2(True)
+        ext.set_stem_split_reg(0)
     x = ref.preprocess_u8(img).permute(0, 2, 3, 1)
     want = _ref64(x, w, b, 2, 3, True).permute(0, 3, 1, 2)
     want = F.max_pool2d(want, 3, 2, 1).permute(0, 2, 3, 1)
