@@ -1405,7 +1405,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_split_patch_default", &set_split_patch_default,
         "A/B: route split 3x3/s1 convs (Cout % 128 == 0) to the halo-patch kernel (tile 60)");
 #endif
-  m.def("set_stem_split_rp2", &set_stem_split_rp2, "A/B: split stem with two conv rows per pass");
+  m.def("set_stem_split_rp2", [](int64_t n) { set_stem_split_rp2((int)n); }, "A/B: split stem conv rows per pass (0/1: one, 2 default, 3)");
   m.def("set_stem_split_reg", [](int64_t n) { set_stem_split_reg((int)n); }, "A/B: register-pooled split stem, 3 / 4 workgroups per CU (0 off)");
   m.def("set_stem_split_niw", [](int64_t n) { set_stem_split_niw((int)n); },
         "A/B: fused split stem, 16-cout A fragments per wave (1 default: 3 workgroups/CU; 2)");

@@ -202,7 +202,7 @@ int conv_glds_pick(int M, int Cout);
 // w * s_c (pre-scaled by 1/acc_scale), bias = folded bias + full sum of w * c_c,
 // psum = [8][8][64] 2D prefix sums of w * c_c over (kh, kw); y = split [B][Hp][Wp][128]
 void set_stem_split_niw(int n);   // A/B: 16-cout fragments per wave (1 default, 2)
-void set_stem_split_rp2(bool on);  // A/B: two conv rows per pass (interleaved MFMA chains)
+void set_stem_split_rp2(int rows); // A/B: conv rows per pass (0/1: one, 2 default, 3; interleaved MFMA chains)
 void set_stem_split_reg(int wgs);   // A/B: register-pooled split stem, 3 / 4 workgroups per CU (0 off)
 void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
                        half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,

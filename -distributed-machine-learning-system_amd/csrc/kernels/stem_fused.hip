@@ -360,8 +360,8 @@ constexpr int LDS = stem::PATCH_BYTES + HP_BYTES;         // 44816
 }  // namespace stem_s
 static int g_stem_split_niw = 1;   // measured: 399 vs 461 us at B = 400 (profiles/r2_v28_stem_split_u8.md)
 void set_stem_split_niw(int n) { g_stem_split_niw = n == 1 ? 1 : 2; }
-static bool g_stem_split_rp2 = true;   // whole graph +0.86 % (profiles/r3_ab_stem_rp2.log)
-void set_stem_split_rp2(bool on) { g_stem_split_rp2 = on; }
+static int g_stem_split_rp2 = 2;   // conv rows per pass: 2 whole graph +0.86 % (profiles/r3_stem_split_rp2.md)
+void set_stem_split_rp2(int rows) { g_stem_split_rp2 = rows == 3 ? 3 : rows >= 2 ? 2 : 0; }
 static int g_stem_split_reg = 0;       // register-pooled kernel with 3 / 4 workgroups per CU (0: off)
 void set_stem_split_reg(int wgs) { g_stem_split_reg = wgs == 3 || wgs == 4 ? wgs : 0; }
 
@@ -413,7 +413,7 @@ __device__ __forceinline__ void tap_range(int o, int n, int& lo, int& hi) {
 // NIWS: 16-cout A fragments per wave (2: two waves share a conv row, 2
 // workgroups per CU by registers; 1: every wave takes all rows for its 16
 // couts, half the A registers, 3 workgroups per CU)
-// RP: conv rows per pass (2: two interleaved MFMA chains; NIWS 1 only)
+// RP: conv rows per pass (2, 3: interleaved MFMA chains; NIWS 1 only)
 template <int NIWS, int RP = 1>
 __global__ void __launch_bounds__(256, NIWS == 1 ? 3 : 2)
 stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w, const float* __restrict__ bias,
@@ -439,7 +439,8 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
   // ---- A fragments: hi and lo of w' = w * s_c, [2][cout][kh][32], registers, once ----
   constexpr int NIW = NIWS, NCH = 4 / NIWS;
   static_assert(RP == 1 || NIWS == 1, "two rows per pass: one cout fragment per wave");
-  static_assert(RP == 1 || ((2 * CRY + KH - 1) * IPC + 2 * 15 + 2 * 3 + PCO) * 8 + 16 <= stem_s::LDS, "dropped row inside LDS");
+  static_assert(RP == 1 || ((2 * (RP * ((CRY + RP - 1) / RP) - 1) + KH - 1) * IPC + 2 * 15 + 2 * 3 + PCO) * 8 + 16 <=
+                                stem_s::LDS, "dropped rows inside LDS");
   const int frow = lane & 15, fch = lane >> 4;
   const int ch0 = (wave % NCH) * NIW;
   half8v fah[KH][NIW], fal[KH][NIW];
@@ -536,27 +537,31 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
           *reinterpret_cast<float4v*>(hp + hp32_off(f, px, 4 * (ch0 + i) + fch)) = o[i];
       }
     };
-    if constexpr (RP == 2) {
-      // two conv rows per pass, their MFMA chains interleaved (each MFMA
-      // depends on the one two back, not the one before); row CRY (past the
-      // tile; its patch rows stay inside the LDS allocation) is computed and dropped
-      for (int f = 0; f < CRY; f += 2) {
+    if constexpr (RP > 1) {
+      // RP conv rows per pass, their MFMA chains interleaved (each MFMA depends
+      // on the one RP back, not the one before); rows past the tile (their patch
+      // rows stay inside the LDS allocation) are computed and dropped
+      for (int f = 0; f < CRY; f += RP) {
         const char* pa = patch + ((2 * f) * IPC + 2 * cx + 2 * fch + PCO) * 8;
-        const char* pc = pa + 2 * IPC * 8;
-        float4v acc0[1] = {float4v{0.f, 0.f, 0.f, 0.f}}, acc1[1] = {float4v{0.f, 0.f, 0.f, 0.f}};
+        float4v acc[RP][1];
+#pragma unroll
+        for (int r = 0; r < RP; ++r) acc[r][0] = float4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kh = 0; kh < KH; ++kh) {
           if (g.ablate & 2) break;
-          const half8v b0 = *reinterpret_cast<const half8v*>(pa + kh * IPC * 8);
-          const half8v b1 = *reinterpret_cast<const half8v*>(pc + kh * IPC * 8);
-          acc0[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[kh][0], b0, acc0[0], 0, 0, 0);
-          acc1[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[kh][0], b1, acc1[0], 0, 0, 0);
-          acc0[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh][0], b0, acc0[0], 0, 0, 0);
-          acc1[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh][0], b1, acc1[0], 0, 0, 0);
+          half8v bq[RP];
+#pragma unroll
+          for (int r = 0; r < RP; ++r) bq[r] = *reinterpret_cast<const half8v*>(pa + (r * 2 * IPC + kh * IPC) * 8);
+#pragma unroll
+          for (int r = 0; r < RP; ++r) acc[r][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[kh][0], bq[r], acc[r][0], 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < RP; ++r) acc[r][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh][0], bq[r], acc[r][0], 0, 0, 0);
         }
         if (g.ablate & 8) continue;
-        row_epi(f, acc0);
-        if (f + 1 < CRY) row_epi(f + 1, acc1);
+        row_epi(f, acc[0]);
+#pragma unroll
+        for (int r = 1; r < RP; ++r)
+          if (f + r < CRY) row_epi(f + r, acc[r]);
       }
     } else {
       for (int f = wave / NCH; f < CRY; f += 4 / NCH) {
@@ -812,7 +817,10 @@ void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, c
     else
       hipLaunchKernelGGL(stem_split_rp_kernel<3>, dim3(grid_r), dim3(256), stem_r::LDS, st, img, w, bias, psum,
                          acc_scale, y, g, start_idx, start_off, max_start, sub);
-  } else if (g_stem_split_niw == 1 && g_stem_split_rp2)
+  } else if (g_stem_split_niw == 1 && g_stem_split_rp2 == 3)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_split_kernel<1, 3>), dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias,
+                       psum, acc_scale, y, g, start_idx, start_off, max_start, sub);
+  else if (g_stem_split_niw == 1 && g_stem_split_rp2)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_split_kernel<1, 2>), dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias,
                        psum, acc_scale, y, g, start_idx, start_off, max_start, sub);
   else if (g_stem_split_niw == 1)

@@ -366,10 +366,10 @@ def test_stem_pack3_split(ops, kh, stride, pad, B, tile):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,hw", [(3, 224), (2, 100), (1, 37)])
-@pytest.mark.parametrize("niw", [2, 1, "rp2", "reg3", "reg4"])
+@pytest.mark.parametrize("niw", [2, 1, "rp2", "rp3", "reg3", "reg4"])
 def test_stem_split_fused(ops, B, hw, niw):
     """uint8 -> normalise -> conv7x7/2 -> +bias -> ReLU -> maxpool3x3/2, split out
-    (niw "rp2": one cout fragment per wave, two conv rows per pass; "regN": the
+    (niw "rpN": one cout fragment per wave, N conv rows per pass; "regN": the
     register-pooled kernel at N workgroups per CU)."""
     from idunno.models import reference as ref
 
@@ -380,13 +380,13 @@ def test_stem_split_fused(ops, B, hw, niw):
     fs, scale, bias, psum = P.pack_stem_split(w, b)
     ext = ops.load()
     ext.set_stem_split_niw(2 if niw == 2 else 1)
-    ext.set_stem_split_rp2(niw == "rp2")
+    ext.set_stem_split_rp2(int(niw[2:]) if str(niw).startswith("rp") else 1)
     ext.set_stem_split_reg(int(niw[3:]) if str(niw).startswith("reg") else 0)
     try:
         y = ops.stem_split(img, fs.to(DEV), bias.to(DEV), psum.to(DEV), scale)
     finally:
         ext.set_stem_split_niw(1)
-        ext.set_stem_split_rp2(True)
+        ext.set_stem_split_rp2(2)
         ext.set_stem_split_reg(0)
     x = ref.preprocess_u8(img).permute(0, 2, 3, 1)
     want = _ref64(x, w, b, 2, 3, True).permute(0, 3, 1, 2)
