@@ -1414,6 +1414,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "A/B: persistent streaming kernel (tile 80) as the default for eligible fp16 1x1/s1 convs");
   m.def("set_conv1x1_stream_mask", &set_conv1x1_stream_mask,
         "A/B: shapes that take the streaming 1x1 kernel by default (1 Cin<=128, 2 Cin 256, 4 Cin 512, 8 stride 2)");
+  m.def("set_conv1x1_stream_lio", &set_conv1x1_stream_lio, "A/B: streaming 1x1 residual / output through per-wave LDS tiles");
+  m.def("set_conv1x1_stream_wgs", [](int64_t n) { set_conv1x1_stream_wgs((int)n); }, "A/B: streaming 1x1 resident workgroups per CU (0 default)");
   m.def("set_conv1x1_stream_split_mask", &set_conv1x1_stream_split_mask,
         "A/B: split-path shapes that take the streaming 1x1 kernel by default (bits as set_conv1x1_stream_mask)");
   m.def("set_conv1x1_split_wide", &set_conv1x1_split_wide, "A/B: 64 couts per wave for split Cin 64 / 128 1x1 convs");

@@ -65,6 +65,13 @@ typedef int int4s __attribute__((ext_vector_type(4)));
 // 8-byte buffer load (offen + SGPR soffset + immediate) that the wait-count pass
 // does not track: the caller counts it in its own vmcnt waits and reg_tie()s
 // the result after them
+__device__ __forceinline__ half4v c1_lds_read_b64(uint32_t addr) {
+  half4v v;
+  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+typedef unsigned int u32x4_c1 __attribute__((ext_vector_type(4)));
+
 template <int IMM>
 __device__ __forceinline__ half4v bload_b64_untracked(int4s rsrc, uint32_t voff, uint32_t soff) {
   half4v v;
@@ -98,7 +105,11 @@ __device__ __forceinline__ void c1_vmcnt() {
 // it is on chip -- the tile is also written to LDS (fp16, exactly the values
 // stored), and each wave computes N2 / NW of its channels -- so the next block
 // never re-reads this block's 4x-wide output.
-template <int K, int NW, int BM, int CW, bool HAS_RES, bool SPLIT = false, int K1 = 0, int N2 = 0>
+// LIO: the residual and the output go through per-wave LDS tiles, so every
+// global access is 16 bytes per lane over whole 64-256-byte row segments (the
+// C/D-fragment layout's 8-byte accesses over 16 rows kept the texture
+// addresser 76-86 % busy on the ResNet50 tails: profiles/r3_pmc_r50_fp16.md).
+template <int K, int NW, int BM, int CW, bool HAS_RES, bool SPLIT = false, int K1 = 0, int N2 = 0, bool LIO = false>
 __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: min waves per SIMD
 (const C1sArgs a) {
   // BM pixels per tile: 64, or 32 for K = 128 (whose 64 A-fragment registers
@@ -119,8 +130,14 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   constexpr int CW2 = N2 / NW, FN2 = N2 ? CW2 / 16 : 1, KK2 = NY / 32;
   static_assert(N2 == 0 || (!SPLIT && CW2 % 16 == 0), "fused next 1x1: fp16, N2 a multiple of 16 * NW");
   constexpr int YROW = NY * 2;            // bytes per pixel row of the LDS output tile
-  constexpr int GS = FN * FM * SP + (N2 ? FN2 * FM : 0);   // stores per wave and item (y, z)
-  constexpr int GR = HAS_RES ? FN * FM * SP : 0;
+  constexpr int ROWW = CW * 2 * SP;        // LIO: bytes of this wave's couts per pixel
+  constexpr int RT = BM * ROWW;            // LIO: bytes of a wave's residual / output tile
+  constexpr int CPRW = ROWW / 16;          // LIO: 16-byte chunks per pixel row (slot = chunk ^ (pixel % CPRW))
+  constexpr int GLI = RT / 1024;           // LIO: 16-byte-per-lane instructions per wave tile
+  static_assert(!LIO || (RT % 1024 == 0 && N2 == 0 && (!SPLIT || CW % 32 == 0) && (CPRW & (CPRW - 1)) == 0),
+                "LIO shapes: whole 1 KiB instructions, contiguous wave row segments");
+  constexpr int GS = LIO ? GLI : FN * FM * SP + (N2 ? FN2 * FM : 0);   // stores per wave and item (y, z)
+  constexpr int GR = HAS_RES ? (LIO ? GLI : FN * FM * SP) : 0;
   static_assert(GS + GX + GR < 64, "vmcnt immediate");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -166,6 +183,16 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   constexpr int OPX = SPLIT ? 2 : 1;     // output / residual halfs per channel
   const unsigned out_bytes = (unsigned)a.M * (unsigned)a.N * (unsigned)(2 * OPX);
   const auto out_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)out_bytes, 0x00020000);
+  // LIO: per-lane byte offset (from the tile's first pixel) of each 16-byte store
+  uint32_t st_off[LIO ? GLI : 1];
+  if constexpr (LIO) {
+#pragma unroll
+    for (int j = 0; j < GLI; ++j) {
+      const int q = j * 1024 + lane * 16;
+      const int p = q / ROWW, c = ((q % ROWW) >> 4) ^ (p & (CPRW - 1));
+      st_off[j] = (uint32_t)((p * a.N * OPX + (SPLIT ? split_off(nw0) : nw0) + c * 8) * 2);
+    }
+  }
 
   // DMA of tile tt into ring buffer buf: instruction ins covers rows 8*(ins%IPS).. of sub-tile ins/IPS;
   // lane l lands in row (l >> 3), slot (l & 7), and fetches chunk slot ^ swz_r(row)
@@ -207,9 +234,24 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   }
   // residual of tile tt (C/D layout: 4 consecutive couts of one pixel per
   // fragment): buffer loads the wait-count pass does not track (counted here)
-  half4v rv[2][HAS_RES ? FN : 1][HAS_RES ? FM : 1][SP];
+  constexpr bool RREG = HAS_RES && !LIO;     // residual prefetched into registers
+  half4v rv[2][RREG ? FN : 1][RREG ? FM : 1][SP];
+  // LIO tiles of this wave: [residual ring 0][residual ring 1] (the current ring
+  // half doubles as the output stage once its residual is in registers), or [output]
+  char* const lio_p = smem + 2 * TILE + (N2 ? BM * NY * 2 : 0) + wave * (HAS_RES ? 2 : 1) * RT;
+  const int colh = SPLIT ? split_off(nw0) : nw0;   // this wave's first half of a pixel row (LIO)
   auto load_res = [&](int tt, auto rb_c) {
-    if constexpr (HAS_RES) {
+    if constexpr (HAS_RES && LIO) {
+      constexpr int rb = decltype(rb_c)::value;
+#pragma unroll
+      for (int j = 0; j < GLI; ++j) {
+        const int q = j * 1024 + lane * 16;
+        const int p = q / ROWW, c = ((q % ROWW) >> 4) ^ (p & (CPRW - 1));
+        const int m = tt * BM + p;
+        const half_t* src = m < a.M ? a.res + (size_t)m * ((size_t)a.N * OPX) + colh + c * 8 : zero;
+        __builtin_amdgcn_global_load_lds((glb_void_c1*)src, (lds_void_c1*)(lio_p + rb * RT + j * 1024), 16, 0, 0);
+      }
+    } else if constexpr (HAS_RES) {
       constexpr int rb = decltype(rb_c)::value;
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
@@ -297,13 +339,85 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
       } else {
         if (more) c1_vmcnt<GS + GX + GR>(); else c1_vmcnt<GS>();
       }
+      if constexpr (RREG) {
 #pragma unroll
-      for (int i = 0; i < FN; ++i)
+        for (int i = 0; i < FN; ++i)
 #pragma unroll
-        for (int j = 0; j < FM; ++j)
+          for (int j = 0; j < FM; ++j)
 #pragma unroll
-          for (int p = 0; p < SP; ++p) reg_tie(rv[buf][i][j][p]);
+            for (int p = 0; p < SP; ++p) reg_tie(rv[buf][i][j][p]);
+      }
     }
+    if constexpr (LIO) {
+      // ---- LIO epilogue: residual fragments from LDS, output through LDS ----
+      const uint32_t tile_l = lds0 + (uint32_t)(lio_p - smem) + (HAS_RES ? buf * RT : 0);
+      auto frag_addr = [&](int j, int off) {   // byte `off` of the wave row of fragment-row pixel j*16+frow
+        const int pp = j * 16 + frow;
+        return tile_l + (uint32_t)(pp * ROWW + ((((off >> 4) ^ (pp & (CPRW - 1)))) << 4) + (off & 8));
+      };
+      half4v rl[HAS_RES ? FN : 1][HAS_RES ? FM : 1][SP];
+      if constexpr (HAS_RES) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j)
+#pragma unroll
+            for (int p = 0; p < SP; ++p) rl[i][j][p] = c1_lds_read_b64(frag_addr(j, c1_frag_off<SPLIT>(i) + 8 * fch + 64 * p));
+        lds_waitcnt<0>();
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j)
+#pragma unroll
+            for (int p = 0; p < SP; ++p) reg_tie(rl[i][j][p]);
+      }
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          float4v v = SPLIT ? acc[i][j] * a.acc_scale + bv[i] : acc[i][j] + bv[i];
+          if constexpr (HAS_RES) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] += (float)rl[i][j][0][e];
+              if constexpr (SPLIT) v[e] += (float)rl[i][j][SP - 1][e];
+            }
+          }
+          if (a.relu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          const int off = c1_frag_off<SPLIT>(i) + 8 * fch;
+          if constexpr (SPLIT) {
+            split_guard(a.ovf, v);
+            half4v h, l;
+            split_f16x4(v, h, l);
+            c1_lds_write_b64(frag_addr(j, off), h);
+            c1_lds_write_b64(frag_addr(j, off + 64), l);
+          } else {
+            half4v o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (half_t)v[e];
+            c1_lds_write_b64(frag_addr(j, off), o);
+          }
+        }
+      lds_waitcnt<0>();
+      // whole row segments back out: lane-linear 16-byte LDS reads, one
+      // 16-byte buffer store per lane (rows past M fall outside the descriptor)
+      half8v ob[GLI];
+#pragma unroll
+      for (int j = 0; j < GLI; ++j) ob[j] = lds_read_b128(tile_l + j * 1024 + lane * 16);
+      lds_waitcnt<0>();
+      const uint32_t soff = (uint32_t)(t * BM) * (uint32_t)a.N * (uint32_t)(2 * OPX);
+#pragma unroll
+      for (int j = 0; j < GLI; ++j) {
+        lds_tie(ob[j]);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c1, ob[j]), out_rsrc, (int)st_off[j], (int)soff, 0);
+      }
+      t = tn;
+      first = false;
+      return more;
+    } else {
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
       const uint32_t soff = (uint32_t)(t * BM + j * 16) * (uint32_t)a.N * (uint32_t)(2 * OPX);
@@ -384,26 +498,49 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
     t = tn;
     first = false;
     return more;
+    }
   };
   while (item(std::integral_constant<int, 0>{}) && item(std::integral_constant<int, 1>{})) {
   }
   c1_vmcnt<0>();
 }
 
-template <int K, int NW, int BM, int CW, bool R, bool SPLIT = false, int K1 = 0, int N2 = 0>
+// resident workgroups per CU of the streaming 1x1 kernels (A/B knob; default
+// 8 / NW = two waves per SIMD; more only where registers and LDS allow)
+static int g_c1s_wgs = 0;
+void set_conv1x1_stream_wgs(int n) { g_c1s_wgs = n; }
+// residual / output through per-wave LDS tiles (the LIO kernels; A/B knob)
+static bool g_c1s_lio = false;
+void set_conv1x1_stream_lio(bool on) { g_c1s_lio = on; }
+
+template <int K, int NW, int BM, int CW, bool R, bool SPLIT = false, int K1 = 0, int N2 = 0, bool LIO = false>
 static void c1s_cfg(C1sArgs a, hipStream_t st) {
+  constexpr int RT = BM * CW * 2 * (SPLIT ? 2 : 1), CPRW = RT / BM / 16;
+  if constexpr (!LIO && N2 == 0 && RT % 1024 == 0 && (!SPLIT || CW % 32 == 0) && (CPRW & (CPRW - 1)) == 0) {
+    if (g_c1s_lio) {
+      c1s_cfg<K, NW, BM, CW, R, SPLIT, K1, N2, true>(a, st);
+      return;
+    }
+  }
   a.nslab = a.N / (NW * CW);
   constexpr int TILE = (SPLIT ? 2 : 1) * (K / 64) * BM * 128;
-  constexpr int LDSB = 2 * TILE + (N2 ? BM * NW * CW * 2 : 0);
+  constexpr int LDSB = 2 * TILE + (N2 ? BM * NW * CW * 2 : 0) + (LIO ? NW * (R ? 2 : 1) * RT : 0);
   a.ntiles = (a.M + BM - 1) / BM;
-  const int per_cu = 8 / NW;                        // two waves per SIMD
+  auto kern = conv1x1_stream_kernel<K, NW, BM, CW, R, SPLIT, K1, N2, LIO>;
+  ensure_lds_attr(reinterpret_cast<const void*>(kern), LDSB);
+  int per_cu = 8 / NW;                              // two waves per SIMD
+  if (g_c1s_wgs > per_cu) {
+    // more resident workgroups (more loads in flight), as many as registers and LDS allow
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kern), 64 * NW, LDSB) ==
+            hipSuccess && occ > per_cu)
+      per_cu = occ < g_c1s_wgs ? occ : g_c1s_wgs;
+  }
   int G = per_cu * device_cu_count();
   G -= G % a.nslab;
   const long items = (long)a.ntiles * a.nslab;
   if (G > items) G = (int)items;
   a.G = G;
-  auto kern = conv1x1_stream_kernel<K, NW, BM, CW, R, SPLIT, K1, N2>;
-  ensure_lds_attr(reinterpret_cast<const void*>(kern), LDSB);
   hipLaunchKernelGGL(kern, dim3(G), dim3(64 * NW), LDSB, st, a);
 }
 

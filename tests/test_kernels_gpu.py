@@ -96,7 +96,9 @@ def test_conv_all_tiles_with_residual(ops, tile, H):
     (1, 9, 64, 256, True), (1, 7, 128, 512, False), (2, 13, 64, 512, True), (40, 56, 64, 256, True),
     (2, 56, 256, 64, False), (3, 14, 256, 1024, True), (2, 20, 256, 128, False), (1, 11, 256, 384, True),
     (2, 28, 512, 128, False), (3, 7, 512, 2048, True)])
-def test_conv1x1_stream(ops, B, H, Cin, Cout, res, stride):
+@pytest.mark.parametrize("lio", [False, True])
+def test_conv1x1_stream(ops, B, H, Cin, Cout, res, stride, lio):
+    """lio: residual and output through per-wave LDS tiles (bit-identical)."""
     from idunno.models.packed import pack_conv_weight
 
     torch.manual_seed(B * 7 + H + Cin + Cout + res + stride)
@@ -106,10 +108,18 @@ def test_conv1x1_stream(ops, B, H, Cin, Cout, res, stride):
     ho = (H - 1) // stride + 1
     r = torch.randn(B, ho, ho, Cout, device=DEV).half() if res else None
     pw, _ = pack_conv_weight(w)
+    ext = ops.load()
     for relu in (True, False):
-        y = ops.conv2d(x, pw.to(DEV), b.to(DEV), 1, 1, stride, 0, relu, residual=r, tile=80)
+        ext.set_conv1x1_stream_lio(lio)
+        try:
+            y = ops.conv2d(x, pw.to(DEV), b.to(DEV), 1, 1, stride, 0, relu, residual=r, tile=80)
+        finally:
+            ext.set_conv1x1_stream_lio(False)
         ref = _ref_conv(x, w.half().float().to(DEV), b.to(DEV), stride, 0, relu, r)
         _check(y, ref)
+        if lio:
+            y0 = ops.conv2d(x, pw.to(DEV), b.to(DEV), 1, 1, stride, 0, relu, residual=r, tile=80)
+            assert torch.equal(y, y0)
         # same rounding as the implicit-GEMM tile: identical fp16 outputs
         y36 = ops.conv2d(x, pw.to(DEV), b.to(DEV), 1, 1, stride, 0, relu, residual=r, tile=36)
         assert (y.float() - y36.float()).abs().max().item() <= 2e-3 * (y36.float().abs().max().item() + 1)
@@ -117,7 +127,8 @@ def test_conv1x1_stream(ops, B, H, Cin, Cout, res, stride):
 
 @pytest.mark.parametrize("B,Ho,K1,K2,Cout,s", [(2, 56, 64, 64, 256, 1), (3, 28, 128, 256, 512, 2), (1, 9, 64, 64, 512, 1),
                                                (2, 13, 128, 256, 128, 2)])
-def test_conv1x1_dual(ops, B, Ho, K1, K2, Cout, s):
+@pytest.mark.parametrize("lio", [False, True])
+def test_conv1x1_dual(ops, B, Ho, K1, K2, Cout, s, lio):
     """Bottleneck expansion 1x1 + 1x1 downsample as one GEMM over [y | x]."""
     from idunno.models.packed import pack_conv_weight
 
@@ -131,7 +142,11 @@ def test_conv1x1_dual(ops, B, Ho, K1, K2, Cout, s):
     p3, _ = pack_conv_weight(w3)
     pd, _ = pack_conv_weight(wd)
     w = torch.cat([p3, pd], 1).to(DEV).contiguous()
-    out = ops.conv1x1_dual(y, x, w, (b3 + bd).to(DEV), s, True)
+    ops.load().set_conv1x1_stream_lio(lio)
+    try:
+        out = ops.conv1x1_dual(y, x, w, (b3 + bd).to(DEV), s, True)
+    finally:
+        ops.load().set_conv1x1_stream_lio(False)
     ref = F.relu(_ref_conv(y, w3.half().float().to(DEV), b3.to(DEV), 1, 0, False)
                  + _ref_conv(x, wd.half().float().to(DEV), bd.to(DEV), s, 0, False))
     assert out.shape == ref.shape

@@ -211,7 +211,8 @@ def test_conv_split_default_tile(ops, B, H, Cin, Cout, k, s, p):
     (2, 56, 64, 256, 1, True), (2, 56, 64, 64, 1, False), (3, 28, 128, 512, 1, True), (2, 14, 256, 1024, 1, True),
     (2, 56, 256, 64, 1, False), (1, 13, 256, 384, 1, False), (2, 28, 512, 128, 1, False), (2, 7, 512, 2048, 1, True),
     (2, 56, 64, 128, 2, False), (2, 28, 256, 512, 2, False), (3, 14, 512, 1024, 2, False), (1, 9, 128, 256, 2, True)])
-def test_conv_split_1x1_stream(ops, B, H, Cin, Cout, s, res):
+@pytest.mark.parametrize("lio", [False, True])
+def test_conv_split_1x1_stream(ops, B, H, Cin, Cout, s, res, lio):
     torch.manual_seed(B * 100 + H + Cin + Cout + s + res)
     x = torch.randn(B, H, H, Cin, device=DEV)
     w = torch.randn(Cout, Cin, 1, 1) / Cin ** 0.5
@@ -220,8 +221,12 @@ def test_conv_split_1x1_stream(ops, B, H, Cin, Cout, s, res):
     r = torch.randn(B, ho, ho, Cout, device=DEV) if res else None
     sw, scale = P.pack_split_weight(w)
     for relu in (True, False):
-        y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, 1, 1, s, 0, relu,
-                             residual=None if r is None else ops.split_from_f32(r), tile=80)
+        ops.load().set_conv1x1_stream_lio(lio)
+        try:
+            y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, 1, 1, s, 0, relu,
+                                 residual=None if r is None else ops.split_from_f32(r), tile=80)
+        finally:
+            ops.load().set_conv1x1_stream_lio(False)
         assert y.shape == (B, ho, ho, 2 * Cout)
         _check(P.from_split(y), _ref64(x, w, b, s, 0, relu, r))
 
@@ -229,7 +234,8 @@ def test_conv_split_1x1_stream(ops, B, H, Cin, Cout, s, res):
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,Ho,K1,K2,Cout,s", [(2, 56, 64, 64, 256, 1), (3, 28, 128, 256, 512, 2), (1, 9, 64, 64, 128, 1),
                                                (2, 13, 128, 256, 64, 2)])
-def test_conv1x1_dual_split(ops, B, Ho, K1, K2, Cout, s):
+@pytest.mark.parametrize("lio", [False, True])
+def test_conv1x1_dual_split(ops, B, Ho, K1, K2, Cout, s, lio):
     """Split bottleneck tail: expansion 1x1 + (strided) 1x1 downsample as one GEMM, vs fp64."""
     torch.manual_seed(B + Ho + K1 + K2 + Cout + s)
     H = (Ho - 1) * s + 1 + (s - 1)
@@ -239,8 +245,12 @@ def test_conv1x1_dual_split(ops, B, Ho, K1, K2, Cout, s):
     wd = torch.randn(Cout, K2, 1, 1) / K2 ** 0.5 * 0.1       # different magnitudes: one shared scale
     b3, bd = torch.randn(Cout) * 0.1, torch.randn(Cout) * 0.1
     sw, scale = P.pack_split_weight(torch.cat([w3, wd], 1))
-    out = ops.conv1x1_dual_split(ops.split_from_f32(y), ops.split_from_f32(x), sw.to(DEV), (b3 + bd).to(DEV), scale,
-                                 s, True)
+    ops.load().set_conv1x1_stream_lio(lio)
+    try:
+        out = ops.conv1x1_dual_split(ops.split_from_f32(y), ops.split_from_f32(x), sw.to(DEV), (b3 + bd).to(DEV),
+                                     scale, s, True)
+    finally:
+        ops.load().set_conv1x1_stream_lio(False)
     assert out.shape == (B, Ho, Ho, 2 * Cout)
     ref = torch.relu(_ref64(y, w3, b3, 1, 0, False) + _ref64(x, wd, bd, s, 0, False))
     _check(P.from_split(out), ref)
