@@ -509,8 +509,9 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
 // 8 / NW = two waves per SIMD; more only where registers and LDS allow)
 static int g_c1s_wgs = 0;
 void set_conv1x1_stream_wgs(int n) { g_c1s_wgs = n; }
-// residual / output through per-wave LDS tiles (the LIO kernels; A/B knob)
-static bool g_c1s_lio = false;
+// residual / output through per-wave LDS tiles (the LIO kernels): ResNet50 b1024
+// fp16 +4.2 %, split +5.7 %, ResNet18 split +0.2 % (profiles/r3_ab_lio.md)
+static bool g_c1s_lio = true;
 void set_conv1x1_stream_lio(bool on) { g_c1s_lio = on; }
 
 template <int K, int NW, int BM, int CW, bool R, bool SPLIT = false, int K1 = 0, int N2 = 0, bool LIO = false>
