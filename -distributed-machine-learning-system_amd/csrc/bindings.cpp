@@ -1415,6 +1415,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_conv1x1_stream_mask", &set_conv1x1_stream_mask,
         "A/B: shapes that take the streaming 1x1 kernel by default (1 Cin<=128, 2 Cin 256, 4 Cin 512, 8 stride 2)");
   m.def("set_conv1x1_stream_lio", &set_conv1x1_stream_lio, "A/B: streaming 1x1 residual / output through per-wave LDS tiles");
+  m.def("set_conv1x1_stream_lio_n2", &set_conv1x1_stream_lio_n2, "A/B: LDS-staged I/O also for the fused-next 1x1 kernels");
   m.def("set_conv1x1_stream_wgs", [](int64_t n) { set_conv1x1_stream_wgs((int)n); }, "A/B: streaming 1x1 resident workgroups per CU (0 default)");
   m.def("set_conv1x1_stream_split_mask", &set_conv1x1_stream_split_mask,
         "A/B: split-path shapes that take the streaming 1x1 kernel by default (bits as set_conv1x1_stream_mask)");

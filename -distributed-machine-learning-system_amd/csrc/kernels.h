@@ -173,6 +173,7 @@ void set_conv1x1_split_wide(bool on);   // A/B: 64 couts per wave for split Cin 
 bool conv1x1_stream_split_default(int C, int stride);
 void set_conv1x1_stream_wgs(int n);   // A/B: resident workgroups per CU (0: two waves per SIMD)
 void set_conv1x1_stream_lio(bool on);  // A/B: residual / output through per-wave LDS tiles
+void set_conv1x1_stream_lio_n2(bool on);  // A/B: ... also for the fused-next kernels
 void set_c64_split_variant(int v);  // layer1 split kernel: 0 = 16 couts/wave, 2/3 = 32 couts/wave (read ring depth)
 int c64_split_variant();
 #ifdef IDUNNO_EXPERIMENTAL

@@ -134,9 +134,16 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   constexpr int RT = BM * ROWW;            // LIO: bytes of a wave's residual / output tile
   constexpr int CPRW = ROWW / 16;          // LIO: 16-byte chunks per pixel row (slot = chunk ^ (pixel % CPRW))
   constexpr int GLI = RT / 1024;           // LIO: 16-byte-per-lane instructions per wave tile
-  static_assert(!LIO || (RT % 1024 == 0 && N2 == 0 && (!SPLIT || CW % 32 == 0) && (CPRW & (CPRW - 1)) == 0),
+  // LIO + N2: y leaves from the block's LDS output tile (GLY whole-row
+  // instructions per wave), z through the wave's tile (GLZ)
+  constexpr int ROW2 = CW2 * 2, CPR2 = N2 ? ROW2 / 16 : 1;
+  constexpr int GLY = N2 ? BM * NY * 2 / 1024 / NW : GLI;
+  constexpr int GLZ = N2 ? BM * ROW2 / 1024 : 0;
+  static_assert(!LIO || (RT % 1024 == 0 && (!SPLIT || CW % 32 == 0) && (CPRW & (CPRW - 1)) == 0),
                 "LIO shapes: whole 1 KiB instructions, contiguous wave row segments");
-  constexpr int GS = LIO ? GLI : FN * FM * SP + (N2 ? FN2 * FM : 0);   // stores per wave and item (y, z)
+  static_assert(!LIO || N2 == 0 || ((BM * NY * 2) % (1024 * NW) == 0 && (BM * ROW2) % 1024 == 0 && ROW2 <= ROWW &&
+                                    (CPR2 & (CPR2 - 1)) == 0 && YROW == 512), "LIO + fused next shapes");
+  constexpr int GS = LIO ? GLY + GLZ : FN * FM * SP + (N2 ? FN2 * FM : 0);   // stores per wave and item (y, z)
   constexpr int GR = HAS_RES ? (LIO ? GLI : FN * FM * SP) : 0;
   static_assert(GS + GX + GR < 64, "vmcnt immediate");
 
@@ -184,8 +191,21 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   const unsigned out_bytes = (unsigned)a.M * (unsigned)a.N * (unsigned)(2 * OPX);
   const auto out_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)out_bytes, 0x00020000);
   // LIO: per-lane byte offset (from the tile's first pixel) of each 16-byte store
-  uint32_t st_off[LIO ? GLI : 1];
-  if constexpr (LIO) {
+  uint32_t st_off[LIO ? GLY : 1], zst_off[LIO && N2 ? GLZ : 1];
+  if constexpr (LIO && N2 > 0) {
+#pragma unroll
+    for (int j = 0; j < GLY; ++j) {        // this wave's rows of the block tile [BM][NY] (chunk ^ (pixel & 15))
+      const int q = (wave * GLY + j) * 1024 + lane * 16;
+      const int p = q / YROW, c = ((q % YROW) >> 4) ^ (p & 15);
+      st_off[j] = (uint32_t)((p * a.N + c * 8) * 2);
+    }
+#pragma unroll
+    for (int j = 0; j < GLZ; ++j) {
+      const int q = j * 1024 + lane * 16;
+      const int p = q / ROW2, c = ((q % ROW2) >> 4) ^ (p & (CPR2 - 1));
+      zst_off[j] = (uint32_t)((p * N2 + wave * CW2 + c * 8) * 2);
+    }
+  } else if constexpr (LIO) {
 #pragma unroll
     for (int j = 0; j < GLI; ++j) {
       const int q = j * 1024 + lane * 16;
@@ -398,10 +418,81 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
             half4v o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = (half_t)v[e];
-            c1_lds_write_b64(frag_addr(j, off), o);
+            if constexpr (N2 > 0) {
+              // the block's output tile [pixel][NY], 16-byte chunk c of row p at c ^ (p & 15)
+              const int pp = j * 16 + frow, c = (wave * CW + i * 16 + 4 * fch) >> 3;
+              c1_lds_write_b64(ytile + pp * YROW + ((c ^ (pp & 15)) << 4) + (fch & 1) * 8, o);
+            } else {
+              c1_lds_write_b64(frag_addr(j, off), o);
+            }
           }
         }
       lds_waitcnt<0>();
+      if constexpr (N2 > 0) {
+        __builtin_amdgcn_s_barrier();       // the whole output tile is in LDS
+        // y: this wave's GLY KiB of the tile, whole rows, 16 bytes per lane
+        half8v yb[GLY];
+#pragma unroll
+        for (int j = 0; j < GLY; ++j) yb[j] = lds_read_b128(ytile + (wave * GLY + j) * 1024 + lane * 16);
+        // z = relu(y_tile . w2^T + b2)
+        float4v acc2[FN2][FM];
+#pragma unroll
+        for (int i = 0; i < FN2; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) acc2[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+        lds_waitcnt<0>();
+        const uint32_t soffy = (uint32_t)(t * BM) * (uint32_t)a.N * 2u;
+#pragma unroll
+        for (int j = 0; j < GLY; ++j) {
+          lds_tie(yb[j]);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c1, yb[j]), out_rsrc, (int)st_off[j],
+                                                 (int)soffy, 0);
+        }
+#pragma unroll
+        for (int kk = 0; kk < KK2; ++kk) {
+          half8v fb2[FM];
+#pragma unroll
+          for (int j = 0; j < FM; ++j) {
+            const int pp = j * 16 + frow, c = 4 * kk + fch;
+            fb2[j] = lds_read_b128(ytile + pp * YROW + ((c ^ (pp & 15)) << 4));
+          }
+          lds_waitcnt<0>();
+#pragma unroll
+          for (int j = 0; j < FM; ++j) lds_tie(fb2[j]);
+#pragma unroll
+          for (int i = 0; i < FN2; ++i)
+#pragma unroll
+            for (int j = 0; j < FM; ++j)
+              acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa2[i][kk], fb2[j], acc2[i][j], 0, 0, 0);
+        }
+        // z through this wave's tile (its residual is in registers already)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+#pragma unroll
+          for (int i = 0; i < FN2; ++i) {
+            const float4v v = acc2[i][j] + bv2[i];
+            half4v o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (half_t)fmaxf(v[e], 0.f);
+            const int pp = j * 16 + frow, off = i * 32 + 8 * fch;
+            c1_lds_write_b64(tile_l + pp * ROW2 + ((((off >> 4) ^ (pp & (CPR2 - 1)))) << 4) + (off & 8), o);
+          }
+        lds_waitcnt<0>();
+        half8v zb[GLZ];
+#pragma unroll
+        for (int j = 0; j < GLZ; ++j) zb[j] = lds_read_b128(tile_l + j * 1024 + lane * 16);
+        lds_waitcnt<0>();
+        const uint32_t soffz = (uint32_t)(t * BM) * (uint32_t)(N2 * 2);
+#pragma unroll
+        for (int j = 0; j < GLZ; ++j) {
+          lds_tie(zb[j]);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c1, zb[j]), z_rsrc, (int)zst_off[j],
+                                                 (int)soffz, 0);
+        }
+        t = tn;
+        first = false;
+        return more;
+      }
       // whole row segments back out: lane-linear 16-byte LDS reads, one
       // 16-byte buffer store per lane (rows past M fall outside the descriptor)
       half8v ob[GLI];
@@ -513,12 +604,17 @@ void set_conv1x1_stream_wgs(int n) { g_c1s_wgs = n; }
 // fp16 +4.2 %, split +5.7 %, ResNet18 split +0.2 % (profiles/r3_ab_lio.md)
 static bool g_c1s_lio = true;
 void set_conv1x1_stream_lio(bool on) { g_c1s_lio = on; }
+static bool g_c1s_lio_n2 = true;       // ... also for the fused-next (N2) kernels: ResNet50 fp16 +3.5 %
+void set_conv1x1_stream_lio_n2(bool on) { g_c1s_lio_n2 = on; }
 
 template <int K, int NW, int BM, int CW, bool R, bool SPLIT = false, int K1 = 0, int N2 = 0, bool LIO = false>
 static void c1s_cfg(C1sArgs a, hipStream_t st) {
   constexpr int RT = BM * CW * 2 * (SPLIT ? 2 : 1), CPRW = RT / BM / 16;
-  if constexpr (!LIO && N2 == 0 && RT % 1024 == 0 && (!SPLIT || CW % 32 == 0) && (CPRW & (CPRW - 1)) == 0) {
-    if (g_c1s_lio) {
+  constexpr int ROW2 = N2 ? N2 / NW * 2 : 16;
+  constexpr bool N2OK = N2 == 0 || ((BM * NW * CW * 2) % (1024 * NW) == 0 && (BM * ROW2) % 1024 == 0 &&
+                                    ROW2 <= CW * 2 && NW * CW == 256);
+  if constexpr (!LIO && N2OK && RT % 1024 == 0 && (!SPLIT || CW % 32 == 0) && (CPRW & (CPRW - 1)) == 0) {
+    if (g_c1s_lio && (N2 == 0 || g_c1s_lio_n2)) {
       c1s_cfg<K, NW, BM, CW, R, SPLIT, K1, N2, true>(a, st);
       return;
     }

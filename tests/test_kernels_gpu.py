@@ -114,11 +114,15 @@ def test_conv1x1_stream(ops, B, H, Cin, Cout, res, stride, lio):
         try:
             y = ops.conv2d(x, pw.to(DEV), b.to(DEV), 1, 1, stride, 0, relu, residual=r, tile=80)
         finally:
-            ext.set_conv1x1_stream_lio(False)
+            ext.set_conv1x1_stream_lio(True)
         ref = _ref_conv(x, w.half().float().to(DEV), b.to(DEV), stride, 0, relu, r)
         _check(y, ref)
         if lio:
-            y0 = ops.conv2d(x, pw.to(DEV), b.to(DEV), 1, 1, stride, 0, relu, residual=r, tile=80)
+            ext.set_conv1x1_stream_lio(False)
+            try:
+                y0 = ops.conv2d(x, pw.to(DEV), b.to(DEV), 1, 1, stride, 0, relu, residual=r, tile=80)
+            finally:
+                ext.set_conv1x1_stream_lio(True)
             assert torch.equal(y, y0)
         # same rounding as the implicit-GEMM tile: identical fp16 outputs
         y36 = ops.conv2d(x, pw.to(DEV), b.to(DEV), 1, 1, stride, 0, relu, residual=r, tile=36)
@@ -146,7 +150,7 @@ def test_conv1x1_dual(ops, B, Ho, K1, K2, Cout, s, lio):
     try:
         out = ops.conv1x1_dual(y, x, w, (b3 + bd).to(DEV), s, True)
     finally:
-        ops.load().set_conv1x1_stream_lio(False)
+        ops.load().set_conv1x1_stream_lio(True)
     ref = F.relu(_ref_conv(y, w3.half().float().to(DEV), b3.to(DEV), 1, 0, False)
                  + _ref_conv(x, wd.half().float().to(DEV), bd.to(DEV), s, 0, False))
     assert out.shape == ref.shape
@@ -154,8 +158,10 @@ def test_conv1x1_dual(ops, B, Ho, K1, K2, Cout, s, lio):
 
 
 @pytest.mark.parametrize("B,H,N2,dual", [(2, 56, 64, False), (3, 20, 128, False), (2, 56, 64, True), (1, 9, 64, True)])
-def test_conv1x1_fused_next(ops, B, H, N2, dual):
-    """Bottleneck tail (residual or dual form) + the next block's reduce 1x1 from the on-chip tile."""
+@pytest.mark.parametrize("lio", [False, True])
+def test_conv1x1_fused_next(ops, B, H, N2, dual, lio):
+    """Bottleneck tail (residual or dual form) + the next block's reduce 1x1 from the on-chip tile
+    (lio: residual, output and z through LDS tiles, bit-identical)."""
     from idunno.models.packed import pack_conv_weight
 
     torch.manual_seed(B + H + N2 + dual)
@@ -167,17 +173,32 @@ def test_conv1x1_fused_next(ops, B, H, N2, dual):
     b2 = torch.randn(N2) * 0.1
     p3, _ = pack_conv_weight(w3)
     p2, _ = pack_conv_weight(w2)
+    ext = ops.load()
     if dual:
         wd = torch.randn(256, 64, 1, 1) / 8
         bd = torch.randn(256) * 0.1
         pd, _ = pack_conv_weight(wd)
-        out, z = ops.conv1x1_fused_next(y, torch.cat([p3, pd], 1).to(DEV).contiguous(), (b3 + bd).to(DEV),
-                                        p2.to(DEV), b2.to(DEV), x2=x)
+        wcat = torch.cat([p3, pd], 1).to(DEV).contiguous()
+        run = lambda: ops.conv1x1_fused_next(y, wcat, (b3 + bd).to(DEV), p2.to(DEV), b2.to(DEV), x2=x)
         ref = F.relu(_ref_conv(y, w3.half().float().to(DEV), b3.to(DEV), 1, 0, False)
                      + _ref_conv(x, wd.half().float().to(DEV), bd.to(DEV), 1, 0, False))
     else:
-        out, z = ops.conv1x1_fused_next(y, p3.to(DEV), b3.to(DEV), p2.to(DEV), b2.to(DEV), residual=x)
+        run = lambda: ops.conv1x1_fused_next(y, p3.to(DEV), b3.to(DEV), p2.to(DEV), b2.to(DEV), residual=x)
         ref = _ref_conv(y, w3.half().float().to(DEV), b3.to(DEV), 1, 0, True, x)
+    ext.set_conv1x1_stream_lio(lio)
+    ext.set_conv1x1_stream_lio_n2(lio)
+    try:
+        out, z = run()
+    finally:
+        ext.set_conv1x1_stream_lio(True)
+        ext.set_conv1x1_stream_lio_n2(True)
+    if lio:
+        ext.set_conv1x1_stream_lio(False)
+        try:
+            out0, z0 = run()
+        finally:
+            ext.set_conv1x1_stream_lio(True)
+        assert torch.equal(out, out0) and torch.equal(z, z0)
     _check(out, ref)
     # z is exactly the reduce conv of the stored (fp16) output
     z_ref = ops.conv2d(out, p2.to(DEV), b2.to(DEV), 1, 1, 1, 0, True, tile=36)

@@ -226,7 +226,7 @@ def test_conv_split_1x1_stream(ops, B, H, Cin, Cout, s, res, lio):
             y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, 1, 1, s, 0, relu,
                                  residual=None if r is None else ops.split_from_f32(r), tile=80)
         finally:
-            ops.load().set_conv1x1_stream_lio(False)
+            ops.load().set_conv1x1_stream_lio(True)
         assert y.shape == (B, ho, ho, 2 * Cout)
         _check(P.from_split(y), _ref64(x, w, b, s, 0, relu, r))
 
@@ -250,7 +250,7 @@ def test_conv1x1_dual_split(ops, B, Ho, K1, K2, Cout, s, lio):
         out = ops.conv1x1_dual_split(ops.split_from_f32(y), ops.split_from_f32(x), sw.to(DEV), (b3 + bd).to(DEV),
                                      scale, s, True)
     finally:
-        ops.load().set_conv1x1_stream_lio(False)
+        ops.load().set_conv1x1_stream_lio(True)
     assert out.shape == (B, Ho, Ho, 2 * Cout)
     ref = torch.relu(_ref64(y, w3, b3, 1, 0, False) + _ref64(x, wd, bd, s, 0, False))
     _check(P.from_split(out), ref)
