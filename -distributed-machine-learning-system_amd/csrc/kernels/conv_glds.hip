@@ -185,8 +185,15 @@ conv_glds_kernel(const ConvArgs a) {
     for (int j = 0; j < GA; ++j)
       dma_buf16(w_rsrc, base + (wave + NW * j) * 1024, a_voff[j], koff);
 #pragma unroll
-    for (int j = 0; j < GB; ++j)
+    for (int j = 0; j < GB; ++j) {
+      // padded B rows (BM .. BMD-1, e.g. 160 .. 191) are never read: no DMA for
+      // them (wave-uniform; NS = 2 waits with vmcnt(0), so the counts need not match)
+      if constexpr (BMD != BM) {
+        static_assert(BMD == BM || (NS == 2 && BM % RPI == 0), "skipped padding instructions need vmcnt(0) waits");
+        if ((wave + NW * j) * RPI >= BM) continue;
+      }
       dma_buf16(x_rsrc, base + A_BYTES + (wave + NW * j) * 1024, b_voff[j], coff);
+    }
     ++i_s;
     if (++i_cb == a.cblk) {
       i_cb = 0;
