@@ -1167,6 +1167,48 @@ torch::Tensor stem_split(torch::Tensor img, torch::Tensor w, torch::Tensor bias,
   return y;
 }
 
+// fp16 programs: exact-u8 stem (pack_stem_split weights, hi parts only) -> fp16 [B,Hp,Wp,64]
+torch::Tensor stem_u8_f16(torch::Tensor img, torch::Tensor w, torch::Tensor bias, torch::Tensor psum, double acc_scale,
+                         c10::optional<torch::Tensor> start, int64_t batch, int64_t start_offset, int64_t window,
+                         int64_t sub) {
+  CHECK_DEV(img);
+  CHECK_DEV(w);
+  CHECK_DEV(bias);
+  CHECK_DEV(psum);
+  CHECK_CONTIG(img);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(bias);
+  CHECK_CONTIG(psum);
+  CHECK_DT(img, torch::kUInt8);
+  CHECK_DT(w, torch::kHalf);
+  CHECK_DT(bias, torch::kFloat);
+  CHECK_DT(psum, torch::kFloat);
+  TORCH_CHECK(w.device() == img.device() && bias.device() == img.device() && psum.device() == img.device(),
+              "operands on different devices");
+  TORCH_CHECK(img.dim() == 4 && img.size(3) == 3, "img must be [B, H, W, 3] uint8");
+  TORCH_CHECK(w.dim() == 3 && w.size(0) == 2 && w.size(1) == 64 && w.size(2) == 7 * 32,
+              "split stem weight must be [2, 64, 7*32]");
+  TORCH_CHECK(bias.numel() == 64, "bias must have 64 entries");
+  TORCH_CHECK(psum.numel() == 8 * 8 * 64, "psum must be [8, 8, 64]");
+  const int H = img.size(1), W = img.size(2);
+  int B;
+  long long max_start;
+  const long long* sp = window_args(img, start, batch, window, sub, B, max_start);
+  TORCH_CHECK(H >= 7 && W >= 7, "image too small");
+  TORCH_CHECK((long)B * H * W * 3 < (1L << 31), "batch too large");
+  const int Hc = (H + 6 - 7) / 2 + 1, Wc = (W + 6 - 7) / 2 + 1;
+  const int Hp = (Hc + 2 - 3) / 2 + 1, Wp = (Wc + 2 - 3) / 2 + 1;
+  TORCH_CHECK((long)B * Hp * Wp * 64 < (1L << 31), "batch too large");
+  auto y = torch::empty({B, Hp, Wp, 64}, img.options().dtype(torch::kHalf));
+  if (B) {
+    stem_u8_f16_launch(img.data_ptr<uint8_t>(), reinterpret_cast<const half_t*>(w.data_ptr()), bias.data_ptr<float>(),
+                       psum.data_ptr<float>(), (float)acc_scale, reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp,
+                       start_offset, max_start, sp ? sub : 0, cur_stream());
+    check_launch("stem_u8_f16");
+  }
+  return y;
+}
+
 torch::Tensor preprocess(torch::Tensor img, c10::optional<torch::Tensor> start, int64_t batch, int64_t start_offset,
                          int64_t window, int64_t sub, bool f32) {
   CHECK_DEV(img);
@@ -1391,6 +1433,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pad"), py::arg("relu"), py::arg("acc_scale"), py::arg("tile") = -1);
   m.def("preprocess_pack3_split", &preprocess_pack3_split, "uint8 HWC -> split-fp16 packed-row stem input",
         py::arg("img"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("start") = py::none(),
+        py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1, py::arg("sub") = 0);
+  m.def("stem_u8_f16", &stem_u8_f16, "fp16 fused ResNet stem in exact-u8 form (pack_stem_split weights)",
+        py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("psum"), py::arg("acc_scale"), py::arg("start") = py::none(),
         py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1, py::arg("sub") = 0);
   m.def("stem_split", &stem_split, "fp32-accurate fused split-fp16 ResNet stem (normalise+conv7x7/2+relu+maxpool)",
         py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("psum"), py::arg("acc_scale"), py::arg("start") = py::none(),

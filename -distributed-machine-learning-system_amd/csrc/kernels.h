@@ -210,6 +210,10 @@ void set_stem_split_reg(int wgs);   // A/B: register-pooled split stem, 3 / 4 wo
 void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
                        half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,
                        long long max_start, long long sub, int* ovf, hipStream_t st);
+// fp16 programs: the same exact-u8 stem with the hi MFMA only, y = fp16 [B][Hp][Wp][64]
+void stem_u8_f16_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
+                        half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,
+                        long long max_start, long long sub, hipStream_t st);
 void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, half_t* y, int B, int H, int W,
                        const long long* start_idx, long long start_off, long long max_start, long long sub,
                        hipStream_t st);

@@ -414,7 +414,10 @@ __device__ __forceinline__ void tap_range(int o, int n, int& lo, int& hi) {
 // workgroups per CU by registers; 1: every wave takes all rows for its 16
 // couts, half the A registers, 3 workgroups per CU)
 // RP: conv rows per pass (2, 3: interleaved MFMA chains; NIWS 1 only)
-template <int NIWS, int RP = 1>
+// F16: the fp16 programs' stem in the same exact-u8 form -- only the hi
+// MFMA (w' rounded to fp16 once; the input u is exact, unlike the normalised
+// fp16 input of stem_fused_kernel) and a plain fp16 [B][Hp][Wp][64] output
+template <int NIWS, int RP = 1, bool F16 = false>
 __global__ void __launch_bounds__(256, NIWS == 1 ? 3 : 2)
 stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w, const float* __restrict__ bias,
                   const float* __restrict__ psum, float acc_scale, half_t* __restrict__ y, const StemGeom g,
@@ -450,7 +453,7 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
     for (int i = 0; i < NIW; ++i) {
       const size_t o = (size_t)((ch0 + i) * 16 + frow) * (KH * 32) + kh * 32 + fch * 8;
       fah[kh][i] = *reinterpret_cast<const half8v*>(w + o);
-      fal[kh][i] = *reinterpret_cast<const half8v*>(w + 64 * KH * 32 + o);
+      if constexpr (!F16) fal[kh][i] = *reinterpret_cast<const half8v*>(w + 64 * KH * 32 + o);
     }
   const float inv_scale = 1.f / acc_scale;           // 2^e: border deltas in accumulator units
 
@@ -555,7 +558,8 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
 #pragma unroll
           for (int r = 0; r < RP; ++r) acc[r][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[kh][0], bq[r], acc[r][0], 0, 0, 0);
 #pragma unroll
-          for (int r = 0; r < RP; ++r) acc[r][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh][0], bq[r], acc[r][0], 0, 0, 0);
+          for (int r = 0; r < RP; ++r)
+            if constexpr (!F16) acc[r][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh][0], bq[r], acc[r][0], 0, 0, 0);
         }
         if (g.ablate & 8) continue;
         row_epi(f, acc[0]);
@@ -576,7 +580,7 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
 #pragma unroll
           for (int i = 0; i < NIW; ++i) {
             acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[kh][i], bu, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh][i], bu, acc[i], 0, 0, 0);
+            if constexpr (!F16) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh][i], bu, acc[i], 0, 0, 0);
           }
         }
         if (g.ablate & 8) continue;
@@ -615,14 +619,24 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
             m0[e] = fmaxf(m0[e] * acc_scale + pb0[e], 0.f);
             m1[e] = fmaxf(m1[e] * acc_scale + pb1[e], 0.f);
           }
-          split_guard(g.ovf, m0);
-          split_guard(g.ovf, m1);
-          half4v h0, l0, h1, l1;
-          split_f16x4(m0, h0, l0);
-          split_f16x4(m1, h1, l1);
-          half_t* dst = y + (((size_t)b * g.Hp + oyp + hr) * g.Wp + ox) * 128 + split_off(8 * c8);
-          *reinterpret_cast<half8v*>(dst) = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-          *reinterpret_cast<half8v*>(dst + 32) = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+          if constexpr (F16) {
+            half8v o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              o[e] = (half_t)m0[e];
+              o[4 + e] = (half_t)m1[e];
+            }
+            *reinterpret_cast<half8v*>(y + (((size_t)b * g.Hp + oyp + hr) * g.Wp + ox) * 64 + 8 * c8) = o;
+          } else {
+            split_guard(g.ovf, m0);
+            split_guard(g.ovf, m1);
+            half4v h0, l0, h1, l1;
+            split_f16x4(m0, h0, l0);
+            split_f16x4(m1, h1, l1);
+            half_t* dst = y + (((size_t)b * g.Hp + oyp + hr) * g.Wp + ox) * 128 + split_off(8 * c8);
+            *reinterpret_cast<half8v*>(dst) = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+            *reinterpret_cast<half8v*>(dst + 32) = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
         }
       }
     }
@@ -829,6 +843,30 @@ void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, c
   else
     hipLaunchKernelGGL(stem_split_kernel<2>, dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias, psum, acc_scale,
                        y, g, start_idx, start_off, max_start, sub);
+}
+
+// fp16 programs: the exact-u8 stem, hi MFMA only, fp16 [B][Hp][Wp][64] out
+void stem_u8_f16_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
+                        half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,
+                        long long max_start, long long sub, hipStream_t st) {
+  using namespace stem;
+  StemGeom g;
+  g.ovf = nullptr;
+  g.B = B;
+  g.H = H;
+  g.W = W;
+  g.Hc = (H + 2 * CP - KH) / CS + 1;
+  g.Wc = (W + 2 * CP - KH) / CS + 1;
+  g.Hp = (g.Hc + 2 * PP - PK) / PS + 1;
+  g.Wp = (g.Wc + 2 * PP - PK) / PS + 1;
+  g.tiles_x = (g.Wp + PTX - 1) / PTX;
+  g.tiles_y = (g.Hp + PTY - 1) / PTY;
+  g.ntiles = B * g.tiles_x * g.tiles_y;
+  g.ablate = g_stem_ablate;
+  const int per = 3 * device_cu_count();
+  const int grid = g.ntiles < per ? g.ntiles : per;
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_split_kernel<1, 2, true>), dim3(grid), dim3(256), stem_s::LDS, st, img, w,
+                     bias, psum, acc_scale, y, g, start_idx, start_off, max_start, sub);
 }
 
 }  // namespace idunno

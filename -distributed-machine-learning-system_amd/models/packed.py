@@ -365,7 +365,8 @@ def make_conv(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, relu: bool, dtype: str
         sp3, s_scale = pack_split_weight_p3(fold_bn_f64(conv.weight, conv.bias, bn)[0])
     c = Conv(pw, b.contiguous(), conv.in_channels, conv.out_channels, conv.kernel_size[0],
              conv.kernel_size[1], conv.stride[0], conv.padding[0], relu, small, None, p3, sw, s_scale, sp3)
-    if dtype == "fp32" and tuple(conv.weight.shape) == (64, 3, 7, 7) and conv.stride[0] == 2 and conv.padding[0] == 3:
+    if tuple(conv.weight.shape) == (64, 3, 7, 7) and conv.stride[0] == 2 and conv.padding[0] == 3:
+        # the exact-u8 stem: split (fp32 programs) or its hi parts alone (fp16, ops.stem_u8_f16)
         c.fs, c.fs_scale, c.fs_bias, c.fs_psum = pack_stem_split(*fold_bn_f64(conv.weight, conv.bias, bn))
     return c
 
@@ -547,6 +548,10 @@ class HipRunner:
         # fp16 ResNet50 layer1: a block's tail kernel also computes the next
         # block's reduce 1x1 from its output tile on chip (ops.conv1x1_fused_next)
         self.fuse_next_1x1 = True
+        # fp16 ResNet stem in the exact-u8 form (stem_split_kernel<.., F16>: uint8 input exact, hi MFMA only);
+        # off: the normalised-fp16 stem_fused_kernel is faster (ResNet18 -3.7 %, ResNet50 -1.8 %,
+        # profiles/r3_ab_stem_u8_f16.md)
+        self.stem_u8 = False
         self.device = torch.device(device or "cuda")
         self.p = program.to(self.device)
         self._graphs: dict[int, tuple] = {}
@@ -633,7 +638,7 @@ class HipRunner:
             if nfront:
                 x = self._split_front(img_u8, start, batch, start_offset, nfront, split)
             elif fused:
-                x = o.stem_fused(img_u8, s.w, s.b, start, batch, start_offset)
+                x = self._stem16(img_u8, start, batch, start_offset)
             else:
                 x = o.conv2d(x, s.w, s.b, s.kh, s.kw, s.stride, s.pad, s.relu)
                 x = o.maxpool2d(x, 3, 2, 1)
@@ -875,7 +880,7 @@ class HipRunner:
         """Kernel-choice switches a captured graph depends on (part of its cache key)."""
         return (self.split, self.split_front, self.split_streams, self.winograd, self.wino_variant, self.pack3,
                 self.pack3_f16, self.side_down, self.stem_parts, self.front_split, self.fuse_stem, self.batch_parts,
-                self.fuse_down, self.fuse_down_1x1, self.fuse_next_1x1)
+                self.fuse_down, self.fuse_down_1x1, self.fuse_next_1x1, self.stem_u8)
 
     def _split_ok(self) -> bool:
         p = self.p
@@ -1035,6 +1040,14 @@ class HipRunner:
             n += 1
         return n
 
+    def _stem16(self, img_u8, start, batch, start_offset, window: int = -1, sub: int = 0):
+        """fp16 fused ResNet stem: the exact-u8 form (``stem_u8``) or the normalised-fp16 kernel."""
+        o, s = self.ops, self.p.stem
+        if self.stem_u8 and s.fs is not None:
+            return o.stem_u8_f16(img_u8, s.fs, s.fs_bias, s.fs_psum, s.fs_scale, start, batch, start_offset,
+                                 window=window, sub=sub)
+        return o.stem_fused(img_u8, s.w, s.b, start, batch, start_offset, window=window, sub=sub)
+
     def _split_front(self, img_u8, start, batch, start_offset, nfront, split):
         """Stem + the first ``nfront`` blocks on ``split`` batch parts; the last
         block of each part writes its slice of the full-batch output."""
@@ -1045,9 +1058,9 @@ class HipRunner:
         for sub in range(0, B, n):
             nb = min(n, B - sub)
             if start is not None:
-                x = o.stem_fused(img_u8, s.w, s.b, start, nb, start_offset, window=B, sub=sub)
+                x = self._stem16(img_u8, start, nb, start_offset, window=B, sub=sub)
             else:
-                x = o.stem_fused(img_u8[sub:sub + nb], s.w, s.b)
+                x = self._stem16(img_u8[sub:sub + nb], None, -1, 0)
             for bi in range(nfront):
                 blk = self.p.blocks[bi]
                 if bi < nfront - 1:

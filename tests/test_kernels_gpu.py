@@ -547,6 +547,24 @@ def test_stem_fused_vs_fp32(ops, B, H):
     _check(y, ref)
 
 
+@pytest.mark.parametrize("B,H", [(3, 224), (2, 64), (1, 100), (2, 37)])
+def test_stem_u8_f16_vs_fp32(ops, B, H):
+    """fp16 exact-u8 stem (split stem kernel, hi MFMA only) vs the fp32 conv of the same image."""
+    from idunno.models.packed import pack_stem_split
+    from idunno.models.reference import preprocess_u8
+
+    torch.manual_seed(H + B + 1)
+    img = torch.randint(0, 256, (B, H, H, 3), dtype=torch.uint8, device=DEV)
+    w = torch.randn(64, 3, 7, 7) / (3 * 49) ** 0.5
+    b = torch.randn(64) * 0.1
+    fs, scale, bias, psum = pack_stem_split(w.double(), b.double())
+    y = ops.stem_u8_f16(img, fs.to(DEV), bias.to(DEV), psum.to(DEV), scale)
+    x = preprocess_u8(img)
+    ref = F.max_pool2d(F.relu(F.conv2d(x, w.to(DEV), b.to(DEV), 2, 3)), 3, 2, 1).permute(0, 2, 3, 1)
+    assert y.dtype == torch.float16 and y.shape == ref.shape
+    _check(y, ref)
+
+
 def test_runner_fused_stem_matches_unfused(ops):
     from idunno.models import HipRunner, build_program
 
