@@ -1471,6 +1471,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_split_wide_l3", &set_split_wide_l3, "A/B: 128x160 split tiles also for 50000 <= M < 100000 (layer3)");
   m.def("set_f16_wide_tile", &set_f16_wide_tile, "A/B: fp16 128x160 tiles for M < 50000 (layer4)");
   m.def("set_f16_wide_all", &set_f16_wide_all, "A/B: fp16 128x160 tiles at every M (128-multiple Cout)");
+  m.def("set_conv_l2_prefetch", [](int64_t m) { set_conv_l2_prefetch((int)m); }, "A/B: conv_glds input-footprint L2 prefetch (bit 0 fp16, bit 1 split)");
   m.def("set_split_wide_all", &set_split_wide_all, "A/B: split 128x160 tiles at every M (128-multiple Cout)");
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");

@@ -70,6 +70,11 @@ __device__ __forceinline__ void dma_buf16(__amdgpu_buffer_rsrc_t rsrc, void* lds
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
 }
 
+// 4-byte-per-lane LDS-DMA: an L2 prefetch whose data lands in a scratch LDS slot
+__device__ __forceinline__ void dma_buf4(__amdgpu_buffer_rsrc_t rsrc, void* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds, 4, voff, 0, 0, 0);
+}
+
 // ds_read_b128 at addr + OFF (OFF an immediate, < 64 KiB)
 template <int OFF>
 __device__ __forceinline__ half8v lds_read_b128_imm(uint32_t addr) {

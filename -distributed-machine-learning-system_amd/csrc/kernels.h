@@ -42,6 +42,7 @@ struct ConvArgs {
   int center_only;
   float acc_scale2;
   int ldr;           // residual pixel stride in halfs (0: the output width, 2*Cout split / Cout fp16)
+  int l2pf;          // conv_glds: prefetch the tile's input footprint into L2 at block start (set by the launchers)
 };
 
 // fp32 (reference-precision) conv: same geometry fields as ConvArgs, f32 tensors.
@@ -143,6 +144,7 @@ void set_f16_wide_all(bool on);      // A/B: ... at every M
 void set_split_wide_tile(bool on);   // A/B: 128x160 tiles for small-M split convs (default on)
 void set_split_wide_l3(bool on);     // A/B: ... also for 50000 <= M < 100000 (layer3)
 void set_split_wide_all(bool on);    // A/B: ... at every M
+void set_conv_l2_prefetch(int mode);  // A/B: conv_glds input-footprint L2 prefetch (bit 0 fp16, bit 1 split)
 // persistent streaming 1x1 fp16 conv, stride 1 or 2 (conv1x1_stream.hip): shapes in conv1x1_stream_supported
 bool conv1x1_stream_supported(int C, int Cout, long M);
 bool conv1x1_stream_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,

@@ -255,6 +255,30 @@ conv_glds_kernel(const ConvArgs a) {
     else issue_buf(buf);
   };
 
+  // L2 prefetch of the tile's input footprint (the contiguous NHWC pixel range
+  // from its first input row, halo included, to its last): one 4-byte LDS-DMA
+  // per 128-byte line into ring slot NS-1, which no real DMA writes before stage
+  // 0's wait (these are older than every ring DMA) and barrier.  The taps' first
+  // touches of the input rows then go to HBM together at block start instead of
+  // stalling the early stages one after another.
+  if constexpr (!P3) {
+    if (a.l2pf && !(second && a.center_only)) {
+      const int hw = a.Ho * a.Wo;
+      const int mlo = m0, mhi = min(m0 + BM, a.M) - 1;
+      const int b0 = mlo / hw, oh0 = (mlo - b0 * hw) / a.Wo;
+      const int b1 = mhi / hw, oh1 = (mhi - b1 * hw) / a.Wo;
+      const int ih_lo = max(oh0 * a.stride - a.pad, 0), ih_hi = min(oh1 * a.stride - a.pad + a.KH - 1, a.H - 1);
+      const long long lo = ((long long)b0 * a.H + ih_lo) * a.W * ldx * 2;
+      const long long hi = ((long long)b1 * a.H + ih_hi + 1) * a.W * ldx * 2;
+      const int nl = (int)min((hi - lo + 127) >> 7, 2048LL);       // 128-byte lines, at most 256 KiB
+      char* dummy = smem + (NS - 1) * STAGE + wave * 256;
+      for (int i = wave * 64; i < nl; i += NW * 64) {
+        const int line = i + lane;
+        dma_buf4(x_rsrc, dummy, line < nl ? (uint32_t)(lo + ((long long)line << 7)) : OOR);
+      }
+    }
+  }
+
   float4v acc[FN][FM];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
@@ -478,6 +502,9 @@ static bool glds_fits(const ConvArgs& a) {
   return xb < (1L << 31) && wb < (1L << 31);
 }
 
+static int g_l2pf = 0;   // conv_glds input-footprint L2 prefetch: bit 0 fp16 convs, bit 1 split convs
+void set_conv_l2_prefetch(int mode) { g_l2pf = mode; }
+
 template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false,
           bool SPLIT = false>
 static void glds_cfg(ConvArgs a, hipStream_t st) {
@@ -589,6 +616,7 @@ static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
 }
 
 bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
+  a.l2pf = (g_l2pf >> 1) & 1;
   if (!glds_fits(a)) return false;
   const bool res = a.res != nullptr;
   if (res) return out_f32 ? glds_dispatch_split<true, true>(a, tile, st) : glds_dispatch_split<true, false>(a, tile, st);
@@ -628,6 +656,7 @@ bool conv_glds_split_p3_launch(ConvArgs a, int tile, hipStream_t st) {
 }
 
 bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
+  a.l2pf = g_l2pf & 1;
   const bool res = a.res != nullptr;
   if (a.cpk > 0) {
     if (res) return false;

@@ -594,3 +594,37 @@ def test_resnet18_fused_downsample_same_logits(ops):
     plain = r.logits(img).double()
     scale = plain.abs().max().item()
     assert (fused - plain).abs().max().item() <= 1e-6 * scale
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [26, 27, 36, 42])
+@pytest.mark.parametrize("B,H,C,Cout,k,s", [(3, 28, 128, 128, 3, 1), (2, 56, 64, 128, 3, 2), (2, 14, 256, 256, 3, 1),
+                                            (4, 7, 512, 512, 3, 1), (2, 28, 128, 256, 1, 2)])
+def test_conv_l2_prefetch_identical(ops, tile, B, H, C, Cout, k, s):
+    """conv_glds input-footprint L2 prefetch (set_conv_l2_prefetch) leaves every output bit unchanged,
+    split and fp16, with and without the residual."""
+    from idunno.models.packed import pack_conv_weight
+
+    torch.manual_seed(B + H + C + Cout + k + s + tile)
+    ext = ops.load()
+    x = torch.randn(B, H, H, C, device=DEV)
+    w = torch.randn(Cout, C, k, k) / (C * k * k) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    pad = k // 2
+    ho = (H + 2 * pad - k) // s + 1
+    r = torch.randn(B, ho, ho, Cout, device=DEV)
+    sw, scale = P.pack_split_weight(w)
+    pw, _ = pack_conv_weight(w)
+    outs = []
+    for mode in (0, 3):
+        ext.set_conv_l2_prefetch(mode)
+        try:
+            ys = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, k, k, s, pad, True,
+                                  residual=ops.split_from_f32(r), tile=tile)
+            yh = ops.conv2d(x.half(), pw.to(DEV), b.to(DEV), k, k, s, pad, True, residual=r.half(), tile=tile)
+            torch.cuda.synchronize()
+        finally:
+            ext.set_conv_l2_prefetch(0)
+        outs.append((ys, yh))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    _check(P.from_split(outs[1][0]), _ref64(x, w, b, s, pad, True, r))
