@@ -379,6 +379,9 @@ conv_glds_kernel(const ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < FM; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+      // keep the hi*hi MFMAs above the second wait: without this barrier the
+      // scheduler sank them below it, so no MFMA issued before every read landed
+      __builtin_amdgcn_sched_barrier(0);
       lds_waitcnt<0>();
 #pragma unroll
       for (int i = 0; i < FN; ++i) lds_tie(fa[1][i]);
@@ -396,6 +399,7 @@ conv_glds_kernel(const ConvArgs a) {
     if constexpr (KK == 2) {
       lds_waitcnt<NR>();                         // chunk 0 landed, chunk 1 may be in flight
       mfma_chunk(0);
+      __builtin_amdgcn_sched_barrier(0);         // (as above: chunk 0's MFMAs stay above the wait)
     }
     lds_waitcnt<0>();
     mfma_chunk(KK - 1);
