@@ -577,6 +577,7 @@ static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
     case 38: glds_cfg<128, 64, 64, 2, 4, 2, R, F>(a, st); return true;    // 8 waves (32x16 wave tile)
     case 39: glds_cfg<128, 128, 32, 2, 4, 4, R, F>(a, st); return true;   // 8 waves, 64 KiB, 3 stages in flight
     case 42: glds_cfg<128, 160, 64, 4, 2, 2, R, F>(a, st); return true;   // 8 waves, B as 192 rows, 80 KiB (small M)
+    case 43: glds_cfg<256, 160, 64, 8, 2, 2, R, F>(a, st); return true;   // 16 waves (32x80 each), B as 256 rows, 128 KiB
     default: return false;
   }
 }
