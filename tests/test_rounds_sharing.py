@@ -192,8 +192,12 @@ def test_two_jobs_share_the_rounds_on_8_ranks():
         print(f"alone: alexnet {t_a:.2f}s resnet18 {t_r:.2f}s; together {t_both:.2f}s; rounds {before} -> {after}")
         # space sharing: about the slower job alone, well under the time-sliced sum
         # (1.2x held in quiet runs; 1.25x seen with the whole CPU suite loading the
-        # 8 processes, hence the margin)
-        assert t_both <= 1.35 * max(t_a, t_r) and t_both <= 0.8 * (t_a + t_r), (t_a, t_r, t_both)
+        # 8 processes, hence the margin).  Under pytest-xdist the other workers
+        # starve these 8 processes unevenly (6.4 s vs 4.8/3.0 s alone seen at -n 4), so
+        # the wall-clock bound is enforced in serial runs only; the round-table
+        # checks above hold either way.
+        if not os.environ.get("PYTEST_XDIST_WORKER"):
+            assert t_both <= 1.35 * max(t_a, t_r) and t_both <= 0.8 * (t_a + t_r), (t_a, t_r, t_both)
 
         # idle gap longer than the collective-op timeout: nothing is posted while idle,
         # so the epoch survives and the next query runs as a round in it
