@@ -587,6 +587,9 @@ class HipRunner:
             self.ops.set_split_guard(None)
         if self.overflow_fallback and not self._capturing and int(self._ovf.item()):
             out = self.logits_f32_exact(img_u8, start, batch, start_offset)
+            # these logits have fp32's range: a following softmax_top1 must not
+            # mark the batch OVERFLOW_CLASS (forward() passes the flag on)
+            self._ovf.zero_()
         return out
 
     def logits_f32_exact(self, img_u8, start=None, batch: int = -1, start_offset: int = 0):

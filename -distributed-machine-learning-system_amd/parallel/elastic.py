@@ -130,6 +130,19 @@ class ElasticGroup:
     def world(self) -> int:
         return len(self.members)
 
+    def describe(self) -> dict:
+        """The live epoch's backend as the process group reports it: name
+        ("nccl" = RCCL on ROCm, "gloo"; "solo" for a one-member group) and
+        size.  Empty when no epoch is formed."""
+        pg = self.pg
+        if pg is None:
+            return {}
+        if isinstance(pg, _Solo):
+            return {"backend": "solo (one member, no collective)", "world": 1, "epoch": self.epoch}
+        name = pg.name() if hasattr(pg, "name") else self.backend
+        return {"backend": str(name).lower(), "world": int(pg.size()), "epoch": self.epoch,
+                "rccl": self.backend == "nccl" and torch.version.hip is not None}
+
     # -- lifecycle ---------------------------------------------------------------
     def _detach(self):
         pg, self.pg = self.pg, None

@@ -443,6 +443,18 @@ class JobState:
                         out.append((model, q, w, s, e, t0))
             return out
 
+    def active_models(self) -> set:
+        """Models with a chunk still running or a coordinator-side job not yet
+        fully submitted: O(open queries + jobs), no copy of the chunk tables
+        (the per-submit / per-round scheduler check).  A job counts as active
+        from its submission to its last result, including the moments between
+        two of its queries, so the other job's split does not flip to "alone"
+        and back at every refill of its window."""
+        with self.lock:
+            act = {m for (m, _q) in self._open}
+            act.update(j["model"] for j in self.jobs.values() if j["next"] <= j["end"])
+            return act
+
     def pending_count(self) -> int:
         with self.lock:
             return sum(self._open.values())

@@ -252,7 +252,7 @@ class Node:
             snap = msgpack.unpackb(f.read(), raw=False, strict_map_key=False)
         self.state.restore(snap["jobs"])
         self.sdfs.restore(snap["sdfs"])
-        self.sched.avg_time.update(snap.get("avg_time", {}))
+        self.sched.adopt(snap.get("avg_time", {}))
         self.logger.warning("restored checkpoint %s (seq %s)", path, snap["jobs"].get("seq"))
         return True
 
@@ -310,9 +310,7 @@ class Node:
         alive = self.membership.alive()
         if qnum is None:
             qnum = self.state.new_query_number(model)
-        with self.state.lock:
-            busy = {m for (m, _q, _w, _s, _e, _t) in self.state.pending()}
-        self.sched.active_jobs = busy | {model}
+        self.sched.active_jobs = self.state.active_models() | {model}
         plan = self.sched.assign(model, start, end, alive)
         now = self.clock()
         self.state.assign(model, qnum, plan, now)
@@ -552,7 +550,7 @@ class Node:
             r = self.transport.request(self.standby, msg, self.cfg.rpc_timeout_s)
         except TransportError:
             return False
-        if r and r.get("ok"):
+        if r and r.get("ok") and "seq" in r:
             self._standby_ack = (epoch, int(r["seq"]))
             return True
         self._standby_ack = None if not r or r.get("resync") else (epoch, int(r.get("seq", 0)))
@@ -573,7 +571,7 @@ class Node:
             if not self.state.apply_deltas(msg["deltas"]):
                 return {"ok": False, "resync": True, "seq": self.state.mirror_seq}
         self.sdfs.restore(msg["sdfs"])
-        self.sched.avg_time.update(msg.get("avg_time", {}))
+        self.sched.adopt(msg.get("avg_time", {}))
         self.meta_seq = self.state.mirror_seq
         return {"ok": True, "seq": self.state.mirror_seq}
 

@@ -94,6 +94,7 @@ class RoundPlane:
         self.rounds_done = 0
         self.rounds_failed = 0
         self.mixed_rounds = 0                 # rounds that carried more than one model
+        self.mixed_splits: dict = {}          # "alexnet:3,resnet18:5" -> rounds with that worker split
         self.max_queries_per_round = 0
         self.parked = True                    # member: waiting on the control plane, nothing posted
         self._inflight: deque = deque()       # this node's posted, unfinished gathers
@@ -189,7 +190,8 @@ class RoundPlane:
         g = self.group
         return {"ok": True, "epoch": g.epoch, "formed": g.formed, "members": list(g.members),
                 "rounds_done": self.rounds_done, "rounds_failed": self.rounds_failed,
-                "mixed_rounds": self.mixed_rounds, "max_queries_per_round": self.max_queries_per_round,
+                "mixed_rounds": self.mixed_rounds, "mixed_splits": dict(self.mixed_splits),
+                "max_queries_per_round": self.max_queries_per_round,
                 "parked": self.parked, "pending_collectives": self.pending_collectives(),
                 "queued": len(self._queue)}
 
@@ -372,7 +374,7 @@ class RoundPlane:
         n = self.node
         if not qs:
             return
-        active = {m for (m, *_r) in n.state.pending()}
+        active = n.state.active_models()
         if len(active) < 2:
             return
         alive = set(n.membership.alive())
@@ -481,9 +483,15 @@ class RoundPlane:
             self._run_chunk(r.table[0], r.seq)
         self._write_header(r.seq)
         r.work = g.post_gather(r.seq)
-        models = {q.model for q in r.queries}
-        if len(models) > 1:
+        per = {}
+        for q in r.queries:
+            per[q.model] = per.get(q.model, 0) + len(q.rows)
+        if len(per) > 1:
+            # the round table gives each member one row, so the models' worker
+            # sets in this round are disjoint by construction
             self.mixed_rounds += 1
+            key = ",".join(f"{m}:{c}" for m, c in sorted(per.items()))
+            self.mixed_splits[key] = self.mixed_splits.get(key, 0) + 1
         self.max_queries_per_round = max(self.max_queries_per_round, len(r.queries))
 
     def _finalize_oldest(self, members: tuple, check) -> None:

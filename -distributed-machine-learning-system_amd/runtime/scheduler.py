@@ -81,9 +81,12 @@ def partition(avg_time: dict[str, float], models, workers: list, budget: int) ->
     workers = list(workers)
     if not models or not workers:
         return {m: [] for m in models}
-    if len(models) > len(workers):
-        return {m: [workers[i % len(workers)]] for i, m in enumerate(models)}
-    eff = min(budget, len(workers))
+    eff = max(1, min(budget, len(workers)))
+    if len(models) > eff:
+        # fewer budgeted workers than active models (more jobs than GPUs, or a
+        # budget below the job count): the models share the eff workers
+        # round-robin, one each
+        return {m: [workers[i % eff]] for i, m in enumerate(models)}
     if len(models) == 1:
         return {models[0]: workers[:eff]}
     sh = time_shares(avg_time, models)
@@ -122,21 +125,29 @@ class FairTimeScheduler:
         self._seen: set = set()
         self._part: dict = {}
 
+    def effective_avg(self, models) -> dict[str, float]:
+        """Per-model average query time for the split: a model with no
+        measurement yet takes the mean of the measured ones (the constructor's
+        placeholder 1.0 s against measured milliseconds would hand it nearly
+        every GPU until its first result)."""
+        seen = [self.avg_time[m] for m in self._seen if m in self.avg_time]
+        fill = sum(seen) / len(seen) if seen else 1.0
+        return {m: (self.avg_time[m] if m in self._seen else fill) for m in models}
+
     def subsets(self, active, workers: list) -> dict[str, list]:
-        """``partition`` of ``workers`` over the ``active`` models, sticky: the
-        previous split is kept while every model's size is within one worker
-        of its exact fair-time share, so EMA jitter does not move a job's GPUs
-        from query to query (a moved subset would collide with the other
-        job's in-flight queries and cost a round of packing)."""
-        key = (frozenset(active), tuple(workers))
+        """``partition`` of ``workers`` over the ``active`` models, fixed while
+        the same jobs run on the same workers: the split is computed when the
+        active set (a job starts or ends), the worker set (a failure / join)
+        or the set of measured models changes, and kept otherwise, so EMA
+        jitter never moves a job's GPUs mid-job (a moved subset collides with
+        the other job's in-flight queries; report Fig 2 keeps 5/5, 4/6
+        splits per query pair)."""
+        active = frozenset(active)
+        key = (active, tuple(workers), frozenset(self._seen & active))
         cur = self._part.get(key)
-        if cur is not None:
-            eff = min(self.budget, len(workers))
-            sh = time_shares(self.avg_time, active)
-            if all(abs(len(cur[m]) - sh[m] * eff) < 1.0 for m in cur):
-                return cur
-        cur = partition(self.avg_time, active, list(workers), self.budget)
-        self._part = {key: cur}
+        if cur is None:
+            cur = partition(self.effective_avg(active), active, list(workers), self.budget)
+            self._part = {key: cur}
         return cur
 
     def observe(self, model: str, normalized_query_time: float) -> None:
@@ -148,11 +159,19 @@ class FairTimeScheduler:
             old = self.avg_time[model]
             self.avg_time[model] = (1 - self.ema) * old + self.ema * float(normalized_query_time)
 
+    def adopt(self, avg_time: dict) -> None:
+        """Take over measured averages (standby mirror, checkpoint restore):
+        they count as measurements, not placeholders."""
+        for m, v in avg_time.items():
+            self.avg_time[m] = float(v)
+            self._seen.add(m)
+
     def n_workers(self, model: str, alive: list) -> int:
         if len(self.active_jobs - {model}) == 0:
             # a single job owns the whole budget
             return max(1, min(self.budget, len(alive)))
-        return max(1, fair_share(self.avg_time, model, self.budget, len(alive), self.active_jobs))
+        act = set(self.active_jobs) | {model}
+        return max(1, fair_share(self.effective_avg(act), model, self.budget, len(alive), act))
 
     def assign(self, model: str, start: int, end: int, alive: list,
                n: int | None = None, shuffle: bool = True) -> list[tuple]:

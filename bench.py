@@ -73,6 +73,8 @@ import time
 BASELINE_IMG_PER_S = 41.0          # 400 img / 9.749 s (ResNet18, 5 workers)
 BASELINE_P50_S = 9.749             # p50 ResNet18 400-image query latency
 BASELINE_COORD_RECOVERY_S = 6.999  # coordinator failure, 1 undone query (report Fig 5)
+BASELINE_WORKER_RECOVERY_S = {1: 5.725, 2: 8.661, 4: 13.425, 6: 19.125, 8: 26.751}   # report Fig 4
+BASELINE_SECOND_JOB_S = {"alexnet_first": 41.159, "resnet18_first": 46.752}   # report Fig 3 medians
 METRIC = "images/sec (whole node) + p50 query latency, ResNet18 bs=400 at 1/2/4/8 GPU"
 QUERY = 400                        # images per query (reference report p.1, ResNet18)
 QUERY_ALEXNET = 500                # AlexNet query size (report p.1)
@@ -110,7 +112,11 @@ def parse(argv=None):
     ap.add_argument("--fail-rank", type=int, default=-1, help="testing: this rank exits 3 after warmup")
     ap.add_argument("--launch-timeout", type=float, default=1500.0, help="seconds before headline ranks are killed")
     ap.add_argument("--system", action="store_true", help="phase 2 only (see docstring)")
-    ap.add_argument("--phase", default="system", choices=["system", "failover"], help=argparse.SUPPRESS)
+    ap.add_argument("--phase", default="system", choices=["system", "failover", "worker"], help=argparse.SUPPRESS)
+    ap.add_argument("--detector", default="reference", choices=["reference", "tuned"], help=argparse.SUPPRESS)
+    ap.add_argument("--kill-chunks", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--worker-kill-chunks", type=lambda v: [int(x) for x in v.split(",")], default=[1, 4, 8],
+                    help="chunks in flight on the killed worker, one cluster per value (report Fig 4)")
     ap.add_argument("--work-dir", default=None, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -121,6 +127,23 @@ def parse(argv=None):
 # ---------------------------------------------------------------------------
 
 def _free_port() -> int:
+    """A rendezvous port P such that P and the node phases' blocks P+200..+215
+    (node listeners) and P+300..+399 (per-epoch TCPStores) are free, below the
+    kernel's ephemeral range (32768+): an outgoing connection of the many node
+    clients can then never take one of them between two phases."""
+    import random
+
+    rng = random.Random()
+    for _ in range(200):
+        p = rng.randrange(20000, 32768 - 400)
+        try:
+            for q in [p, *range(p + 200, p + 216), *range(p + 300, p + 400)]:
+                with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+                    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+                    s.bind(("127.0.0.1", q))
+        except OSError:
+            continue
+        return p
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
@@ -227,44 +250,98 @@ def _system_phase(a, work: str) -> dict:
     return d
 
 
-def _failover_phase(a, work: str) -> dict:
-    """Phase 3: SIGKILL the coordinator process mid-job (the standby times it)."""
-    out = os.path.join(work, "failover.json")
+def _kill_phase(a, work: str, phase: str, tag: str, extra: list, driver: int) -> dict:
+    """Phases 3-4: max(N, 2) node processes; the driving node writes a marker
+    naming the rank to SIGKILL (the coordinator, or a worker holding chunks)
+    and the launcher kills that process at once and stamps the time."""
+    sub = os.path.join(work, tag)
+    os.makedirs(sub, exist_ok=True)
+    out = os.path.join(sub, "out.json")
     n = max(a.gpus, 2)
     port = _free_port()
-    argv = _phase_argv(a, "failover", out, work)
+    argv = _phase_argv(a, phase, out, sub) + extra
     procs = [_spawn(argv, _child_env("node", r, n, port, local=r % a.gpus)) for r in range(n)]
-    marker, killed = os.path.join(work, "kill_now"), os.path.join(work, "killed_at")
+    marker, killed = os.path.join(sub, "kill_now"), os.path.join(sub, "killed_at")
     state = {"done": False}
 
     def poll():
         if not state["done"] and os.path.exists(marker):
-            procs[0].send_signal(signal.SIGKILL)          # the coordinator, mid-job
+            try:
+                with open(marker) as f:
+                    victim = int(f.read().strip() or "0")
+            except (OSError, ValueError):
+                return                                    # being written
+            procs[victim].send_signal(signal.SIGKILL)
             t = time.time()
             with open(killed + ".tmp", "w") as f:
                 f.write(repr(t))
             os.replace(killed + ".tmp", killed)
             state["done"] = True
 
+    drv = procs[driver % n]
     deadline = time.time() + a.extras_timeout
     try:
         while time.time() < deadline:
             poll()
-            if procs[-1].poll() is not None:               # the standby wrote its result and left
+            if drv.poll() is not None:                     # the driver wrote its result and left
                 break
-            if any(p.poll() not in (None, 0) for p in procs[1:]):
+            if any(p.poll() not in (None, 0, -signal.SIGKILL) for p in procs):
                 break
             time.sleep(0.02)
     finally:
         _stop_all(procs)
     d = _read_json(out)
     if d is None:
-        return {"extras_error": f"failover phase failed (standby rc={procs[-1].returncode})"}
+        return {"extras_error": f"{tag} phase failed (driver rc={drv.returncode})"}
     return d
+
+
+def _failover_phase(a, work: str) -> dict:
+    """Phase 3: SIGKILL the coordinator mid-job, timed by the standby.  First
+    with the reference's detector (0.3 s ping / 2 s timeout,
+    mp4_machinelearning.py:191-220, 845-851), then with the tuned one
+    (0.1 s / 1 s) as ``coord_failover_tuned_*`` keys."""
+    d = _kill_phase(a, work, "failover", "failover_ref", ["--detector", "reference"], driver=-1)
+    if "extras_error" in d:
+        return d
+    t = _kill_phase(a, work, "failover", "failover_tuned", ["--detector", "tuned"], driver=-1)
+    if "extras_error" in t:
+        d["extras_error"] = t["extras_error"]
+        return d
+    for k in ("coord_failover_recovery_s", "coord_failover_detect_s", "coord_failover_all_done_s",
+              "coord_failover_images_exact", "coord_failover_failure_timeout_s", "coord_failover_heartbeat_s"):
+        d[k.replace("coord_failover_", "coord_failover_tuned_")] = t.get(k)
+    return d
+
+
+def _worker_failover_phase(a, work: str) -> dict:
+    """Phase 4 (report Fig 4): a worker paused while k of its chunks are in
+    flight is SIGKILLed; the coordinator times detection (reference 0.3 s /
+    2 s detector), re-dispatch to the survivors and the last re-run chunk's
+    result, for k in 1, 4, 8 (one cluster per k)."""
+    out = {}
+    rec = {}
+    for k in a.worker_kill_chunks:
+        d = _kill_phase(a, work, "worker", f"worker_k{k}", ["--kill-chunks", str(k)], driver=0)
+        if "extras_error" in d:
+            return d
+        rec[str(k)] = d
+    first = next(iter(rec.values()))
+    out["worker_failover_recovery_s"] = {k: v["recovery_s"] for k, v in rec.items()}
+    out["worker_failover_detect_s"] = {k: v["detect_s"] for k, v in rec.items()}
+    out["worker_failover_chunks_on_victim"] = {k: v["chunks_on_victim"] for k, v in rec.items()}
+    out["worker_failover_images_exact"] = all(v["images_exact"] for v in rec.values())
+    out["worker_failover_nodes"] = first["nodes"]
+    out["worker_failover_rounds"] = first["rounds"]
+    out["worker_failover_survivor_world"] = {k: v.get("survivor_world") for k, v in rec.items()}
+    out["worker_failover_failure_timeout_s"] = first["failure_timeout_s"]
+    out["worker_failover_ref_s"] = {k: BASELINE_WORKER_RECOVERY_S.get(int(k)) for k in rec}
+    return out
 
 
 def _phase_argv(a, phase: str, out: str, work: str) -> list:
     argv = ["--gpus", str(a.gpus), "--steps", str(a.steps), "--warmup", str(a.warmup), "--model", a.model,
+            "--worker-kill-chunks", ",".join(str(k) for k in a.worker_kill_chunks),
             "--dtype", a.dtype, "--fp32-impl", a.fp32_impl, "--batch", str(a.batch), "--seed", str(a.seed),
             "--two-job-queries", str(a.two_job_queries), "--failover-queries", str(a.failover_queries),
             "--phase", phase, "--json-out", out, "--work-dir", work, "--launch-timeout", str(a.extras_timeout)]
@@ -291,7 +368,8 @@ def launcher(a, argv) -> int:
             return 0
         if not a.no_system:
             t0 = time.time()
-            for name, fn in (("system", _system_phase), ("failover", _failover_phase)):
+            for name, fn in (("system", _system_phase), ("failover", _failover_phase),
+                             ("worker failover", _worker_failover_phase)):
                 try:
                     d = fn(a, work)
                 except Exception as e:  # noqa: BLE001
@@ -415,6 +493,8 @@ def run_rank(a) -> int:
         host = [torch.empty(W, plane.max_chunk, 2, dtype=torch.int32, pin_memory=gpu) for _ in range(2)] \
             if coord else None
         lat, pending = [], []
+        gtimes = []            # (start, end) CUDA events / host seconds around each timed round's gather
+        timing = [False]
 
         def ingest():
             ev, table, slot, t0 = pending.pop(0)
@@ -443,7 +523,18 @@ def run_rank(a) -> int:
                 print(f"bench: rank {env.rank} failing on purpose (--fail-rank)", file=sys.stderr, flush=True)
                 os._exit(3)
             run()
-            plane.gather(None, None)
+            if timing[0] and gpu:
+                g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                g0.record()
+                plane.gather(None, None)
+                g1.record()
+                gtimes.append((g0, g1))
+            elif timing[0]:
+                g0 = time.perf_counter()
+                plane.gather(None, None)
+                gtimes.append(time.perf_counter() - g0)
+            else:
+                plane.gather(None, None)
             if coord:
                 slot = q % 2
                 host[slot].copy_(plane.gathered_all, non_blocking=gpu)
@@ -465,15 +556,23 @@ def run_rank(a) -> int:
             step(q)
         drain()
         lat.clear()
+        timing[0] = True
         t_start = time.perf_counter()
         for q in range(warmup, warmup + steps):
             step(q)
         drain()
         elapsed = time.perf_counter() - t_start
+        timing[0] = False
+        per_rank = [elapsed]
         if env.distributed:
+            # every rank's own timed region; the step time is the slowest rank's
             t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
+            outs = [torch.zeros_like(t) for _ in range(W)]
+            dist.all_gather(outs, t)
+            per_rank = [float(x.item()) for x in outs]
+            elapsed = max(per_rank)
+        g_us = [1000.0 * g0.elapsed_time(g1) for g0, g1 in gtimes] if gpu else [1e6 * x for x in gtimes]
+        gtimes.clear()
         p50_loaded = statistics.median(lat) if lat else None
         lat.clear()
         for q in range(warmup + steps, warmup + steps + max(5, min(steps, 20))):
@@ -482,7 +581,9 @@ def run_rank(a) -> int:
         p50 = statistics.median(lat) if lat else None
         recorded = state.images_done(a.model) if coord else None
         return {"elapsed": elapsed, "ips": per_round * steps / elapsed, "p50": p50, "p50_loaded": p50_loaded,
-                "recorded": recorded, "label": label}
+                "recorded": recorded, "label": label,
+                "rank_ms": [1000.0 * x / steps for x in per_rank],
+                "gather_us": statistics.median(g_us) if g_us else None}
 
     # ---- headline: weak scaling at the headline precision --------------------
     runner = None
@@ -546,6 +647,14 @@ def run_rank(a) -> int:
             "p50_query_latency_loaded_s": round(head["p50_loaded"], 6) if head["p50_loaded"] else None,
             "p50_vs_baseline_speedup": round(BASELINE_P50_S / p50, 1) if p50 and headline else None,
             "results_recorded": head["recorded"],
+            # readiness keys: the collective the timed rounds ran on, read from the
+            # live process group, the per-rank spread of the step time and the gather's own time
+            "comm_backend": (dist.get_backend() if env.distributed else "none (single rank: no collective)"),
+            "comm_world": dist.get_world_size() if env.distributed else 1,
+            "rccl": bool(env.distributed and dist.get_backend() == "nccl" and torch.version.hip is not None),
+            "ms_per_step_rank_min": round(min(head["rank_ms"]), 4),
+            "ms_per_step_rank_max": round(max(head["rank_ms"]), 4),
+            "gather_us_per_round": round(head["gather_us"], 1) if head["gather_us"] is not None else None,
             **extras,
         }
         if runner is not None:
@@ -598,8 +707,13 @@ def run_node(a) -> int:
                         fp32_impl=a.fp32_impl, max_chunk=max(2048, B), rpc_timeout_s=60.0, worker_budget=W,
                         dataset_size=10 ** 9, collective_port_offset=100,
                         batch_size={"resnet18": QUERY * W, "alexnet": QUERY_ALEXNET * W, a.model: B * W})
-    if a.phase == "failover":
-        cfg.update(heartbeat_period_s=0.1, failure_timeout_s=1.0, metadata_period_s=0.2)
+    if a.phase in ("failover", "worker"):
+        # reference detector: 0.3 s ping period, 2 s timeout (mp4_machinelearning.py:191-220, 845-851);
+        # tuned: 0.1 s / 1 s
+        if a.detector == "tuned":
+            cfg.update(heartbeat_period_s=0.1, failure_timeout_s=1.0, metadata_period_s=0.2)
+        else:
+            cfg.update(heartbeat_period_s=0.3, failure_timeout_s=2.0, metadata_period_s=0.2)
     name = cfg.node_name(rank)
     ex = FakeExecutor() if a.dry_run else HipExecutor(dev, seed=a.seed, dtype=a.dtype, fp32_impl=a.fp32_impl)
     node = Node(cfg, name, TcpTransport(name, cfg.address, cfg.address(name)), ex)
@@ -609,7 +723,7 @@ def run_node(a) -> int:
     if rank != 0:
         _wait_port(cfg.address(cfg.coordinator_name), 120)   # the coordinator listens first
     node.start(join=True)
-    driver = (rank == 0) if a.phase == "system" else (rank == n - 1)
+    driver = (rank == n - 1) if a.phase == "failover" else (rank == 0)
     if not driver:
         t_end = time.time() + a.launch_timeout
         while node.alive_flag and time.time() < t_end:
@@ -617,7 +731,12 @@ def run_node(a) -> int:
         node.stop()
         return 0
     try:
-        res = _drive_system(a, node, W, B) if a.phase == "system" else _drive_failover(a, node, n)
+        if a.phase == "system":
+            res = _drive_system(a, node, W, B)
+        elif a.phase == "failover":
+            res = _drive_failover(a, node, n)
+        else:
+            res = _drive_worker_failover(a, node, n)
         with open(a.json_out + ".tmp", "w") as f:
             f.write(json.dumps(res) + "\n")
         os.replace(a.json_out + ".tmp", a.json_out)
@@ -735,7 +854,36 @@ def _drive_system(a, node, W: int, B: int) -> dict:
                 "two_job_query_images": bs,
                 "workers_per_query_alexnet": per["alexnet"], "workers_per_query_resnet18": per["resnet18"],
                 "two_job_mixed_rounds": (r1.get("mixed_rounds", 0) - r0.get("mixed_rounds", 0)) if r1 else None,
+                # worker split of every round that ran both jobs (disjoint by construction: one row
+                # per member), counted over the timed jobs: one entry = the split never moved
+                "two_job_mixed_splits": {k: v - r0.get("mixed_splits", {}).get(k, 0)
+                                         for k, v in r1.get("mixed_splits", {}).items()
+                                         if v > r0.get("mixed_splits", {}).get(k, 0)} if r1 else None,
                 "sched_avg_time_s": {m: round(v, 6) for m, v in node.sched.avg_time.items()}})
+
+    # time to start a second job (report Fig 3: 40-42 s AlexNet first, 45-49 s ResNet18 first): job A
+    # runs; job B is submitted; until B's first query has finished
+    def second_job(first: str, second: str, q: int = 4) -> float:
+        fq = {m: st.finished_queries.get(m, 0) for m in bs}
+        cl.submit_job(base_img[0], base_img[0] + q * bs[first] - 1, first)
+        done[first] += q * bs[first]
+        assert wait_for(lambda: st.finished_queries.get(first, 0) > fq[first], 120, 0.001), st.summary()
+        t = time.perf_counter()
+        cl.submit_job(base_img[0] + 5 * 10 ** 5, base_img[0] + 5 * 10 ** 5 + q * bs[second] - 1, second)
+        done[second] += q * bs[second]
+        assert wait_for(lambda: st.finished_queries.get(second, 0) > fq[second], 120, 0.0005), st.summary()
+        dt = time.perf_counter() - t
+        base_img[0] += 10 ** 6
+        assert wait_for(lambda: all(st.images_done(m) >= done[m] for m in bs) and st.pending_count() == 0,
+                        300, 0.002), st.summary()
+        return dt
+
+    sj = {"alexnet_first": second_job("alexnet", "resnet18"), "resnet18_first": second_job("resnet18", "alexnet")}
+    out["second_job_start_s"] = {k: round(v, 4) for k, v in sj.items()}
+    out["second_job_start_ref_s"] = BASELINE_SECOND_JOB_S
+    grp = node.rounds.group.describe() if node.rounds is not None else {}
+    out["system_comm_backend"] = grp.get("backend", "tcp (no collective)")
+    out["system_comm_world"] = grp.get("world", 1)
     return out
 
 
@@ -762,8 +910,9 @@ def _drive_failover(a, node, n: int) -> dict:
     assert wait_for(lambda: st.images_done(model) >= min(2, Q - 1) * bs, 120, 0.002), st.summary()
     done_at_kill = st.images_done(model)
     work = a.work_dir or tempfile.gettempdir()
-    with open(os.path.join(work, "kill_now"), "w") as f:
-        f.write("1")
+    with open(os.path.join(work, "kill_now.tmp"), "w") as f:
+        f.write("0")                                  # the coordinator's rank
+    os.replace(os.path.join(work, "kill_now.tmp"), os.path.join(work, "kill_now"))
     killed = os.path.join(work, "killed_at")
     assert wait_for(lambda: os.path.exists(killed), 30, 0.001), "launcher did not kill the coordinator"
     with open(killed) as f:
@@ -776,14 +925,75 @@ def _drive_failover(a, node, n: int) -> dict:
     ok = wait_for(lambda: st.images_done(model) >= total and st.pending_count() == 0, 120, 0.002)
     t_all = time.time()
     rec = max(0.0, t_restored - t_kill)
+    survivor = {}
+    if node.rounds is not None:
+        # the epoch this node formed as the new coordinator (not the old one it was a member of)
+        g = node.rounds.group
+        wait_for(lambda: g.formed and g.members[:1] == [node.name], 15, 0.01)
+        survivor = g.describe() if g.members[:1] == [node.name] else {}
     return {"coord_failover_recovery_s": round(rec, 4),
             "coord_failover_detect_s": round(t_prom - t_kill, 4),
             "coord_failover_all_done_s": round(t_all - t_kill, 4),
             "coord_failover_undone_queries": Q - done_at_kill // bs,
             "coord_failover_images_exact": bool(ok and st.images_done(model) == total),
             "coord_failover_nodes": n, "coord_failover_failure_timeout_s": node.cfg.failure_timeout_s,
+            "coord_failover_heartbeat_s": node.cfg.heartbeat_period_s,
             "coord_failover_vs_baseline_speedup": round(BASELINE_COORD_RECOVERY_S / rec, 1) if rec > 0 else None,
-            "coord_failover_rounds": bool(node.cfg.collective_rounds)}
+            "coord_failover_rounds": bool(node.cfg.collective_rounds),
+            # the epoch the promoted standby formed over the survivors (RCCL at N >= 2)
+            "coord_failover_survivor_world": survivor.get("world"),
+            "coord_failover_survivor_backend": survivor.get("backend")}
+
+
+def _drive_worker_failover(a, node, n: int) -> dict:
+    """Coordinator (rank 0): pause a worker (fault-injection delay), submit k
+    queries so k of its chunks are in flight, have the launcher SIGKILL it,
+    then time the detection, the re-dispatch and the last result (report
+    Fig 4: "3 s + n * send time", 5.7 s for 1 task ... 26.8 s for 8)."""
+    from idunno.runtime.client import Client
+    from idunno.runtime.messages import Type
+    from idunno.runtime.transport import wait_for
+
+    _cluster_ready(node, n)
+    cfg = node.cfg
+    victim_rank = 1 if n >= 3 else n - 1          # a worker; the standby only when there is no other
+    victim = cfg.node_name(victim_rank)
+    cl = Client(node)
+    st = node.state
+    model = a.model
+    k = a.kill_chunks
+    detected = {}
+    node.membership.on_failure.insert(0, lambda nd: detected.setdefault(nd, time.time()))   # before re-dispatch
+    # the victim stalls before each chunk: its chunks pile up as in-flight work
+    assert node.transport.send(victim, {"t": Type.KILL, "mode": "delay", "seconds": 600.0})
+    node.sched.budget = n                             # every query spans every node, the victim included
+    per_q = cfg.batch_for(model)
+    base = 5 * 10 ** 7
+    for i in range(k):
+        cl.submit(model, base + i * per_q, base + (i + 1) * per_q - 1)
+    assert wait_for(lambda: len(st.chunks_of(victim)) >= k, 30, 0.002), st.cvm()
+    time.sleep(0.2)                                   # the others' chunks of these queries finish
+    held = len(st.chunks_of(victim))
+    work = a.work_dir or tempfile.gettempdir()
+    with open(os.path.join(work, "kill_now.tmp"), "w") as f:
+        f.write(str(victim_rank))
+    os.replace(os.path.join(work, "kill_now.tmp"), os.path.join(work, "kill_now"))
+    killed = os.path.join(work, "killed_at")
+    assert wait_for(lambda: os.path.exists(killed), 30, 0.001), "launcher did not kill the worker"
+    with open(killed) as f:
+        t_kill = float(f.read())
+    total = k * per_q
+    ok = wait_for(lambda: st.images_done(model) >= total and st.pending_count() == 0, 120, 0.002)
+    t_done = time.time()
+    survivor = {}
+    if node.rounds is not None:
+        wait_for(lambda: node.rounds.group.formed and node.rounds.group.world == n - 1, 15, 0.01)
+        survivor = node.rounds.group.describe()
+    return {"recovery_s": round(t_done - t_kill, 4),
+            "detect_s": round(detected[victim] - t_kill, 4) if victim in detected else None,
+            "chunks_on_victim": held, "images_exact": bool(ok and st.images_done(model) == total),
+            "nodes": n, "rounds": bool(cfg.collective_rounds), "survivor_world": survivor.get("world"),
+            "survivor_backend": survivor.get("backend"), "failure_timeout_s": cfg.failure_timeout_s}
 
 
 def numerics_check(runner, a, device, n: int = 8) -> dict:

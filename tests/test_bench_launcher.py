@@ -56,10 +56,39 @@ def test_bench_self_launch_dry_run(n):
     assert max(wa) <= n and max(wr) <= n and min(wa) >= 1 and min(wr) >= 1
     if n > 1:
         assert d["two_job_mixed_rounds"] >= 1          # both models' chunks in the same rounds
-        assert max(a + b for a, b in zip(wa[-3:], wr[-3:])) <= n
+        # while both jobs run they hold complementary, fixed GPU subsets (report
+        # Fig 2): every mixed round of the timed jobs has the same split, a + r = n
+        splits = d["two_job_mixed_splits"]
+        assert len(splits) == 1, splits
+        (key,) = splits
+        cnt = dict(kv.split(":") for kv in key.split(","))
+        a_n, r_n = int(cnt["alexnet"]), int(cnt["resnet18"])
+        assert a_n >= 1 and r_n >= 1 and a_n + r_n == n, key
+        # each job's queries run on its subset, or on every GPU while it runs alone
+        assert set(wa) <= {a_n, n} and set(wr) <= {r_n, n}, (wa, wr)
     assert d["coord_failover_images_exact"] is True
     assert d["coord_failover_recovery_s"] <= d["coord_failover_failure_timeout_s"] + 1.0, d
     assert d["coord_failover_undone_queries"] >= 1
+    # like-for-like fault tolerance -- the reference detector (0.3 s / 2 s)
+    # for the headline failover key, the tuned one as extra keys, a worker-failure phase
+    # (report Fig 4) and the second-job start time (report Fig 3)
+    assert d["coord_failover_heartbeat_s"] == 0.3 and d["coord_failover_failure_timeout_s"] == 2.0
+    assert d["coord_failover_tuned_failure_timeout_s"] == 1.0 and d["coord_failover_tuned_images_exact"] is True
+    assert d["coord_failover_rounds"] is (n >= 2)           # N >= 2: one node per GPU, collective rounds
+    assert d["worker_failover_rounds"] is (n >= 2)
+    if n >= 2:
+        assert d["coord_failover_survivor_world"] == n - 1
+        assert d["worker_failover_survivor_world"] == {"1": n - 1, "4": n - 1, "8": n - 1}
+    assert d["worker_failover_chunks_on_victim"] == {"1": 1, "4": 4, "8": 8}
+    assert d["worker_failover_images_exact"] is True
+    for k, t in d["worker_failover_recovery_s"].items():
+        assert 0 < t <= d["worker_failover_failure_timeout_s"] + 3.0, d["worker_failover_recovery_s"]
+    assert set(d["second_job_start_s"]) == {"alexnet_first", "resnet18_first"}
+    assert all(0 < v < 30 for v in d["second_job_start_s"].values())
+    # readiness keys: the live process group the timed rounds used
+    assert d["comm_world"] == n and (d["comm_backend"] == "gloo") == (n > 1)
+    assert d["ms_per_step_rank_min"] <= d["ms_per_step_rank_max"]
+    assert d["system_comm_world"] == n
 
 
 def test_bench_rank_failure_exits_nonzero():

@@ -41,3 +41,58 @@ def test_scheduler_assign_and_ema():
     assert s.n_workers("resnet18", alive) > s.n_workers("alexnet", alive)
     s.observe("resnet18", 3.0)
     assert abs(s.avg_time["resnet18"] - (0.7 * 9 + 0.3 * 3)) < 1e-9
+
+
+def test_partition_budget_below_model_count():
+    """budget 1 with two active jobs used to raise ValueError."""
+    from idunno.runtime.scheduler import partition
+
+    ws = [f"rank{i}" for i in range(8)]
+    p = partition({"alexnet": 1.0, "resnet18": 2.0}, ["alexnet", "resnet18"], ws, budget=1)
+    assert p == {"alexnet": ["rank0"], "resnet18": ["rank0"]}
+    p = partition({"a": 1, "b": 1, "c": 1}, ["a", "b", "c"], ws[:2], budget=8)
+    assert sorted(len(v) for v in p.values()) == [1, 1, 1]
+    s = FairTimeScheduler(budget=1, seed=0)
+    s.active_jobs = {"alexnet"}
+    plan = s.assign("resnet18", 0, 399, ws)
+    assert [(w, st, e) for w, st, e in plan] == [("rank0", 0, 399)]
+
+
+def test_subsets_fixed_under_ema_jitter():
+    """While the same two jobs run on the same workers the split never moves,
+    whatever the EMA does; it is recomputed when a job starts / ends, a worker
+    dies, or a model gets its first measurement."""
+    import random
+
+    s = FairTimeScheduler(budget=8, seed=0)
+    ws = [f"rank{i}" for i in range(8)]
+    both = {"alexnet", "resnet18"}
+    first = s.subsets(both, ws)                       # no measurements: equal split
+    assert [len(first["alexnet"]), len(first["resnet18"])] == [4, 4]
+    s.observe("alexnet", 3.0)                         # first measurements: recompute once
+    s.observe("resnet18", 5.0)
+    p0 = s.subsets(both, ws)
+    assert (len(p0["alexnet"]), len(p0["resnet18"])) == (3, 5)      # slower model gets more
+    assert set(p0["alexnet"]).isdisjoint(p0["resnet18"])
+    rng = random.Random(7)
+    for _ in range(200):                              # EMA jitter: +-60 %
+        s.observe("alexnet", 3.0 * rng.uniform(0.4, 1.6))
+        s.observe("resnet18", 5.0 * rng.uniform(0.4, 1.6))
+        assert s.subsets(both, ws) == p0
+        for m in both:                                # and every query lands on its subset
+            s.active_jobs = both
+            plan = s.assign(m, 0, 399, ws)
+            assert [w for w, _, _ in plan] == p0[m]
+    # a worker failure re-partitions over the survivors
+    p1 = s.subsets(both, ws[:7])
+    assert sum(len(v) for v in p1.values()) == 7 and set(p1["alexnet"]).isdisjoint(p1["resnet18"])
+    # a job alone takes every GPU
+    s.active_jobs = {"resnet18"}
+    assert len(s.assign("resnet18", 0, 399, ws)) == 8
+
+
+def test_adopted_averages_count_as_measurements():
+    s = FairTimeScheduler(budget=8)
+    s.adopt({"alexnet": 2.0, "resnet18": 6.0})
+    p = s.subsets({"alexnet", "resnet18"}, [f"r{i}" for i in range(8)])
+    assert (len(p["alexnet"]), len(p["resnet18"])) == (2, 6)

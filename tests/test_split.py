@@ -529,6 +529,12 @@ def test_split_activations_past_fp16_range_match_fp64(ops):
     err = (got - want).abs().max().item() / scale
     assert err <= 2e-5, f"rel logit err {err:.2e}"
     assert torch.equal(got.argmax(1), want.argmax(1))
+    # the eager forward() classifies the rerun logits: no OVERFLOW_CLASS rows,
+    # one f32 rerun per call (the stale flag marked every row -2)
+    cls, prob = r.forward(img)
+    assert r.overflow_reruns == 2
+    assert torch.equal(cls.cpu().long(), want.argmax(1))
+    assert abs(float(prob[0]) - torch.softmax(want, 1).max(1).values[0].item()) < 1e-4
     # a captured graph marks the batch instead (no host read inside the graph) ...
     sin, replay = r.capture(4)
     sin.copy_(img)
