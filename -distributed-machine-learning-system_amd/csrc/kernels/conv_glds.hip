@@ -43,6 +43,154 @@ __device__ __forceinline__ void wait_stages(int pending_stages) {
   wait_vmcnt<0>();
 }
 
+typedef float float16v __attribute__((ext_vector_type(16)));
+
+// Main loop + epilogue of the MF32 split tiles (see conv_glds_kernel): the
+// caller has issued the ring's first NS-1 stages; ``issue(buf)`` issues the
+// next stage's DMA into ring slot ``buf``.
+template <int BN, int BM, int WN, int WM, int NS, int G, int STAGE, int A_BYTES, bool HAS_RES, bool OUT_F32,
+          typename Issue>
+__device__ __forceinline__ void conv_glds_mf32_body(const ConvArgs& a, char* smem, int wave, int lane, int nK, int n0,
+                                                    int m0, bool second, Issue& issue) {
+  constexpr int RB = 128;                                   // 64 halfs per row (32 channels x hi, lo)
+  constexpr int TN = BN / WN, TM = BM / WM;
+  constexpr int F32N = TN / 32, F32M = TM / 32;
+  const int wn = wave / WM, wm = wave % WM;
+  float16v acc[F32N][F32M];
+#pragma unroll
+  for (int i = 0; i < F32N; ++i)
+#pragma unroll
+    for (int j = 0; j < F32M; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // per-lane byte offsets (within a stage) of fragment 0 for (k-step t, plane p):
+  // chunk 4p + 2t + (lane >> 5) of row (lane & 31); fragments 32 rows apart share
+  // the row swizzle (period 16), so fragment i is + i * 32 rows (an immediate)
+  const int hl = lane >> 5, r32 = lane & 31;
+  uint32_t fa[2][2], fb[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int ch = 4 * p + 2 * t + hl;
+      const int ra = wn * TN + r32, rb = wm * TM + r32;
+      fa[t][p] = (uint32_t)(ra * RB + ((ch ^ swz_r(ra, 8)) << 4));
+      fb[t][p] = (uint32_t)(A_BYTES + rb * RB + ((ch ^ swz_r(rb, 8)) << 4));
+    }
+  static_assert(32 * RB * (F32N > F32M ? F32N : F32M) <= 65536, "fragment offsets must fit the ds immediate");
+
+  for (int s = 0; s < nK; ++s) {
+    const int ahead = min(NS - 2, nK - 1 - s);
+    wait_stages<G, NS>(ahead);
+    __builtin_amdgcn_s_barrier();
+    if (s + NS - 1 < nK) issue((s + NS - 1) % NS);
+
+    const uint32_t base = lds_addr(smem) + (s % NS) * STAGE;
+    half8v ah[2][F32N], al[2][F32N], bh[2][F32M], bl[2][F32M];
+    // hi planes first (both k-steps), then lo: hi*hi issues as soon as they land
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < F32N; ++i) ah[t][i] = lds_read_b128_step<32 * RB>(base + fa[t][0], i);
+#pragma unroll
+      for (int j = 0; j < F32M; ++j) bh[t][j] = lds_read_b128_step<32 * RB>(base + fb[t][0], j);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < F32N; ++i) al[t][i] = lds_read_b128_step<32 * RB>(base + fa[t][1], i);
+#pragma unroll
+      for (int j = 0; j < F32M; ++j) bl[t][j] = lds_read_b128_step<32 * RB>(base + fb[t][1], j);
+    }
+    constexpr int NLO = 2 * (F32N + F32M);
+    lds_waitcnt<NLO>();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < F32N; ++i) lds_tie(ah[t][i]);
+#pragma unroll
+      for (int j = 0; j < F32M; ++j) lds_tie(bh[t][j]);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < F32N; ++i)
+#pragma unroll
+        for (int j = 0; j < F32M; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t][i], bh[t][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);          // hi*hi stays above the second wait
+    lds_waitcnt<0>();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < F32N; ++i) lds_tie(al[t][i]);
+#pragma unroll
+      for (int j = 0; j < F32M; ++j) lds_tie(bl[t][j]);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < F32N; ++i)
+#pragma unroll
+        for (int j = 0; j < F32M; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t][i], bl[t][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t][i], bh[t][j], acc[i][j], 0, 0, 0);
+        }
+  }
+
+  // ---- epilogue: x 2^-e, +bias (+split residual) (+ReLU), split (or fp32) NHWC store ----
+  // the ring is drained (last wait vmcnt(0)): ordinary loads; one cout fragment at a time
+  const float acc_scale = second ? a.acc_scale2 : a.acc_scale;
+  const bool relu = a.relu && !second;
+#pragma unroll
+  for (int i = 0; i < F32N; ++i) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int n = n0 + wn * TN + i * 32 + 8 * g + 4 * hl;
+      if (n >= a.Cout) continue;
+      const float4v bv = *reinterpret_cast<const float4v*>(a.bias + n);
+      half4v rh[F32M], rl[F32M];
+      if constexpr (HAS_RES) {
+#pragma unroll
+        for (int j = 0; j < F32M; ++j) {
+          const int m = m0 + wm * TM + j * 32 + r32;
+          const size_t off = m < a.M ? (size_t)m * (a.ldr ? a.ldr : 2 * a.Cout) + split_off(n) : 0;
+          rh[j] = *reinterpret_cast<const half4v*>(a.res + off);
+          rl[j] = *reinterpret_cast<const half4v*>(a.res + off + 32);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < F32M; ++j) {
+        const int m = m0 + wm * TM + j * 32 + r32;
+        if (m >= a.M) continue;
+        float4v v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = acc[i][j][4 * g + q] * acc_scale + bv[q];
+        if constexpr (HAS_RES) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += (float)rh[j][q] + (float)rl[j][q];
+        }
+        if (relu) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+        }
+        if constexpr (OUT_F32) {
+          *reinterpret_cast<float4v*>(static_cast<float*>(a.y) + (size_t)m * a.ldy + n) = v;
+        } else {
+          split_guard(a.ovf, v);
+          half4v h, l;
+          split_f16x4(v, h, l);
+          half_t* yp = static_cast<half_t*>(a.y) + (size_t)m * a.ldy + split_off(n);
+          *reinterpret_cast<half4v*>(yp) = h;
+          *reinterpret_cast<half4v*>(yp + 32) = l;
+        }
+      }
+    }
+  }
+}
+
+
 // P3: RGB stem on packed rows (preprocess_pack3_f16, x = [B][H][nc][wp] halfs):
 // the 3*KW halfs of one kernel row are contiguous in the row copy in which
 // they start 16-byte aligned; K = (kh, 16-byte chunk), ceil(3*KW/8) chunks per
@@ -58,15 +206,28 @@ __device__ __forceinline__ void wait_stages(int pending_stages) {
 // are pre-scaled by 2^e (max |w| ~ 2^14, so their lo parts stay normal) and
 // the epilogue multiplies by a.acc_scale = 2^-e (exact).  Residual in, output
 // out in the same split layout (or fp32 with OUT_F32).
+//
+// MF32: the split product on v_mfma_f32_32x32x16_f16 instead of 16x16x32 --
+// half the MFMA instructions per stage (12 instead of 24 for a 64x32 wave
+// tile), so the stage's DMA issue, fragment reads, waits and barrier fit in
+// the longer gaps (a 32x32x16 MFMA leaves 24 of its 32 issue cycles, a
+// 16x16x32 one 8 of 16; the split loop was issue-bound, docs/KERNELS.md).
+// Same LDS image and swizzle: a 32x32x16 operand fragment is 32 rows x 16 k,
+// lane l reads row l & 31, chunk 2t + (l >> 5) of k-step t (+4 for the lo
+// plane); the row XOR is conflict-free for these lane groups too.  C/D
+// layout: register r of a 32x32 accumulator is row 8(r/4) + 4(l>>5) + r%4,
+// column l & 31, so each lane still stores 4 consecutive output channels.
 template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false,
-          bool SPLIT = false>
+          bool SPLIT = false, bool MF32 = false>
 __global__ void __launch_bounds__(64 * WN * WM, (BM % 64 != 0 && WN * WM == 8) ? 4 : 1)   // 2nd: min waves per SIMD
 conv_glds_kernel(const ConvArgs a) {
   static_assert(!SPLIT || BK == 64, "split stages are 32 channels x (hi, lo)");
+  static_assert(!MF32 || (SPLIT && !P3), "32x32x16 tiles: split convs");
   constexpr int NW = WN * WM;
   constexpr int NT = 64 * NW;
   constexpr int TN = BN / WN, TM = BM / WM;
-  constexpr int FN = TN / 16, FM = TM / 16;
+  static_assert(!MF32 || (TN % 32 == 0 && TM % 32 == 0), "32x32 wave fragments");
+  constexpr int FN = MF32 ? 1 : TN / 16, FM = MF32 ? 1 : TM / 16;
   constexpr int CPR = BK / 8;                 // 16-byte chunks per row
   constexpr int RB = BK * 2;                  // bytes per row
   constexpr int RPI = 64 / CPR;               // rows per DMA instruction (1 KiB)
@@ -277,6 +438,15 @@ conv_glds_kernel(const ConvArgs a) {
         dma_buf4(x_rsrc, dummy, line < nl ? (uint32_t)(lo + ((long long)line << 7)) : OOR);
       }
     }
+  }
+
+  if constexpr (MF32) {
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+      if (p < nK) issue(p);
+    conv_glds_mf32_body<BN, BM, WN, WM, NS, G, STAGE, A_BYTES, HAS_RES, OUT_F32>(a, smem, wave, lane, nK, n0, m0,
+                                                                                 second, issue);
+    return;
   }
 
   float4v acc[FN][FM];
@@ -510,7 +680,7 @@ static int g_l2pf = 0;   // conv_glds input-footprint L2 prefetch: bit 0 fp16 co
 void set_conv_l2_prefetch(int mode) { g_l2pf = mode; }
 
 template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false,
-          bool SPLIT = false>
+          bool SPLIT = false, bool MF32 = false>
 static void glds_cfg(ConvArgs a, hipStream_t st) {
   a.tiles_n = (a.Cout + BN - 1) / BN;
   a.tiles_m = (a.M + BM - 1) / BM;
@@ -526,7 +696,7 @@ static void glds_cfg(ConvArgs a, hipStream_t st) {
   constexpr int RPI_ = 64 / (BK / 8), NW_ = WN * WM;
   constexpr int BMD = (BM + RPI_ * NW_ - 1) / (RPI_ * NW_) * (RPI_ * NW_);
   const size_t lds = (size_t)NS * (BN + BMD) * BK * 2;
-  auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32, P3, SPLIT>;
+  auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32, P3, SPLIT, MF32>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), (int)lds);   // per (kernel, device), launch_util.h
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WN * WM), lds, st, a);
 }
@@ -577,7 +747,6 @@ static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
     case 38: glds_cfg<128, 64, 64, 2, 4, 2, R, F>(a, st); return true;    // 8 waves (32x16 wave tile)
     case 39: glds_cfg<128, 128, 32, 2, 4, 4, R, F>(a, st); return true;   // 8 waves, 64 KiB, 3 stages in flight
     case 42: glds_cfg<128, 160, 64, 4, 2, 2, R, F>(a, st); return true;   // 8 waves, B as 192 rows, 80 KiB (small M)
-    case 43: glds_cfg<256, 160, 64, 8, 2, 2, R, F>(a, st); return true;   // 16 waves (32x80 each), B as 256 rows, 128 KiB
     default: return false;
   }
 }
@@ -616,6 +785,11 @@ static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
     // 128 x 160 (B staged as 192 rows): 0.96 waves of blocks on ResNet layer4
     // at B = 400 where 128 x 64 tiles make 1.6 (the partial last wave idles)
     case 42: glds_cfg<128, 160, 64, 4, 2, 2, R, F, false, true>(a, st); return true;    // 8 waves, 80 KiB
+    // 32x32x16 MFMA tiles (MF32): 56 = tile 36's shape (64x32 wave tiles), 57 = 128 x 128 on 4 waves
+    // (64x64 wave tiles), 58 = 128 x 192 on 8 waves (32x96 wave tiles, the layer4-sized GEMMs)
+    case 56: glds_cfg<128, 128, 64, 2, 4, 2, R, F, false, true, true>(a, st); return true;
+    case 57: glds_cfg<128, 128, 64, 2, 2, 2, R, F, false, true, true>(a, st); return true;
+    case 58: glds_cfg<128, 192, 64, 4, 2, 2, R, F, false, true, true>(a, st); return true;
     default: return false;
   }
 }
@@ -636,8 +810,13 @@ static bool g_split_wide_l3 = false;
 void set_split_wide_l3(bool on) { g_split_wide_l3 = on; }
 static bool g_split_wide_all = false;
 void set_split_wide_all(bool on) { g_split_wide_all = on; }
+static int g_split_mf32 = 0;
+void set_split_mf32(int mode) { g_split_mf32 = mode; }
+int split_mf32() { return g_split_mf32; }
 int conv_glds_split_pick(int M, int Cout) {
   if (Cout % 128 == 0) {
+    if ((g_split_mf32 & 1) && M >= 50000) return 56;
+    if ((g_split_mf32 & 2) && M < 50000) return 58;
     if (g_split_wide && g_split_wide_all) return 42;
     if (g_split_wide && g_split_wide_l3 && M >= 50000 && M < 100000) return 42;   // layer3: 1.91 vs 2.39 waves
     if (M >= 50000) return 36;

@@ -10,10 +10,11 @@ Replaces the reference's per-chunk TCP messages on the hot path
         one RCCL gather of packed top-1 results (int32 class + fp32 prob,
         8 B/image, 3.2 KB for a 400-image chunk) to the coordinator rank
         (and, optionally, a second one to the standby rank).
-  * M9  data variant -> ``scatter``: the coordinator holds a query's images in
-        HBM and sends every rank its chunk with one grouped point-to-point
-        send per peer, so the 7 xGMI links of the root carry the shards
-        concurrently (60 MB for a 400-image query, 7.5 MB per rank at 8).
+  * M9  data variant -> ``scatter`` / ``scatter_async``: the coordinator
+        holds a query's images in HBM and sends every rank its chunk with one
+        grouped point-to-point send per peer, so the 7 xGMI links of the root
+        carry the shards concurrently (60 MB per 400-image chunk); bench.py
+        measures it double-buffered against compute (``images_per_s_scatter``).
 In steady state images do not cross the fabric at all: every rank stages its
 own shard host->HBM (``idunno.runtime.data.HbmStager`` / ``SdfsSource``) and
 ``scatter`` is used only when the images live on the coordinator.
@@ -176,6 +177,35 @@ class QueryPlane:
         for req in dist.batch_isend_irecv([dist.P2POp(dist.irecv, buf, self.coord, self.group)]):
             req.wait()
         return buf
+
+    def scatter_async(self, images: torch.Tensor | None, chunks, out: torch.Tensor) -> list:
+        """Non-blocking fixed-size scatter into ``out`` (every rank's receive
+        buffer, [n, ...]): the coordinator sends rank r the rows
+        ``images[chunks[r][0]:chunks[r][1] + 1]`` (one grouped P2P op per peer:
+        the root's 7 xGMI links carry the shards concurrently) and copies its
+        own chunk into ``out``.  Returns the requests; ``wait_scatter`` makes
+        the CURRENT stream wait for them (RCCL) -- the host does not block.
+
+        Ordering on RCCL: the communication stream waits for the work queued
+        on the current stream when the ops are posted, so post a buffer's
+        next scatter BEFORE queuing the compute that overlaps it and AFTER the
+        compute that last read that buffer."""
+        if self.env.rank == self.coord:
+            s0, e0 = chunks[self.coord]
+            out[: e0 - s0 + 1].copy_(images[s0:e0 + 1], non_blocking=True)
+            ops = [dist.P2POp(dist.isend, images[s:e + 1], peer, self.group)
+                   for peer, (s, e) in enumerate(chunks) if peer != self.coord]
+        else:
+            s, e = chunks[self.env.rank]
+            ops = [dist.P2POp(dist.irecv, out[: e - s + 1], self.coord, self.group)]
+        if not ops or not self.env.distributed:
+            return []
+        return dist.batch_isend_irecv(ops)
+
+    @staticmethod
+    def wait_scatter(reqs: list) -> None:
+        for r in reqs:
+            r.wait()
 
     # -- M11 --------------------------------------------------------------------
     @property

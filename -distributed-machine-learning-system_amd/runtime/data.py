@@ -81,6 +81,10 @@ class HbmStager:
         self.pinned = [torch.empty(per, dtype=torch.uint8, pin_memory=self.gpu) for _ in range(nbuf)]
         self._done = [None] * nbuf        # event of the last copy out of each buffer
         self.lock = threading.Lock()
+        self.bytes_staged = 0
+        # optional GPU timeline: ("h2d", start event, end event, bytes) per stage() call
+        # on the side stream (bench.py lines it up against the forwards' events)
+        self.timeline: list | None = None
 
     def stage(self, data: bytes | np.ndarray, shape: tuple) -> torch.Tensor:
         """Copy host bytes to a new device tensor of ``shape`` (uint8).  The
@@ -95,6 +99,10 @@ class HbmStager:
         nb = len(self.pinned)
         with self.lock:
             ev = None
+            tl = self.timeline
+            if tl is not None:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record(self.stream)
             for i, off in enumerate(range(0, src.size, step)):
                 b = i % nb
                 n = min(step, src.size - off)
@@ -106,6 +114,11 @@ class HbmStager:
                     ev = torch.cuda.Event()
                     ev.record(self.stream)
                 self._done[b] = ev
+            if tl is not None:
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record(self.stream)
+                tl.append(("h2d", ev0, ev1, src.size))
+            self.bytes_staged += src.size
         if ev is not None:
             torch.cuda.current_stream(self.device).wait_event(ev)
         return out.view(*shape)

@@ -346,6 +346,14 @@ class JobState:
             self._bump("result", model, qnum, start, end, now)
             return True
 
+    def record_results(self, recs, now: float | None = None) -> int:
+        """Ingest several finished chunks [(model, qnum, worker, s, e, cls,
+        prob)] under one lock hold (a collective round); returns how many were
+        new.  Same semantics as ``record_result`` per chunk."""
+        now = self.clock() if now is None else now
+        with self.lock:
+            return sum(1 for m, q, w, s, e, c, p in recs if self.record_result(m, q, w, s, e, c, p, now))
+
     def reopen_unheld(self) -> int:
         """Chunks marked finished in the replicated tables whose images this
         node never received (their RESULT reached only the old coordinator)

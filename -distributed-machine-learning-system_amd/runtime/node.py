@@ -83,6 +83,7 @@ class Node:
         self._meta_lock = threading.Lock()          # one standby push at a time
         self.device = getattr(executor, "device", None)  # GPU of this node (None = CPU)
         self.rounds = None                          # collective round plane (cfg.collective_rounds)
+        self.gpu_timeline: list | None = None       # bench: ("fwd", ev0, ev1, n) per round chunk when set
         self.transport.dead_check = self._peer_dead
         self.membership.on_failure.append(self._on_node_failure)
         self.membership.on_master_failure.append(self._on_master_failure)
@@ -408,6 +409,20 @@ class Node:
         if new:
             with self._progress:
                 self._progress.notify_all()
+
+    def _ingest_round(self, recs: list, now: float, seq: int = -1) -> int:
+        """Coordinator: every chunk of one finished collective round,
+        [(model, qnum, worker, s, e, cls, prob)], in one job-state call; one
+        trace event and one progress notification per round.  Returns the
+        number of new chunks."""
+        if not recs:
+            return 0
+        new = self.state.record_results(recs, now)
+        self.tracer.instant("round.ingest", seq=seq, chunks=len(recs), new=new)
+        if new:
+            with self._progress:
+                self._progress.notify_all()
+        return new
 
     MAX_CHUNK_RETRIES = 3
 

@@ -108,6 +108,13 @@ class RoundPlane:
         self._hdr = None
         self._tag = 0
         self._next_seq = 0                    # coordinator: seq of the next round of this epoch
+        self._mirror_q = None                 # coordinator: rounds waiting for the standby mirror thread
+        # coordinator host time: building / posting rounds and ingesting them (host_s), and
+        # blocked on a gather (host_wait_s); bench.py reports host_s per round
+        self.host_s = 0.0
+        self.host_wait_s = 0.0
+        self.host_post_s = 0.0                # of host_s: posting (descriptors, own chunk, gather)
+        self.host_send_s = 0.0                # of host_post_s: ROUND descriptor sends
 
     # -- lifecycle -------------------------------------------------------------------
     def start(self) -> None:
@@ -193,6 +200,8 @@ class RoundPlane:
                 "mixed_rounds": self.mixed_rounds, "mixed_splits": dict(self.mixed_splits),
                 "max_queries_per_round": self.max_queries_per_round,
                 "parked": self.parked, "pending_collectives": self.pending_collectives(),
+                "host_s": self.host_s, "host_wait_s": self.host_wait_s, "host_post_s": self.host_post_s,
+                "host_send_s": self.host_send_s,
                 "queued": len(self._queue)}
 
     def pending_collectives(self) -> int:
@@ -251,6 +260,9 @@ class RoundPlane:
                 evs = run_packed(model, imgs, send[:cnt])
                 if evs is not None:
                     self._timings.append((mid, cnt, evs))
+                    tl = n.gpu_timeline
+                    if tl is not None:
+                        tl.append(("fwd", evs[0], evs[1], cnt))
             else:
                 t0 = time.perf_counter()
                 cls, prob = n.executor.run(model, imgs, s, e)
@@ -408,7 +420,9 @@ class RoundPlane:
                     self._finalize_oldest(members, check)
                 while inflight and inflight[0].work.is_completed():
                     self._finalize_oldest(members, check)
+                tb = time.perf_counter()
                 qs, stale = self._build(members)
+                self.host_s += time.perf_counter() - tb
                 for q in stale:
                     self._fallback_query(q)
                 if not qs:
@@ -427,10 +441,14 @@ class RoundPlane:
                         return        # hand back to the driver loop now and then (cheap)
                     continue
                 idle_since = time.monotonic()
+                tp = time.perf_counter()
                 r = _Round(self._next_seq, qs, self._table(members, qs))
                 self._next_seq += 1
                 inflight.append(r)
                 self._post(r, members)
+                dt = time.perf_counter() - tp
+                self.host_s += dt
+                self.host_post_s += dt
             while inflight:
                 self._finalize_oldest(members, check)
             self._stop_epoch()
@@ -474,11 +492,15 @@ class RoundPlane:
 
     def _post(self, r: _Round, members: tuple) -> None:
         n, g = self.node, self.group
-        for i, m in enumerate(members[1:], 1):
-            row = r.table[i]
-            msg = {"t": Type.ROUND, "epoch": g.epoch, "seq": r.seq, "row": list(row) if row else None}
-            if not n.transport.send(m, msg):
-                raise RoundAbandoned(f"ROUND {r.seq} to {m} not delivered")
+        ts = time.perf_counter()
+        # ONE frame with the whole descriptor table (member i reads row i), encoded
+        # once and written to every member's link
+        msg = {"t": Type.ROUND, "epoch": g.epoch, "seq": r.seq,
+               "rows": [list(row) if row else None for row in r.table]}
+        lost = n.transport.multicast(members[1:], msg)
+        if lost:
+            raise RoundAbandoned(f"ROUND {r.seq} to {lost} not delivered")
+        self.host_send_s += time.perf_counter() - ts
         if r.table[0] is not None:
             self._run_chunk(r.table[0], r.seq)
         self._write_header(r.seq)
@@ -501,14 +523,19 @@ class RoundPlane:
         self._inflight.popleft()
 
     def _finalize(self, r: _Round, members: tuple, check) -> None:
-        """Wait for round ``r``'s gather, ingest every chunk, feed the members'
-        measured compute times to the scheduler, mirror the results to the
-        standby in one message."""
+        """Wait for round ``r``'s gather, ingest every chunk with ONE job-state
+        call, feed the members' measured compute times to the scheduler, and
+        hand the round to the standby mirror thread (the
+        host work per round is one lock hold plus O(members) array views; the
+        TCP send to the standby never runs on this thread)."""
         n, g = self.node, self.group
+        t_wait = time.perf_counter()
         arr = g.collect(r.seq, r.work, check)
+        t0 = time.perf_counter()
+        self.host_wait_s += t0 - t_wait
         mc = g.max_chunk
         now = time.time()
-        batch = []
+        recs = []
         for i, row in enumerate(r.table):
             us, hmid, cnt = int(arr[i, mc, 0]), int(arr[i, mc, 1]), int(arr[i, mc + 1, 0])
             if cnt > 0 and hmid in MODEL_NAMES:
@@ -526,14 +553,37 @@ class RoundPlane:
                             n.name, MODEL_NAMES[mid], qnum, s, e, members[i])
                 n._send_job(members[i], MODEL_NAMES[mid], qnum, s, e)
                 continue
-            res = {"t": Type.RESULT, "model": MODEL_NAMES[mid], "qnum": qnum, "start": s, "end": e,
-                   "worker": members[i], "cls": cls.tobytes(), "prob": prob.tobytes(),
-                   "epoch": n.membership.epoch, "t_done": now}
-            n._ingest_result(dict(res, src=n.name))
-            batch.append(res)
+            recs.append((MODEL_NAMES[mid], qnum, members[i], s, e, cls, prob))
+        n._ingest_round(recs, now, seq=r.seq)
         self.rounds_done += 1
-        if batch and n.standby != n.name and n.membership.is_alive(n.standby):
-            n.transport.send(n.standby, {"t": Type.RESULTS, "results": batch})
+        if recs and n.standby != n.name and n.membership.is_alive(n.standby):
+            self._mirror(recs, now)
+        self.host_s += time.perf_counter() - t0
+
+    def _mirror(self, recs: list, now: float) -> None:
+        """Queue a finished round for the standby (RESULTS message built and
+        sent on the mirror thread).  Results are idempotent by chunk key, and
+        a mirror that falls behind only delays the standby's copy."""
+        if self._mirror_q is None:
+            import queue
+
+            self._mirror_q = queue.Queue()
+
+            def run():
+                n = self.node
+                while n.alive_flag:
+                    item = self._mirror_q.get()
+                    if item is None:
+                        return
+                    rs, t = item
+                    batch = [{"t": Type.RESULT, "model": m, "qnum": q, "start": s, "end": e, "worker": w,
+                              "cls": c.tobytes(), "prob": p.tobytes(), "epoch": n.membership.epoch, "t_done": t}
+                             for m, q, w, s, e, c, p in rs]
+                    if n.standby != n.name and n.membership.is_alive(n.standby):
+                        n.transport.send(n.standby, {"t": Type.RESULTS, "results": batch})
+
+            threading.Thread(target=run, name=f"{self.node.name}-mirror", daemon=True).start()
+        self._mirror_q.put((recs, now))
 
     def _stop_epoch(self) -> None:
         """End an idle epoch cleanly: every member gets STOP as its next round
@@ -622,6 +672,7 @@ class RoundPlane:
         g = self.group
         check = self._check_member(members[0])
         inflight = self._inflight
+        me = members.index(self.node.name)
         abandoned = False
         seq = 0
         try:
@@ -633,7 +684,8 @@ class RoundPlane:
                     break
                 while inflight and inflight[0][0] <= seq - g.depth:
                     g.release(inflight.popleft()[1], check)
-                row = msg.get("row")
+                rows = msg.get("rows")
+                row = rows[me] if rows is not None else msg.get("row")
                 if row is not None:
                     self._run_chunk(row, seq)
                 self._write_header(seq)

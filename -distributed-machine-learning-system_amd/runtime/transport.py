@@ -59,6 +59,15 @@ class BaseTransport:
         msg.setdefault("src", self.name)
         return self._send_raw(dst, msg)
 
+    def multicast(self, dsts, msg: dict) -> list[str]:
+        """Send one message to several peers; returns the peers it did not
+        reach.  TCP encodes the frame once and writes the same bytes to every
+        link (a round's descriptor table goes to all members this way)."""
+        if self.closed:
+            return list(dsts)
+        msg.setdefault("src", self.name)
+        return [d for d in dsts if not self._send_raw(d, msg)]
+
     def request(self, dst: str, msg: dict, timeout: float = 5.0) -> dict:
         rid = next(self._rid)
         fut: Future = Future()
@@ -274,8 +283,17 @@ class TcpTransport(BaseTransport):
             except OSError:
                 pass
 
-    def _send_raw(self, dst: str, msg: dict) -> bool:
+    def multicast(self, dsts, msg: dict) -> list[str]:
+        if self.closed:
+            return list(dsts)
+        msg.setdefault("src", self.name)
         data = encode(msg)
+        return [d for d in dsts if not self._send_bytes(d, data)]
+
+    def _send_raw(self, dst: str, msg: dict) -> bool:
+        return self._send_bytes(dst, encode(msg))
+
+    def _send_bytes(self, dst: str, data: bytes) -> bool:
         with self._olock:
             lk = self._out_locks.setdefault(dst, threading.Lock())
         with lk:

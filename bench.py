@@ -105,6 +105,10 @@ def parse(argv=None):
     ap.add_argument("--extras-timeout", type=float, default=150.0,
                     help="seconds per system / failover phase (bounded: the driver gives the whole run 600 s)")
     ap.add_argument("--two-job-queries", type=int, default=10, help="queries per job in the two-job run")
+    ap.add_argument("--sdfs-images", type=int, default=4000,
+                    help="N=1 system phase: images put into SDFS as 500-image shards, then served cold and warm")
+    ap.add_argument("--sdfs-trace", default=None, help="write the SDFS cold pass's H2D / forward GPU timeline "
+                                                      "(chrome trace JSON) here")
     ap.add_argument("--failover-queries", type=int, default=12, help="queries of the job the failover kills into")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
@@ -344,6 +348,7 @@ def _phase_argv(a, phase: str, out: str, work: str) -> list:
             "--worker-kill-chunks", ",".join(str(k) for k in a.worker_kill_chunks),
             "--dtype", a.dtype, "--fp32-impl", a.fp32_impl, "--batch", str(a.batch), "--seed", str(a.seed),
             "--two-job-queries", str(a.two_job_queries), "--failover-queries", str(a.failover_queries),
+            "--sdfs-images", str(a.sdfs_images), *(["--sdfs-trace", a.sdfs_trace] if a.sdfs_trace else []),
             "--phase", phase, "--json-out", out, "--work-dir", work, "--launch-timeout", str(a.extras_timeout)]
     if a.dry_run:
         argv.append("--dry-run")
@@ -480,11 +485,49 @@ def run_rank(a) -> int:
 
     def make_run(runner, batch):
         if runner is None:
-            return FakeRunner(env.device).window(dataset, batch, start_dev, send)
+            r = FakeRunner(env.device).window(dataset, batch, start_dev, send)
+            return lambda q: r()
         if a.no_graph:
-            return lambda: runner.forward(dataset, start_dev, batch, 0, send)
+            return lambda q: runner.forward(dataset, start_dev, batch, 0, send)
         _, run = runner.capture_window(dataset, batch, start=start_dev, start_offset=0, packed=send)
-        return run
+        return lambda q: run()
+
+    def make_scatter_run(runner, batch, per_round):
+        """M9 data variant: the images live only in the coordinator's HBM.
+        Round q's chunks are scattered to the ranks (grouped P2P, RCCL over
+        xGMI) into one of two receive buffers while round q-1 computes on the
+        other; each rank's captured forward reads its receive buffer."""
+        shape = (batch, 224, 224, 3) if not a.dry_run else (batch, 4, 4, 3)
+        bufs = [torch.zeros(shape, dtype=torch.uint8, device=env.device) for _ in range(2)]
+        src = dataset if not a.dry_run else (torch.zeros((D,) + shape[1:], dtype=torch.uint8) if coord else None)
+        if runner is None:
+            fakes = [FakeRunner(env.device).window(dataset, batch, start_dev, send) for _ in range(2)]
+        else:
+            fakes = []
+            for b in bufs:
+                st0, rep = runner.capture_window(b, batch, packed=send)
+                st0.zero_()
+                fakes.append(rep)
+        posted = {}
+
+        def chunks_of(q):
+            off = (q * per_round) % (D - max(per_round, plane.max_chunk) + 1)
+            return split_range(off, off + per_round - 1, W)
+
+        def run(q):
+            if q not in posted:
+                posted[q] = plane.scatter_async(src, chunks_of(q), bufs[q % 2])
+            # round q+1's scatter goes on the RCCL stream BEFORE round q's forward is
+            # queued: it waits only for round q-1 (the last reader of its buffer)
+            posted[q + 1] = plane.scatter_async(src, chunks_of(q + 1), bufs[(q + 1) % 2])
+            plane.wait_scatter(posted.pop(q))
+            fakes[q % 2]()
+
+        def finish():
+            for reqs in posted.values():
+                plane.wait_scatter(reqs)
+            posted.clear()
+        return run, finish
 
     def measure(run, per_round: int, steps: int, warmup: int, label: str):
         """Time `steps` pipelined rounds of `per_round` images (split over the
@@ -522,7 +565,7 @@ def run_rank(a) -> int:
             if a.fail_rank == env.rank and q == warmup:
                 print(f"bench: rank {env.rank} failing on purpose (--fail-rank)", file=sys.stderr, flush=True)
                 os._exit(3)
-            run()
+            run(q)
             if timing[0] and gpu:
                 g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 g0.record()
@@ -618,6 +661,15 @@ def run_rank(a) -> int:
                                f"ms_per_step_fp32_{alt}": round(1000 * m3["elapsed"] / a.steps, 4)})
             if coord:
                 extras.update(numerics_check(runner, a, env.device))
+        if W > 1:
+            # M9 data variant: images only in the coordinator's HBM,
+            # scattered every round over RCCL, double-buffered against compute
+            srun, sfinish = make_scatter_run(runner, B, W * B)
+            sc = measure(srun, W * B, a.steps, a.warmup, "scatter")
+            sfinish()
+            extras.update({"images_per_s_scatter": round(sc["ips"], 2),
+                           "ms_per_step_scatter": round(1000 * sc["elapsed"] / a.steps, 4),
+                           "scatter_mb_per_round": round((W - 1) * B * 150528 / 1e6, 1)})
 
     if coord:
         ips = head["ips"]
@@ -795,10 +847,12 @@ def _drive_system(a, node, W: int, B: int) -> dict:
     submit(a.warmup)
     assert wait_done(nxt[0]), st.summary()
     lat0 = len(st.query_latency[a.model])
+    ra = node.rounds.stats() if node.rounds is not None else None
     t0 = time.perf_counter()
     submit(a.steps)
     assert wait_done(nxt[0]), st.summary()
     elapsed = time.perf_counter() - t0
+    rb = node.rounds.stats() if node.rounds is not None else None
     loaded = sorted(st.query_latency[a.model][lat0:])
     lat1 = len(st.query_latency[a.model])
     for _ in range(max(5, min(a.steps, 20))):   # unloaded: one query at a time
@@ -815,6 +869,17 @@ def _drive_system(a, node, W: int, B: int) -> dict:
                               if node.rounds is not None else "local JOB queue")
                            + " -> job-state ingest"),
            "system_results_recorded": st.images_done(a.model)}
+    if ra is not None and rb["rounds_done"] > ra["rounds_done"]:
+        # the coordinator's own host work per round (plan, post, ingest; not the gather wait)
+        nr = rb["rounds_done"] - ra["rounds_done"]
+        out["system_host_ms_per_round"] = round(1000 * (rb["host_s"] - ra["host_s"]) / nr, 4)
+        out["system_host_wait_ms_per_round"] = round(1000 * (rb["host_wait_s"] - ra["host_wait_s"]) / nr, 4)
+        out["system_rounds"] = nr
+        out["system_host_post_ms_per_round"] = round(1000 * (rb["host_post_s"] - ra["host_post_s"]) / nr, 4)
+        out["system_host_send_ms_per_round"] = round(1000 * (rb["host_send_s"] - ra["host_send_s"]) / nr, 4)
+
+    if W == 1 and a.sdfs_images > 0:
+        out.update(_sdfs_pass(a, node, per_q, wait_for))
 
     # two concurrent jobs: AlexNet + ResNet18 (report Fig 2), coordinator-side jobs
     bs = {"alexnet": QUERY_ALEXNET * W, "resnet18": QUERY * W}
@@ -884,6 +949,88 @@ def _drive_system(a, node, W: int, B: int) -> dict:
     grp = node.rounds.group.describe() if node.rounds is not None else {}
     out["system_comm_backend"] = grp.get("backend", "tcp (no collective)")
     out["system_comm_world"] = grp.get("world", 1)
+    return out
+
+
+def _timeline_overlap(tl: list) -> tuple[float, list]:
+    """Fraction of the H2D staging time (side stream) that ran while a forward
+    (private compute stream) was executing, from the recorded CUDA events, and
+    the intervals as (kind, start ms, end ms, n) on one clock."""
+    if not tl:
+        return 0.0, []
+    ref = tl[0][1]
+    iv = [(k, ref.elapsed_time(e0), ref.elapsed_time(e1), n) for k, e0, e1, n in tl]
+    fw = sorted((t0, t1) for k, t0, t1, _ in iv if k == "fwd")
+    tot = ov = 0.0
+    for k, t0, t1, _ in iv:
+        if k != "h2d":
+            continue
+        tot += t1 - t0
+        ov += sum(max(0.0, min(t1, f1) - max(t0, f0)) for f0, f1 in fw)
+    return (ov / tot if tot > 0 else 0.0), iv
+
+
+def _sdfs_pass(a, node, per_q: int, wait_for) -> dict:
+    """SDFS -> HBM on the measured path: the synthetic
+    dataset is put into SDFS as 500-image uint8 shards, then the same ResNet18
+    queries are served from ``SdfsSource`` -- cold (every shard read from the
+    node's SDFS store and staged host -> HBM through pinned ping-pong buffers
+    on a side stream while the previous round computes) and warm (HBM-cached
+    shards).  Reference: images are read from local disk per image,
+    alexnet_resnet.py:24,49."""
+    import torch
+
+    from idunno.runtime.data import SdfsSource, put_synthetic_dataset
+
+    st, cfg = node.state, node.cfg
+    n_img = max(per_q, a.sdfs_images // per_q * per_q)
+    t = time.perf_counter()
+    shards = put_synthetic_dataset(node.sdfs, n_img, cfg.data_seed, shard_images=500)
+    put_s = time.perf_counter() - t
+    keep = node.source
+    src = SdfsSource(node.sdfs, node.device if node.device is not None else "cpu", shard_images=500,
+                     peer_copy=False)
+    gpu = src.device.type == "cuda"
+    node.source = src
+    out = {}
+    try:
+        def run_pass(label):
+            done0 = st.images_done(a.model)
+            t0 = time.perf_counter()
+            for q0 in range(0, n_img, per_q):
+                node.submit_query(a.model, q0, q0 + per_q - 1)
+            assert wait_for(lambda: st.images_done(a.model) >= done0 + n_img and st.pending_count() == 0,
+                            300, 0.0005), st.summary()
+            return time.perf_counter() - t0
+
+        tl = [] if gpu else None
+        src.stager.timeline = tl
+        node.gpu_timeline = tl
+        b0 = src.stager.bytes_staged
+        cold = run_pass("cold")
+        node.gpu_timeline = src.stager.timeline = None
+        staged = src.stager.bytes_staged - b0
+        if gpu:
+            torch.cuda.synchronize(src.device)
+        ovl, iv = _timeline_overlap(tl) if gpu else (None, [])
+        warm = run_pass("warm")
+        h2d_ms = sum(t1 - t0 for k, t0, t1, _ in iv if k == "h2d")
+        out = {"value_system_sdfs_cold": round(n_img / cold, 2), "value_system_sdfs_warm": round(n_img / warm, 2),
+               "sdfs_cold_to_warm": round(warm / cold, 4), "sdfs_images": n_img, "sdfs_shards": shards,
+               "sdfs_put_gb_per_s": round(n_img * 150528 / put_s / 1e9, 3),
+               "sdfs_bytes_staged": staged,
+               "hbm_stage_gb_per_s": round(staged / (h2d_ms * 1e-3) / 1e9, 2) if h2d_ms > 0 else None,
+               "sdfs_h2d_overlap_frac": round(ovl, 4) if ovl is not None else None,
+               "sdfs_path": "SDFS store (local replica) -> pinned ping-pong -> hipMemcpyAsync on a side stream -> "
+                            "HBM shard cache -> rounds"}
+        if a.sdfs_trace and iv:
+            ev = [{"name": k, "ph": "X", "ts": 1000.0 * t0, "dur": 1000.0 * (t1 - t0), "pid": 0,
+                   "tid": 1 if k == "h2d" else 0, "args": {"n": n}} for k, t0, t1, n in iv]
+            with open(a.sdfs_trace, "w") as f:
+                json.dump({"traceEvents": ev, "displayTimeUnit": "ms"}, f)
+    finally:
+        node.source = keep
+        node.gpu_timeline = None
     return out
 
 

@@ -114,6 +114,52 @@ def test_scatter_images_over_gloo():
     assert res == {r: True for r in range(world)}
 
 
+def _scatter_async_worker(rank, world, port, q):
+    """bench.py's scatter rounds: fixed-size chunks into two receive buffers,
+    round r+1 posted before round r is consumed (double buffering)."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import numpy as np
+    import torch.distributed as dist
+
+    from idunno.parallel.dataplane import QueryPlane, init_from_env
+    from idunno.runtime.data import synth_images_cpu
+    from idunno.runtime.scheduler import split_range
+
+    env = init_from_env(backend="gloo")
+    plane = QueryPlane(env, coordinator=0, max_chunk=6)
+    B, D = 6, 60
+    src = torch.from_numpy(synth_images_cpu(9, 0, D)) if rank == 0 else None
+    bufs = [torch.zeros(B, 224, 224, 3, dtype=torch.uint8) for _ in range(2)]
+    chunks = lambda r: split_range(r * world * B % (D - world * B + 1), r * world * B % (D - world * B + 1)  # noqa
+                                   + world * B - 1, world)
+    ok, posted = True, {0: plane.scatter_async(src, chunks(0), bufs[0])}
+    for r in range(5):
+        posted[r + 1] = plane.scatter_async(src, chunks(r + 1), bufs[(r + 1) % 2])
+        plane.wait_scatter(posted.pop(r))
+        s, e = chunks(r)[rank]
+        ok &= np.array_equal(bufs[r % 2].numpy(), synth_images_cpu(9, s, e - s + 1))
+    plane.wait_scatter(posted.pop(5))
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_scatter_async_double_buffered_over_gloo():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_scatter_async_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res == {r: True for r in range(world)}
+
+
 def _bench_pattern_worker(rank, world, port, q):
     """bench.py's round: the forward reads its window start from the broadcast
     descriptor row in place and writes packed (class, prob bits) straight into

@@ -72,14 +72,13 @@ def test_conv_big(ops, B, H, Cin, Cout, k, s, p):
     _check(y, ref)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3] + list(range(10, 40)) + [42, 43])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3] + list(range(10, 40)) + [42])
 @pytest.mark.parametrize("H", [14, 9])
 def test_conv_all_tiles_with_residual(ops, tile, H):
     from idunno.models.packed import pack_conv_weight
 
     torch.manual_seed(tile * 31 + H)
-    # tile 43 (256 couts per block): a full and a half-empty cout tile
-    B, Cin, Cout = 2, 128, 256 if tile == 17 or (tile == 43 and H == 14) else 128
+    B, Cin, Cout = 2, 128, 256 if tile == 17 else 128
     x = torch.randn(B, H, H, Cin, device=DEV).half()
     w = torch.randn(Cout, Cin, 3, 3) / (Cin * 9) ** 0.5
     b = torch.randn(Cout) * 0.1

@@ -42,7 +42,7 @@ def test_fair_share_reads_each_models_own_average():
     assert fair_share(t, "resnet50", 8, 8, {"alexnet", "resnet50"}) == round(30 / 36 * 8)
     assert fair_share(t, "alexnet", 8, 8, {"alexnet", "resnet50"}) == round(6 / 36 * 8)
     s = FairTimeScheduler(budget=8, seed=0)
-    s.avg_time.update(t)
+    s.adopt(t)                        # measured averages (unmeasured models split evenly)
     s.active_jobs = {"alexnet", "resnet50"}
     plan = s.assign("resnet50", 0, 1023, [f"n{i}" for i in range(8)])
     assert len(plan) == 7 and sum(e - b + 1 for _, b, e in plan) == 1024

@@ -80,11 +80,12 @@ def main():
         nbytes = (torch.Size(xs).numel() * xe + torch.Size(ys).numel() * ye + (rb or 0))
         gflop = 0.0
         if n in ("conv2d", "conv2d_split") and len(ys) == 4:
+            # N from the weights (rows = output channels), not from the output tensor: a
+            # split output carries 2 halfs per channel, an fp32 (OUT_F32) one 1 float --
+            # halving the last dim miscounted the f32-output split conv
             w = args[1]
             k = w.shape[1] if n == "conv2d" else w.shape[1] // 2
-            gflop = 2.0 * torch.Size(ys[:3]).numel() * ys[3] * k / 1e9
-            if n == "conv2d_split":
-                gflop = 2.0 * torch.Size(ys[:3]).numel() * (ys[3] // 2) * k / 1e9
+            gflop = 2.0 * torch.Size(ys[:3]).numel() * w.shape[0] * k / 1e9
         gbs = nbytes / (us * 1e-6) / 1e9
         tf = gflop / (us * 1e-6) / 1e3 if gflop else 0.0
         kind = n + ("+res" if rb else "")
