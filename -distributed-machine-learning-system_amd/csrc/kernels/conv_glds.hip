@@ -45,11 +45,14 @@ __device__ __forceinline__ void wait_stages(int pending_stages) {
 
 typedef float float16v __attribute__((ext_vector_type(16)));
 
-// Main loop + epilogue of the MF32 split tiles (see conv_glds_kernel): the
-// caller has issued the ring's first NS-1 stages; ``issue(buf)`` issues the
-// next stage's DMA into ring slot ``buf``.
+// Main loop + epilogue of the MF32 tiles (see conv_glds_kernel): the caller
+// has issued the ring's first NS-1 stages; ``issue(buf)`` issues the next
+// stage's DMA into ring slot ``buf``.  SPLIT: a stage row is 32 channels x
+// (hi, lo), products hi*hi (first wait) then hi*lo + lo*hi; fp16: a stage row
+// is 64 channels = 4 k-steps of 16, k-steps 0-1 after the first wait, 2-3
+// after the second.
 template <int BN, int BM, int WN, int WM, int NS, int G, int STAGE, int A_BYTES, bool HAS_RES, bool OUT_F32,
-          typename Issue>
+          bool SPLIT, typename Issue>
 __device__ __forceinline__ void conv_glds_mf32_body(const ConvArgs& a, char* smem, int wave, int lane, int nK, int n0,
                                                     int m0, bool second, Issue& issue) {
   constexpr int RB = 128;                                   // 64 halfs per row (32 channels x hi, lo)
@@ -134,14 +137,18 @@ __device__ __forceinline__ void conv_glds_mf32_body(const ConvArgs& a, char* sme
       for (int i = 0; i < F32N; ++i)
 #pragma unroll
         for (int j = 0; j < F32M; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t][i], bl[t][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t][i], bh[t][j], acc[i][j], 0, 0, 0);
+          if constexpr (SPLIT) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t][i], bl[t][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t][i], bh[t][j], acc[i][j], 0, 0, 0);
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t][i], bl[t][j], acc[i][j], 0, 0, 0);
+          }
         }
   }
 
   // ---- epilogue: x 2^-e, +bias (+split residual) (+ReLU), split (or fp32) NHWC store ----
   // the ring is drained (last wait vmcnt(0)): ordinary loads; one cout fragment at a time
-  const float acc_scale = second ? a.acc_scale2 : a.acc_scale;
+  const float acc_scale = SPLIT ? (second ? a.acc_scale2 : a.acc_scale) : 1.f;
   const bool relu = a.relu && !second;
 #pragma unroll
   for (int i = 0; i < F32N; ++i) {
@@ -155,9 +162,15 @@ __device__ __forceinline__ void conv_glds_mf32_body(const ConvArgs& a, char* sme
 #pragma unroll
         for (int j = 0; j < F32M; ++j) {
           const int m = m0 + wm * TM + j * 32 + r32;
-          const size_t off = m < a.M ? (size_t)m * (a.ldr ? a.ldr : 2 * a.Cout) + split_off(n) : 0;
-          rh[j] = *reinterpret_cast<const half4v*>(a.res + off);
-          rl[j] = *reinterpret_cast<const half4v*>(a.res + off + 32);
+          if constexpr (SPLIT) {
+            const size_t off = m < a.M ? (size_t)m * (a.ldr ? a.ldr : 2 * a.Cout) + split_off(n) : 0;
+            rh[j] = *reinterpret_cast<const half4v*>(a.res + off);
+            rl[j] = *reinterpret_cast<const half4v*>(a.res + off + 32);
+          } else {
+            const size_t off = m < a.M ? (size_t)m * (a.ldr ? a.ldr : a.Cout) + n : 0;
+            rh[j] = *reinterpret_cast<const half4v*>(a.res + off);
+            rl[j] = half4v{0, 0, 0, 0};
+          }
         }
       }
 #pragma unroll
@@ -177,6 +190,11 @@ __device__ __forceinline__ void conv_glds_mf32_body(const ConvArgs& a, char* sme
         }
         if constexpr (OUT_F32) {
           *reinterpret_cast<float4v*>(static_cast<float*>(a.y) + (size_t)m * a.ldy + n) = v;
+        } else if constexpr (!SPLIT) {
+          half4v o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
+          *reinterpret_cast<half4v*>(static_cast<half_t*>(a.y) + (size_t)m * a.ldy + n) = o;
         } else {
           split_guard(a.ovf, v);
           half4v h, l;
@@ -222,7 +240,7 @@ template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT
 __global__ void __launch_bounds__(64 * WN * WM, (BM % 64 != 0 && WN * WM == 8) ? 4 : 1)   // 2nd: min waves per SIMD
 conv_glds_kernel(const ConvArgs a) {
   static_assert(!SPLIT || BK == 64, "split stages are 32 channels x (hi, lo)");
-  static_assert(!MF32 || (SPLIT && !P3), "32x32x16 tiles: split convs");
+  static_assert(!MF32 || (BK == 64 && !P3), "32x32x16 tiles: BK 64, NHWC convs");
   constexpr int NW = WN * WM;
   constexpr int NT = 64 * NW;
   constexpr int TN = BN / WN, TM = BM / WM;
@@ -444,7 +462,7 @@ conv_glds_kernel(const ConvArgs a) {
 #pragma unroll
     for (int p = 0; p < NS - 1; ++p)
       if (p < nK) issue(p);
-    conv_glds_mf32_body<BN, BM, WN, WM, NS, G, STAGE, A_BYTES, HAS_RES, OUT_F32>(a, smem, wave, lane, nK, n0, m0,
+    conv_glds_mf32_body<BN, BM, WN, WM, NS, G, STAGE, A_BYTES, HAS_RES, OUT_F32, SPLIT>(a, smem, wave, lane, nK, n0, m0,
                                                                                  second, issue);
     return;
   }
@@ -601,7 +619,7 @@ conv_glds_kernel(const ConvArgs a) {
       }
     }
   };
-  const float acc_scale = second ? a.acc_scale2 : a.acc_scale;
+  const float acc_scale = SPLIT ? (second ? a.acc_scale2 : a.acc_scale) : 1.f;
   const bool relu = a.relu && !second;
   if constexpr (HAS_RES && LATE_RES && !RES_PER_I) {
 #pragma unroll
@@ -747,6 +765,10 @@ static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
     case 38: glds_cfg<128, 64, 64, 2, 4, 2, R, F>(a, st); return true;    // 8 waves (32x16 wave tile)
     case 39: glds_cfg<128, 128, 32, 2, 4, 4, R, F>(a, st); return true;   // 8 waves, 64 KiB, 3 stages in flight
     case 42: glds_cfg<128, 160, 64, 4, 2, 2, R, F>(a, st); return true;   // 8 waves, B as 192 rows, 80 KiB (small M)
+    // 32x32x16 MFMA (MF32) fp16 tiles: the shapes of split 56 / 57 / 58
+    case 90: glds_cfg<128, 128, 64, 2, 4, 2, R, F, false, false, true>(a, st); return true;
+    case 91: glds_cfg<128, 128, 64, 2, 2, 2, R, F, false, false, true>(a, st); return true;
+    case 92: glds_cfg<128, 192, 64, 4, 2, 2, R, F, false, false, true>(a, st); return true;
     default: return false;
   }
 }
