@@ -812,6 +812,9 @@ static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
     case 56: glds_cfg<128, 128, 64, 2, 4, 2, R, F, false, true, true>(a, st); return true;
     case 57: glds_cfg<128, 128, 64, 2, 2, 2, R, F, false, true, true>(a, st); return true;
     case 58: glds_cfg<128, 192, 64, 4, 2, 2, R, F, false, true, true>(a, st); return true;
+    // Cout 64 (ResNet layer1): 55 = 64 x 256 on 8 waves, 59 = 64 x 128 on 4 waves (64x32 wave tiles)
+    case 55: glds_cfg<64, 256, 64, 1, 8, 2, R, F, false, true, true>(a, st); return true;
+    case 59: glds_cfg<64, 128, 64, 1, 4, 2, R, F, false, true, true>(a, st); return true;
     default: return false;
   }
 }
@@ -882,10 +885,14 @@ void set_f16_wide_tile(bool on) { g_f16_wide = on; }
 // +3.4 % (profiles/r3_ab_f16_wide_all.md; per-layer: profiles/r3_f16_big_tiles.log)
 static bool g_f16_wide_all = true;
 void set_f16_wide_all(bool on) { g_f16_wide_all = on; }
+static int g_f16_mf32 = 0;
+void set_f16_mf32(int mode) { g_f16_mf32 = mode; }
 int conv_glds_pick(int M, int Cout) {
   // sweeps r1 #3/#4: BK=64 double buffering with 2-3 workgroups/CU beats deeper
   // rings; 8 waves per 128x128 tile (4 waves/SIMD) best where M is large
   if (Cout % 128 == 0) {
+    if ((g_f16_mf32 & 1) && M >= 50000) return (g_f16_mf32 & 4) ? 92 : 90;
+    if ((g_f16_mf32 & 2) && M < 50000) return 92;
     if (g_f16_wide && g_f16_wide_all) return 42;
     return M >= 50000 ? 36 : (g_f16_wide ? 42 : 34);   // 128x128 8-wave | 128x64
   }

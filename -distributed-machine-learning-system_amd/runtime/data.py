@@ -136,7 +136,8 @@ class SdfsSource:
     replica over TCP and staged host->HBM; every shard this node caches is
     announced to the SDFS master so peers can do the same (``peer_copy``)."""
 
-    def __init__(self, sdfs, device, shard_images: int = 500, cache_bytes: int = 32 << 30, peer_copy: bool = True):
+    def __init__(self, sdfs, device, shard_images: int = 500, cache_bytes: int = 32 << 30, peer_copy: bool = True,
+                 readahead: int = 1):
         self.sdfs = sdfs
         self.device = torch.device(device)
         self.S = int(shard_images)
@@ -148,6 +149,13 @@ class SdfsSource:
         self.fetches = 0
         self.peer_fetches = 0
         self.peer_copy = peer_copy and self.device.type == "cuda"
+        # sequential readahead: a request for shard k starts shard k+1 .. k+readahead on
+        # a background thread, so its SDFS read and H2D copy (side stream) run while the
+        # current chunk computes instead of in front of the next one
+        self.readahead = int(readahead)
+        self._inflight: dict[int, object] = {}     # shard -> Future of a background fetch
+        self._pool = None
+        self.readahead_hits = 0
         if self.device.type == "cuda":
             sdfs.hbm_provider = self.export_shard
 
@@ -171,11 +179,52 @@ class SdfsSource:
         torch.cuda.current_stream(self.device).synchronize()     # staged bytes have landed
         return export_tensor(t, consumer_pid)
 
+    def _prefetch(self, k: int) -> None:
+        """Start fetching shard k in the background unless cached or in flight."""
+        with self.lock:
+            if k in self.cache or k in self._inflight:
+                return
+            if self._pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+
+                self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="sdfs-readahead")
+            dev = self.device
+
+            def run():
+                import contextlib
+
+                ctx = torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()
+                try:
+                    with ctx:
+                        return self._fetch(k)
+                finally:
+                    with self.lock:
+                        self._inflight.pop(k, None)
+            self._inflight[k] = self._pool.submit(run)
+
     def _shard(self, k: int) -> torch.Tensor:
         with self.lock:
             t = self.cache.get(k)
             if t is not None:
                 self.cache.move_to_end(k)
+                return t
+            fut = self._inflight.get(k)
+        if fut is not None:
+            try:
+                t = fut.result()
+                self.readahead_hits += 1
+                if self.device.type == "cuda":
+                    # its H2D ran on the stager's side stream: order the consumer after it
+                    torch.cuda.current_stream(self.device).wait_stream(self.stager.stream)
+                return t
+            except Exception:  # noqa: BLE001  (fetch again below; a missing shard raises there)
+                pass
+        return self._fetch(k)
+
+    def _fetch(self, k: int) -> torch.Tensor:
+        with self.lock:
+            t = self.cache.get(k)
+            if t is not None:
                 return t
         name = shard_name(k)
         got = self.sdfs.fetch_hbm(name, self.device) if self.peer_copy else None
@@ -209,6 +258,9 @@ class SdfsSource:
     def get(self, start: int, end: int) -> torch.Tensor:
         parts = []
         i = start
+        last = end // self.S
+        for r in range(1, self.readahead + 1):
+            self._prefetch(last + r)
         while i <= end:
             k = i // self.S
             sh = self._shard(k)

@@ -866,6 +866,7 @@ def _drive_system(a, node, W: int, B: int) -> dict:
     assert wait_done(nxt[0]), st.summary()
     lat0 = len(st.query_latency[a.model])
     ra = node.rounds.stats() if node.rounds is not None else None
+    t_wall0 = time.time()
     t0 = time.perf_counter()
     submit(a.steps)
     assert wait_done(nxt[0]), st.summary()
@@ -894,6 +895,13 @@ def _drive_system(a, node, W: int, B: int) -> dict:
         out["system_host_wait_ms_per_round"] = round(1000 * (rb["host_wait_s"] - ra["host_wait_s"]) / nr, 4)
         out["system_rounds"] = nr
         out["system_host_post_ms_per_round"] = round(1000 * (rb["host_post_s"] - ra["host_post_s"]) / nr, 4)
+        # where the coordinator's own chunk spends its host time (tracer spans of the timed rounds)
+        with node.tracer.lock:
+            evs = [e for e in node.tracer.events if e[0] == "X" and e[2] >= t_wall0]
+        for nm in ("round.stage", "round.launch"):
+            d = [e[3] for e in evs if e[1] == nm]
+            if d:
+                out[f"system_{nm.replace('.', '_')}_ms"] = round(1000 * statistics.mean(d), 4)
         out["system_host_send_ms_per_round"] = round(1000 * (rb["host_send_s"] - ra["host_send_s"]) / nr, 4)
 
     if W == 1 and a.sdfs_images > 0:

@@ -76,3 +76,48 @@ def test_deeplearning_api_bs1_cpu_path(tmp_path):
     Image.fromarray(np.full((256, 256, 3), 90, np.uint8)).save(d / "test_0.JPEG")
     res_j, _ = deeplearning("resnet", "resnet", 0, 0, device="cpu", root=str(tmp_path))
     assert len(res_j) == 1 and res_j[0][0] == "test_0.JPEG"
+
+
+class _ShardStore:
+    """Minimal SDFS stand-in: shard bytes by name, with a read counter."""
+
+    def __init__(self, seed, n, per):
+        from idunno.runtime.data import shard_name
+
+        self.files = {shard_name(k): synth_images_cpu(seed, k * per, min(per, n - k * per)).tobytes()
+                      for k in range(-(-n // per))}
+        self.reads = []
+
+    def get_bytes_ver(self, name):
+        self.reads.append(name)
+        d = self.files.get(name)
+        return None if d is None else (d, 1)
+
+    def fetch_hbm(self, name, device):
+        return None
+
+    def announce_hbm(self, *a, **k):
+        pass
+
+
+def test_sdfs_source_readahead_prefetches_next_shard():
+    """A request for shard k starts shard k+1 in the background (sequential
+    readahead), so the next chunk's read + H2D overlap the current compute."""
+    import time
+
+    from idunno.runtime.data import SdfsSource, shard_name
+
+    store = _ShardStore(5, 30, 10)
+    src = SdfsSource(store, "cpu", shard_images=10, peer_copy=False, readahead=1)
+    x = src.get(0, 9)
+    assert torch.equal(x, torch.from_numpy(synth_images_cpu(5, 0, 10)))
+    for _ in range(200):                                 # shard 1 lands in the background
+        if src.cached(10, 19):
+            break
+        time.sleep(0.01)
+    assert src.cached(10, 19) and store.reads[:2] == [shard_name(0), shard_name(1)]
+    y = src.get(12, 21)                                  # spans shards 1 and 2: 1 cached, 2 prefetched by now or fetched
+    assert torch.equal(y, torch.from_numpy(synth_images_cpu(5, 12, 10)))
+    assert store.reads.count(shard_name(1)) == 1        # never read twice
+    src.get(25, 29)                                      # readahead past the last shard: harmless
+    assert torch.equal(src.get(20, 29), torch.from_numpy(synth_images_cpu(5, 20, 10)))
