@@ -216,6 +216,10 @@ class JobState:
         elif op == "result":
             model, qnum, start, end, now = args
             self._mark_finished((model, qnum), int(start), int(end), now)
+        elif op == "results":                           # one collective round (record_results bulk)
+            model, qnum, chunks, now = args
+            for start, end in chunks:
+                self._mark_finished((model, qnum), int(start), int(end), now)
         elif op == "reassign":
             failed, new_worker, chunk, now = args
             self._reassign_locked(failed, new_worker, tuple(chunk), now, emit=False)
@@ -349,10 +353,74 @@ class JobState:
     def record_results(self, recs, now: float | None = None) -> int:
         """Ingest several finished chunks [(model, qnum, worker, s, e, cls,
         prob)] under one lock hold (a collective round); returns how many were
-        new.  Same semantics as ``record_result`` per chunk."""
+        new.  Same semantics as ``record_result`` per chunk.  The common case
+        -- every chunk of the round is a fresh answer to a running chunk of
+        one query -- is done in bulk: one pass over the query's entries, one
+        interval merge, one window entry and ONE replication op; anything else
+        (duplicates, re-split ranges, several queries) takes the per-chunk path."""
         now = self.clock() if now is None else now
         with self.lock:
+            if recs and self._bulk_ok(recs):
+                return self._record_bulk(recs, now)
             return sum(1 for m, q, w, s, e, c, p in recs if self.record_result(m, q, w, s, e, c, p, now))
+
+    def _bulk_ok(self, recs) -> bool:
+        model, qnum = recs[0][0], recs[0][1]
+        key = (model, qnum)
+        if key not in self._open or any(r[0] != model or r[1] != qnum for r in recs):
+            return False
+        running = {(x[0], x[1], x[2]) for x in self.worker_set.get(key, []) if x[3] == "w"}
+        if any((w, int(s), int(e)) not in running or (model, qnum, int(s), int(e)) in self._done_keys
+               for _, _, w, s, e, _, _ in recs):
+            return False
+        ivs = self._done_imgs.get(key, [])
+        rng = sorted((int(r[3]), int(r[4])) for r in recs)
+        if any(a[1] >= b[0] for a, b in zip(rng, rng[1:])):
+            return False                                   # overlapping chunks: per-chunk dedupe
+        return not any(a <= e and s <= b for s, e in rng for a, b in ivs)
+
+    def _record_bulk(self, recs, now: float) -> int:
+        model, qnum = recs[0][0], recs[0][1]
+        key = (model, qnum)
+        ents = self.worker_set[key]
+        pos = {(x[0], x[1], x[2]): i for i, x in enumerate(ents) if x[3] == "w"}
+        bs = self.batchsize.get(model, 1)
+        tot = 0
+        res = self.results[f"{model} {qnum}"]
+        chunks = []
+        for _, _, w, s, e, c, p in recs:
+            s, e = int(s), int(e)
+            i = pos[(w, s, e)]
+            t_start = ents[i][4]
+            ents[i] = (w, s, e, "f", t_start, now)
+            vm = self.working_vm_set.get(w)
+            if vm is not None:
+                try:
+                    vm.remove((model, qnum, s, e))
+                except ValueError:
+                    pass
+                if not vm:
+                    self.working_vm_set.pop(w, None)
+            self._done_keys.add((model, qnum, s, e))
+            n = e - s + 1
+            tot += n
+            self._ptime_win[model].append((now, (now - t_start) / n * bs))
+            res.append(ChunkResult(s, e, np.asarray(c, dtype=np.int32), np.asarray(p, dtype=np.float32), w))
+            chunks.append([s, e])
+        self._open_add(key, -len(recs))
+        for s, e in sorted(chunks):
+            _add_interval(self._done_imgs[key], s, e)
+        if key not in self._open:
+            self.finished_queries[model] += 1
+            t0 = self.query_submit_time.get(key)
+            if t0 is not None:
+                self.query_latency[model].append(now - t0)
+        self.finished_images[model] += tot
+        self._rate_win[model].append((now, tot))
+        self._expire(model, now)
+        self._c2_dirty.add(model)
+        self._bump("results", model, qnum, chunks, now)
+        return len(recs)
 
     def reopen_unheld(self) -> int:
         """Chunks marked finished in the replicated tables whose images this
