@@ -1392,6 +1392,15 @@ std::vector<torch::Tensor> softmax_top1(torch::Tensor logits, c10::optional<torc
   return {cls, prob};
 }
 
+// hipGraphLaunch of an instantiated graph (torch.cuda.CUDAGraph.raw_cuda_graph_exec())
+// on the current stream, and nothing else: the round paths replay one graph per
+// chunk and must not wait on the device in between (HipRunner._replayer).
+void graph_launch(int64_t exec) {
+  TORCH_CHECK(exec != 0, "graph_launch: no instantiated graph");
+  const hipError_t e = hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(exec), cur_stream());
+  TORCH_CHECK(e == hipSuccess, "hipGraphLaunch failed: ", hipGetErrorString(e));
+}
+
 torch::Tensor synth_images(int64_t seed, int64_t start, int64_t n, int64_t hw, torch::Device dev) {
   TORCH_CHECK(dev.is_cuda(), "synth_images needs a GPU device");
   TORCH_CHECK(n >= 0 && start >= 0 && (hw * hw * 3) % 8 == 0, "bad synth_images args");
@@ -1518,6 +1527,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "split range guard flag (int32 device tensor) for this thread's split launches; None = off",
         py::arg("flag") = py::none());
   m.def("synth_images", &synth_images, "deterministic synthetic uint8 images [n,hw,hw,3]");
+  m.def("graph_launch", &graph_launch, "hipGraphLaunch(exec, current stream): a replay without any host wait");
   m.def("pick_tile", &pick_tile, "tile id the conv heuristic picks for (M, Cout)");
   m.def("set_stem_workgroups_per_cu", &set_stem_workgroups_per_cu,
         "fused stem: persistent workgroups per CU (1-3, default 3)");

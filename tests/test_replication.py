@@ -100,3 +100,35 @@ def test_coordinator_cost_flat_over_100k_queries():
     q = js.new_query_number("resnet18")
     js.assign("resnet18", q, [("a", 0, 9)])
     assert len(js.deltas_since(seq)) == 2
+
+
+def test_bulk_round_ingest_matches_per_chunk_and_replicates():
+    """record_results (one collective round of one query, bulk path) leaves the
+    same tables as per-chunk record_result, and its single 'results' log op
+    brings a standby to the same state; duplicates / partial overlaps fall back
+    to the per-chunk path."""
+    import numpy as np
+
+    from idunno.runtime.jobstate import JobState
+
+    a, b, standby = JobState(), JobState(), JobState()
+    W, B = 8, 50
+    cls, prob = np.arange(B, dtype=np.int32), np.full(B, 0.25, np.float32)
+    for q in range(1, 6):
+        plan = [(f"node{r:02d}", q * 1000 + r * B, q * 1000 + (r + 1) * B - 1) for r in range(W)]
+        for st in (a, b):
+            st.assign("resnet18", q, plan, now=1.0)
+        recs = [("resnet18", q, w, s, e, cls, prob) for w, s, e in plan]
+        assert a.record_results(recs, now=2.0) == W
+        for r in recs:
+            b.record_result(*r, now=2.0)
+    # a duplicate round and a round overlapping finished images: per-chunk path, nothing new
+    assert a.record_results(recs, now=3.0) == 0
+    sa, sb = a.snapshot(), b.snapshot()
+    for k in sa:
+        if k != "seq":
+            assert sa[k] == sb[k], k
+    assert a.inference_result_list() == b.inference_result_list()
+    assert any(op == "results" for _, op, _ in a._log)
+    assert standby.apply_deltas(a.deltas_since(0))
+    assert standby.pending_count() == 0 and standby.cq() == a.cq() and standby.cvm() == a.cvm()

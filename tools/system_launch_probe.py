@@ -21,7 +21,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=40)
     ap.add_argument("--batch", type=int, default=400)
     ap.add_argument("--model", default="resnet18")
+    ap.add_argument("--direct", action="store_true", help="hipGraphLaunch via ops.graph_launch, not CUDAGraph.replay")
     a = ap.parse_args()
+    from idunno import ops
     from idunno.runtime.data import SyntheticSource
     from idunno.runtime.executor import HipExecutor
 
@@ -56,7 +58,11 @@ def main():
                 t4 = time.perf_counter()
                 sin.copy_(imgs)
                 t5 = time.perf_counter()
-                replay()
+                if a.direct:
+                    g = r._graphs[r._capture_key(a.batch, packed, 0)][0]
+                    ops.load().graph_launch(g.raw_cuda_graph_exec())
+                else:
+                    replay()
                 t6 = time.perf_counter()
                 ev1.record(s)
             torch.cuda.current_stream(dev).wait_stream(s)
