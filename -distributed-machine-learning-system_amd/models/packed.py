@@ -563,6 +563,9 @@ class HipRunner:
         self.overflow_fallback = True
         self.overflow_reruns = 0
         self._capturing = False
+        # replay captured graphs with a bare hipGraphLaunch (ops.graph_launch) instead of
+        # torch.cuda.CUDAGraph.replay (tools/system_launch_probe.py measures both)
+        self.direct_launch = False
 
     # -- eager forward ------------------------------------------------------
     def _guarded(self) -> bool:
@@ -1130,12 +1133,18 @@ class HipRunner:
         the captured inputs alive: the graph holds raw device pointers, so a
         caller that drops the runner and keeps only the closure must not let
         the weights go back to the allocator."""
+        direct = self.direct_launch and hasattr(g, "raw_cuda_graph_exec")
+        launch = self.ops.load().graph_launch if direct else None
+
         def replay():
             # several nodes may share a process (and a GPU): a replay while another
             # thread is capturing fails on ROCm ("prepare for replay during
             # capturing stage"), so replays and captures are mutually exclusive
             with _CAPTURE_LOCK:
-                g.replay()
+                if direct:
+                    launch(g.raw_cuda_graph_exec())      # hipGraphLaunch on the current stream only
+                else:
+                    g.replay()
             return sout
         replay._keep = (self, keep)
         return replay
