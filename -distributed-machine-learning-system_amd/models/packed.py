@@ -23,6 +23,8 @@ without a GPU).
 """
 from __future__ import annotations
 
+import os
+
 import math
 import threading
 from dataclasses import dataclass, field
@@ -565,7 +567,7 @@ class HipRunner:
         self._capturing = False
         # replay captured graphs with a bare hipGraphLaunch (ops.graph_launch) instead of
         # torch.cuda.CUDAGraph.replay (tools/system_launch_probe.py measures both)
-        self.direct_launch = False
+        self.direct_launch = os.environ.get("IDUNNO_DIRECT_LAUNCH", "0") == "1"
 
     # -- eager forward ------------------------------------------------------
     def _guarded(self) -> bool:

@@ -113,6 +113,7 @@ class RoundPlane:
         # blocked on a gather (host_wait_s); bench.py reports host_s per round
         self.host_s = 0.0
         self.host_wait_s = 0.0
+        self.launch_cpu_s = 0.0               # thread CPU time of this node's chunk launches
         self.host_post_s = 0.0                # of host_s: posting (descriptors, own chunk, gather)
         self.host_send_s = 0.0                # of host_post_s: ROUND descriptor sends
 
@@ -201,7 +202,7 @@ class RoundPlane:
                 "max_queries_per_round": self.max_queries_per_round,
                 "parked": self.parked, "pending_collectives": self.pending_collectives(),
                 "host_s": self.host_s, "host_wait_s": self.host_wait_s, "host_post_s": self.host_post_s,
-                "host_send_s": self.host_send_s,
+                "host_send_s": self.host_send_s, "launch_cpu_s": self.launch_cpu_s,
                 "queued": len(self._queue)}
 
     def pending_collectives(self) -> int:
@@ -254,6 +255,7 @@ class RoundPlane:
         with n.tracer.span("round.stage", **tags):
             imgs = n.source.get(s, e) if n.source is not None else None
         run_packed = getattr(n.executor, "run_packed", None)
+        c0 = time.thread_time()
         with n.tracer.span("round.launch", **tags):
             if run_packed is not None and imgs is not None and imgs.device.type == "cuda" and \
                     send.device == imgs.device:
@@ -268,6 +270,7 @@ class RoundPlane:
                 cls, prob = n.executor.run(model, imgs, s, e)
                 self._timings.append((mid, cnt, time.perf_counter() - t0))
                 pack_into(send, cls, prob)
+        self.launch_cpu_s += time.thread_time() - c0     # this thread's CPU time in the launch (vs its wall span)
         n.chunks_done += 1
 
     def _write_header(self, seq: int) -> None:

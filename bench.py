@@ -866,6 +866,11 @@ def _drive_system(a, node, W: int, B: int) -> dict:
     assert wait_done(nxt[0]), st.summary()
     lat0 = len(st.query_latency[a.model])
     ra = node.rounds.stats() if node.rounds is not None else None
+    import torch
+
+    dev = node.device if node.device is not None else None
+    gpu_node = dev is not None and torch.device(dev).type == "cuda"
+    ms0 = torch.cuda.memory_stats(dev) if gpu_node else {}
     t_wall0 = time.time()
     t0 = time.perf_counter()
     submit(a.steps)
@@ -895,6 +900,11 @@ def _drive_system(a, node, W: int, B: int) -> dict:
         out["system_host_wait_ms_per_round"] = round(1000 * (rb["host_wait_s"] - ra["host_wait_s"]) / nr, 4)
         out["system_rounds"] = nr
         out["system_host_post_ms_per_round"] = round(1000 * (rb["host_post_s"] - ra["host_post_s"]) / nr, 4)
+        out["system_launch_cpu_ms"] = round(1000 * (rb["launch_cpu_s"] - ra["launch_cpu_s"]) / nr, 4)
+        if gpu_node:
+            ms1 = torch.cuda.memory_stats(dev)
+            for k in ("num_device_alloc", "num_device_free", "num_alloc_retries", "num_sync_all_streams"):
+                out[f"system_alloc_{k}"] = ms1.get(k, 0) - ms0.get(k, 0)
         # where the coordinator's own chunk spends its host time (tracer spans of the timed rounds)
         with node.tracer.lock:
             evs = [e for e in node.tracer.events if e[0] == "X" and e[2] >= t_wall0]
