@@ -833,12 +833,27 @@ def _wait_port(addr, timeout: float) -> None:
             time.sleep(0.05)
 
 
+def _wait_progress(node, pred, timeout: float) -> bool:
+    """Wait until ``pred()`` holds, woken by the node's result-ingest
+    notifications (``Node._progress``), not by polling."""
+    end = time.monotonic() + timeout
+    with node._progress:
+        while not pred():
+            left = end - time.monotonic()
+            if left <= 0:
+                return bool(pred())
+            node._progress.wait(min(left, 0.05))
+    return True
+
+
 def _cluster_ready(node, n: int, timeout: float = 120.0) -> None:
     from idunno.runtime.transport import wait_for
 
     assert wait_for(lambda: len(node.membership.alive()) == n, timeout), node.membership.table()
     if node.cfg.collective_rounds and node.is_coordinator:
-        assert wait_for(lambda: node.rounds.group.formed and len(node.rounds.group.members) == n, timeout)
+        # formed AND healthy: queries submitted before the plane is marked healthy take the TCP path
+        assert wait_for(lambda: node.rounds.group.formed and node.rounds.healthy
+                        and len(node.rounds.group.members) == n, timeout)
 
 
 def _drive_system(a, node, W: int, B: int) -> dict:
@@ -860,7 +875,10 @@ def _drive_system(a, node, W: int, B: int) -> dict:
             cl.submit(a.model, s0, s0 + per_q - 1)
 
     def wait_done(target, timeout=300):
-        return wait_for(lambda: st.images_done(a.model) >= target and st.pending_count() == 0, timeout, 0.001)
+        # block on the coordinator's progress condition (notified per ingested round)
+        # instead of polling: a 1 ms polling thread competes with the round driver
+        # for the interpreter lock
+        return _wait_progress(node, lambda: st.images_done(a.model) >= target and st.pending_count() == 0, timeout)
 
     submit(a.warmup)
     assert wait_done(nxt[0]), st.summary()
