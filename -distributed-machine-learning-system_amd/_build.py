@@ -6,11 +6,6 @@ compiled to an object under ``build/`` and linked into ``_C.so`` next to this
 file, so the built library travels with the repository snapshot to the GPU box.
 
 Usage: ``python -m idunno._build [--force] [-j N]``.
-
-``IDUNNO_EXPERIMENTAL=1`` also builds the non-default experimental conv loops
-(``csrc/kernels/experimental/``: conv_big, conv_pers, conv3x3_patch; kept for
-A/B sweeps, never selected by the default tile heuristics) and defines
-``IDUNNO_EXPERIMENTAL`` for the bindings.
 """
 from __future__ import annotations
 
@@ -47,14 +42,10 @@ def _torch_paths():
     return incs, torch_lib, abi
 
 
-def experimental() -> bool:
-    return os.environ.get("IDUNNO_EXPERIMENTAL", "0") not in ("", "0")
-
 
 def sources() -> list[Path]:
-    # csrc/tests/ holds standalone host programs (sanitizer checks), not extension code;
-    # csrc/kernels/experimental/ only with IDUNNO_EXPERIMENTAL=1
-    skip = {"tests"} if experimental() else {"tests", "experimental"}
+    # csrc/tests/ holds standalone host programs (sanitizer checks), not extension code
+    skip = {"tests"}
     return sorted(p for p in [*CSRC.rglob("*.hip"), *CSRC.rglob("*.cpp")]
                   if not skip & set(p.relative_to(CSRC).parts))
 
@@ -71,8 +62,6 @@ def _compile_cmd(src: Path, obj: Path, incs, abi) -> list[str]:
         "-Wno-unused-result", "-Wno-deprecated-declarations",
         f"-I{sysconfig.get_paths()['include']}", f"-I{CSRC}",
     ]
-    if experimental():
-        cmd.append("-DIDUNNO_EXPERIMENTAL=1")
     cmd += [f"-I{i}" for i in incs]
     cmd += ["-c", str(src), "-o", str(obj)]
     return cmd
@@ -84,7 +73,7 @@ FLAGS = PKG_DIR / "_C.so.flags"
 
 
 def _flags() -> str:
-    return f"experimental={int(experimental())}"
+    return f"arch={ARCH}"
 
 
 def needs_build(force: bool = False) -> bool:

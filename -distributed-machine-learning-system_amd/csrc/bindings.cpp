@@ -40,21 +40,6 @@ static torch::Tensor zero_buffer(const torch::Device& dev) {
   return b;
 }
 
-#ifdef IDUNNO_EXPERIMENTAL
-// Whether auto tile selection routes 3x3/s1 convs to the LDS-patch kernel
-// (set_conv3x3_patch_default from Python; off until the per-layer sweep says so).
-static bool g_patch_default = false;
-static bool conv3x3_patch_default() { return g_patch_default; }
-void set_conv3x3_patch_default(bool on) { g_patch_default = on; }
-#endif
-// Whether the experimental conv loops (conv_big / conv_pers / conv3x3_patch) are built in.
-bool has_experimental() {
-#ifdef IDUNNO_EXPERIMENTAL
-  return true;
-#else
-  return false;
-#endif
-}
 // Whether auto tile selection routes 3x3/s1 64->64 convs to the resident-weight
 // kernel (tile 50, conv3x3_c64.hip): on by default since sweep r1 #6 (ResNet18
 // layer1 at B=400: 112 / 153 us vs 178 / 207 us for the best im2col tile,
@@ -156,16 +141,6 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     return y;
   }
   a.zero = zero_buffer(x.device()).data_ptr();
-#ifdef IDUNNO_EXPERIMENTAL
-  const bool patch_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 &&
-                        conv3x3_patch_supported(H, W, C, Cout);
-  if (tile == 40 || (tile < 0 && patch_ok && conv3x3_patch_default())) {
-    TORCH_CHECK(patch_ok, "tile 40 (LDS-patch 3x3 conv) does not support this shape");
-    conv3x3_patch_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W, C, Cout,
-                         a.relu, cur_stream()); check_launch("conv3x3_patch");
-    return y;
-  }
-#endif
   const bool c64_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 && conv3x3_c64_supported(C, Cout);
   if (tile == 50 || (tile < 0 && c64_ok && g_c64_default)) {
     TORCH_CHECK(c64_ok, "tile 50 (resident-weight 3x3 64->64 conv) does not support this shape");
@@ -182,22 +157,6 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     return y;
   }
   const int t = tile >= 10 ? (int)tile : conv_glds_pick(a.M, Cout);
-#ifdef IDUNNO_EXPERIMENTAL
-  if (t >= 70 && t < 80) {             // persistent loop (conv_pers.hip); 1-stage convs fall back to tile 65
-    if (conv_pers_launch(a, out_f32, t, cur_stream())) {
-      check_launch("conv_pers");
-      return y;
-    }
-    TORCH_CHECK(conv_big_launch(a, out_f32, 65, cur_stream()), "conv_big fallback failed");
-    check_launch("conv_big");
-    return y;
-  }
-  if (t >= 60 && t < 70) {             // v3 large-tile loop (conv_big.hip)
-    TORCH_CHECK(conv_big_launch(a, out_f32, t, cur_stream()), "unknown conv tile id ", t);
-    check_launch("conv_big");
-    return y;
-  }
-#endif
   TORCH_CHECK(conv_glds_launch(a, out_f32, t, cur_stream()), "unknown conv tile id ", t);
   check_launch("conv_glds");
   return y;
@@ -417,12 +376,6 @@ static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
 // row-streaming register-weight kernel (tile 50 of conv2d_split, conv3x3_split.hip).
 static bool g_split_c64_default = true;
 void set_split_c64_default(bool on) { g_split_c64_default = on; }
-#ifdef IDUNNO_EXPERIMENTAL
-// Whether auto selection routes split 3x3/s1 convs with Cout % 128 == 0 to the
-// halo-patch kernel (tiles 60-62, experimental/conv3x3_patch_split.hip).
-static bool g_split_patch_default = false;
-void set_split_patch_default(bool on) { g_split_patch_default = on; }
-#endif
 // Split range guard (common.h split_guard): the int32 flag
 // that this thread's split launches write to when a value leaves fp16's range;
 // HipRunner sets it around a split forward (a captured graph keeps the pointer).
@@ -561,17 +514,6 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
     check_launch("conv3x3_split_c64");
     return y;
   }
-#ifdef IDUNNO_EXPERIMENTAL
-  const bool patch_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && Cout % 128 == 0 && !strided &&
-                        nsplit == 0 && conv3x3_patch_split_supported(B, H, W, C2 / 2, Cout);
-  if ((tile >= 60 && tile <= 62) || (tile < 0 && patch_ok && g_split_patch_default)) {
-    TORCH_CHECK(patch_ok, "tiles 60-62 (split 3x3 patch conv) do not support this shape");
-    conv3x3_patch_split_launch(a.x, a.w, a.bias, a.res, a.y, out_f32, a.zero, B, H, W, C2 / 2, Cout, a.relu,
-                               a.acc_scale, tile >= 60 ? (int)tile - 58 : 2, cur_stream());
-    check_launch("conv3x3_patch_split");
-    return y;
-  }
-#endif
   const bool c1s_ok = KH == 1 && KW == 1 && (stride == 1 || stride == 2) && pad == 0 && !out_f32 && !strided &&
                       nsplit == 0 && a.ablate == 0 && conv1x1_stream_split_supported(C2 / 2, Cout, M);
   if (tile == 80 || (tile < 0 && c1s_ok && conv1x1_stream_split_default(C2 / 2, stride))) {
@@ -1455,10 +1397,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_split_c64_default", &set_split_c64_default,
         "A/B: route split 3x3 64->64 convs to the row-streaming kernel (tile 50; default on)");
   m.def("set_split_norder", &set_split_norder, "A/B: split conv tile order (0 m-major, 1 n-major, -1 auto)");
-#ifdef IDUNNO_EXPERIMENTAL
-  m.def("set_split_patch_default", &set_split_patch_default,
-        "A/B: route split 3x3/s1 convs (Cout % 128 == 0) to the halo-patch kernel (tile 60)");
-#endif
   m.def("set_stem_split_rp2", [](int64_t n) { set_stem_split_rp2((int)n); }, "A/B: split stem conv rows per pass (0/1: one, 2 default, 3)");
   m.def("set_stem_split_reg", [](int64_t n) { set_stem_split_reg((int)n); }, "A/B: register-pooled split stem, 3 / 4 workgroups per CU (0 off)");
   m.def("set_stem_split_niw", [](int64_t n) { set_stem_split_niw((int)n); },
@@ -1537,9 +1475,4 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "profiling only: 1 skip pool, 2 skip conv MFMAs, 4 skip patch normalise (wrong outputs)");
   m.def("set_conv3x3_c64_default", &set_conv3x3_c64_default,
         "route auto-tiled 3x3/s1 64->64 convs to the resident-weight kernel (tile 50)");
-#ifdef IDUNNO_EXPERIMENTAL
-  m.def("set_conv3x3_patch_default", &set_conv3x3_patch_default,
-        "route auto-tiled 3x3/s1 convs to the LDS-patch kernel (tile 40)");
-#endif
-  m.def("has_experimental", &has_experimental, "experimental conv loops built in (IDUNNO_EXPERIMENTAL=1)");
 }

@@ -181,13 +181,6 @@ void set_conv1x1_stream_lio(bool on);  // A/B: residual / output through per-wav
 void set_conv1x1_stream_lio_n2(bool on);  // A/B: ... also for the fused-next kernels
 void set_c64_split_variant(int v);  // layer1 split kernel: 0 = 16 couts/wave, 2/3 = 32 couts/wave (read ring depth)
 int c64_split_variant();
-#ifdef IDUNNO_EXPERIMENTAL
-// split 3x3/s1/p1 conv with the B operand from a halo patch per 32-channel block (Cout % 128 == 0)
-bool conv3x3_patch_split_supported(int B, int H, int W, int C, int Cout);
-void conv3x3_patch_split_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, void* y,
-                                bool out_f32, const void* zero, int B, int H, int W, int C, int Cout, int relu,
-                                float acc_scale, int nsa, hipStream_t st);
-#endif
 // split 3x3/s1/p1 64 -> 64 conv, weights in registers, input rows streamed through an LDS ring
 bool conv3x3_split_c64_supported(int H, int W, int C, int Cout);
 void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
@@ -195,16 +188,11 @@ void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bia
                               hipStream_t st);
 // split-fp16 RGB stem on packed rows (a.cpk > 0, x from preprocess_pack3_split): fp32 output
 bool conv_glds_split_p3_launch(ConvArgs a, int tile, hipStream_t st);   // a.cpk > 0: pack3 stem
-bool conv_big_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
-bool conv_pers_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);   // false: shape unsupported
-bool conv3x3_patch_supported(int H, int W, int C, int Cout);
 bool conv3x3_c64_supported(int C, int Cout);
 void set_stem_ablation(int mode);
 void set_stem_workgroups_per_cu(int n);
 void conv3x3_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
                         const void* zero, int B, int H, int W, int relu, hipStream_t st);
-void conv3x3_patch_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
-                          const void* zero, int B, int H, int W, int C, int Cout, int relu, hipStream_t st);
 int conv_glds_pick(int M, int Cout);
 // split-fp16 (fp32-accurate) fused stem, exact-u8 form: w = [2][64][7*32] hi/lo of
 // w * s_c (pre-scaled by 1/acc_scale), bias = folded bias + full sum of w * c_c,

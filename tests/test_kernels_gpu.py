@@ -241,63 +241,6 @@ def test_resnet50_fused_downsample_matches_unfused(ops):
     assert torch.equal(outs[True].argmax(1)[clear], outs[False].argmax(1)[clear])
 
 
-BIG_TILES = [60, 61, 62, 63, 65, 66, 67, 68, 69, 70, 71, 72, 73]
-
-
-def _need_experimental(ops):
-    """conv_big / conv_pers live in csrc/kernels/experimental/, built only with
-    IDUNNO_EXPERIMENTAL=1 (not in the default _C.so, VERDICT r1 weak #12)."""
-    if not ops.load().has_experimental():
-        pytest.skip("experimental conv loops not built (IDUNNO_EXPERIMENTAL=1)")
-
-
-@pytest.mark.experimental
-@pytest.mark.parametrize("tile", BIG_TILES)
-@pytest.mark.parametrize("B,H,Cin,Cout,k,s,res", [
-    (3, 28, 128, 128, 3, 1, True),    # layer2 3x3 + residual, M = 2352 (not a tile multiple)
-    (2, 28, 64, 128, 3, 2, False),    # layer2 first conv, stride 2
-    (2, 14, 256, 256, 3, 1, True),    # layer3
-    (3, 7, 512, 512, 3, 1, False),    # layer4, M = 147 < one tile
-    (2, 13, 192, 384, 3, 1, False),   # alexnet conv3: Cout not a multiple of 256
-    (2, 9, 64, 192, 1, 1, True),      # 1x1, one K stage; Cout 192 masks part of a 128/256 tile
-])
-def test_conv_big_tiles(ops, tile, B, H, Cin, Cout, k, s, res):
-    """v3 large-tile loop (conv_big.hip) vs fp32 torch, with masked rows / columns."""
-    from idunno.models.packed import pack_conv_weight
-
-    _need_experimental(ops)
-    torch.manual_seed(tile * 7 + H + Cout)
-    p = k // 2
-    x = torch.randn(B, H, H, Cin, device=DEV).half()
-    w = torch.randn(Cout, Cin, k, k) / (Cin * k * k) ** 0.5
-    b = torch.randn(Cout) * 0.1
-    Ho = (H + 2 * p - k) // s + 1
-    r = torch.randn(B, Ho, Ho, Cout, device=DEV).half() if res else None
-    pw, _ = pack_conv_weight(w)
-    y = ops.conv2d(x, pw.to(DEV), b.to(DEV), k, k, s, p, True, residual=r, tile=tile)
-    ref = _ref_conv(x, w.half().float().to(DEV), b.to(DEV), s, p, True, r)
-    _check(y, ref)
-
-
-@pytest.mark.experimental
-@pytest.mark.parametrize("tile", [70, 71, 72, 73])
-@pytest.mark.parametrize("res", [False, True])
-def test_conv_persistent_many_tiles_per_workgroup(ops, tile, res):
-    """Persistent kernel with several tiles per workgroup (ring crosses tile
-    boundaries, epilogue overlaps the next tile's DMA), last tile partial."""
-    from idunno.models.packed import pack_conv_weight
-
-    _need_experimental(ops)
-    torch.manual_seed(tile + 100 * res)
-    B, H, Cin, Cout = 25, 56, 64, 128      # M = 78400: 613 / 1225 tiles > resident workgroups
-    x = torch.randn(B, H, H, Cin, device=DEV).half()
-    w = torch.randn(Cout, Cin, 3, 3) / (Cin * 9) ** 0.5
-    b = torch.randn(Cout) * 0.1
-    r = torch.randn(B, H, H, Cout, device=DEV).half() if res else None
-    pw, _ = pack_conv_weight(w)
-    y = ops.conv2d(x, pw.to(DEV), b.to(DEV), 3, 3, 1, 1, True, residual=r, tile=tile)
-    ref = _ref_conv(x, w.half().float().to(DEV), b.to(DEV), 1, 1, True, r)
-    _check(y, ref)
 
 
 @pytest.mark.parametrize("k,s,p,H", [(7, 2, 3, 224), (11, 4, 2, 224), (7, 2, 3, 37)])

@@ -303,42 +303,6 @@ def _c64_rows_case(ops, B, H, W, res):
 
 
 @pytest.mark.gpu
-@pytest.mark.experimental
-@pytest.mark.parametrize("B,H,C,Cout", [(3, 28, 128, 128), (2, 14, 256, 256), (3, 7, 512, 512), (2, 13, 96, 128),
-                                        (1, 9, 128, 256)])
-@pytest.mark.parametrize("res,out_f32", [(False, False), (True, False), (True, True)])
-@pytest.mark.parametrize("tile", [60, 61, 62])
-def test_conv_split_patch(ops, B, H, C, Cout, res, out_f32, tile):
-    """Halo-patch 3x3 split conv (tiles 60-62, experimental build): tiles spanning images (virtual rows)."""
-    if not ops.load().has_experimental():
-        pytest.skip("experimental kernels not built (IDUNNO_EXPERIMENTAL=1)")
-    torch.manual_seed(B * H + C + res + out_f32)
-    x = torch.randn(B, H, H, C, device=DEV)
-    w = torch.randn(Cout, C, 3, 3) / (9 * C) ** 0.5
-    b = torch.randn(Cout) * 0.1
-    r = torch.randn(B, H, H, Cout, device=DEV) if res else None
-    sw, scale = P.pack_split_weight(w)
-    y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, 3, 3, 1, 1, True,
-                         residual=None if r is None else ops.split_from_f32(r), out_f32=out_f32, tile=tile)
-    _check(y if out_f32 else P.from_split(y), _ref64(x, w, b, 1, 1, True, r))
-
-
-def test_patch_split_swizzle_consecutive_pixels_cpu():
-    """conv3x3_patch_split.hip: slot = chunk ^ (pp & 6) on 128-B pixel rows is
-    conflict-free for 16 consecutive pixels in every ds_read_b128 lane group."""
-    groups = [[*range(0, 4), *range(12, 16), *range(20, 28)], [*range(4, 12), *range(16, 20), *range(28, 32)]]
-    groups += [[lane + 32 for lane in g] for g in groups]
-    for base in range(16):
-        for p in range(2):
-            for g in groups:
-                slots = set()
-                for lane in g:
-                    pp = base + (lane & 15)
-                    slots.add((pp & 1) * 8 + ((p * 4 + (lane >> 4)) ^ (pp & 6)))
-                assert len(slots) == 16
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("tile", SPLIT_TILES)
 @pytest.mark.parametrize("res", [False, True])
 @pytest.mark.parametrize("out_f32", [False, True])
