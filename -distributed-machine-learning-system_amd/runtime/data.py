@@ -154,6 +154,7 @@ class SdfsSource:
         # current chunk computes instead of in front of the next one
         self.readahead = int(readahead)
         self._inflight: dict[int, object] = {}     # shard -> Future of a background fetch
+        self._absent: set = set()                 # shards a readahead found missing (past the dataset's end)
         self._pool = None
         self.readahead_hits = 0
         if self.device.type == "cuda":
@@ -182,7 +183,7 @@ class SdfsSource:
     def _prefetch(self, k: int) -> None:
         """Start fetching shard k in the background unless cached or in flight."""
         with self.lock:
-            if k in self.cache or k in self._inflight:
+            if k in self.cache or k in self._inflight or k in self._absent:
                 return
             if self._pool is None:
                 from concurrent.futures import ThreadPoolExecutor
@@ -197,6 +198,10 @@ class SdfsSource:
                 try:
                     with ctx:
                         return self._fetch(k)
+                except KeyError:
+                    with self.lock:
+                        self._absent.add(k)              # not asked again by readahead
+                    raise
                 finally:
                     with self.lock:
                         self._inflight.pop(k, None)

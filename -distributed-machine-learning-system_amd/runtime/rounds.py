@@ -126,6 +126,8 @@ class RoundPlane:
         self._wake.set()
         with self.cv:
             self.cv.notify_all()
+        if self._mirror_q is not None:
+            self._mirror_q.put(None)              # the standby mirror thread exits
 
     def join(self, timeout: float = 5.0) -> None:
         """Wait for the driver thread and (bounded) for background epoch aborts
