@@ -74,22 +74,33 @@ def init_from_env(backend: str | None = None, timeout_s: float = 300.0, cpu: boo
 class QueryPlane:
     """Collective dispatch / gather between the coordinator rank and workers."""
 
-    def __init__(self, env: Env, coordinator: int = 0, max_chunk: int = 512, group=None):
+    def __init__(self, env: Env, coordinator: int = 0, max_chunk: int = 512, group=None, nbuf: int = 1):
         self.env = env
         self.coord = coordinator
         self.max_chunk = max_chunk
         self.group = group
+        self.nbuf = nbuf
         dev = env.device
-        self._desc = torch.full((env.world, 4), NO_WORK, dtype=torch.int64, device=dev)
-        # one contiguous [world, max_chunk, 2] buffer on the coordinator; the
+        # nbuf slots of descriptor table / send buffer / gathered round: with 2, round
+        # q+1's descriptor broadcast and round q's gather run on the collective stream
+        # while the other slot's forward computes (post_dispatch / post_gather)
+        self._descs = torch.full((nbuf, env.world, 4), NO_WORK, dtype=torch.int64, device=dev)
+        self._desc = self._descs[0]
+        # one contiguous [world, max_chunk, 2] buffer per slot on the coordinator; the
         # per-rank gather outputs are views of it, so the whole round's results
         # come to the host with ONE device->host copy (``gathered_all``)
-        self.gathered_all = torch.zeros(env.world, max_chunk, 2, dtype=torch.int32, device=dev) \
-            if env.rank == coordinator else None
-        self._gathered = list(self.gathered_all.unbind(0)) if env.rank == coordinator else None
-        # send buffer; a single rank's results are already in place (no copy)
-        self._pack = self._gathered[0] if env.world == 1 else \
-            torch.zeros(max_chunk, 2, dtype=torch.int32, device=dev)
+        coord = env.rank == coordinator
+        self._gathered_slots = [torch.zeros(env.world, max_chunk, 2, dtype=torch.int32, device=dev)
+                                for _ in range(nbuf)] if coord else None
+        self.gathered_all = self._gathered_slots[0] if coord else None
+        self._gathered = list(self.gathered_all.unbind(0)) if coord else None
+        # send buffers; a single rank's results are already in place (no copy)
+        if env.world == 1:
+            self._packs = [g[0] for g in self._gathered_slots]
+        else:
+            self._packs = [torch.zeros(max_chunk, 2, dtype=torch.int32, device=dev) for _ in range(nbuf)]
+        self._pack = self._packs[0]
+        self._desc_host = None
 
     # -- M9 ---------------------------------------------------------------------
     def dispatch(self, table: list[tuple[int, int, int, int]] | None) -> tuple[int, int, int, int]:
@@ -130,6 +141,50 @@ class QueryPlane:
             return dist.gather(self._pack, self._gathered, dst=self.coord, group=self.group, async_op=True)
         return dist.gather(self._pack, None, dst=self.coord, group=self.group, async_op=True)
 
+    # -- double-buffered rounds (bench.py's raw loop at N > 1) -------------------------
+    def row_start_slot(self, slot: int) -> torch.Tensor:
+        return self._descs[slot, self.env.rank, 2:3]
+
+    def send_slot(self, slot: int) -> torch.Tensor:
+        return self._packs[slot]
+
+    def gathered_slot(self, slot: int) -> torch.Tensor | None:
+        return self._gathered_slots[slot] if self._gathered_slots is not None else None
+
+    def post_dispatch(self, table, slot: int, hslot: int):
+        """Descriptor table of a round into slot ``slot`` (coordinator: staged
+        through pinned host buffer ``hslot % 4``) and its broadcast, without
+        waiting: returns the Work (None on one rank).  Post it BEFORE queuing
+        the forward that overlaps it and after the forward that last read the
+        slot (the collective stream waits for the work queued before it)."""
+        if self._desc_host is None:
+            pin = self.env.device.type == "cuda"
+            self._desc_host = [torch.full((self.env.world, 4), NO_WORK, dtype=torch.int64, pin_memory=pin)
+                               for _ in range(4)]
+        d = self._descs[slot]
+        if self.env.rank == self.coord:
+            assert table is not None and len(table) == self.env.world
+            h = self._desc_host[hslot % 4]
+            h.copy_(torch.tensor(table, dtype=torch.int64))
+            d.copy_(h, non_blocking=True)
+        if not self.env.distributed:
+            return None
+        return dist.broadcast(d, src=self.coord, group=self.group, async_op=True)
+
+    def post_gather(self, slot: int):
+        """Gather of slot ``slot``'s send buffer into its gathered round
+        (coordinator), without waiting; None on one rank."""
+        if not self.env.distributed:
+            return None
+        outs = list(self._gathered_slots[slot].unbind(0)) if self.env.rank == self.coord else None
+        return dist.gather(self._packs[slot], outs, dst=self.coord, group=self.group, async_op=True)
+
+    @staticmethod
+    def wait_work(work) -> None:
+        """The current stream (RCCL) waits for ``work``; the host does not."""
+        if work is not None:
+            work.wait()
+
     def dispatch_device(self, table: list[tuple[int, int, int, int]] | None, slot: int = 0) -> torch.Tensor:
         """Asynchronous dispatch: no host synchronisation anywhere.
 
@@ -138,10 +193,10 @@ class QueryPlane:
         in flight), copies it to the device and broadcasts it; every rank gets
         back a *device* view of its own row, which the forward graph consumes
         directly (e.g. as the shard window start)."""
-        if not hasattr(self, "_desc_host"):
+        if self._desc_host is None:
             pin = self.env.device.type == "cuda"
             self._desc_host = [torch.full((self.env.world, 4), NO_WORK, dtype=torch.int64, pin_memory=pin)
-                               for _ in range(2)]
+                               for _ in range(4)]
         if self.env.rank == self.coord:
             assert table is not None and len(table) == self.env.world
             h = self._desc_host[slot % 2]

@@ -100,6 +100,9 @@ def parse(argv=None):
     ap.add_argument("--dataset-images", type=int, default=2000,
                     help="synthetic images replicated in every rank's HBM (grown to fit a round)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="N > 1: keep the descriptor broadcast and result gather between the forwards "
+                         "(default: double-buffered, overlapped with the next round's forward)")
     ap.add_argument("--no-extras", action="store_true", help="skip the strong-scaling / fp16 / numerics extras")
     ap.add_argument("--no-system", action="store_true", help="skip phases 2-3 (system + failover)")
     ap.add_argument("--extras-timeout", type=float, default=150.0,
@@ -497,7 +500,7 @@ def run_rank(a) -> int:
         from idunno import ops
         dataset = ops.synth_images(a.seed + 1234, 0, D, env.device)
 
-    plane = QueryPlane(env, coordinator=0, max_chunk=max(B, strong_chunk))
+    plane = QueryPlane(env, coordinator=0, max_chunk=max(B, strong_chunk), nbuf=2)
     start_dev, send = plane.row_start(), plane.send_buffer
     model_id = 1 if a.model.startswith("resnet") else 0
 
@@ -509,6 +512,22 @@ def run_rank(a) -> int:
             return lambda q: runner.forward(dataset, start_dev, batch, 0, send)
         _, run = runner.capture_window(dataset, batch, start=start_dev, start_offset=0, packed=send)
         return lambda q: run()
+
+    def make_slot_runs(runner, batch):
+        """Pipelined variant (N > 1): one captured forward per descriptor/result
+        slot of the double-buffered plane, so round q+1's descriptor broadcast
+        and round q's gather run on the RCCL stream under the other slot's
+        forward."""
+        runs = []
+        for slot in range(2):
+            st, pk = plane.row_start_slot(slot), plane.send_slot(slot)
+            if runner is None:
+                runs.append(FakeRunner(env.device).window(dataset, batch, st, pk))
+            elif a.no_graph:
+                runs.append(lambda st=st, pk=pk: runner.forward(dataset, st, batch, 0, pk))
+            else:
+                runs.append(runner.capture_window(dataset, batch, start=st, start_offset=0, packed=pk)[1])
+        return lambda q: runs[q % 2]()
 
     def make_scatter_run(runner, batch, per_round):
         """M9 data variant: the images live only in the coordinator's HBM.
@@ -547,9 +566,17 @@ def run_rank(a) -> int:
             posted.clear()
         return run, finish
 
-    def measure(run, per_round: int, steps: int, warmup: int, label: str):
+    def measure(run, per_round: int, steps: int, warmup: int, label: str, pipelined: bool = False):
         """Time `steps` pipelined rounds of `per_round` images (split over the
-        ranks), then `unloaded` rounds one at a time for the p50 latency."""
+        ranks), then `unloaded` rounds one at a time for the p50 latency.
+
+        ``pipelined`` (``run`` from ``make_slot_runs``): round q alternates
+        between the plane's two slots; the broadcast of round q+1's
+        descriptors is posted before round q's forward and round q's gather
+        is waited for only after round q+1's forward is queued, so at N > 1
+        neither collective sits between two forwards on the compute stream."""
+        if pipelined:
+            return measure_pipelined(run, per_round, steps, warmup, label)
         state = JobState() if coord else None
         host = [torch.empty(W, plane.max_chunk, 2, dtype=torch.int32, pin_memory=gpu) for _ in range(2)] \
             if coord else None
@@ -644,7 +671,122 @@ def run_rank(a) -> int:
         return {"elapsed": elapsed, "ips": per_round * steps / elapsed, "p50": p50, "p50_loaded": p50_loaded,
                 "recorded": recorded, "label": label,
                 "rank_ms": [1000.0 * x / steps for x in per_rank],
-                "gather_us": statistics.median(g_us) if g_us else None}
+                "gather_us": statistics.median(g_us) if g_us else None,
+                "verified": verify(state)}
+
+    def verify(state) -> bool | None:
+        """--dry-run: every recorded chunk holds the fake forward's classes for
+        ITS images (global index % 1000), i.e. no slot mix-up between the
+        descriptors, the forwards and the gathered rounds."""
+        if not (coord and a.dry_run):
+            return None
+        with state.lock:
+            chunks = [c for v in state.results.values() for c in v]
+        return bool(chunks) and all(
+            np.array_equal(c.cls, np.arange(c.start, c.end + 1) % 1000) for c in chunks)
+
+    def measure_pipelined(run, per_round: int, steps: int, warmup: int, label: str):
+        state = JobState() if coord else None
+        host = [torch.empty(W, plane.max_chunk, 2, dtype=torch.int32, pin_memory=gpu) for _ in range(2)] \
+            if coord else None
+        lat, pending, posted, gathers = [], [], {}, []
+        t0s, tables = {}, {}
+
+        def table_of(q):
+            off = (q * per_round) % (D - max(per_round, plane.max_chunk) + 1)
+            chunks = split_range(off, off + per_round - 1, W)
+            return chunks, [(model_id, q, s, e) for s, e in chunks]
+
+        def post(q):
+            tab = None
+            if coord:
+                chunks, tab = table_of(q)
+                tables[q] = (chunks, tab)
+            posted[q] = plane.post_dispatch(tab, slot=q % 2, hslot=q)
+
+        def ingest():
+            ev, q = pending.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            t1 = time.perf_counter()
+            res = host[q % 2].numpy()
+            cls_all, prob_all = res[:, :, 0], res[:, :, 1].view(np.float32)
+            _, tab = tables.pop(q)
+            for r, row in enumerate(tab):
+                n = row[3] - row[2] + 1
+                state.record_result(a.model, row[1], f"rank{r}", row[2], row[3], cls_all[r, :n].copy(),
+                                    prob_all[r, :n].copy(), t1)
+            lat.append(time.perf_counter() - t0s.pop(q))
+
+        def finish_gather():
+            """The compute stream waits for the oldest posted gather; the
+            coordinator copies that round to the host and ingests the round
+            before it (whose copy has had a forward's time to land)."""
+            q, work = gathers.pop(0)
+            plane.wait_work(work)
+            if coord:
+                host[q % 2].copy_(plane.gathered_slot(q % 2), non_blocking=gpu)
+                ev = None
+                if gpu:
+                    ev = torch.cuda.Event()
+                    ev.record()
+                if pending:
+                    ingest()
+                pending.append((ev, q))
+
+        def step(q: int, nxt: bool):
+            t0s[q] = time.perf_counter()
+            if q not in posted:
+                post(q)
+            if coord:
+                chunks, _ = tables[q]
+                state.assign(a.model, q, [(f"rank{r}", s, e) for r, (s, e) in enumerate(chunks)], t0s[q])
+            if nxt:
+                post(q + 1)          # RCCL stream: waits only for round q-1 (last reader of slot (q+1)%2)
+            plane.wait_work(posted.pop(q))
+            if a.fail_rank == env.rank and q == warmup:
+                print(f"bench: rank {env.rank} failing on purpose (--fail-rank)", file=sys.stderr, flush=True)
+                os._exit(3)
+            run(q)
+            if gathers:
+                finish_gather()      # round q-1's gather ran under round q's forward
+            gathers.append((q, plane.post_gather(q % 2)))
+
+        def drain():
+            while gathers:
+                finish_gather()
+            if coord:
+                while pending:
+                    ingest()
+            barrier()
+
+        for q in range(warmup):
+            step(q, q + 1 < warmup)
+        drain()
+        lat.clear()
+        t_start = time.perf_counter()
+        for q in range(warmup, warmup + steps):
+            step(q, q + 1 < warmup + steps)
+        drain()
+        elapsed = time.perf_counter() - t_start
+        per_rank = [elapsed]
+        if env.distributed:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
+            outs = [torch.zeros_like(t) for _ in range(W)]
+            dist.all_gather(outs, t)
+            per_rank = [float(x.item()) for x in outs]
+            elapsed = max(per_rank)
+        p50_loaded = statistics.median(lat) if lat else None
+        lat.clear()
+        for q in range(warmup + steps, warmup + steps + max(5, min(steps, 20))):
+            step(q, False)
+            drain()
+        p50 = statistics.median(lat) if lat else None
+        recorded = state.images_done(a.model) if coord else None
+        return {"elapsed": elapsed, "ips": per_round * steps / elapsed, "p50": p50, "p50_loaded": p50_loaded,
+                "recorded": recorded, "label": label,
+                "rank_ms": [1000.0 * x / steps for x in per_rank], "gather_us": None,
+                "verified": verify(state)}
 
     # ---- headline: weak scaling at the headline precision --------------------
     runner = None
@@ -652,11 +794,23 @@ def run_rank(a) -> int:
         from idunno.models import HipRunner, build_program, program_flops
         runner = HipRunner(build_program(a.model, seed=a.seed, dtype=a.dtype), env.device)
         runner.split = a.fp32_impl == "split"
-    head = measure(make_run(runner, B), W * B, a.steps, a.warmup, "weak")
-    extras = {}
+    pipe = W > 1 and not a.no_pipeline
+
+    def make(r, batch):
+        return make_slot_runs(r, batch) if pipe else make_run(r, batch)
+
+    head = measure(make(runner, B), W * B, a.steps, a.warmup, "weak", pipelined=pipe)
+    extras = {"pipelined_collectives": pipe}
+    serial = None
+    if pipe:
+        # the same rounds with the broadcast and gather between the forwards on the
+        # compute stream: what the pipelining saves, and the gather's own time
+        serial = measure(make_run(runner, B), W * B, a.steps, a.warmup, "weak-serial")
+        extras.update({"value_serial_collectives": round(serial["ips"], 2),
+                       "ms_per_step_serial_collectives": round(1000 * serial["elapsed"] / a.steps, 4)})
     if not a.no_extras:
         # strong scaling: ONE 400-image query split over the W ranks
-        strong = measure(make_run(runner, strong_chunk), QUERY, a.steps, a.warmup, "strong")
+        strong = measure(make(runner, strong_chunk), QUERY, a.steps, a.warmup, "strong", pipelined=pipe)
         extras.update({
             "images_per_s_strong": round(strong["ips"], 2),
             "p50_query_latency_strong_s": round(strong["p50"], 6) if strong["p50"] else None,
@@ -717,6 +871,7 @@ def run_rank(a) -> int:
             "p50_query_latency_loaded_s": round(head["p50_loaded"], 6) if head["p50_loaded"] else None,
             "p50_vs_baseline_speedup": round(BASELINE_P50_S / p50, 1) if p50 and headline else None,
             "results_recorded": head["recorded"],
+            **({"results_verified": head["verified"]} if head["verified"] is not None else {}),
             # readiness keys: the collective the timed rounds ran on, read from the
             # live process group, the per-rank spread of the step time and the gather's own time
             "comm_backend": (dist.get_backend() if env.distributed else "none (single rank: no collective)"),
@@ -724,7 +879,8 @@ def run_rank(a) -> int:
             "rccl": bool(env.distributed and dist.get_backend() == "nccl" and torch.version.hip is not None),
             "ms_per_step_rank_min": round(min(head["rank_ms"]), 4),
             "ms_per_step_rank_max": round(max(head["rank_ms"]), 4),
-            "gather_us_per_round": round(head["gather_us"], 1) if head["gather_us"] is not None else None,
+            "gather_us_per_round": (round(serial["gather_us"], 1) if serial and serial["gather_us"] is not None else
+                                    round(head["gather_us"], 1) if head["gather_us"] is not None else None),
             **extras,
         }
         if runner is not None:

@@ -41,6 +41,11 @@ def test_bench_self_launch_dry_run(n):
     assert d["scaling"] == "weak" and d["higher_is_better"] is True
     # warmup + timed + >= 5 unloaded latency rounds, 400 images per GPU each
     assert d["results_recorded"] == (warmup + steps + 5) * 400 * n
+    # every chunk holds its own images' classes (no slot mix-up in the double-buffered rounds)
+    assert d["results_verified"] is True
+    assert d["pipelined_collectives"] is (n > 1)
+    if n > 1:
+        assert d["value_serial_collectives"] > 0 and d["gather_us_per_round"] > 0
     assert d["strong_chunk_per_gpu"] == -(-400 // n)
     assert d["images_per_s_strong"] > 0 and d["p50_query_latency_strong_s"] > 0
     for k in ("metric", "value", "unit", "ms_per_step", "vs_baseline", "dtype", "data", "config"):
