@@ -320,9 +320,3 @@ def pack_into(send: torch.Tensor, cls, prob) -> None:
     n = c.numel()
     send[:n, 0].copy_(c.to(send.device))
     send[:n, 1].copy_(p.to(send.device))
-
-
-def unpack_row(row: np.ndarray, n: int) -> tuple[np.ndarray, np.ndarray]:
-    """(cls int32 [n], prob fp32 [n]) from one gathered host row."""
-    r = row[:n]
-    return np.ascontiguousarray(r[:, 0]), np.ascontiguousarray(r[:, 1]).view(np.float32)

@@ -51,10 +51,10 @@ import threading
 import time
 from collections import deque
 
+import numpy as np
 import torch
 
-from ..parallel.elastic import HDR_ROWS, MODEL_IDS, MODEL_NAMES, ElasticGroup, RoundAbandoned, pack_into, \
-    unpack_row
+from ..parallel.elastic import HDR_ROWS, MODEL_IDS, MODEL_NAMES, ElasticGroup, RoundAbandoned, pack_into
 from .messages import Type
 from .scheduler import split_range
 
@@ -541,16 +541,24 @@ class RoundPlane:
         mc = g.max_chunk
         now = time.time()
         recs = []
+        # the whole round at once: one copy of the class and probability planes
+        # (every chunk's arrays are row views of them, so the host ring slot can be
+        # reused), one header read and one out-of-range test for all members
+        cls_all = np.ascontiguousarray(arr[:, :mc, 0])
+        prob_all = np.ascontiguousarray(arr[:, :mc, 1]).view(np.float32)
+        hdr = arr[:, mc:mc + HDR_ROWS, :].reshape(len(arr), 2 * HDR_ROWS).tolist()  # (us, model id, n, tag)
+        lens = np.array([0 if row is None else row[3] - row[2] + 1 for row in r.table])
+        bad = ((cls_all < 0) & (np.arange(mc) < lens[:, None])).any(axis=1).tolist()
         for i, row in enumerate(r.table):
-            us, hmid, cnt = int(arr[i, mc, 0]), int(arr[i, mc, 1]), int(arr[i, mc + 1, 0])
+            us, hmid, cnt = hdr[i][0], hdr[i][1], hdr[i][2]
             if cnt > 0 and hmid in MODEL_NAMES:
                 model = MODEL_NAMES[hmid]
                 n.sched.observe(model, us * 1e-6 / cnt * self.cfg.batch_for(model))
             if row is None:
                 continue
             mid, qnum, s, e = row
-            cls, prob = unpack_row(arr[i], e - s + 1)
-            if (cls < 0).any():
+            cls, prob = cls_all[i, :e - s + 1], prob_all[i, :e - s + 1]
+            if bad[i]:
                 # the member's split forward left fp16's range (class -2): the chunk
                 # goes to it again as a TCP JOB, whose executor path reruns it on
                 # the all-f32 kernels

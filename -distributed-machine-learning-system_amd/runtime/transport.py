@@ -17,6 +17,8 @@ transfer) never blocks the receive path.
 """
 from __future__ import annotations
 
+import ctypes
+import errno
 import itertools
 import logging
 import random
@@ -29,6 +31,38 @@ from concurrent.futures import TimeoutError as FuturesTimeout
 from .messages import FrameReader, Type, encode
 
 log = logging.getLogger("idunno.transport")
+
+
+# Frames go out through libc ``send`` called via a PyDLL handle, i.e. WITHOUT
+# releasing the GIL, and with MSG_DONTWAIT: a control frame to a localhost peer
+# fits the socket buffer and is copied in a few microseconds.  ``socket.sendall``
+# releases and re-acquires the GIL around every call, and on a busy host each
+# re-acquire can queue behind the node's other threads (receivers, heartbeats,
+# the round loop): a 7-peer multicast paid that convoy seven times.  A send
+# that would block (full buffer) finishes through ``sendall`` as before.
+try:
+    _LIBC = ctypes.PyDLL(None, use_errno=True)
+    _SEND = _LIBC.send
+    _SEND.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+    _SEND.restype = ctypes.c_ssize_t
+except (OSError, AttributeError):          # pragma: no cover - non-glibc host
+    _SEND = None
+_MSG_DONTWAIT, _MSG_NOSIGNAL = 0x40, 0x4000
+
+
+def _send_frame(sock: socket.socket, data: bytes) -> None:
+    """``sock.sendall(data)``, holding the GIL for the common non-blocking case."""
+    n = 0
+    if _SEND is not None:
+        n = _SEND(sock.fileno(), data, len(data), _MSG_DONTWAIT | _MSG_NOSIGNAL)
+        if n == len(data):
+            return
+        if n < 0:
+            e = ctypes.get_errno()
+            if e not in (errno.EAGAIN, errno.EWOULDBLOCK, errno.EINTR):
+                raise OSError(e, "send failed")
+            n = 0
+    sock.sendall(memoryview(data)[n:])
 
 
 class TransportError(RuntimeError):
@@ -299,7 +333,7 @@ class TcpTransport(BaseTransport):
         with lk:
             for attempt in (0, 1):
                 try:
-                    self._conn(dst).sendall(data)
+                    _send_frame(self._conn(dst), data)
                     return True
                 except OSError:
                     self._drop(dst)
