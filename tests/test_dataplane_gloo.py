@@ -216,3 +216,74 @@ def test_bench_round_pattern_over_gloo(world):
     assert len(out) == 4 * world * 8
     for (_q, i), (c, p) in out.items():
         assert c == (i * 7919 + 13) % 1000 and p == 0.25
+
+
+def _pipelined_worker(rank, world, port, q):
+    """bench.py's double-buffered round at N > 1: round q+1's descriptors are
+    broadcast into the other slot before round q's forward runs, and round q's
+    gather is finished only after round q+1's forward; every slot's results
+    must still belong to that slot's round."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from idunno.parallel.dataplane import QueryPlane, init_from_env, unpack
+
+    env = init_from_env(backend="gloo")
+    B, rounds = 8, 7
+    plane = QueryPlane(env, coordinator=0, max_chunk=B, nbuf=2)
+
+    def table(q_):
+        return [(1, q_, 100 * q_ + r * B, 100 * q_ + r * B + B - 1) for r in range(world)]
+
+    def forward(slot):
+        s0 = int(plane.row_start_slot(slot).item())
+        idx = torch.arange(s0, s0 + B, dtype=torch.int32)
+        plane.send_slot(slot)[:B, 0] = (idx * 31 + 5) % 1000
+        plane.send_slot(slot)[:B, 1] = torch.full((B,), 0.5).view(torch.int32)
+
+    out, posted, gathers = {}, {}, []
+
+    def finish():
+        q_, work = gathers.pop(0)
+        plane.wait_work(work)
+        if env.rank == 0:
+            host = plane.gathered_slot(q_ % 2).clone()
+            for r in range(world):
+                c, _ = unpack(host[r], B)
+                out[(q_, r)] = c.tolist()
+
+    for q_ in range(rounds):
+        if q_ not in posted:
+            posted[q_] = plane.post_dispatch(table(q_) if env.rank == 0 else None, q_ % 2, q_)
+        if q_ + 1 < rounds:
+            posted[q_ + 1] = plane.post_dispatch(table(q_ + 1) if env.rank == 0 else None, (q_ + 1) % 2, q_ + 1)
+        plane.wait_work(posted.pop(q_))
+        forward(q_ % 2)
+        if gathers:
+            finish()
+        gathers.append((q_, plane.post_gather(q_ % 2)))
+    while gathers:
+        finish()
+    if env.rank == 0:
+        ok = len(out) == rounds * world and all(
+            c == [((table(q_)[r][2] + i) * 31 + 5) % 1000 for i in range(B)] for (q_, r), c in out.items())
+        q.put(ok)
+    if env.distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_double_buffered_rounds_over_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert ok is True
