@@ -19,6 +19,7 @@ worker's device:
 """
 from __future__ import annotations
 
+import os
 import threading
 from collections import OrderedDict
 
@@ -85,6 +86,81 @@ class HbmStager:
         # optional GPU timeline: ("h2d", start event, end event, bytes) per stage() call
         # on the side stream (bench.py lines it up against the forwards' events)
         self.timeline: list | None = None
+        self._readers = None              # preadv thread pool of stage_file (lazy)
+
+    READ_THREADS = 4
+
+    def stage_file(self, path: str, shape: tuple) -> torch.Tensor:
+        """Stage a file's bytes into a new device tensor of ``shape`` (uint8)
+        without a host copy of the file: each piece is read with ``os.preadv``
+        by READ_THREADS threads straight into a pinned ping-pong buffer (the
+        reads release the GIL), then DMA'd on the side stream while the next
+        piece is read into the other buffer.  A bytes object of a large file
+        costs fresh page faults on every read (~1.5 GB/s on these hosts); the
+        pinned buffers are faulted in once."""
+        nbytes = int(np.prod(shape))
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            if os.fstat(fd).st_size < nbytes:
+                raise ValueError(f"{path}: {os.fstat(fd).st_size} bytes, need {nbytes}")
+            if not self.gpu:
+                buf = np.empty(nbytes, np.uint8)
+                self._pread(fd, memoryview(buf), 0)
+                self.bytes_staged += nbytes
+                return torch.from_numpy(buf).view(*shape)
+            out = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            step = self.pinned[0].numel()
+            nb = len(self.pinned)
+            with self.lock:
+                ev = None
+                tl = self.timeline
+                if tl is not None:
+                    ev0 = torch.cuda.Event(enable_timing=True)
+                    ev0.record(self.stream)
+                for i, off in enumerate(range(0, nbytes, step)):
+                    b = i % nb
+                    n = min(step, nbytes - off)
+                    if self._done[b] is not None:
+                        self._done[b].synchronize()
+                    self._pread(fd, memoryview(self.pinned[b].numpy())[:n], off)
+                    with torch.cuda.stream(self.stream):
+                        out[off:off + n].copy_(self.pinned[b][:n], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(self.stream)
+                    self._done[b] = ev
+                if tl is not None:
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev1.record(self.stream)
+                    tl.append(("h2d", ev0, ev1, nbytes))
+                self.bytes_staged += nbytes
+        finally:
+            os.close(fd)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+        return out.view(*shape)
+
+    def _pread(self, fd: int, dst: memoryview, off: int) -> None:
+        """Fill ``dst`` from file offset ``off`` with parallel preadv calls."""
+        n = len(dst)
+        nt = max(1, min(self.READ_THREADS, n >> 22))          # >= 4 MiB per thread
+        part = -(-n // nt)
+
+        def work(i):
+            mv, pos = dst[i * part:min(n, (i + 1) * part)], off + i * part
+            while len(mv):
+                k = os.preadv(fd, [mv], pos)
+                if k <= 0:
+                    raise EOFError(f"short read at {pos}")
+                mv, pos = mv[k:], pos + k
+        if nt == 1:
+            work(0)
+            return
+        if self._readers is None:
+            from concurrent.futures import ThreadPoolExecutor
+
+            self._readers = ThreadPoolExecutor(max_workers=self.READ_THREADS, thread_name_prefix="stage-read")
+        for f in [self._readers.submit(work, i) for i in range(nt)]:
+            f.result()
 
     def stage(self, data: bytes | np.ndarray, shape: tuple) -> torch.Tensor:
         """Copy host bytes to a new device tensor of ``shape`` (uint8).  The
@@ -93,6 +169,7 @@ class HbmStager:
         src = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) \
             else np.ascontiguousarray(data).reshape(-1).view(np.uint8)
         if not self.gpu:
+            self.bytes_staged += src.size
             return torch.from_numpy(src.copy()).view(*shape)
         out = torch.empty(src.size, dtype=torch.uint8, device=self.device)
         step = self.pinned[0].numel()
@@ -157,6 +234,7 @@ class SdfsSource:
         self._absent: set = set()                 # shards a readahead found missing (past the dataset's end)
         self._pool = None
         self.readahead_hits = 0
+        self.local_reads = 0                      # shards streamed from this node's own replica file
         if self.device.type == "cuda":
             sdfs.hbm_provider = self.export_shard
 
@@ -237,12 +315,24 @@ class SdfsSource:
             t, ver = got
             self.peer_fetches += 1
         else:
-            got = self.sdfs.get_bytes_ver(name)
-            if got is None:
-                raise KeyError(f"missing SDFS shard {name}")
-            data, ver = got
-            n = len(data) // IMG_BYTES
-            t = self.stager.stage(data, (n, HW, HW, 3))
+            # this node's own replica streams from its file into the pinned buffers;
+            # another node's replica comes over the transport as bytes
+            loc = self.sdfs.local_file(name) if hasattr(self.sdfs, "local_file") else None
+            if loc is not None:
+                path, ver = loc
+                try:
+                    n = os.path.getsize(path) // IMG_BYTES
+                    t = self.stager.stage_file(path, (n, HW, HW, 3))
+                    self.local_reads += 1
+                except OSError:                   # replaced by a newer version meanwhile
+                    loc = None
+            if loc is None:
+                got = self.sdfs.get_bytes_ver(name)
+                if got is None:
+                    raise KeyError(f"missing SDFS shard {name}")
+                data, ver = got
+                n = len(data) // IMG_BYTES
+                t = self.stager.stage(data, (n, HW, HW, 3))
         dropped = []
         with self.lock:
             self.fetches += 1

@@ -321,6 +321,21 @@ class Sdfs:
                 continue
         return None
 
+    def local_file(self, name: str) -> tuple[str, int] | None:
+        """(path, version) of this node's own replica of the current version of
+        ``name``, or None (not a replica holder / file gone).  Lets a reader
+        stream the file straight into its own buffers (``HbmStager.stage_file``)
+        instead of materialising it as a bytes object."""
+        try:
+            loc = self._req(self._master(), {"t": Type.GET, "name": name})
+        except Exception:  # noqa: BLE001
+            return None
+        if not loc.get("exists") or self.node.name not in loc.get("replicas", []):
+            return None
+        ver = int(loc["ver"])
+        p = self.store._path(name, ver)
+        return (str(p), ver) if p.exists() else None
+
     def get_bytes(self, name: str, ver: int | None = None) -> bytes | None:
         return self._fetch(name, ver)
 

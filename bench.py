@@ -1089,7 +1089,7 @@ def _drive_system(a, node, W: int, B: int) -> dict:
         out["system_host_send_ms_per_round"] = round(1000 * (rb["host_send_s"] - ra["host_send_s"]) / nr, 4)
 
     if W == 1 and a.sdfs_images > 0:
-        out.update(_sdfs_pass(a, node, per_q, wait_for))
+        out.update(_sdfs_pass(a, node, per_q))
 
     # two concurrent jobs: AlexNet + ResNet18 (report Fig 2), coordinator-side jobs
     bs = {"alexnet": QUERY_ALEXNET * W, "resnet18": QUERY * W}
@@ -1180,7 +1180,7 @@ def _timeline_overlap(tl: list) -> tuple[float, list]:
     return (ov / tot if tot > 0 else 0.0), iv
 
 
-def _sdfs_pass(a, node, per_q: int, wait_for) -> dict:
+def _sdfs_pass(a, node, per_q: int) -> dict:
     """SDFS -> HBM on the measured path: the synthetic
     dataset is put into SDFS as 500-image uint8 shards, then the same ResNet18
     queries are served from ``SdfsSource`` -- cold (every shard read from the
@@ -1199,7 +1199,7 @@ def _sdfs_pass(a, node, per_q: int, wait_for) -> dict:
     put_s = time.perf_counter() - t
     keep = node.source
     src = SdfsSource(node.sdfs, node.device if node.device is not None else "cpu", shard_images=500,
-                     peer_copy=False)
+                     peer_copy=False, readahead=2)
     gpu = src.device.type == "cuda"
     node.source = src
     out = {}
@@ -1209,8 +1209,8 @@ def _sdfs_pass(a, node, per_q: int, wait_for) -> dict:
             t0 = time.perf_counter()
             for q0 in range(0, n_img, per_q):
                 node.submit_query(a.model, q0, q0 + per_q - 1)
-            assert wait_for(lambda: st.images_done(a.model) >= done0 + n_img and st.pending_count() == 0,
-                            300, 0.0005), st.summary()
+            assert _wait_progress(node, lambda: st.images_done(a.model) >= done0 + n_img and st.pending_count() == 0,
+                                  300), st.summary()
             return time.perf_counter() - t0
 
         tl = [] if gpu else None
@@ -1231,8 +1231,9 @@ def _sdfs_pass(a, node, per_q: int, wait_for) -> dict:
                "sdfs_bytes_staged": staged,
                "hbm_stage_gb_per_s": round(staged / (h2d_ms * 1e-3) / 1e9, 2) if h2d_ms > 0 else None,
                "sdfs_h2d_overlap_frac": round(ovl, 4) if ovl is not None else None,
-               "sdfs_path": "SDFS store (local replica) -> pinned ping-pong -> hipMemcpyAsync on a side stream -> "
-                            "HBM shard cache -> rounds"}
+               "sdfs_local_file_reads": src.local_reads, "sdfs_readahead_hits": src.readahead_hits,
+               "sdfs_path": "SDFS store (local replica file) -> parallel preadv into pinned ping-pong buffers -> "
+                            "hipMemcpyAsync on a side stream -> HBM shard cache -> rounds (2-shard readahead)"}
         if a.sdfs_trace and iv:
             ev = [{"name": k, "ph": "X", "ts": 1000.0 * t0, "dur": 1000.0 * (t1 - t0), "pid": 0,
                    "tid": 1 if k == "h2d" else 0, "args": {"n": n}} for k, t0, t1, n in iv]

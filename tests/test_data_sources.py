@@ -121,3 +121,42 @@ def test_sdfs_source_readahead_prefetches_next_shard():
     assert store.reads.count(shard_name(1)) == 1        # never read twice
     src.get(25, 29)                                      # readahead past the last shard: harmless
     assert torch.equal(src.get(20, 29), torch.from_numpy(synth_images_cpu(5, 20, 10)))
+
+
+def test_stage_file_parallel_preadv(tmp_path):
+    """HbmStager.stage_file reads a file with parallel preadv calls straight
+    into its buffers (CPU here; pinned ping-pong + side-stream DMA on a GPU)."""
+    from idunno.runtime.data import HbmStager
+
+    data = np.random.default_rng(1).integers(0, 256, 20 << 20, dtype=np.uint8)
+    p = tmp_path / "blob"
+    p.write_bytes(data.tobytes() + b"tail")               # longer than the staged shape: ignored
+    st = HbmStager("cpu")
+    t = st.stage_file(str(p), (20, 1 << 20))
+    assert t.shape == (20, 1 << 20) and np.array_equal(t.reshape(-1).numpy(), data)
+    try:
+        st.stage_file(str(p), (21, 1 << 20))
+        raise AssertionError("short file accepted")
+    except ValueError:
+        pass
+
+
+def test_sdfs_source_streams_local_replica_file(tmp_path):
+    """A shard this node holds a replica of is streamed from its file
+    (``local_file``) instead of coming back as a bytes object."""
+    from idunno.runtime.data import SdfsSource, shard_name
+
+    class LocalStore(_ShardStore):
+        def local_file(self, name):
+            d = self.files.get(name)
+            if d is None or name == shard_name(2):         # shard 2: another node's replica
+                return None
+            p = tmp_path / name.replace("/", "_")
+            p.write_bytes(d)
+            return str(p), 1
+
+    store = LocalStore(6, 30, 10)
+    src = SdfsSource(store, "cpu", shard_images=10, peer_copy=False, readahead=0)
+    x = src.get(0, 29)
+    assert torch.equal(x, torch.from_numpy(synth_images_cpu(6, 0, 30)))
+    assert src.local_reads == 2 and store.reads == [shard_name(2)]
