@@ -47,6 +47,7 @@ collective posted, so no RCCL kernel spins on an idle GPU.
 from __future__ import annotations
 
 import logging
+import os
 import threading
 import time
 from collections import deque
@@ -304,6 +305,24 @@ class RoundPlane:
 
     # -- driver thread ---------------------------------------------------------------------
     def _driver(self) -> None:
+        """Round driver thread.  IDUNNO_PROFILE_DRIVER=<path>: the coordinator's
+        driver thread runs under cProfile and dumps its stats there on exit
+        (host-cost diagnostics; bench.py --system)."""
+        path = os.environ.get("IDUNNO_PROFILE_DRIVER")
+        if not path or not self.node.is_coordinator:
+            self._drive()
+            return
+        import cProfile
+
+        pr = cProfile.Profile()
+        pr.enable()
+        try:
+            self._drive()
+        finally:
+            pr.disable()
+            pr.dump_stats(path)
+
+    def _drive(self) -> None:
         n = self.node
         while n.alive_flag:
             self._wake.wait(0.1)
