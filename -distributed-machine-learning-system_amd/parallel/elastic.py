@@ -309,14 +309,22 @@ class ElasticGroup:
                 host.copy_(self._gathered[slot], non_blocking=True)
             self._d2h.synchronize()
         else:
-            host.copy_(self._gathered[slot])
+            # numpy copy: a torch op would drop and re-take the GIL around 33 KB
+            h = host.numpy()
+            np.copyto(h, self._gathered[slot].numpy())
+            return h
         return host.numpy()
 
 
 def pack_into(send: torch.Tensor, cls, prob) -> None:
     """Write host (cls int32 [n], prob fp32 [n]) into a send buffer slot."""
-    c = torch.as_tensor(np.ascontiguousarray(cls, np.int32))
-    p = torch.as_tensor(np.ascontiguousarray(prob, np.float32)).view(torch.int32)
-    n = c.numel()
-    send[:n, 0].copy_(c.to(send.device))
-    send[:n, 1].copy_(p.to(send.device))
+    c = np.ascontiguousarray(cls, np.int32)
+    p = np.ascontiguousarray(prob, np.float32).view(np.int32)
+    n = c.size
+    if send.device.type == "cpu":
+        s = send.numpy()                     # in place, without a GIL round-trip per torch op
+        s[:n, 0] = c
+        s[:n, 1] = p
+        return
+    send[:n, 0].copy_(torch.as_tensor(c).to(send.device))
+    send[:n, 1].copy_(torch.as_tensor(p).to(send.device))

@@ -88,12 +88,12 @@ class HbmStager:
         self.timeline: list | None = None
         self._readers = None              # preadv thread pool of stage_file (lazy)
 
-    READ_THREADS = 4
+    READ_THREADS = 8
 
     def stage_file(self, path: str, shape: tuple) -> torch.Tensor:
         """Stage a file's bytes into a new device tensor of ``shape`` (uint8)
         without a host copy of the file: each piece is read with ``os.preadv``
-        by READ_THREADS threads straight into a pinned ping-pong buffer (the
+        by up to READ_THREADS threads straight into a pinned ping-pong buffer (the
         reads release the GIL), then DMA'd on the side stream while the next
         piece is read into the other buffer.  A bytes object of a large file
         costs fresh page faults on every read (~1.5 GB/s on these hosts); the

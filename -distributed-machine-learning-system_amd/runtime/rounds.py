@@ -291,17 +291,17 @@ class RoundPlane:
                 us, mid, cnt = int(t * 1e6), m, c
                 self._timings.popleft()
         self._tag += 1
-        vals = torch.tensor([us, mid, cnt, self._tag], dtype=torch.int32).view(HDR_ROWS, 2)
+        vals = (us, mid, cnt, self._tag)
         hdr = self.group.header(seq)
         if hdr.device.type == "cuda":
             if self._hdr is None:
                 self._hdr = [torch.zeros(HDR_ROWS, 2, dtype=torch.int32, pin_memory=True)
                              for _ in range(self.HDR_RING)]
             p = self._hdr[seq % self.HDR_RING]
-            p.copy_(vals)
+            p.numpy().reshape(-1)[:] = vals
             hdr.copy_(p, non_blocking=True)
         else:
-            hdr.copy_(vals)
+            hdr.numpy().reshape(-1)[:] = vals
 
     # -- driver thread ---------------------------------------------------------------------
     def _driver(self) -> None:
@@ -568,11 +568,18 @@ class RoundPlane:
         hdr = arr[:, mc:mc + HDR_ROWS, :].reshape(len(arr), 2 * HDR_ROWS).tolist()  # (us, model id, n, tag)
         lens = np.array([0 if row is None else row[3] - row[2] + 1 for row in r.table])
         bad = ((cls_all < 0) & (np.arange(mc) < lens[:, None])).any(axis=1).tolist()
-        for i, row in enumerate(r.table):
-            us, hmid, cnt = hdr[i][0], hdr[i][1], hdr[i][2]
+        # one scheduler observation per model per round: the members' summed compute
+        # time over their summed images (a per-image time), scaled to the model's batch
+        obs = {}
+        for us, hmid, cnt, _ in hdr:
             if cnt > 0 and hmid in MODEL_NAMES:
-                model = MODEL_NAMES[hmid]
-                n.sched.observe(model, us * 1e-6 / cnt * self.cfg.batch_for(model))
+                o = obs.setdefault(hmid, [0, 0])
+                o[0] += us
+                o[1] += cnt
+        for hmid, (us, cnt) in obs.items():
+            model = MODEL_NAMES[hmid]
+            n.sched.observe(model, us * 1e-6 / cnt * self.cfg.batch_for(model))
+        for i, row in enumerate(r.table):
             if row is None:
                 continue
             mid, qnum, s, e = row

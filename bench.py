@@ -1199,7 +1199,7 @@ def _sdfs_pass(a, node, per_q: int) -> dict:
     put_s = time.perf_counter() - t
     keep = node.source
     src = SdfsSource(node.sdfs, node.device if node.device is not None else "cpu", shard_images=500,
-                     peer_copy=False, readahead=2)
+                     peer_copy=False, readahead=4)
     gpu = src.device.type == "cuda"
     node.source = src
     out = {}
@@ -1233,7 +1233,7 @@ def _sdfs_pass(a, node, per_q: int) -> dict:
                "sdfs_h2d_overlap_frac": round(ovl, 4) if ovl is not None else None,
                "sdfs_local_file_reads": src.local_reads, "sdfs_readahead_hits": src.readahead_hits,
                "sdfs_path": "SDFS store (local replica file) -> parallel preadv into pinned ping-pong buffers -> "
-                            "hipMemcpyAsync on a side stream -> HBM shard cache -> rounds (2-shard readahead)"}
+                            "hipMemcpyAsync on a side stream -> HBM shard cache -> rounds (4-shard readahead)"}
         if a.sdfs_trace and iv:
             ev = [{"name": k, "ph": "X", "ts": 1000.0 * t0, "dur": 1000.0 * (t1 - t0), "pid": 0,
                    "tid": 1 if k == "h2d" else 0, "args": {"n": n}} for k, t0, t1, n in iv]
