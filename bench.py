@@ -75,6 +75,7 @@ BASELINE_P50_S = 9.749             # p50 ResNet18 400-image query l
 BASELINE_COORD_RECOVERY_S = 6.999  # coordinator failure, 1 undone query (report Fig 5)
 BASELINE_WORKER_RECOVERY_S = {1: 5.725, 2: 8.661, 4: 13.425, 6: 19.125, 8: 26.751}   # report Fig 4
 BASELINE_SECOND_JOB_S = {"alexnet_first": 41.159, "resnet18_first": 46.752}   # report Fig 3 medians
+REF_WORKER_START_DELAY_S = 3.0     # reference sleep before every chunk (mp4_machinelearning.py:594)
 METRIC = "images/sec (whole node) + p50 query latency, ResNet18 bs=400 at 1/2/4/8 GPU"
 QUERY = 400                        # images per query (reference report p.1, ResNet18)
 QUERY_ALEXNET = 500                # AlexNet query size (report p.1)
@@ -111,6 +112,8 @@ def parse(argv=None):
                     help="seconds for all phases after the headline together; a phase that would start "
                          "past it is skipped (extras_skipped), so the headline line always comes out in time")
     ap.add_argument("--two-job-queries", type=int, default=10, help="queries per job in the two-job run")
+    ap.add_argument("--ref-delay-queries", type=int, default=3,
+                    help="queries timed with the reference's 3 s worker start delay (0: skip)")
     ap.add_argument("--sdfs-images", type=int, default=4000,
                     help="N=1 system phase: images put into SDFS as 500-image shards, then served cold and warm")
     ap.add_argument("--sdfs-trace", default=None, help="write the SDFS cold pass's H2D / forward GPU timeline "
@@ -361,6 +364,7 @@ def _phase_argv(a, phase: str, out: str, work: str) -> list:
             "--worker-kill-chunks", ",".join(str(k) for k in a.worker_kill_chunks),
             "--dtype", a.dtype, "--fp32-impl", a.fp32_impl, "--batch", str(a.batch), "--seed", str(a.seed),
             "--two-job-queries", str(a.two_job_queries), "--failover-queries", str(a.failover_queries),
+            "--ref-delay-queries", str(a.ref_delay_queries),
             "--sdfs-images", str(a.sdfs_images), *(["--sdfs-trace", a.sdfs_trace] if a.sdfs_trace else []),
             "--phase", phase, "--json-out", out, "--work-dir", work, "--launch-timeout", str(a.extras_timeout)]
     if a.dry_run:
@@ -1103,8 +1107,8 @@ def _drive_system(a, node, W: int, B: int) -> dict:
             cl.submit_job(base_img[0], base_img[0] + q * bs[m] - 1, m)
             done[m] += q * bs[m]
         base_img[0] += 10 ** 6
-        ok = wait_for(lambda: all(st.images_done(m) >= done[m] for m in bs) and st.pending_count() == 0,
-                      300, 0.002)
+        ok = _wait_progress(node, lambda: all(st.images_done(m) >= done[m] for m in bs) and st.pending_count() == 0,
+                            300)
         assert ok, st.summary()
         return time.perf_counter() - t, qn0
 
@@ -1142,20 +1146,43 @@ def _drive_system(a, node, W: int, B: int) -> dict:
         fq = {m: st.finished_queries.get(m, 0) for m in bs}
         cl.submit_job(base_img[0], base_img[0] + q * bs[first] - 1, first)
         done[first] += q * bs[first]
-        assert wait_for(lambda: st.finished_queries.get(first, 0) > fq[first], 120, 0.001), st.summary()
+        assert _wait_progress(node, lambda: st.finished_queries.get(first, 0) > fq[first], 120), st.summary()
         t = time.perf_counter()
         cl.submit_job(base_img[0] + 5 * 10 ** 5, base_img[0] + 5 * 10 ** 5 + q * bs[second] - 1, second)
         done[second] += q * bs[second]
-        assert wait_for(lambda: st.finished_queries.get(second, 0) > fq[second], 120, 0.0005), st.summary()
+        assert _wait_progress(node, lambda: st.finished_queries.get(second, 0) > fq[second], 120), st.summary()
         dt = time.perf_counter() - t
         base_img[0] += 10 ** 6
-        assert wait_for(lambda: all(st.images_done(m) >= done[m] for m in bs) and st.pending_count() == 0,
-                        300, 0.002), st.summary()
+        assert _wait_progress(node, lambda: all(st.images_done(m) >= done[m] for m in bs) and st.pending_count() == 0,
+                              300), st.summary()
         return dt
 
     sj = {"alexnet_first": second_job("alexnet", "resnet18"), "resnet18_first": second_job("resnet18", "alexnet")}
     out["second_job_start_s"] = {k: round(v, 4) for k, v in sj.items()}
     out["second_job_start_ref_s"] = BASELINE_SECOND_JOB_S
+
+    # like-for-like latency ("numbers also reported with those sleeps
+    # enabled"): the reference sleeps 3 s before every chunk (mp4_machinelearning.py:594);
+    # with that delay on the coordinator's own chunk every query waits for it
+    if a.ref_delay_queries > 0:
+        delay0 = node.cfg.worker_start_delay_s
+        node.cfg.worker_start_delay_s = REF_WORKER_START_DELAY_S
+        lat = []
+        try:
+            for i in range(a.ref_delay_queries):
+                d0 = st.images_done(a.model)
+                q0 = base_img[0] + i * per_q
+                t = time.perf_counter()
+                node.submit_query(a.model, q0, q0 + per_q - 1)
+                assert _wait_progress(node, lambda: st.images_done(a.model) >= d0 + per_q and st.pending_count() == 0,
+                                      60), st.summary()
+                lat.append(time.perf_counter() - t)
+        finally:
+            node.cfg.worker_start_delay_s = delay0
+        base_img[0] += 10 ** 6
+        out.update({"p50_query_latency_ref_delay_s": round(statistics.median(lat), 4),
+                    "ref_worker_start_delay_s": REF_WORKER_START_DELAY_S,
+                    "p50_query_latency_ref_delay_vs_baseline": round(BASELINE_P50_S / statistics.median(lat), 2)})
     grp = node.rounds.group.describe() if node.rounds is not None else {}
     out["system_comm_backend"] = grp.get("backend", "tcp (no collective)")
     out["system_comm_world"] = grp.get("world", 1)

@@ -31,7 +31,7 @@ def _line(out: str) -> dict:
 @pytest.mark.parametrize("n", [1, 2, 8])
 def test_bench_self_launch_dry_run(n):
     steps, warmup = 3, 1
-    r = _run("--gpus", str(n), "--steps", str(steps), "--warmup", str(warmup))
+    r = _run("--gpus", str(n), "--steps", str(steps), "--warmup", str(warmup), "--ref-delay-queries", "1")
     assert r.returncode == 0, r.stderr[-2000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == n
@@ -88,6 +88,8 @@ def test_bench_self_launch_dry_run(n):
     assert d["worker_failover_images_exact"] is True
     for k, t in d["worker_failover_recovery_s"].items():
         assert 0 < t <= d["worker_failover_failure_timeout_s"] + 3.0, d["worker_failover_recovery_s"]
+    # like-for-like latency with the reference's 3 s sleep before every chunk
+    assert d["ref_worker_start_delay_s"] == 3.0 and 3.0 <= d["p50_query_latency_ref_delay_s"] < 6.0
     assert set(d["second_job_start_s"]) == {"alexnet_first", "resnet18_first"}
     assert all(0 < v < 30 for v in d["second_job_start_s"].values())
     # readiness keys: the live process group the timed rounds used
