@@ -235,6 +235,8 @@ class ElasticGroup:
             self._gathered = [s.unsqueeze(0) for s in self._send]       # the send buffer IS the round
         elif self.rank == 0:
             self._gathered = [torch.zeros(world, rows, 2, dtype=torch.int32, device=dev) for _ in range(D)]
+            # per-slot gather output lists, built once (not one unbind per round)
+            self._gather_outs = [[list(g.unbind(0))] for g in self._gathered]
         if self.rank == 0:
             gpu = dev.type == "cuda"
             self._host = [torch.zeros(world, rows, 2, dtype=torch.int32, pin_memory=gpu) for _ in range(D)]
@@ -264,7 +266,7 @@ class ElasticGroup:
         opts = dist.GatherOptions()
         opts.rootRank = 0
         slot = seq % self.depth
-        outs = [list(self._gathered[slot].unbind(0))] if self.rank == 0 else []
+        outs = self._gather_outs[slot] if self.rank == 0 else []
         return pg.gather(outs, [self._send[slot]], opts)
 
     def wait(self, work, check=None) -> None:

@@ -367,17 +367,24 @@ class JobState:
     def _bulk_ok(self, recs) -> bool:
         model, qnum = recs[0][0], recs[0][1]
         key = (model, qnum)
-        if key not in self._open or any(r[0] != model or r[1] != qnum for r in recs):
+        if key not in self._open:
             return False
-        running = {(x[0], x[1], x[2]) for x in self.worker_set.get(key, []) if x[3] == "w"}
-        if any((w, int(s), int(e)) not in running or (model, qnum, int(s), int(e)) in self._done_keys
-               for _, _, w, s, e, _, _ in recs):
-            return False
-        ivs = self._done_imgs.get(key, [])
-        rng = sorted((int(r[3]), int(r[4])) for r in recs)
-        if any(a[1] >= b[0] for a, b in zip(rng, rng[1:])):
-            return False                                   # overlapping chunks: per-chunk dedupe
-        return not any(a <= e and s <= b for s, e in rng for a, b in ivs)
+        running = {(x[0], x[1], x[2]) for x in self.worker_set.get(key, ()) if x[3] == "w"}
+        done = self._done_keys
+        rng = []
+        for r in recs:
+            if r[0] != model or r[1] != qnum:
+                return False
+            s, e = int(r[3]), int(r[4])
+            if (r[2], s, e) not in running or (model, qnum, s, e) in done:
+                return False
+            rng.append((s, e))
+        rng.sort()
+        for a, b in zip(rng, rng[1:]):
+            if a[1] >= b[0]:
+                return False                               # overlapping chunks: per-chunk dedupe
+        ivs = self._done_imgs.get(key)
+        return not ivs or not any(a <= e and s <= b for s, e in rng for a, b in ivs)
 
     def _record_bulk(self, recs, now: float) -> int:
         model, qnum = recs[0][0], recs[0][1]
@@ -388,28 +395,44 @@ class JobState:
         tot = 0
         res = self.results[f"{model} {qnum}"]
         chunks = []
+        vms = self.working_vm_set
+        done = self._done_keys
+        pw = self._ptime_win[model]
         for _, _, w, s, e, c, p in recs:
             s, e = int(s), int(e)
             i = pos[(w, s, e)]
             t_start = ents[i][4]
             ents[i] = (w, s, e, "f", t_start, now)
-            vm = self.working_vm_set.get(w)
+            vm = vms.get(w)
             if vm is not None:
                 try:
                     vm.remove((model, qnum, s, e))
                 except ValueError:
                     pass
                 if not vm:
-                    self.working_vm_set.pop(w, None)
-            self._done_keys.add((model, qnum, s, e))
+                    del vms[w]
+            done.add((model, qnum, s, e))
             n = e - s + 1
             tot += n
-            self._ptime_win[model].append((now, (now - t_start) / n * bs))
-            res.append(ChunkResult(s, e, np.asarray(c, dtype=np.int32), np.asarray(p, dtype=np.float32), w))
+            pw.append((now, (now - t_start) / n * bs))
+            res.append(ChunkResult(s, e, c if type(c) is np.ndarray and c.dtype == np.int32 else
+                                   np.asarray(c, dtype=np.int32),
+                                   p if type(p) is np.ndarray and p.dtype == np.float32 else
+                                   np.asarray(p, dtype=np.float32), w))
             chunks.append([s, e])
         self._open_add(key, -len(recs))
-        for s, e in sorted(chunks):
-            _add_interval(self._done_imgs[key], s, e)
+        # the round's chunks are usually one contiguous range: merge them first, then
+        # into the query's done intervals once per run
+        chunks.sort()
+        ivs = self._done_imgs[key]
+        cs, ce = chunks[0]
+        for s, e in chunks[1:]:
+            if s == ce + 1:
+                ce = e
+            else:
+                _add_interval(ivs, cs, ce)
+                cs, ce = s, e
+        _add_interval(ivs, cs, ce)
         if key not in self._open:
             self.finished_queries[model] += 1
             t0 = self.query_submit_time.get(key)
