@@ -159,8 +159,11 @@ class HbmStager:
             from concurrent.futures import ThreadPoolExecutor
 
             self._readers = ThreadPoolExecutor(max_workers=self.READ_THREADS, thread_name_prefix="stage-read")
-        for f in [self._readers.submit(work, i) for i in range(nt)]:
-            f.result()
+        futs = [self._readers.submit(work, i) for i in range(nt)]
+        errs = [f.exception() for f in futs]        # every read has ended before the fd can close
+        for e in errs:
+            if e is not None:
+                raise e
 
     def stage(self, data: bytes | np.ndarray, shape: tuple) -> torch.Tensor:
         """Copy host bytes to a new device tensor of ``shape`` (uint8).  The
