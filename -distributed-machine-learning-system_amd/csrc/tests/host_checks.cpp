@@ -119,7 +119,6 @@ int main() {
   check_xcd_remap();
   check_swizzle("conv_glds swz_r", 8, [](int r) { return swz_r(r, 8); });
   check_swizzle("conv_glds swz_r", 4, [](int r) { return swz_r(r, 4); });
-  check_swizzle("conv3x3_patch/conv_big swz8", 8, [](int r) { return swz8(r); });
   check_swizzle("conv3x3_c64 c64_swz", 8, [](int r) { return c64_swz(r); });
   check_wino_raw();
   std::printf("host_checks: %d failure(s)\n", g_fail);

@@ -34,7 +34,4 @@ __host__ __device__ __forceinline__ int wino_raw_swz(int p) { return ((p >> 2) &
 // conv3x3_c64: 128-byte rows (64 channels)
 __host__ __device__ __forceinline__ int c64_swz(int row) { return row & 6; }
 
-// conv3x3_patch / conv_big: 128-byte rows
-__host__ __device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
-
 }  // namespace idunno

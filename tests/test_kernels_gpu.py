@@ -56,7 +56,7 @@ CONV_CASES = [
 
 
 @pytest.mark.parametrize("B,H,Cin,Cout,k,s,p", CONV_CASES)
-def test_conv_big(ops, B, H, Cin, Cout, k, s, p):
+def test_conv_shapes(ops, B, H, Cin, Cout, k, s, p):
     from idunno.models.packed import pack_conv_weight
 
     torch.manual_seed(B * 1000 + H + Cin + Cout + k)
