@@ -566,8 +566,10 @@ class RoundPlane:
         cls_all = np.ascontiguousarray(arr[:, :mc, 0])
         prob_all = np.ascontiguousarray(arr[:, :mc, 1]).view(np.float32)
         hdr = arr[:, mc:mc + HDR_ROWS, :].reshape(len(arr), 2 * HDR_ROWS).tolist()  # (us, model id, n, tag)
-        lens = np.array([0 if row is None else row[3] - row[2] + 1 for row in r.table])
-        bad = ((cls_all < 0) & (np.arange(mc) < lens[:, None])).any(axis=1).tolist()
+        bad = None
+        if cls_all.min() < 0:             # rare: some row holds a range-guard mark (or stale tail)
+            lens = np.array([0 if row is None else row[3] - row[2] + 1 for row in r.table])
+            bad = ((cls_all < 0) & (np.arange(mc) < lens[:, None])).any(axis=1).tolist()
         # one scheduler observation per model per round: the members' summed compute
         # time over their summed images (a per-image time), scaled to the model's batch
         obs = {}
@@ -584,7 +586,7 @@ class RoundPlane:
                 continue
             mid, qnum, s, e = row
             cls, prob = cls_all[i, :e - s + 1], prob_all[i, :e - s + 1]
-            if bad[i]:
+            if bad is not None and bad[i]:
                 # the member's split forward left fp16's range (class -2): the chunk
                 # goes to it again as a TCP JOB, whose executor path reruns it on
                 # the all-f32 kernels

@@ -4,6 +4,7 @@ import os
 import socket
 import threading
 import time
+import types
 
 import numpy as np
 import pytest
@@ -191,3 +192,49 @@ def test_config_env_and_file(tmp_path):
     assert cfg.standby_name == "node03" and cfg.address("node02") == ("127.0.0.1", 20002)
     with pytest.raises(KeyError):
         cfg.update(bogus=1)
+
+
+def test_round_finalize_reruns_range_guard_rows_only():
+    """RoundPlane._finalize: a row whose split forward left fp16's range (class
+    -2 inside its chunk) goes back to its member as a TCP JOB (f32 rerun); rows
+    with stale negatives only past their chunk's end are ingested as usual; the
+    scheduler gets one observation per model per round."""
+    import numpy as np
+
+    from idunno.config import ClusterConfig
+    from idunno.parallel.elastic import HDR_ROWS, MODEL_IDS
+    from idunno.runtime.rounds import RoundPlane, _Round
+
+    mc, W = 16, 3
+    arr = np.zeros((W, mc + HDR_ROWS, 2), np.int32)
+    arr[:, :mc, 0] = np.arange(mc)[None, :] + 100 * np.arange(W)[:, None]
+    arr[:, :mc, 1] = np.float32(0.5).view(np.int32)
+    arr[1, 3, 0] = -2                          # inside member 1's chunk (4 images): rerun
+    arr[2, 10, 0] = -2                         # member 2's chunk has 6 images: stale tail, ignored
+    mid = MODEL_IDS["resnet18"]
+    for i, (us, cnt) in enumerate([(400, 4), (800, 4), (600, 6)]):
+        arr[i, mc] = (us, mid)
+        arr[i, mc + 1] = (cnt, 1)
+
+    class G:
+        max_chunk = mc
+
+        def collect(self, seq, work, check):
+            return arr
+
+    sent, ingested, observed = [], [], []
+    node = types.SimpleNamespace(
+        name="node00", standby="node00", sched=types.SimpleNamespace(observe=lambda m, t: observed.append((m, t))),
+        _send_job=lambda *a: sent.append(a), _ingest_round=lambda recs, now, seq: ingested.extend(recs),
+        membership=types.SimpleNamespace(is_alive=lambda n: True))
+    rp = RoundPlane.__new__(RoundPlane)
+    rp.node, rp.group, rp.cfg = node, G(), ClusterConfig()
+    rp.host_s = rp.host_wait_s = 0.0
+    rp.rounds_done = 0
+    table = [(mid, 7, 0, 3), (mid, 7, 4, 7), (mid, 7, 8, 13)]
+    rp._finalize(_Round(1, [], table), ("node00", "node01", "node02"), None)
+    assert sent == [("node01", "resnet18", 7, 4, 7)]
+    assert [(r[2], r[3], r[4]) for r in ingested] == [("node00", 0, 3), ("node02", 8, 13)]
+    assert list(ingested[1][5]) == list(range(200, 206)) and np.all(ingested[1][6] == 0.5)
+    assert len(observed) == 1 and observed[0][0] == "resnet18"
+    assert abs(observed[0][1] - 1800e-6 / 14 * rp.cfg.batch_for("resnet18")) < 1e-12
