@@ -101,6 +101,9 @@ def parse(argv=None):
     ap.add_argument("--dataset-images", type=int, default=2000,
                     help="synthetic images replicated in every rank's HBM (grown to fit a round)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="N > 1 on a box with fewer GPUs: gloo collectives on GPU tensors, ranks share "
+                         "cuda:(local_rank %% device_count) -- exercises the multi-rank GPU path, not RCCL")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N > 1: keep the descriptor broadcast and result gather between the forwards "
                          "(default: double-buffered, overlapped with the next round's forward)")
@@ -473,7 +476,10 @@ def run_rank(a) -> int:
     from idunno.runtime.jobstate import JobState
     from idunno.runtime.scheduler import split_range
 
-    env = init_from_env(backend="gloo" if a.dry_run else None, cpu=a.dry_run)
+    if a.rehearse_gloo and not a.dry_run:
+        # rehearsal of the N > 1 path on a box with fewer GPUs than ranks (see --rehearse-gloo)
+        os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+    env = init_from_env(backend="gloo" if (a.dry_run or a.rehearse_gloo) else None, cpu=a.dry_run)
     if env.world != a.gpus:
         print(json.dumps({"error": f"--gpus {a.gpus} but WORLD_SIZE={env.world}"}), flush=True)
         return 2
@@ -570,7 +576,7 @@ def run_rank(a) -> int:
             posted.clear()
         return run, finish
 
-    def measure(run, per_round: int, steps: int, warmup: int, label: str, pipelined: bool = False):
+    def measure(run, per_round: int, steps: int, warmup: int, label: str, pipelined: bool = False, runner=None):
         """Time `steps` pipelined rounds of `per_round` images (split over the
         ranks), then `unloaded` rounds one at a time for the p50 latency.
 
@@ -580,7 +586,7 @@ def run_rank(a) -> int:
         is waited for only after round q+1's forward is queued, so at N > 1
         neither collective sits between two forwards on the compute stream."""
         if pipelined:
-            return measure_pipelined(run, per_round, steps, warmup, label)
+            return measure_pipelined(run, per_round, steps, warmup, label, runner)
         state = JobState() if coord else None
         host = [torch.empty(W, plane.max_chunk, 2, dtype=torch.int32, pin_memory=gpu) for _ in range(2)] \
             if coord else None
@@ -676,20 +682,40 @@ def run_rank(a) -> int:
                 "recorded": recorded, "label": label,
                 "rank_ms": [1000.0 * x / steps for x in per_rank],
                 "gather_us": statistics.median(g_us) if g_us else None,
-                "verified": verify(state)}
+                "verified": verify(state, runner)}
 
-    def verify(state) -> bool | None:
-        """--dry-run: every recorded chunk holds the fake forward's classes for
-        ITS images (global index % 1000), i.e. no slot mix-up between the
-        descriptors, the forwards and the gathered rounds."""
-        if not (coord and a.dry_run):
+    def verify(state, runner=None) -> bool | None:
+        """Every recorded chunk holds the classes of ITS images, i.e. no slot
+        mix-up between the descriptors, the forwards and the gathered rounds.
+        --dry-run: all chunks against the fake forward (global index % 1000).
+        GPU: the coordinator recomputes the last timed round's chunks of up to
+        three ranks (its own, rank 1, the last) with an eager forward over the
+        same images of its replica and compares classes (probabilities to 1e-6)."""
+        if not coord:
             return None
         with state.lock:
             chunks = [c for v in state.results.values() for c in v]
-        return bool(chunks) and all(
-            np.array_equal(c.cls, np.arange(c.start, c.end + 1) % 1000) for c in chunks)
+        if a.dry_run:
+            return bool(chunks) and all(
+                np.array_equal(c.cls, np.arange(c.start, c.end + 1) % 1000) for c in chunks)
+        if runner is None or not chunks:
+            return None
+        last = max(chunks, key=lambda c: c.start)
+        key = next(k for k, v in state.results.items() if any(c is last for c in v))
+        pick = {f"rank{r}" for r in {0, 1, W - 1}}
+        ok = True
+        for c in state.results[key]:
+            if c.worker not in pick:
+                continue
+            n = c.end - c.start + 1
+            st0 = torch.tensor([c.start], dtype=torch.int64, device=env.device)
+            cls, prob = runner.forward(dataset, st0, n, 0)
+            torch.cuda.synchronize()
+            ok &= bool(np.array_equal(cls.cpu().numpy(), c.cls)) and \
+                bool(np.allclose(prob.cpu().numpy(), c.prob, rtol=0, atol=1e-6))
+        return ok
 
-    def measure_pipelined(run, per_round: int, steps: int, warmup: int, label: str):
+    def measure_pipelined(run, per_round: int, steps: int, warmup: int, label: str, runner=None):
         state = JobState() if coord else None
         host = [torch.empty(W, plane.max_chunk, 2, dtype=torch.int32, pin_memory=gpu) for _ in range(2)] \
             if coord else None
@@ -790,7 +816,7 @@ def run_rank(a) -> int:
         return {"elapsed": elapsed, "ips": per_round * steps / elapsed, "p50": p50, "p50_loaded": p50_loaded,
                 "recorded": recorded, "label": label,
                 "rank_ms": [1000.0 * x / steps for x in per_rank], "gather_us": None,
-                "verified": verify(state)}
+                "verified": verify(state, runner)}
 
     # ---- headline: weak scaling at the headline precision --------------------
     runner = None
@@ -803,7 +829,7 @@ def run_rank(a) -> int:
     def make(r, batch):
         return make_slot_runs(r, batch) if pipe else make_run(r, batch)
 
-    head = measure(make(runner, B), W * B, a.steps, a.warmup, "weak", pipelined=pipe)
+    head = measure(make(runner, B), W * B, a.steps, a.warmup, "weak", pipelined=pipe, runner=runner)
     extras = {"pipelined_collectives": pipe}
     serial = None
     if pipe:
