@@ -59,6 +59,8 @@ class ClusterConfig:
     # run queries as RCCL/gloo rounds when the group is healthy; None = auto:
     # on for GPU nodes started one per process by idunno.launch
     collective_rounds: bool | None = None
+    collective_backend: str = ""             # "" = auto (RCCL on GPU nodes, gloo on CPU); "gloo" on GPU
+                                             # tensors rehearses N nodes on fewer GPUs (bench --rehearse-gloo)
     collective_port_offset: int = 500        # TCPStore port = base_port + offset + epoch % 100
     collective_timeout_s: float = 30.0       # rendezvous timeout; a round's liveness comes from membership
     collective_op_timeout_s: float = 120.0   # backstop for one pending collective (process-group timeout)

@@ -82,7 +82,8 @@ class RoundPlane:
     def __init__(self, node, device):
         self.node = node
         self.cfg = cfg = node.cfg
-        self.group = ElasticGroup(device, timeout_s=cfg.collective_timeout_s, max_chunk=cfg.max_chunk,
+        self.group = ElasticGroup(device, backend=cfg.collective_backend or None,
+                                  timeout_s=cfg.collective_timeout_s, max_chunk=cfg.max_chunk,
                                   op_timeout_s=cfg.collective_op_timeout_s, abort_join_s=cfg.abort_join_s,
                                   depth=cfg.round_depth)
         self.lock = threading.Lock()

@@ -372,6 +372,8 @@ def _phase_argv(a, phase: str, out: str, work: str) -> list:
             "--phase", phase, "--json-out", out, "--work-dir", work, "--launch-timeout", str(a.extras_timeout)]
     if a.dry_run:
         argv.append("--dry-run")
+    if a.rehearse_gloo:
+        argv.append("--rehearse-gloo")
     return argv
 
 
@@ -949,6 +951,8 @@ def run_node(a) -> int:
     if not a.dry_run and not gpu:
         print(json.dumps({"error": "bench.py phases 2-3 need a GPU (MI355X); use --dry-run on CPU"}), flush=True)
         return 2
+    if gpu and a.rehearse_gloo:
+        local %= max(1, torch.cuda.device_count())       # N nodes on fewer GPUs, gloo rounds
     dev = torch.device("cuda", local) if gpu else torch.device("cpu")
     if gpu:
         torch.cuda.set_device(dev)
@@ -962,7 +966,8 @@ def run_node(a) -> int:
     cfg = ClusterConfig(num_nodes=n, base_port=base, store_root=tmp, collective_rounds=rounds, dtype=a.dtype,
                         fp32_impl=a.fp32_impl, max_chunk=max(2048, B), rpc_timeout_s=60.0, worker_budget=W,
                         dataset_size=10 ** 9, collective_port_offset=100,
-                        batch_size={"resnet18": QUERY * W, "alexnet": QUERY_ALEXNET * W, a.model: B * W})
+                        batch_size={"resnet18": QUERY * W, "alexnet": QUERY_ALEXNET * W, a.model: B * W},
+                        collective_backend="gloo" if a.rehearse_gloo else "")
     if a.phase in ("failover", "worker"):
         # reference detector: 0.3 s ping period, 2 s timeout (mp4_machinelearning.py:191-220, 845-851);
         # tuned: 0.1 s / 1 s
