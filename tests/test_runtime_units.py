@@ -238,3 +238,32 @@ def test_round_finalize_reruns_range_guard_rows_only():
     assert list(ingested[1][5]) == list(range(200, 206)) and np.all(ingested[1][6] == 0.5)
     assert len(observed) == 1 and observed[0][0] == "resnet18"
     assert abs(observed[0][1] - 1800e-6 / 14 * rp.cfg.batch_for("resnet18")) < 1e-12
+
+
+def test_send_frame_falls_back_when_the_socket_buffer_is_full():
+    """transport._send_frame: the GIL-holding non-blocking send takes what fits
+    and the rest goes through sendall; a closed peer raises OSError."""
+    from idunno.runtime.transport import _send_frame
+
+    a, b = socket.socketpair()
+    a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4096)
+    data = os.urandom(4 << 20)                     # far larger than the send buffer
+    got = bytearray()
+
+    def rd():
+        while len(got) < len(data):
+            chunk = b.recv(1 << 16)
+            if not chunk:
+                break
+            got.extend(chunk)
+    th = threading.Thread(target=rd)
+    th.start()
+    _send_frame(a, b"x" * 10)                       # fits: one non-blocking send
+    _send_frame(a, data[10:])
+    th.join(30)
+    assert bytes(got) == b"x" * 10 + data[10:]
+    b.close()
+    with pytest.raises(OSError):
+        for _ in range(64):                         # the peer is gone: EPIPE / ECONNRESET
+            _send_frame(a, data[:1 << 16])
+    a.close()
