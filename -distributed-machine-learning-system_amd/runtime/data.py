@@ -288,6 +288,12 @@ class SdfsSource:
                         self._inflight.pop(k, None)
             self._inflight[k] = self._pool.submit(run)
 
+    def prefetch(self, start: int, end: int) -> None:
+        """Start staging every shard of images [start, end] in the background
+        (in request order, behind shards already queued)."""
+        for k in range(start // self.S, end // self.S + 1):
+            self._prefetch(k)
+
     def _shard(self, k: int) -> torch.Tensor:
         with self.lock:
             t = self.cache.get(k)

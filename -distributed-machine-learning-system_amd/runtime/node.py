@@ -316,6 +316,13 @@ class Node:
         now = self.clock()
         self.state.assign(model, qnum, plan, now)
         self.tracer.instant("query.submit", model=model, q=qnum, start=start, end=end, workers=len(plan))
+        prefetch = getattr(self.source, "prefetch", None)
+        if prefetch is not None:
+            # this node's own chunk starts staging (SDFS shard -> HBM, background
+            # thread) at submission, not when its round comes up
+            for w, s, e in plan:
+                if w == self.name:
+                    prefetch(s, e)
         if self.rounds is not None and self.rounds.try_enqueue(model, qnum, plan):
             self.logger.info("query %s %s [%d,%d] -> collective round %s", model, qnum, start, end, plan)
             return {"ok": True, "qnum": qnum, "plan": [list(p) for p in plan], "round": True}

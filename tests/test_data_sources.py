@@ -160,3 +160,22 @@ def test_sdfs_source_streams_local_replica_file(tmp_path):
     x = src.get(0, 29)
     assert torch.equal(x, torch.from_numpy(synth_images_cpu(6, 0, 30)))
     assert src.local_reads == 2 and store.reads == [shard_name(2)]
+
+
+def test_sdfs_source_prefetch_range_stages_in_background():
+    """SdfsSource.prefetch(start, end): every shard of the range is staged by
+    the readahead thread before any get() asks for it."""
+    import time
+
+    from idunno.runtime.data import SdfsSource, shard_name
+
+    store = _ShardStore(8, 40, 10)
+    src = SdfsSource(store, "cpu", shard_images=10, peer_copy=False, readahead=0)
+    src.prefetch(5, 34)                                  # shards 0..3
+    for _ in range(300):
+        if src.cached(0, 39):
+            break
+        time.sleep(0.01)
+    assert src.cached(0, 39) and sorted(store.reads) == [shard_name(k) for k in range(4)]
+    assert torch.equal(src.get(5, 34), torch.from_numpy(synth_images_cpu(8, 5, 30)))
+    assert len(store.reads) == 4                         # nothing read twice
