@@ -236,10 +236,11 @@ __device__ __forceinline__ void conv_glds_mf32_body(const ConvArgs& a, char* sme
 // layout: register r of a 32x32 accumulator is row 8(r/4) + 4(l>>5) + r%4,
 // column l & 31, so each lane still stores 4 consecutive output channels.
 template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false,
-          bool SPLIT = false, bool MF32 = false>
+          bool SPLIT = false, bool MF32 = false, bool DEEPB = false>
 __global__ void __launch_bounds__(64 * WN * WM, (BM % 64 != 0 && WN * WM == 8) ? 4 : 1)   // 2nd: min waves per SIMD
 conv_glds_kernel(const ConvArgs a) {
   static_assert(!SPLIT || BK == 64, "split stages are 32 channels x (hi, lo)");
+  static_assert(!DEEPB || (SPLIT && !P3 && !MF32 && NS == 2), "deep-B ring: split NHWC tiles, A ring of 2");
   static_assert(!MF32 || (BK == 64 && !P3), "32x32x16 tiles: BK 64, NHWC convs");
   constexpr int NW = WN * WM;
   constexpr int NT = 64 * NW;
@@ -440,7 +441,7 @@ conv_glds_kernel(const ConvArgs a) {
   // 0's wait (these are older than every ring DMA) and barrier.  The taps' first
   // touches of the input rows then go to HBM together at block start instead of
   // stalling the early stages one after another.
-  if constexpr (!P3) {
+  if constexpr (!P3 && !DEEPB) {
     if (a.l2pf && !(second && a.center_only)) {
       const int hw = a.Ho * a.Wo;
       const int mlo = m0, mhi = min(m0 + BM, a.M) - 1;
@@ -501,11 +502,102 @@ conv_glds_kernel(const ConvArgs a) {
     }
   }
 
+  const int frow = lane & 15, fch = lane >> 4;
+  if constexpr (DEEPB) {
+    // Deep-B ring (split tiles, round 4): A (weights, L2-resident: every block of a
+    // layer reads the same panel) keeps a 2-slot ring, B (pixels, whose first
+    // touches miss L2) gets 3 slots, so a B stage is issued TWO stages ahead and
+    // its miss latency has two stages of MFMAs to hide under.  LDS: 2 A + 3 B
+    // slots = 80 KiB (two blocks per CU, as tile 42).  Issue order per stage:
+    // A(s+1), B(s+2); at the top of stage s, vmcnt(GB) leaves only B(s+1) in flight
+    // (vmcnt retires in order), i.e. A(s) and B(s) have landed.
+    constexpr int B_BYTES = BMD * RB;
+    char* const a_ring = smem;
+    char* const b_ring = smem + 2 * A_BYTES;
+    int ia_s = i_s;                            // A's own stage counter (B uses i_s / i_cb / i_kw / i_kh)
+    auto issue_a = [&](int slot) {
+      char* base = a_ring + slot * A_BYTES;
+      const int koff = ia_s * BK * 2;
+#pragma unroll
+      for (int j = 0; j < GA; ++j) dma_buf16(w_rsrc, base + (wave + NW * j) * 1024, a_voff[j], koff);
+      ++ia_s;
+    };
+    auto issue_b = [&](int slot) {
+      char* base = b_ring + slot * B_BYTES;
+      if (i_cb == 0) set_tap();
+      const int coff = i_cb * BK * 2;
+#pragma unroll
+      for (int j = 0; j < GB; ++j) dma_buf16(x_rsrc, base + (wave + NW * j) * 1024, b_voff[j], coff);
+      ++i_s;
+      if (++i_cb == a.cblk) {
+        i_cb = 0;
+        if (++i_kw == a.KW) {
+          i_kw = 0;
+          ++i_kh;
+        }
+      }
+    };
+    issue_a(0);
+    issue_b(0);
+    if (nK > 1) issue_b(1);
+    uint32_t fa_off[2], fb_off[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = fch + 4 * kk;
+      const int ra = wn * TN + frow, rb = wm * TM + frow;
+      fa_off[kk] = (uint32_t)(ra * RB + ((ch ^ swz_r(ra, CPR)) << 4));
+      fb_off[kk] = (uint32_t)(rb * RB + ((ch ^ swz_r(rb, CPR)) << 4));
+    }
+    const uint32_t lds0 = lds_addr(smem);
+    int as = 0, bs = 0;                        // ring slots of stage s
+    for (int s = 0; s < nK; ++s) {
+      if (s + 1 < nK) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // slots (s+1)%2 and (s+2)%3 were last read in stage s-1: free after the barrier
+      if (s + 1 < nK) issue_a(as ^ 1);
+      if (s + 2 < nK) issue_b(bs == 0 ? 2 : bs - 1);
+      const uint32_t abase = lds0 + as * A_BYTES, bbase = lds0 + 2 * A_BYTES + bs * B_BYTES;
+      constexpr int NR = FN + FM;
+      half8v fa[2][FN], fb[2][FM];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i) fa[kk][i] = lds_read_b128_step<16 * RB>(abase + fa_off[kk], i);
+#pragma unroll
+        for (int j = 0; j < FM; ++j) fb[kk][j] = lds_read_b128_step<16 * RB>(bbase + fb_off[kk], j);
+      }
+      lds_waitcnt<NR>();
+#pragma unroll
+      for (int i = 0; i < FN; ++i) lds_tie(fa[0][i]);
+#pragma unroll
+      for (int j = 0; j < FM; ++j) lds_tie(fb[0][j]);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      lds_waitcnt<0>();
+#pragma unroll
+      for (int i = 0; i < FN; ++i) lds_tie(fa[1][i]);
+#pragma unroll
+      for (int j = 0; j < FM; ++j) lds_tie(fb[1][j]);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[0][i], fb[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[1][i], fb[0][j], acc[i][j], 0, 0, 0);
+        }
+      as ^= 1;
+      bs = bs == 2 ? 0 : bs + 1;
+    }
+  } else {
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < nK) issue(p);
 
-  const int frow = lane & 15, fch = lane >> 4;
   // per-lane LDS byte offsets (within a stage) of fragment 0 of each K chunk
   uint32_t frag_a[BK / 32], frag_b[BK / 32];
 #pragma unroll
@@ -592,6 +684,7 @@ conv_glds_kernel(const ConvArgs a) {
     lds_waitcnt<0>();
     mfma_chunk(KK - 1);
   }
+  }   // !DEEPB
 
   // ---- epilogue: bias (+residual) (+ReLU), NHWC store --------------------
   // late residual: the ring is drained (last wait was vmcnt(0)), so ordinary
@@ -698,7 +791,7 @@ static int g_l2pf = 0;   // conv_glds input-footprint L2 prefetch: bit 0 fp16 co
 void set_conv_l2_prefetch(int mode) { g_l2pf = mode; }
 
 template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false,
-          bool SPLIT = false, bool MF32 = false>
+          bool SPLIT = false, bool MF32 = false, bool DEEPB = false>
 static void glds_cfg(ConvArgs a, hipStream_t st) {
   a.tiles_n = (a.Cout + BN - 1) / BN;
   a.tiles_m = (a.M + BM - 1) / BM;
@@ -713,8 +806,8 @@ static void glds_cfg(ConvArgs a, hipStream_t st) {
   const int grid = a.tiles_n * a.tiles_m * (a.ksplit > 1 ? a.ksplit : 1);
   constexpr int RPI_ = 64 / (BK / 8), NW_ = WN * WM;
   constexpr int BMD = (BM + RPI_ * NW_ - 1) / (RPI_ * NW_) * (RPI_ * NW_);
-  const size_t lds = (size_t)NS * (BN + BMD) * BK * 2;
-  auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32, P3, SPLIT, MF32>;
+  const size_t lds = DEEPB ? (size_t)(2 * BN + 3 * BMD) * BK * 2 : (size_t)NS * (BN + BMD) * BK * 2;
+  auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32, P3, SPLIT, MF32, DEEPB>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), (int)lds);   // per (kernel, device), launch_util.h
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WN * WM), lds, st, a);
 }
@@ -813,6 +906,8 @@ static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
     case 57: glds_cfg<128, 128, 64, 2, 2, 2, R, F, false, true, true>(a, st); return true;
     case 58: glds_cfg<128, 192, 64, 4, 2, 2, R, F, false, true, true>(a, st); return true;
     // Cout 64 (ResNet layer1): 55 = 64 x 256 on 8 waves, 59 = 64 x 128 on 4 waves (64x32 wave tiles)
+    // deep-B ring (2 weight slots, 3 pixel slots, 80 KiB): tile 36's shape
+    case 60: glds_cfg<128, 128, 64, 2, 4, 2, R, F, false, true, false, true>(a, st); return true;
     case 55: glds_cfg<64, 256, 64, 1, 8, 2, R, F, false, true, true>(a, st); return true;
     case 59: glds_cfg<64, 128, 64, 1, 4, 2, R, F, false, true, true>(a, st); return true;
     default: return false;
@@ -838,13 +933,16 @@ void set_split_wide_all(bool on) { g_split_wide_all = on; }
 static int g_split_mf32 = 0;
 void set_split_mf32(int mode) { g_split_mf32 = mode; }
 int split_mf32() { return g_split_mf32; }
+static bool g_split_deepb = false;
+void set_split_deepb(bool on) { g_split_deepb = on; }
+bool split_deepb() { return g_split_deepb; }
 int conv_glds_split_pick(int M, int Cout) {
   if (Cout % 128 == 0) {
     if ((g_split_mf32 & 1) && M >= 50000) return 56;
     if ((g_split_mf32 & 2) && M < 50000) return 58;
     if (g_split_wide && g_split_wide_all) return 42;
     if (g_split_wide && g_split_wide_l3 && M >= 50000 && M < 100000) return 42;   // layer3: 1.91 vs 2.39 waves
-    if (M >= 50000) return 36;
+    if (M >= 50000) return g_split_deepb ? 60 : 36;
     // layer4-sized GEMMs: 128 x 160 tiles make ~1 full wave of blocks where
     // 128 x 64 made 1.6 (whole-graph A/B: profiles/r2_v29_split_wide_tile.md)
     return g_split_wide ? 42 : 34;

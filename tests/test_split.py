@@ -271,7 +271,7 @@ def test_resnet50_split_fused_downsample_matches_unfused(ops):
     assert (outs[True] - outs[False]).abs().max().item() <= 2e-5 * scale
 
 
-SPLIT_TILES = [26, 27, 34, 36, 38, 42, 55, 56, 57, 58, 59]   # 55-59: 32x32x16 MFMA (MF32)
+SPLIT_TILES = [26, 27, 34, 36, 38, 42, 55, 56, 57, 58, 59, 60]   # 55-59: 32x32x16 MFMA (MF32); 60: deep-B ring
 
 
 @pytest.mark.gpu
@@ -318,6 +318,24 @@ def test_conv_split_tiles(ops, tile, res, out_f32):
                          residual=None if r is None else ops.split_from_f32(r), out_f32=out_f32, tile=tile)
     ref = _ref64(x, w, b, 1, 1, True, r)
     _check(y if out_f32 else P.from_split(y), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,k", [(32, 1), (64, 1), (96, 1), (32, 3)])
+@pytest.mark.parametrize("res", [False, True])
+def test_conv_split_deepb_short_k(ops, cin, k, res):
+    """Tile 60 (deep-B ring) at 1, 2, 3 and 9 stages: the prologue and the
+    last-stage vmcnt(0) paths of the 3-slot pixel ring."""
+    torch.manual_seed(cin + k + res)
+    B, H, Cout = 2, 17, 256
+    x = torch.randn(B, H, H, cin, device=DEV)
+    w = torch.randn(Cout, cin, k, k) / (cin * k * k) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    r = torch.randn(B, H, H, Cout, device=DEV) if res else None
+    sw, scale = P.pack_split_weight(w)
+    y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, k, k, 1, k // 2, True,
+                         residual=None if r is None else ops.split_from_f32(r), tile=60)
+    _check(P.from_split(y), _ref64(x, w, b, 1, k // 2, True, r))
 
 
 @pytest.mark.gpu
@@ -520,7 +538,8 @@ def test_split_activations_past_fp16_range_match_fp64(ops):
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,H,C,Cout,tile", [(2, 56, 64, 128, -1), (3, 28, 128, 256, -1), (2, 14, 256, 512, -1),
                                              (3, 13, 64, 128, 36), (2, 9, 128, 256, 42), (1, 15, 64, 128, 34),
-                                             (3, 13, 64, 128, 56), (2, 9, 128, 256, 58)])
+                                             (3, 13, 64, 128, 56), (2, 9, 128, 256, 58),
+                                             (3, 13, 64, 128, 60), (2, 9, 128, 256, 60)])
 def test_conv_split_dual_downsample(ops, B, H, C, Cout, tile):
     torch.manual_seed(B + H + C)
     x = torch.randn(B, H, H, C, device=DEV)
