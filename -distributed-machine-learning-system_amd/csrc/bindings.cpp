@@ -1424,6 +1424,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("split_mf32", &split_mf32);
   m.def("set_split_deepb", &set_split_deepb, "A/B: split M >= 50000 tile 36 -> 60 (pixel ring of 3 slots)");
   m.def("split_deepb", &split_deepb);
+  m.def("set_f16_deepb", &set_f16_deepb, "A/B: fp16 M >= 50000 -> tile 61 (pixel ring of 3 slots)");
   m.def("set_f16_mf32", &set_f16_mf32, "A/B: fp16 tiles on 32x32x16 MFMAs (bit 0: M >= 50000 -> 90 (92 with bit 2), bit 1: M < 50000 -> 92)");
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");

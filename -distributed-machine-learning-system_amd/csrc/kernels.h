@@ -147,6 +147,7 @@ void set_split_wide_all(bool on);    // A/B: ... at every M
 void set_split_mf32(int mode);       // split tiles on 32x32x16 MFMAs: bit 0 M >= 50000 (56), bit 1 M < 50000 (58)
 int split_mf32();
 void set_split_deepb(bool on);       // split tile 36 -> 60 (3-slot pixel ring, 80 KiB)
+void set_f16_deepb(bool on);         // fp16 M >= 50000, Cout % 128 == 0 -> tile 61 (3-slot pixel ring)
 bool split_deepb();
 void set_f16_mf32(int mode);        // fp16 tiles on 32x32x16 MFMAs: bit 0 M >= 50000 (90, or 92 with bit 2), bit 1 M < 50000 (92)
 void set_conv_l2_prefetch(int mode);  // A/B: conv_glds input-footprint L2 prefetch (bit 0 fp16, bit 1 split)

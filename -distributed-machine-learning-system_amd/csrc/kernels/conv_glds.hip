@@ -240,7 +240,7 @@ template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT
 __global__ void __launch_bounds__(64 * WN * WM, (BM % 64 != 0 && WN * WM == 8) ? 4 : 1)   // 2nd: min waves per SIMD
 conv_glds_kernel(const ConvArgs a) {
   static_assert(!SPLIT || BK == 64, "split stages are 32 channels x (hi, lo)");
-  static_assert(!DEEPB || (SPLIT && !P3 && !MF32 && NS == 2), "deep-B ring: split NHWC tiles, A ring of 2");
+  static_assert(!DEEPB || (!P3 && !MF32 && NS == 2 && BK == 64), "deep-B ring: BK-64 NHWC tiles, A ring of 2");
   static_assert(!MF32 || (BK == 64 && !P3), "32x32x16 tiles: BK 64, NHWC convs");
   constexpr int NW = WN * WM;
   constexpr int NT = 64 * NW;
@@ -567,6 +567,8 @@ conv_glds_kernel(const ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < FM; ++j) fb[kk][j] = lds_read_b128_step<16 * RB>(bbase + fb_off[kk], j);
       }
+      // chunk 0 (SPLIT: the hi planes) as soon as its fragments land, then chunk 1
+      // (SPLIT: hi*lo + lo*hi; fp16: the stage's second 32 channels)
       lds_waitcnt<NR>();
 #pragma unroll
       for (int i = 0; i < FN; ++i) lds_tie(fa[0][i]);
@@ -587,8 +589,12 @@ conv_glds_kernel(const ConvArgs a) {
       for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[0][i], fb[1][j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[1][i], fb[0][j], acc[i][j], 0, 0, 0);
+          if constexpr (SPLIT) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[0][i], fb[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[1][i], fb[0][j], acc[i][j], 0, 0, 0);
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
+          }
         }
       as ^= 1;
       bs = bs == 2 ? 0 : bs + 1;
@@ -858,6 +864,7 @@ static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
     case 38: glds_cfg<128, 64, 64, 2, 4, 2, R, F>(a, st); return true;    // 8 waves (32x16 wave tile)
     case 39: glds_cfg<128, 128, 32, 2, 4, 4, R, F>(a, st); return true;   // 8 waves, 64 KiB, 3 stages in flight
     case 42: glds_cfg<128, 160, 64, 4, 2, 2, R, F>(a, st); return true;   // 8 waves, B as 192 rows, 80 KiB (small M)
+    case 61: glds_cfg<128, 128, 64, 2, 4, 2, R, F, false, false, false, true>(a, st); return true;   // deep-B ring, 80 KiB
     // 32x32x16 MFMA (MF32) fp16 tiles: the shapes of split 56 / 57 / 58
     case 90: glds_cfg<128, 128, 64, 2, 4, 2, R, F, false, false, true>(a, st); return true;
     case 91: glds_cfg<128, 128, 64, 2, 2, 2, R, F, false, false, true>(a, st); return true;
@@ -985,10 +992,13 @@ static bool g_f16_wide_all = true;
 void set_f16_wide_all(bool on) { g_f16_wide_all = on; }
 static int g_f16_mf32 = 0;
 void set_f16_mf32(int mode) { g_f16_mf32 = mode; }
+static bool g_f16_deepb = false;
+void set_f16_deepb(bool on) { g_f16_deepb = on; }
 int conv_glds_pick(int M, int Cout) {
   // sweeps r1 #3/#4: BK=64 double buffering with 2-3 workgroups/CU beats deeper
   // rings; 8 waves per 128x128 tile (4 waves/SIMD) best where M is large
   if (Cout % 128 == 0) {
+    if (g_f16_deepb && M >= 50000) return 61;
     if ((g_f16_mf32 & 1) && M >= 50000) return (g_f16_mf32 & 4) ? 92 : 90;
     if ((g_f16_mf32 & 2) && M < 50000) return 92;
     if (g_f16_wide && g_f16_wide_all) return 42;

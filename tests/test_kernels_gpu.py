@@ -72,7 +72,7 @@ def test_conv_shapes(ops, B, H, Cin, Cout, k, s, p):
     _check(y, ref)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3] + list(range(10, 40)) + [42, 90, 91, 92])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3] + list(range(10, 40)) + [42, 61, 90, 91, 92])
 @pytest.mark.parametrize("H", [14, 9])
 def test_conv_all_tiles_with_residual(ops, tile, H):
     from idunno.models.packed import pack_conv_weight
