@@ -80,7 +80,8 @@ def main():
         ph, xh = ph.to(dev), x.half()
         rh = res.half() if res is not None else None
         r["f16_us"] = timeit(lambda: ops.conv2d(xh, ph, b, c.kh, c.kw, c.stride, c.pad, True, residual=rh))
-        best_us, best_t = min((v, k) for k, v in r.items() if isinstance(k, int))
+        timed = [(v, k) for k, v in r.items() if isinstance(k, int)]
+        best_us, best_t = min(timed) if timed else (r["def_us"], r["default"])   # no listed tile fits the shape
         r["best_tile"], r["best_us"] = best_t, best_us
         r["tf_best"] = flops / best_us / 1e6
         tot["def"] += r["def_us"]
