@@ -53,7 +53,7 @@ _MSG_DONTWAIT, _MSG_NOSIGNAL = 0x40, 0x4000
 def _send_frame(sock: socket.socket, data: bytes) -> None:
     """``sock.sendall(data)``, holding the GIL for the common non-blocking case."""
     n = 0
-    if _SEND is not None:
+    if _SEND is not None and type(data) is bytes:
         n = _SEND(sock.fileno(), data, len(data), _MSG_DONTWAIT | _MSG_NOSIGNAL)
         if n == len(data):
             return
