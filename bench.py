@@ -481,6 +481,7 @@ def run_rank(a) -> int:
     if a.rehearse_gloo and not a.dry_run:
         # rehearsal of the N > 1 path on a box with fewer GPUs than ranks (see --rehearse-gloo)
         os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+    t_rank0 = time.perf_counter()
     env = init_from_env(backend="gloo" if (a.dry_run or a.rehearse_gloo) else None, cpu=a.dry_run)
     if env.world != a.gpus:
         print(json.dumps({"error": f"--gpus {a.gpus} but WORLD_SIZE={env.world}"}), flush=True)
@@ -831,7 +832,15 @@ def run_rank(a) -> int:
     def make(r, batch):
         return make_slot_runs(r, batch) if pipe else make_run(r, batch)
 
+    def progress(what: str) -> None:
+        """One line per finished phase on stderr (rank 0): long multi-rank runs
+        show where they are."""
+        if coord:
+            print(f"bench: rank 0 {what} ({time.perf_counter() - t_rank0:.1f} s)", file=sys.stderr, flush=True)
+
+    progress("model ready")
     head = measure(make(runner, B), W * B, a.steps, a.warmup, "weak", pipelined=pipe, runner=runner)
+    progress("headline measured")
     extras = {"pipelined_collectives": pipe}
     serial = None
     if pipe:
@@ -843,6 +852,7 @@ def run_rank(a) -> int:
     if not a.no_extras:
         # strong scaling: ONE 400-image query split over the W ranks
         strong = measure(make(runner, strong_chunk), QUERY, a.steps, a.warmup, "strong", pipelined=pipe)
+        progress("strong scaling measured")
         extras.update({
             "images_per_s_strong": round(strong["ips"], 2),
             "p50_query_latency_strong_s": round(strong["p50"], 6) if strong["p50"] else None,
@@ -856,6 +866,7 @@ def run_rank(a) -> int:
                            f"ms_per_step_{other}": round(1000 * m2["elapsed"] / a.steps, 4),
                            f"p50_query_latency_{other}_s": round(m2["p50"], 6) if m2["p50"] else None})
             del r2
+            progress(f"{other} measured")
             if a.dtype == "fp32":
                 alt = "f32mfma" if a.fp32_impl == "split" else "split"
                 runner.split = alt == "split"
@@ -865,7 +876,9 @@ def run_rank(a) -> int:
                                f"ms_per_step_fp32_{alt}": round(1000 * m3["elapsed"] / a.steps, 4)})
             if coord:
                 extras.update(numerics_check(runner, a, env.device))
-        if W > 1:
+            progress("numerics checked")
+        if W > 1 and not a.rehearse_gloo:
+            # (a rehearsal skips it: gloo moves GPU tensors point-to-point through the host)
             # M9 data variant: images only in the coordinator's HBM,
             # scattered every round over RCCL, double-buffered against compute
             srun, sfinish = make_scatter_run(runner, B, W * B)
