@@ -579,6 +579,58 @@ def run_rank(a) -> int:
             posted.clear()
         return run, finish
 
+    def record_round(state, res, tab, t1):
+        """Coordinator: one gathered round (host int32 [W, max_chunk, 2]) into the job state."""
+        cls_all, prob_all = res[:, :, 0], res[:, :, 1].view(np.float32)
+        for r, row in enumerate(tab):
+            n = row[3] - row[2] + 1
+            state.record_result(a.model, row[1], f"rank{r}", row[2], row[3], cls_all[r, :n].copy(),
+                                prob_all[r, :n].copy(), t1)
+
+    def table_of(q, per_round):
+        """Round q's chunks (one per rank) and descriptor rows."""
+        off = (q * per_round) % (D - max(per_round, plane.max_chunk) + 1)
+        chunks = split_range(off, off + per_round - 1, W)
+        return chunks, [(model_id, q, s, e) for s, e in chunks]
+
+    def fail_on_purpose(q, warmup):
+        if a.fail_rank == env.rank and q == warmup:
+            print(f"bench: rank {env.rank} failing on purpose (--fail-rank)", file=sys.stderr, flush=True)
+            os._exit(3)
+
+    def run_phases(step, drain, lat, steps, warmup, timing=None):
+        """Warmup rounds, then EXACTLY ``steps`` timed rounds (each rank's own
+        region between a drain + barrier on both sides; the slowest rank's
+        counts), then >= 5 unloaded rounds one at a time for the p50 latency.
+        ``step(q, nxt)``: round q, with round q+1 to follow in this phase."""
+        for q in range(warmup):
+            step(q, q + 1 < warmup)
+        drain()
+        lat.clear()
+        if timing is not None:
+            timing[0] = True
+        t_start = time.perf_counter()
+        for q in range(warmup, warmup + steps):
+            step(q, q + 1 < warmup + steps)
+        drain()
+        elapsed = time.perf_counter() - t_start
+        if timing is not None:
+            timing[0] = False
+        per_rank = [elapsed]
+        if env.distributed:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
+            outs = [torch.zeros_like(t) for _ in range(W)]
+            dist.all_gather(outs, t)
+            per_rank = [float(x.item()) for x in outs]
+            elapsed = max(per_rank)
+        p50_loaded = statistics.median(lat) if lat else None
+        lat.clear()
+        for q in range(warmup + steps, warmup + steps + max(5, min(steps, 20))):
+            step(q, False)
+            drain()
+        p50 = statistics.median(lat) if lat else None
+        return elapsed, per_rank, p50_loaded, p50
+
     def measure(run, per_round: int, steps: int, warmup: int, label: str, pipelined: bool = False, runner=None):
         """Time `steps` pipelined rounds of `per_round` images (split over the
         ranks), then `unloaded` rounds one at a time for the p50 latency.
@@ -587,13 +639,29 @@ def run_rank(a) -> int:
         between the plane's two slots; the broadcast of round q+1's
         descriptors is posted before round q's forward and round q's gather
         is waited for only after round q+1's forward is queued, so at N > 1
-        neither collective sits between two forwards on the compute stream."""
-        if pipelined:
-            return measure_pipelined(run, per_round, steps, warmup, label, runner)
+        neither collective sits between two forwards on the compute stream.
+        Otherwise both collectives sit between the forwards (and the gather is
+        timed: ``gather_us``)."""
         state = JobState() if coord else None
         host = [torch.empty(W, plane.max_chunk, 2, dtype=torch.int32, pin_memory=gpu) for _ in range(2)] \
             if coord else None
         lat, pending = [], []
+        step, drain, gtimes, timing = (pipelined_round if pipelined else serial_round)(
+            run, per_round, warmup, state, host, lat, pending)
+        elapsed, per_rank, p50_loaded, p50 = run_phases(step, drain, lat, steps, warmup, timing)
+        g_us = ([1000.0 * g0.elapsed_time(g1) for g0, g1 in gtimes] if gpu else [1e6 * x for x in gtimes]) \
+            if gtimes else []
+        recorded = state.images_done(a.model) if coord else None
+        return {"elapsed": elapsed, "ips": per_round * steps / elapsed, "p50": p50, "p50_loaded": p50_loaded,
+                "recorded": recorded, "label": label,
+                "rank_ms": [1000.0 * x / steps for x in per_rank],
+                "gather_us": statistics.median(g_us) if g_us else None,
+                "verified": verify(state, runner)}
+
+    def serial_round(run, per_round, warmup, state, host, lat, pending):
+        """Round q: descriptor broadcast, forward, gather, one after another on
+        the compute stream; the coordinator copies the round to pinned memory
+        and ingests the round before it."""
         gtimes = []            # (start, end) CUDA events / host seconds around each timed round's gather
         timing = [False]
 
@@ -601,28 +669,17 @@ def run_rank(a) -> int:
             ev, table, slot, t0 = pending.pop(0)
             if ev is not None:
                 ev.synchronize()
-            t1 = time.perf_counter()
-            res = host[slot].numpy()
-            cls_all, prob_all = res[:, :, 0], res[:, :, 1].view(np.float32)
-            for r, row in enumerate(table):
-                n = row[3] - row[2] + 1
-                state.record_result(a.model, row[1], f"rank{r}", row[2], row[3], cls_all[r, :n].copy(),
-                                    prob_all[r, :n].copy(), t1)
+            record_round(state, host[slot].numpy(), table, time.perf_counter())
             lat.append(time.perf_counter() - t0)
 
-        def step(q: int):
+        def step(q: int, nxt: bool):
             t0 = time.perf_counter()
             table = None
             if coord:
-                off = (q * per_round) % (D - max(per_round, plane.max_chunk) + 1)
-                chunks = split_range(off, off + per_round - 1, W)
-                qnum = q
-                table = [(model_id, qnum, s, e) for s, e in chunks]
-                state.assign(a.model, qnum, [(f"rank{r}", s, e) for r, (s, e) in enumerate(chunks)], t0)
+                chunks, table = table_of(q, per_round)
+                state.assign(a.model, q, [(f"rank{r}", s, e) for r, (s, e) in enumerate(chunks)], t0)
             plane.dispatch_device(table, slot=q)
-            if a.fail_rank == env.rank and q == warmup:
-                print(f"bench: rank {env.rank} failing on purpose (--fail-rank)", file=sys.stderr, flush=True)
-                os._exit(3)
+            fail_on_purpose(q, warmup)
             run(q)
             if timing[0] and gpu:
                 g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -652,40 +709,66 @@ def run_rank(a) -> int:
                 while pending:
                     ingest()
             barrier()
+        return step, drain, gtimes, timing
 
-        for q in range(warmup):
-            step(q)
-        drain()
-        lat.clear()
-        timing[0] = True
-        t_start = time.perf_counter()
-        for q in range(warmup, warmup + steps):
-            step(q)
-        drain()
-        elapsed = time.perf_counter() - t_start
-        timing[0] = False
-        per_rank = [elapsed]
-        if env.distributed:
-            # every rank's own timed region; the step time is the slowest rank's
-            t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
-            outs = [torch.zeros_like(t) for _ in range(W)]
-            dist.all_gather(outs, t)
-            per_rank = [float(x.item()) for x in outs]
-            elapsed = max(per_rank)
-        g_us = [1000.0 * g0.elapsed_time(g1) for g0, g1 in gtimes] if gpu else [1e6 * x for x in gtimes]
-        gtimes.clear()
-        p50_loaded = statistics.median(lat) if lat else None
-        lat.clear()
-        for q in range(warmup + steps, warmup + steps + max(5, min(steps, 20))):
-            step(q)
-            drain()
-        p50 = statistics.median(lat) if lat else None
-        recorded = state.images_done(a.model) if coord else None
-        return {"elapsed": elapsed, "ips": per_round * steps / elapsed, "p50": p50, "p50_loaded": p50_loaded,
-                "recorded": recorded, "label": label,
-                "rank_ms": [1000.0 * x / steps for x in per_rank],
-                "gather_us": statistics.median(g_us) if g_us else None,
-                "verified": verify(state, runner)}
+    def pipelined_round(run, per_round, warmup, state, host, lat, pending):
+        """Round q on slot q % 2 of the double-buffered plane (see ``measure``)."""
+        posted, gathers, t0s, tables = {}, [], {}, {}
+
+        def post(q):
+            tab = None
+            if coord:
+                tables[q] = table_of(q, per_round)
+                tab = tables[q][1]
+            posted[q] = plane.post_dispatch(tab, slot=q % 2, hslot=q)
+
+        def ingest():
+            ev, q = pending.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            record_round(state, host[q % 2].numpy(), tables.pop(q)[1], time.perf_counter())
+            lat.append(time.perf_counter() - t0s.pop(q))
+
+        def finish_gather():
+            """The compute stream waits for the oldest posted gather; the
+            coordinator copies that round to the host and ingests the round
+            before it (whose copy has had a forward's time to land)."""
+            q, work = gathers.pop(0)
+            plane.wait_work(work)
+            if coord:
+                host[q % 2].copy_(plane.gathered_slot(q % 2), non_blocking=gpu)
+                ev = None
+                if gpu:
+                    ev = torch.cuda.Event()
+                    ev.record()
+                if pending:
+                    ingest()
+                pending.append((ev, q))
+
+        def step(q: int, nxt: bool):
+            t0s[q] = time.perf_counter()
+            if q not in posted:
+                post(q)
+            if coord:
+                chunks, _ = tables[q]
+                state.assign(a.model, q, [(f"rank{r}", s, e) for r, (s, e) in enumerate(chunks)], t0s[q])
+            if nxt:
+                post(q + 1)          # RCCL stream: waits only for round q-1 (last reader of slot (q+1)%2)
+            plane.wait_work(posted.pop(q))
+            fail_on_purpose(q, warmup)
+            run(q)
+            if gathers:
+                finish_gather()      # round q-1's gather ran under round q's forward
+            gathers.append((q, plane.post_gather(q % 2)))
+
+        def drain():
+            while gathers:
+                finish_gather()
+            if coord:
+                while pending:
+                    ingest()
+            barrier()
+        return step, drain, [], None
 
     def verify(state, runner=None) -> bool | None:
         """Every recorded chunk holds the classes of ITS images, i.e. no slot
@@ -717,109 +800,6 @@ def run_rank(a) -> int:
             ok &= bool(np.array_equal(cls.cpu().numpy(), c.cls)) and \
                 bool(np.allclose(prob.cpu().numpy(), c.prob, rtol=0, atol=1e-6))
         return ok
-
-    def measure_pipelined(run, per_round: int, steps: int, warmup: int, label: str, runner=None):
-        state = JobState() if coord else None
-        host = [torch.empty(W, plane.max_chunk, 2, dtype=torch.int32, pin_memory=gpu) for _ in range(2)] \
-            if coord else None
-        lat, pending, posted, gathers = [], [], {}, []
-        t0s, tables = {}, {}
-
-        def table_of(q):
-            off = (q * per_round) % (D - max(per_round, plane.max_chunk) + 1)
-            chunks = split_range(off, off + per_round - 1, W)
-            return chunks, [(model_id, q, s, e) for s, e in chunks]
-
-        def post(q):
-            tab = None
-            if coord:
-                chunks, tab = table_of(q)
-                tables[q] = (chunks, tab)
-            posted[q] = plane.post_dispatch(tab, slot=q % 2, hslot=q)
-
-        def ingest():
-            ev, q = pending.pop(0)
-            if ev is not None:
-                ev.synchronize()
-            t1 = time.perf_counter()
-            res = host[q % 2].numpy()
-            cls_all, prob_all = res[:, :, 0], res[:, :, 1].view(np.float32)
-            _, tab = tables.pop(q)
-            for r, row in enumerate(tab):
-                n = row[3] - row[2] + 1
-                state.record_result(a.model, row[1], f"rank{r}", row[2], row[3], cls_all[r, :n].copy(),
-                                    prob_all[r, :n].copy(), t1)
-            lat.append(time.perf_counter() - t0s.pop(q))
-
-        def finish_gather():
-            """The compute stream waits for the oldest posted gather; the
-            coordinator copies that round to the host and ingests the round
-            before it (whose copy has had a forward's time to land)."""
-            q, work = gathers.pop(0)
-            plane.wait_work(work)
-            if coord:
-                host[q % 2].copy_(plane.gathered_slot(q % 2), non_blocking=gpu)
-                ev = None
-                if gpu:
-                    ev = torch.cuda.Event()
-                    ev.record()
-                if pending:
-                    ingest()
-                pending.append((ev, q))
-
-        def step(q: int, nxt: bool):
-            t0s[q] = time.perf_counter()
-            if q not in posted:
-                post(q)
-            if coord:
-                chunks, _ = tables[q]
-                state.assign(a.model, q, [(f"rank{r}", s, e) for r, (s, e) in enumerate(chunks)], t0s[q])
-            if nxt:
-                post(q + 1)          # RCCL stream: waits only for round q-1 (last reader of slot (q+1)%2)
-            plane.wait_work(posted.pop(q))
-            if a.fail_rank == env.rank and q == warmup:
-                print(f"bench: rank {env.rank} failing on purpose (--fail-rank)", file=sys.stderr, flush=True)
-                os._exit(3)
-            run(q)
-            if gathers:
-                finish_gather()      # round q-1's gather ran under round q's forward
-            gathers.append((q, plane.post_gather(q % 2)))
-
-        def drain():
-            while gathers:
-                finish_gather()
-            if coord:
-                while pending:
-                    ingest()
-            barrier()
-
-        for q in range(warmup):
-            step(q, q + 1 < warmup)
-        drain()
-        lat.clear()
-        t_start = time.perf_counter()
-        for q in range(warmup, warmup + steps):
-            step(q, q + 1 < warmup + steps)
-        drain()
-        elapsed = time.perf_counter() - t_start
-        per_rank = [elapsed]
-        if env.distributed:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
-            outs = [torch.zeros_like(t) for _ in range(W)]
-            dist.all_gather(outs, t)
-            per_rank = [float(x.item()) for x in outs]
-            elapsed = max(per_rank)
-        p50_loaded = statistics.median(lat) if lat else None
-        lat.clear()
-        for q in range(warmup + steps, warmup + steps + max(5, min(steps, 20))):
-            step(q, False)
-            drain()
-        p50 = statistics.median(lat) if lat else None
-        recorded = state.images_done(a.model) if coord else None
-        return {"elapsed": elapsed, "ips": per_round * steps / elapsed, "p50": p50, "p50_loaded": p50_loaded,
-                "recorded": recorded, "label": label,
-                "rank_ms": [1000.0 * x / steps for x in per_rank], "gather_us": None,
-                "verified": verify(state, runner)}
 
     # ---- headline: weak scaling at the headline precision --------------------
     runner = None
