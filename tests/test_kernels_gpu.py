@@ -414,6 +414,28 @@ def test_hipgraph_replay_matches_eager(ops):
     assert torch.allclose(p0, p1)
 
 
+def test_direct_graph_launch_matches_replay(ops):
+    """IDUNNO_DIRECT_LAUNCH: the captured graph launched with hipGraphLaunch on
+    the current stream (ops graph_launch) gives the torch replay's results."""
+    from idunno.models import HipRunner, build_program
+
+    shard = ops.synth_images(7, 0, 24, "cuda")
+    outs = []
+    for direct in (False, True):
+        runner = HipRunner(build_program("resnet18", seed=4))
+        runner.direct_launch = direct
+        start, run = runner.capture_window(shard, 8)
+        res = []
+        for s0 in (0, 9, 16):
+            start.fill_(s0)
+            c, p = run()
+            res.append((c.clone(), p.clone()))
+        torch.cuda.synchronize()
+        outs.append(res)
+    for (c0, p0), (c1, p1) in zip(*outs):
+        assert torch.equal(c0, c1) and torch.equal(p0, p1)
+
+
 @pytest.mark.parametrize("fuse", [True, False])
 def test_device_window_graph_matches_slices(ops, fuse):
     from idunno.models import HipRunner, build_program
