@@ -105,6 +105,9 @@ def test_sdfs_shard_peer_copy_between_nodes():
     try:
         put_synthetic_dataset(c.nodes["node00"].sdfs, 100, c.cfg.data_seed, shard_images=50)
         a, b = c.nodes["node01"], c.nodes["node02"]
+        # no readahead: node01 must hold shard 0 only (its background fetch of
+        # shard 1 would make that a peer copy too, depending on timing)
+        a.source.readahead = b.source.readahead = 0
         ta = a.source.get(0, 49)
         torch.cuda.synchronize()
         assert a.source.peer_fetches == 0
