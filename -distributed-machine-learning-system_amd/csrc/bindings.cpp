@@ -525,6 +525,33 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
   }
   const int t = tile >= 0 ? (int)tile : conv_glds_split_pick(a.M, Cout);
   a.norder = split_norder((Cout + 127) / 128, Kpad);
+  const int nk_total = (int)(KH * KW) * (C2 / 64);
+  const int ks = nsplit == 0 ? conv_split_ksplit(a.M, Cout, t, nk_total) : 1;
+  if (ks > 1) {
+    // small M: K slices into fp32 partials in one launch, then one combine
+    // (bias, residual, ReLU, split + range guard) -- conv_glds.hip conv_split_ksplit
+    TORCH_CHECK((long)ks * M * Cout < (1L << 31), "split-K partials too large for int32 indexing");
+    auto part = torch::empty({ks, M, (int64_t)Cout}, x.options().dtype(torch::kFloat));
+    auto zb = zero_f32(x.device(), Cout);
+    ConvArgs b = a;
+    b.bias = zb.data_ptr<float>();
+    b.res = nullptr;
+    b.ldr = 0;
+    b.y = part.data_ptr<float>();
+    b.ldy = Cout;
+    b.relu = 0;
+    b.ovf = nullptr;
+    b.ksplit = ks;
+    b.kslice = 0;
+    b.ysplit = (long)M * Cout;
+    b.kstage = nk_total / ks;
+    TORCH_CHECK(conv_glds_split_launch(b, true, t, cur_stream()), "unknown split conv tile id ", t);
+    check_launch("conv_glds_split (split-K)");
+    splitk_reduce_res_launch(part.data_ptr<float>(), ks, (long)M * Cout, Cout, a.bias, rp, (int)rP, a.relu, a.y,
+                             (int)ych, out_f32, a.ovf, cur_stream());
+    check_launch("splitk_reduce_res");
+    return y;
+  }
   TORCH_CHECK(conv_glds_split_launch(a, out_f32, t, cur_stream()), "unknown split conv tile id ", t);
   check_launch("conv_glds_split");
   return y;
@@ -1424,6 +1451,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("split_mf32", &split_mf32);
   m.def("set_split_deepb", &set_split_deepb, "A/B: split M >= 50000 tile 36 -> 60 (pixel ring of 3 slots)");
   m.def("split_deepb", &split_deepb);
+  m.def("set_split_ksplit", &set_split_ksplit, "split convs at small M: 0 off, -1 auto, k > 1 force k K-slices");
+  m.def("split_ksplit", &split_ksplit);
+  m.def("conv_split_ksplit_for", [](int64_t M, int64_t Cout, int64_t nk) {
+    return conv_split_ksplit((int)M, (int)Cout, conv_glds_split_pick((int)M, (int)Cout), (int)nk);
+  }, "K slices the auto pick gives a split conv of M pixels x Cout with nk K stages");
   m.def("set_f16_deepb", &set_f16_deepb, "A/B: fp16 M >= 50000 -> tile 61 (pixel ring of 3 slots)");
   m.def("set_f16_mf32", &set_f16_mf32, "A/B: fp16 tiles on 32x32x16 MFMAs (bit 0: M >= 50000 -> 90 (92 with bit 2), bit 1: M < 50000 -> 92)");
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");

@@ -43,6 +43,8 @@ struct ConvArgs {
   float acc_scale2;
   int ldr;           // residual pixel stride in halfs (0: the output width, 2*Cout split / Cout fp16)
   int l2pf;          // conv_glds: prefetch the tile's input footprint into L2 at block start (set by the launchers)
+  int kstage;        // conv split-K (small M): block s / tiles runs K stages [s*kstage, (s+1)*kstage) of the
+                     // (kh, kw, cblk) loop into fp32 partials y + s*ysplit (kslice 0); 0: off
 };
 
 // fp32 (reference-precision) conv: same geometry fields as ConvArgs, f32 tensors.
@@ -147,6 +149,11 @@ void set_split_wide_all(bool on);    // A/B: ... at every M
 void set_split_mf32(int mode);       // split tiles on 32x32x16 MFMAs: bit 0 M >= 50000 (56), bit 1 M < 50000 (58)
 int split_mf32();
 void set_split_deepb(bool on);       // split tile 36 -> 60 (3-slot pixel ring, 80 KiB)
+void set_split_ksplit(int mode);     // split convs, small M: 0 off, -1 auto (fill the chip), k > 1 force k slices
+int split_ksplit();
+int conv_split_ksplit(int M, int Cout, int tile, int nk_total);   // K slices for a split conv (1: none)
+void splitk_reduce_res_launch(const float* part, int S, long MN, int N, const float* bias, const half_t* res,
+                              int ldr, int relu, void* y, int ldy, bool out_f32, int* ovf, hipStream_t st);
 void set_f16_deepb(bool on);         // fp16 M >= 50000, Cout % 128 == 0 -> tile 61 (3-slot pixel ring)
 bool split_deepb();
 void set_f16_mf32(int mode);        // fp16 tiles on 32x32x16 MFMAs: bit 0 M >= 50000 (90, or 92 with bit 2), bit 1 M < 50000 (92)

@@ -332,6 +332,14 @@ conv_glds_kernel(const ConvArgs a) {
     i_s = (i_kh * a.KW + i_kw) * a.cblk;
     nK = a.cblk;
   }
+  if (a.kstage > 0) {                          // conv split-K: this block's contiguous run of K stages
+    i_s = split * a.kstage;
+    i_cb = i_s % a.cblk;
+    const int tap = i_s / a.cblk;
+    i_kw = tap % a.KW;
+    i_kh = tap / a.KW;
+    nK = a.kstage;
+  }
   // Buffer-resource DMA (every non-P3 conv; operands must fit 2 GiB, glds_cfg):
   // per-lane byte offsets are fixed -- A for the whole launch, B per kernel
   // tap (recomputed when the channel block wraps) -- and the stage's K offset
@@ -357,6 +365,7 @@ conv_glds_kernel(const ConvArgs a) {
       b_voff[j] = ok ? (uint32_t)((b_base[j] + (ih * a.W + iw) * ldx) * 2) : OOR;
     }
   };
+  if (i_cb != 0) set_tap();                    // a split-K slice that starts inside a tap
   auto issue_buf = [&](int buf) {
     char* base = smem + buf * STAGE;
     if (i_cb == 0) set_tap();
@@ -943,6 +952,37 @@ int split_mf32() { return g_split_mf32; }
 static bool g_split_deepb = false;
 void set_split_deepb(bool on) { g_split_deepb = on; }
 bool split_deepb() { return g_split_deepb; }
+// conv split-K for small M (strong scaling: a 400-image query over 8 GPUs is 50
+// images per GPU, and ResNet layer4 then makes 64 blocks of tile 42 on 256 CUs):
+// K slices of whole (kh, kw, cblk) stage runs in ONE launch into fp32 partials,
+// then splitk_reduce_res adds bias (+ residual), ReLU and re-splits.
+static int g_split_ksplit = -1;
+void set_split_ksplit(int mode) { g_split_ksplit = mode; }
+int split_ksplit() { return g_split_ksplit; }
+static void split_tile_dims(int tile, int& bn, int& bm) {
+  switch (tile) {
+    case 42: bn = 128; bm = 160; return;
+    case 27: case 59: bn = 64; bm = 128; return;
+    case 34: case 38: bn = 128; bm = 64; return;
+    case 55: bn = 64; bm = 256; return;
+    case 58: bn = 128; bm = 192; return;
+    default: bn = 128; bm = 128; return;
+  }
+}
+int conv_split_ksplit(int M, int Cout, int tile, int nk_total) {
+  if (g_split_ksplit == 0 || nk_total < 8) return 1;
+  int bn, bm;
+  split_tile_dims(tile, bn, bm);
+  const long blocks = (long)((M + bm - 1) / bm) * ((Cout + bn - 1) / bn);
+  if (g_split_ksplit > 1) return nk_total % g_split_ksplit == 0 ? g_split_ksplit : 1;   // forced (tests, A/B)
+  const long target = 2L * device_cu_count();  // two blocks per CU
+  int s = 1;
+  // double the slices while the grid stays within one wave of two blocks per CU,
+  // each slice keeps >= 4 stages and the slices divide the K loop evenly
+  while (s < 8 && blocks * s * 2 <= target && nk_total % (s * 2) == 0 && nk_total / (s * 2) >= 4) s *= 2;
+  return s;
+}
+
 int conv_glds_split_pick(int M, int Cout) {
   if (Cout % 128 == 0) {
     if ((g_split_mf32 & 1) && M >= 50000) return 56;

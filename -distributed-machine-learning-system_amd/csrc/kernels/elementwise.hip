@@ -247,6 +247,47 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, int S, long
   }
 }
 
+// Split-K combine for convs: y = act(sum_s part[s] + bias (+ split residual)), split
+// [M][ldy] or fp32 [M][ldy] out, range-guarded (common.h split_guard).
+__global__ void splitk_reduce_res_kernel(const float* __restrict__ part, int S, long MN, int N,
+                                         const float* __restrict__ bias, const half_t* __restrict__ res, int ldr,
+                                         int relu, void* __restrict__ y, int ldy, int out_f32, int* ovf) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= MN) return;
+  float4v v = *reinterpret_cast<const float4v*>(part + i);
+  for (int s = 1; s < S; ++s) v += *reinterpret_cast<const float4v*>(part + (long)s * MN + i);
+  const long m = i / N;
+  const int n = (int)(i - m * N);
+  v += *reinterpret_cast<const float4v*>(bias + n);
+  if (res != nullptr) {
+    const half_t* rp = res + m * ldr + split_off(n);
+    const half4v h = *reinterpret_cast<const half4v*>(rp), l = *reinterpret_cast<const half4v*>(rp + 32);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += (float)h[e] + (float)l[e];
+  }
+  if (relu) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+  }
+  if (out_f32) {
+    *reinterpret_cast<float4v*>(static_cast<float*>(y) + m * ldy + n) = v;
+  } else {
+    split_guard(ovf, v);
+    half4v h, l;
+    split_f16x4(v, h, l);
+    half_t* yp = static_cast<half_t*>(y) + m * ldy + split_off(n);
+    *reinterpret_cast<half4v*>(yp) = h;
+    *reinterpret_cast<half4v*>(yp + 32) = l;
+  }
+}
+
+void splitk_reduce_res_launch(const float* part, int S, long MN, int N, const float* bias, const half_t* res,
+                              int ldr, int relu, void* y, int ldy, bool out_f32, int* ovf, hipStream_t st) {
+  const long threads = (MN + 3) / 4;
+  hipLaunchKernelGGL(splitk_reduce_res_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, part, S,
+                     MN, N, bias, res, ldr, relu, y, ldy, out_f32 ? 1 : 0, ovf);
+}
+
 void splitk_reduce_split_launch(const float* part, int S, long MN, int N, const float* bias, int relu, half_t* y,
                                 int* ovf, hipStream_t st) {
   const long threads = (MN + 3) / 4;

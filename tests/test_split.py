@@ -321,6 +321,37 @@ def test_conv_split_tiles(ops, tile, res, out_f32):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B,H,cin,cout,k,s,ks", [(2, 9, 128, 256, 3, 1, 2), (2, 9, 128, 256, 3, 1, 3),
+                                               (3, 7, 256, 512, 3, 1, 8), (2, 13, 64, 128, 3, 2, 6),
+                                               (2, 14, 256, 512, 1, 2, 4), (1, 7, 512, 512, 3, 1, -1)])
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("out_f32", [False, True])
+def test_conv_split_ksplit(ops, B, H, cin, cout, k, s, ks, res, out_f32):
+    """Small-M split-K (K slices of whole stage runs into fp32 partials, one
+    combine with bias / residual / ReLU / re-split): forced k slices (k = 8 over
+    72 stages starts slices inside a tap) and the auto pick (-1) at M = 49."""
+    ext = ops.load()
+    keep = ext.split_ksplit()
+    ext.set_split_ksplit(ks)
+    try:
+        torch.manual_seed(B + H + cin + ks)
+        x = torch.randn(B, H, H, cin, device=DEV)
+        w = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
+        b = torch.randn(cout) * 0.1
+        pad = k // 2
+        ho = (H + 2 * pad - k) // s + 1
+        r = torch.randn(B, ho, ho, cout, device=DEV) if res else None
+        sw, scale = P.pack_split_weight(w)
+        y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, k, k, s, pad, True,
+                             residual=None if r is None else ops.split_from_f32(r), out_f32=out_f32)
+        _check(y if out_f32 else P.from_split(y), _ref64(x, w, b, s, pad, True, r))
+        if ks == -1:
+            assert ext.conv_split_ksplit_for(B * ho * ho, cout, k * k * (2 * cin // 64)) > 1
+    finally:
+        ext.set_split_ksplit(keep)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cin,k", [(32, 1), (64, 1), (96, 1), (32, 3)])
 @pytest.mark.parametrize("res", [False, True])
 def test_conv_split_deepb_short_k(ops, cin, k, res):
