@@ -970,7 +970,8 @@ static void split_tile_dims(int tile, int& bn, int& bm) {
   }
 }
 int conv_split_ksplit(int M, int Cout, int tile, int nk_total) {
-  if (g_split_ksplit == 0 || nk_total < 8) return 1;
+  // the 32x32x16 tiles (55-59) have their own epilogue without split-K partial slices
+  if (g_split_ksplit == 0 || nk_total < 8 || (tile >= 55 && tile <= 59)) return 1;
   int bn, bm;
   split_tile_dims(tile, bn, bm);
   const long blocks = (long)((M + bm - 1) / bm) * ((Cout + bn - 1) / bn);
