@@ -471,8 +471,11 @@ def test_model_split_vs_fp64_oracle(ops, name, B):
         assert torch.equal(r.logits(img).double().cpu(), got)
         r.split_front = None
     if name.startswith("resnet") and B >= 64:
-        r.split_streams = 2                    # two half-batch streams: same numbers
-        assert torch.equal(r.logits(img).double().cpu(), got)
+        # two half-batch streams: the same numbers, up to the summation order of
+        # the small-M split-K (a half batch's layer4 runs as K slices)
+        r.split_streams = 2
+        got2 = r.logits(img).double().cpu()
+        assert (got2 - got).abs().max().item() <= 2e-6 * got.abs().max().item()
         torch.cuda.synchronize()
         r.split_streams = None
     n = min(B, 8)
