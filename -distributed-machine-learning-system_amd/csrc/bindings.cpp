@@ -58,6 +58,8 @@ void set_conv3x3_c64_default(bool on) { g_c64_default = on; }
 //   w   : [Cout, Kpad] fp16, K ordered (kh, kw, c) [big] or (kh, kw8, c4) [small]
 //   bias: [Cout] fp32
 //   res : optional [B, Ho, Wo, Cout] fp16
+static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
+
 torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
                           c10::optional<torch::Tensor> res, int64_t KH, int64_t KW, int64_t stride,
                           int64_t pad, bool relu, bool out_f32, int64_t tile, c10::optional<torch::Tensor> out) {
@@ -157,6 +159,29 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
     return y;
   }
   const int t = tile >= 10 ? (int)tile : conv_glds_pick(a.M, Cout);
+  const int ks = C % 64 == 0 ? conv_f16_ksplit(a.M, Cout, t, (int)(KH * KW) * (C / 64)) : 1;
+  if (ks > 1) {
+    // small M: K slices into fp32 partials, one combine (conv2d_split_impl, conv_glds.hip conv_split_ksplit)
+    TORCH_CHECK((long)ks * M * Cout < (1L << 31), "split-K partials too large for int32 indexing");
+    auto part = torch::empty({ks, M, (int64_t)Cout}, x.options().dtype(torch::kFloat));
+    auto zb = zero_f32(x.device(), Cout);
+    ConvArgs b = a;
+    b.bias = zb.data_ptr<float>();
+    b.res = nullptr;
+    b.y = part.data_ptr<float>();
+    b.ldy = Cout;
+    b.relu = 0;
+    b.ksplit = ks;
+    b.kslice = 0;
+    b.ysplit = (long)M * Cout;
+    b.kstage = (int)(KH * KW) * (C / 64) / ks;
+    TORCH_CHECK(conv_glds_launch(b, true, t, cur_stream()), "unknown conv tile id ", t);
+    check_launch("conv_glds (split-K)");
+    splitk_reduce_res_launch(part.data_ptr<float>(), ks, (long)M * Cout, Cout, a.bias, rp, Cout, a.relu, a.y, Cout,
+                             out_f32 ? 3 : 2, nullptr, cur_stream());
+    check_launch("splitk_reduce_res");
+    return y;
+  }
   TORCH_CHECK(conv_glds_launch(a, out_f32, t, cur_stream()), "unknown conv tile id ", t);
   check_launch("conv_glds");
   return y;
@@ -548,7 +573,7 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
     TORCH_CHECK(conv_glds_split_launch(b, true, t, cur_stream()), "unknown split conv tile id ", t);
     check_launch("conv_glds_split (split-K)");
     splitk_reduce_res_launch(part.data_ptr<float>(), ks, (long)M * Cout, Cout, a.bias, rp, (int)rP, a.relu, a.y,
-                             (int)ych, out_f32, a.ovf, cur_stream());
+                             (int)ych, out_f32 ? 1 : 0, a.ovf, cur_stream());
     check_launch("splitk_reduce_res");
     return y;
   }
@@ -1453,6 +1478,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("split_deepb", &split_deepb);
   m.def("set_split_ksplit", &set_split_ksplit, "split convs at small M: 0 off, -1 auto, k > 1 force k K-slices");
   m.def("split_ksplit", &split_ksplit);
+  m.def("set_f16_ksplit", &set_f16_ksplit, "fp16 convs at small M: 0 off, -1 auto, k > 1 force k K-slices");
+  m.def("f16_ksplit", &f16_ksplit);
   m.def("conv_split_ksplit_for", [](int64_t M, int64_t Cout, int64_t nk) {
     return conv_split_ksplit((int)M, (int)Cout, conv_glds_split_pick((int)M, (int)Cout), (int)nk);
   }, "K slices the auto pick gives a split conv of M pixels x Cout with nk K stages");

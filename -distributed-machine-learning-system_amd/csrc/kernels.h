@@ -152,8 +152,12 @@ void set_split_deepb(bool on);       // split tile 36 -> 60 (3-slot pixel ring, 
 void set_split_ksplit(int mode);     // split convs, small M: 0 off, -1 auto (fill the chip), k > 1 force k slices
 int split_ksplit();
 int conv_split_ksplit(int M, int Cout, int tile, int nk_total);   // K slices for a split conv (1: none)
+// fmt: 0 split residual/output, 1 split residual + fp32 output, 2 fp16 residual/output, 3 fp16 residual + fp32 output
 void splitk_reduce_res_launch(const float* part, int S, long MN, int N, const float* bias, const half_t* res,
-                              int ldr, int relu, void* y, int ldy, bool out_f32, int* ovf, hipStream_t st);
+                              int ldr, int relu, void* y, int ldy, int fmt, int* ovf, hipStream_t st);
+void set_f16_ksplit(int mode);       // fp16 convs at small M: 0 off, -1 auto, k > 1 force
+int f16_ksplit();
+int conv_f16_ksplit(int M, int Cout, int tile, int nk_total);
 void set_f16_deepb(bool on);         // fp16 M >= 50000, Cout % 128 == 0 -> tile 61 (3-slot pixel ring)
 bool split_deepb();
 void set_f16_mf32(int mode);        // fp16 tiles on 32x32x16 MFMAs: bit 0 M >= 50000 (90, or 92 with bit 2), bit 1 M < 50000 (92)

@@ -984,6 +984,18 @@ int conv_split_ksplit(int M, int Cout, int tile, int nk_total) {
   return s;
 }
 
+static int g_f16_ksplit = -1;
+void set_f16_ksplit(int mode) { g_f16_ksplit = mode; }
+int f16_ksplit() { return g_f16_ksplit; }
+int conv_f16_ksplit(int M, int Cout, int tile, int nk_total) {
+  if (tile >= 90) return 1;                      // 32x32x16 fp16 tiles: no partial slices in their epilogue
+  const int keep = g_split_ksplit;
+  g_split_ksplit = g_f16_ksplit;                 // same rule, the fp16 switch
+  const int s = conv_split_ksplit(M, Cout, tile, nk_total);
+  g_split_ksplit = keep;
+  return s;
+}
+
 int conv_glds_split_pick(int M, int Cout) {
   if (Cout % 128 == 0) {
     if ((g_split_mf32 & 1) && M >= 50000) return 56;

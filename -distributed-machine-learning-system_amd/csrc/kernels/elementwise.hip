@@ -249,9 +249,11 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, int S, long
 
 // Split-K combine for convs: y = act(sum_s part[s] + bias (+ split residual)), split
 // [M][ldy] or fp32 [M][ldy] out, range-guarded (common.h split_guard).
+// fmt: 0 split-fp16 residual and output, 1 split residual and fp32 output,
+// 2 fp16 residual and fp16 output, 3 fp16 residual and fp32 output
 __global__ void splitk_reduce_res_kernel(const float* __restrict__ part, int S, long MN, int N,
                                          const float* __restrict__ bias, const half_t* __restrict__ res, int ldr,
-                                         int relu, void* __restrict__ y, int ldy, int out_f32, int* ovf) {
+                                         int relu, void* __restrict__ y, int ldy, int fmt, int* ovf) {
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= MN) return;
   float4v v = *reinterpret_cast<const float4v*>(part + i);
@@ -259,18 +261,27 @@ __global__ void splitk_reduce_res_kernel(const float* __restrict__ part, int S, 
   const long m = i / N;
   const int n = (int)(i - m * N);
   v += *reinterpret_cast<const float4v*>(bias + n);
-  if (res != nullptr) {
+  if (res != nullptr && fmt < 2) {
     const half_t* rp = res + m * ldr + split_off(n);
     const half4v h = *reinterpret_cast<const half4v*>(rp), l = *reinterpret_cast<const half4v*>(rp + 32);
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] += (float)h[e] + (float)l[e];
+  } else if (res != nullptr) {
+    const half4v h = *reinterpret_cast<const half4v*>(res + m * ldr + n);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += (float)h[e];
   }
   if (relu) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
   }
-  if (out_f32) {
+  if (fmt == 1 || fmt == 3) {
     *reinterpret_cast<float4v*>(static_cast<float*>(y) + m * ldy + n) = v;
+  } else if (fmt == 2) {
+    half4v o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (half_t)v[e];
+    *reinterpret_cast<half4v*>(static_cast<half_t*>(y) + m * ldy + n) = o;
   } else {
     split_guard(ovf, v);
     half4v h, l;
@@ -282,10 +293,10 @@ __global__ void splitk_reduce_res_kernel(const float* __restrict__ part, int S, 
 }
 
 void splitk_reduce_res_launch(const float* part, int S, long MN, int N, const float* bias, const half_t* res,
-                              int ldr, int relu, void* y, int ldy, bool out_f32, int* ovf, hipStream_t st) {
+                              int ldr, int relu, void* y, int ldy, int fmt, int* ovf, hipStream_t st) {
   const long threads = (MN + 3) / 4;
   hipLaunchKernelGGL(splitk_reduce_res_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, part, S,
-                     MN, N, bias, res, ldr, relu, y, ldy, out_f32 ? 1 : 0, ovf);
+                     MN, N, bias, res, ldr, relu, y, ldy, fmt, ovf);
 }
 
 void splitk_reduce_split_launch(const float* part, int S, long MN, int N, const float* bias, int relu, half_t* y,

@@ -72,6 +72,33 @@ def test_conv_shapes(ops, B, H, Cin, Cout, k, s, p):
     _check(y, ref)
 
 
+@pytest.mark.parametrize("B,H,cin,cout,k,s,ks", [(2, 9, 128, 256, 3, 1, 2), (2, 9, 128, 256, 3, 1, 3),
+                                               (3, 7, 512, 512, 3, 1, 8), (2, 13, 128, 128, 3, 2, 6),
+                                               (2, 14, 256, 512, 1, 2, 4), (1, 7, 512, 512, 3, 1, -1)])
+@pytest.mark.parametrize("res", [False, True])
+def test_conv_f16_ksplit(ops, B, H, cin, cout, k, s, ks, res):
+    """fp16 convs at small M as K slices + one combine (forced slice counts; -1:
+    the auto pick at M = 49) against the fp32 reference."""
+    from idunno.models.packed import pack_conv_weight
+
+    ext = ops.load()
+    keep = ext.f16_ksplit()
+    ext.set_f16_ksplit(ks)
+    try:
+        torch.manual_seed(B + H + cin + ks + res)
+        x = torch.randn(B, H, H, cin, device=DEV).half()
+        w = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
+        b = torch.randn(cout) * 0.1
+        pad = k // 2
+        ho = (H + 2 * pad - k) // s + 1
+        r = torch.randn(B, ho, ho, cout, device=DEV).half() if res else None
+        pw, small = pack_conv_weight(w)
+        y = ops.conv2d(x, pw.to(DEV), b.to(DEV), k, k, s, pad, True, residual=r)
+        _check(y, _ref_conv(x, w.half().float().to(DEV), b.to(DEV), s, pad, True, r))
+    finally:
+        ext.set_f16_ksplit(keep)
+
+
 @pytest.mark.parametrize("tile", [0, 1, 2, 3] + list(range(10, 40)) + [42, 61, 90, 91, 92])
 @pytest.mark.parametrize("H", [14, 9])
 def test_conv_all_tiles_with_residual(ops, tile, H):
