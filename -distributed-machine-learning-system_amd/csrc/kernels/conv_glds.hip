@@ -989,6 +989,10 @@ void set_f16_ksplit(int mode) { g_f16_ksplit = mode; }
 int f16_ksplit() { return g_f16_ksplit; }
 int conv_f16_ksplit(int M, int Cout, int tile, int nk_total) {
   if (tile >= 90) return 1;                      // 32x32x16 fp16 tiles: no partial slices in their epilogue
+  switch (tile) {                                // BK = 32 tiles: nk_total (counted in 64-channel stages) differs
+    case 11: case 13: case 18: case 19: case 20: case 21: case 22: case 28: case 31: case 32: case 39: return 1;
+    default: break;
+  }
   const int keep = g_split_ksplit;
   g_split_ksplit = g_f16_ksplit;                 // same rule, the fp16 switch
   const int s = conv_split_ksplit(M, Cout, tile, nk_total);
