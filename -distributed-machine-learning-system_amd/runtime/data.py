@@ -363,8 +363,6 @@ class SdfsSource:
         parts = []
         i = start
         last = end // self.S
-        for r in range(1, self.readahead + 1):
-            self._prefetch(last + r)
         while i <= end:
             k = i // self.S
             sh = self._shard(k)
@@ -374,6 +372,10 @@ class SdfsSource:
                 raise KeyError(f"image {i} beyond shard {k}")
             parts.append(sh[lo:hi + 1])
             i = k * self.S + hi + 1
+        # readahead once this request's shards are in hand: a background fetch that
+        # took the stager first would put a whole shard in front of the one needed now
+        for r in range(1, self.readahead + 1):
+            self._prefetch(last + r)
         return parts[0] if len(parts) == 1 else torch.cat(parts, 0)
 
 
