@@ -98,8 +98,10 @@ def test_collective_rounds_with_failures():
         # SIGKILL the coordinator: this standby promotes itself and re-forms as rank 0
         procs[0].send_signal(signal.SIGKILL)
         assert wait_for(lambda: me.is_coordinator, 10)
+        # the promoted coordinator's epoch is formed and healthy (no re-form still
+        # pending from the failure detector) before the next query is timed
         assert wait_for(lambda: me.rounds.group.formed and me.rounds.group.rank == 0
-                        and len(me.rounds.group.members) == 2, 30)
+                        and len(me.rounds.group.members) == 2 and me.rounds.healthy, 30)
         before = me.rounds.rounds_done
         cl.inference(2000, 2399, "resnet18")
         s = cl.wait_idle(20, {"resnet18": 2400})
