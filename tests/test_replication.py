@@ -90,9 +90,11 @@ def test_coordinator_cost_flat_over_100k_queries():
                 js.record_result("resnet18", q, w, s, e, np.zeros(200, np.int32), np.ones(200, np.float32))
         return (time.perf_counter() - t0) / n
 
-    first = batch(10_000)
+    # best of 5 windows of 2k queries at each end: the check is about growth with
+    # history, not about a busy host's scheduling spikes
+    first = min(batch(2_000) for _ in range(5))
     batch(80_000)
-    last = batch(10_000)
+    last = min(batch(2_000) for _ in range(5))
     assert js.pending_count() == 0 and js.images_done("resnet18") == 100_000 * 400
     assert last < 2.0 * first + 20e-6, f"per-query cost grew: {first * 1e6:.1f} -> {last * 1e6:.1f} us"
     # a push after one more query carries a handful of entries, not the history
