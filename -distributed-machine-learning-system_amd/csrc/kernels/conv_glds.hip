@@ -969,19 +969,22 @@ static void split_tile_dims(int tile, int& bn, int& bm) {
     default: bn = 128; bm = 128; return;
   }
 }
-int conv_split_ksplit(int M, int Cout, int tile, int nk_total) {
+static int ksplit_rule(int mode, int M, int Cout, int tile, int nk_total) {
   // the 32x32x16 tiles (55-59) have their own epilogue without split-K partial slices
-  if (g_split_ksplit == 0 || nk_total < 8 || (tile >= 55 && tile <= 59)) return 1;
+  if (mode == 0 || nk_total < 8 || (tile >= 55 && tile <= 59)) return 1;
   int bn, bm;
   split_tile_dims(tile, bn, bm);
   const long blocks = (long)((M + bm - 1) / bm) * ((Cout + bn - 1) / bn);
-  if (g_split_ksplit > 1) return nk_total % g_split_ksplit == 0 ? g_split_ksplit : 1;   // forced (tests, A/B)
+  if (mode > 1) return nk_total % mode == 0 ? mode : 1;   // forced (tests, A/B)
   const long target = 2L * device_cu_count();  // two blocks per CU
   int s = 1;
   // double the slices while the grid stays within one wave of two blocks per CU,
   // each slice keeps >= 4 stages and the slices divide the K loop evenly
   while (s < 8 && blocks * s * 2 <= target && nk_total % (s * 2) == 0 && nk_total / (s * 2) >= 4) s *= 2;
   return s;
+}
+int conv_split_ksplit(int M, int Cout, int tile, int nk_total) {
+  return ksplit_rule(g_split_ksplit, M, Cout, tile, nk_total);
 }
 
 static int g_f16_ksplit = -1;
@@ -993,11 +996,7 @@ int conv_f16_ksplit(int M, int Cout, int tile, int nk_total) {
     case 11: case 13: case 18: case 19: case 20: case 21: case 22: case 28: case 31: case 32: case 39: return 1;
     default: break;
   }
-  const int keep = g_split_ksplit;
-  g_split_ksplit = g_f16_ksplit;                 // same rule, the fp16 switch
-  const int s = conv_split_ksplit(M, Cout, tile, nk_total);
-  g_split_ksplit = keep;
-  return s;
+  return ksplit_rule(g_f16_ksplit, M, Cout, tile, nk_total);   // same rule, the fp16 switch
 }
 
 int conv_glds_split_pick(int M, int Cout) {
