@@ -1478,6 +1478,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("split_deepb", &split_deepb);
   m.def("set_split_ksplit", &set_split_ksplit, "split convs at small M: 0 off, -1 auto, k > 1 force k K-slices");
   m.def("split_ksplit", &split_ksplit);
+  m.def("set_ksplit_cap4", &set_ksplit_cap4, "A/B: the auto split-K rule uses at most 4 K slices (default 8)");
   m.def("set_f16_ksplit", &set_f16_ksplit, "fp16 convs at small M: 0 off, -1 auto, k > 1 force k K-slices");
   m.def("f16_ksplit", &f16_ksplit);
   m.def("conv_split_ksplit_for", [](int64_t M, int64_t Cout, int64_t nk) {

@@ -151,6 +151,7 @@ int split_mf32();
 void set_split_deepb(bool on);       // split tile 36 -> 60 (3-slot pixel ring, 80 KiB)
 void set_split_ksplit(int mode);     // split convs, small M: 0 off, -1 auto (fill the chip), k > 1 force k slices
 int split_ksplit();
+void set_ksplit_cap4(bool on);       // A/B: the auto split-K rule stops at 4 slices instead of 8
 int conv_split_ksplit(int M, int Cout, int tile, int nk_total);   // K slices for a split conv (1: none)
 // fmt: 0 split residual/output, 1 split residual + fp32 output, 2 fp16 residual/output, 3 fp16 residual + fp32 output
 void splitk_reduce_res_launch(const float* part, int S, long MN, int N, const float* bias, const half_t* res,

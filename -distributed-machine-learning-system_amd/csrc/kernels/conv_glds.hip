@@ -958,6 +958,8 @@ bool split_deepb() { return g_split_deepb; }
 // then splitk_reduce_res adds bias (+ residual), ReLU and re-splits.
 static int g_split_ksplit = -1;
 void set_split_ksplit(int mode) { g_split_ksplit = mode; }
+static int g_ksplit_cap = 8;             // most K slices the auto rule uses
+void set_ksplit_cap4(bool on) { g_ksplit_cap = on ? 4 : 8; }
 int split_ksplit() { return g_split_ksplit; }
 static void split_tile_dims(int tile, int& bn, int& bm) {
   switch (tile) {
@@ -980,7 +982,7 @@ static int ksplit_rule(int mode, int M, int Cout, int tile, int nk_total) {
   int s = 1;
   // double the slices while the grid stays within one wave of two blocks per CU,
   // each slice keeps >= 4 stages and the slices divide the K loop evenly
-  while (s < 8 && blocks * s * 2 <= target && nk_total % (s * 2) == 0 && nk_total / (s * 2) >= 4) s *= 2;
+  while (s < g_ksplit_cap && blocks * s * 2 <= target && nk_total % (s * 2) == 0 && nk_total / (s * 2) >= 4) s *= 2;
   return s;
 }
 int conv_split_ksplit(int M, int Cout, int tile, int nk_total) {
