@@ -10,6 +10,7 @@
 #include <mutex>
 
 #include "kernels.h"
+#include "launch_util.h"
 
 using namespace idunno;
 
@@ -401,6 +402,9 @@ static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
 // row-streaming register-weight kernel (tile 50 of conv2d_split, conv3x3_split.hip).
 static bool g_split_c64_default = true;
 void set_split_c64_default(bool on) { g_split_c64_default = on; }
+// auto selection of the band-staged 3x3 kernel (tile 70) for split 3x3/s1 convs
+static bool g_split_band_default = true;
+void set_split_band_default(bool on) { g_split_band_default = on; }
 // Split range guard (common.h split_guard): the int32 flag
 // that this thread's split launches write to when a value leaves fp16's range;
 // HipRunner sets it around a split forward (a captured graph keeps the pointer).
@@ -539,6 +543,19 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
     check_launch("conv3x3_split_c64");
     return y;
   }
+  // band-staged 3x3 kernel (conv3x3_band.hip, tile 70): ResNet layers 2-4 at batches
+  // that give every CU at least two tiles (smaller grids keep the im2col tiles + split-K)
+  const bool band_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && nsplit == 0 &&
+                       conv3x3_band_supported(H, W, C2 / 2, Cout);
+  if (tile == 70 || (tile < 0 && band_ok && g_split_band_default &&
+                     conv3x3_band_tiles(B, W, Cout) >= 2 * device_cu_count())) {
+    TORCH_CHECK(band_ok, "tile 70 (band-staged split 3x3 conv) does not support this shape");
+    TORCH_CHECK(conv3x3_band_launch(a.x, (int)xP, a.w, a.bias, rp, (int)rP, a.y, (int)ych, out_f32, B, H, W, C2 / 2,
+                                    Cout, a.relu, a.acc_scale, a.ovf, 0, 0, cur_stream()),
+                "band conv: tensor too large for 32-bit buffer offsets");
+    check_launch("conv3x3_band");
+    return y;
+  }
   const bool c1s_ok = KH == 1 && KW == 1 && (stride == 1 || stride == 2) && pad == 0 && !out_f32 && !strided &&
                       nsplit == 0 && a.ablate == 0 && conv1x1_stream_split_supported(C2 / 2, Cout, M);
   if (tile == 80 || (tile < 0 && c1s_ok && conv1x1_stream_split_default(C2 / 2, stride))) {
@@ -579,6 +596,47 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
   }
   TORCH_CHECK(conv_glds_split_launch(a, out_f32, t, cur_stream()), "unknown split conv tile id ", t);
   check_launch("conv_glds_split");
+  return y;
+}
+
+// Band-staged split 3x3/s1/p1 conv with an explicit persistent-grid cap (tests:
+// max_grid < tiles makes every workgroup run several tiles through one DMA ring).
+torch::Tensor conv3x3_band_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias, c10::optional<torch::Tensor> res,
+                                 bool relu, double acc_scale, bool out_f32, int64_t max_grid, int64_t flags) {
+  CHECK_DEV(x);
+  CHECK_DEV(w);
+  CHECK_DEV(bias);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(bias);
+  CHECK_DT(x, torch::kHalf);
+  CHECK_DT(w, torch::kHalf);
+  CHECK_DT(bias, torch::kFloat);
+  const int64_t xP = nhwc_pixel_stride(x, "x");
+  const int B = x.size(0), H = x.size(1), W = x.size(2), C2 = x.size(3), Cout = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == 9 * C2 && bias.numel() == Cout, "split weight must be [Cout, 9*2C]");
+  TORCH_CHECK(w.device() == x.device() && bias.device() == x.device(), "operands on different devices");
+  TORCH_CHECK(conv3x3_band_supported(H, W, C2 / 2, Cout), "band conv: unsupported shape");
+  const int64_t ych = out_f32 ? Cout : 2 * Cout;
+  auto y = torch::empty({B, H, W, ych}, x.options().dtype(out_f32 ? torch::kFloat : torch::kHalf));
+  const half_t* rp = nullptr;
+  int64_t rP = 2 * Cout;
+  if (res.has_value() && res->defined()) {
+    auto& r = *res;
+    CHECK_DEV(r);
+    CHECK_DT(r, torch::kHalf);
+    rP = nhwc_pixel_stride(r, "residual");
+    TORCH_CHECK(r.device() == x.device() && r.size(0) == B && r.size(1) == H && r.size(2) == W && r.size(3) == 2 * Cout,
+                "residual shape mismatch (split [B, H, W, 2*Cout])");
+    rp = reinterpret_cast<const half_t*>(r.data_ptr());
+  }
+  if (B == 0) return y;
+  TORCH_CHECK(conv3x3_band_launch(reinterpret_cast<const half_t*>(x.data_ptr()), (int)xP,
+                                  reinterpret_cast<const half_t*>(w.data_ptr()), bias.data_ptr<float>(), rp, (int)rP,
+                                  y.data_ptr(), (int)ych, out_f32, B, H, W, C2 / 2, Cout, relu ? 1 : 0, (float)acc_scale,
+                                  out_f32 ? nullptr : split_guard_for(x.device()), (int)max_grid, (int)flags,
+                                  cur_stream()),
+              "band conv: tensor too large for 32-bit buffer offsets");
+  check_launch("conv3x3_band");
   return y;
 }
 
@@ -1446,6 +1504,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_split", &linear_split, "fp32-accurate FC on split fp16, split-K in one launch + combine",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("acc_scale"), py::arg("relu"), py::arg("out_f32"),
         py::arg("splits"), py::arg("tile") = -1);
+  m.def("conv3x3_band_split", &conv3x3_band_split,
+        "band-staged split 3x3/s1/p1 conv (tile 70) with a persistent-grid cap (0: one workgroup per CU)",
+        py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res") = py::none(), py::arg("relu") = true,
+        py::arg("acc_scale") = 1.0, py::arg("out_f32") = false, py::arg("max_grid") = 0, py::arg("flags") = 0);
+  m.def("conv3x3_band_tiles", &conv3x3_band_tiles, "band conv tile count for (B, W, Cout)");
+  m.def("set_split_band_default", &set_split_band_default,
+        "A/B: auto-route split 3x3/s1 convs of ResNet layers 2-4 to the band-staged kernel (tile 70)");
   m.def("set_split_c64_default", &set_split_c64_default,
         "A/B: route split 3x3 64->64 convs to the row-streaming kernel (tile 50; default on)");
   m.def("set_split_norder", &set_split_norder, "A/B: split conv tile order (0 m-major, 1 n-major, -1 auto)");
