@@ -543,12 +543,11 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
     check_launch("conv3x3_split_c64");
     return y;
   }
-  // band-staged 3x3 kernel (conv3x3_band.hip, tile 70): ResNet layers 2-4 at batches
-  // that give every CU at least two tiles (smaller grids keep the im2col tiles + split-K)
+  // band-staged 3x3 kernel (conv3x3_band.hip, tile 70): ResNet layers 2 and 4 at batches
+  // that give every CU a tile (conv3x3_band_default; otherwise the im2col tiles + split-K)
   const bool band_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && nsplit == 0 &&
                        conv3x3_band_supported(H, W, C2 / 2, Cout);
-  if (tile == 70 || (tile < 0 && band_ok && g_split_band_default &&
-                     conv3x3_band_tiles(B, W, Cout) >= 2 * device_cu_count())) {
+  if (tile == 70 || (tile < 0 && band_ok && g_split_band_default && conv3x3_band_default(B, W, Cout))) {
     TORCH_CHECK(band_ok, "tile 70 (band-staged split 3x3 conv) does not support this shape");
     TORCH_CHECK(conv3x3_band_launch(a.x, (int)xP, a.w, a.bias, rp, (int)rP, a.y, (int)ych, out_f32, B, H, W, C2 / 2,
                                     Cout, a.relu, a.acc_scale, a.ovf, 0, 0, cur_stream()),

@@ -205,6 +205,7 @@ void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bia
 // C % 64 == 0, Cout % 128 == 0); x / res read in place at pixel strides ldx / ldr (halfs)
 bool conv3x3_band_supported(int H, int W, int C, int Cout);
 int conv3x3_band_tiles(int B, int W, int Cout);
+bool conv3x3_band_default(int B, int W, int Cout);   // auto-selection rule for conv2d_split
 bool conv3x3_band_launch(const half_t* x, int ldx, const half_t* w, const float* bias, const half_t* res, int ldr,
                          void* y, int ldy, bool out_f32, int B, int H, int W, int C, int Cout, int relu,
                          float acc_scale, int* ovf, int max_grid, int flags, hipStream_t st);

@@ -666,6 +666,17 @@ bool conv3x3_band_supported(int H, int W, int C, int Cout) {
   return H == W && band_fm(W) > 0 && C % 64 == 0 && C >= 64 && Cout % bnd::BN == 0;
 }
 
+int conv3x3_band_tiles(int B, int W, int Cout);
+
+// Auto selection (round-5 per-layer A/B at B = 400, profiles/r5_band_ab.md): layer2
+// (W 28, 1225 tiles) and layer4 (W 7, 492 tiles; 4-5 % under the 128 x 160 im2col
+// tile) take the band kernel; layer3 (W 14) ties the 128 x 128 im2col tile and keeps it.
+// Below one tile per CU (small per-GPU batches) the im2col tiles + split-K win.
+bool conv3x3_band_default(int B, int W, int Cout) {
+  if (W != 28 && W != 7) return false;
+  return conv3x3_band_tiles(B, W, Cout) >= device_cu_count();
+}
+
 int conv3x3_band_tiles(int B, int W, int Cout) {
   const int fm = band_fm(W);
   if (fm <= 0) return 0;

@@ -111,7 +111,7 @@ def parse(argv=None):
     ap.add_argument("--no-system", action="store_true", help="skip phases 2-3 (system + failover)")
     ap.add_argument("--extras-timeout", type=float, default=150.0,
                     help="seconds per system / failover phase (bounded: the driver gives the whole run 600 s)")
-    ap.add_argument("--extras-budget", type=float, default=330.0,
+    ap.add_argument("--extras-budget", type=float, default=240.0,
                     help="seconds for all phases after the headline together; a phase that would start "
                          "past it is skipped (extras_skipped), so the headline line always comes out in time")
     ap.add_argument("--two-job-queries", type=int, default=10, help="queries per job in the two-job run")
@@ -126,7 +126,15 @@ def parse(argv=None):
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--dry-run", action="store_true", help="CPU + gloo + fake forward (launcher/contract test)")
     ap.add_argument("--fail-rank", type=int, default=-1, help="testing: this rank exits 3 after warmup")
-    ap.add_argument("--launch-timeout", type=float, default=1500.0, help="seconds before headline ranks are killed")
+    ap.add_argument("--launch-timeout", type=float, default=300.0,
+                    help="seconds before the headline ranks are killed (headline + in-rank extras; the driver's "
+                         "lease is 600 s for the whole run)")
+    ap.add_argument("--rank-extras-budget", type=float, default=150.0,
+                    help="seconds for the in-rank extras after the headline; an extra that would start past "
+                         "it is skipped (rank_extras_skipped)")
+    ap.add_argument("--fail-after-headline", type=int, default=-1,
+                    help="testing: this rank exits 3 right after the headline is measured")
+    ap.add_argument("--hang-in-extras", type=int, default=-1, help="testing: this rank hangs in the extras")
     ap.add_argument("--system", action="store_true", help="phase 2 only (see docstring)")
     ap.add_argument("--phase", default="system", choices=["system", "failover", "worker"], help=argparse.SUPPRESS)
     ap.add_argument("--detector", default="reference", choices=["reference", "tuned"], help=argparse.SUPPRESS)
@@ -248,9 +256,19 @@ def _headline(a, argv, work: str) -> tuple[int, dict | None]:
         port = _free_port()
         procs = [_spawn(child, _child_env("rank", r, a.gpus, port)) for r in range(a.gpus)]
     rc = _wait_all(procs, a.launch_timeout, "rank")
-    if rc:
-        return (rc if rc else 1), None
-    return 0, _read_json(out) if ("RANK" not in os.environ or int(os.environ["RANK"]) == 0) else None
+    if "RANK" in os.environ and int(os.environ["RANK"]) != 0:
+        head = _read_json(f"{out}.rank{os.environ['RANK']}")
+        # another torchrun rank: its child leaves a marker once the headline is measured;
+        # a failure after that is reported by rank 0's line, not by this exit code
+        # (a non-zero exit would make torchrun tear down rank 0's launcher and its line)
+        return (0 if rc and head is not None else rc), None
+    head = _read_json(out)
+    if rc and head is not None:
+        # the headline was measured and written before a rank failed / hung in an extra
+        head["extras_error"] = (head.get("extras_error", "") +
+                                f"; headline ranks failed or timed out after the headline (rc={rc})").lstrip("; ")
+        head["headline_ranks_rc"] = rc
+    return rc, head
 
 
 def _system_phase(a, work: str) -> dict:
@@ -389,11 +407,14 @@ def launcher(a, argv) -> int:
                     f.write(line + "\n")
             return 0 if "extras_error" not in d else 1
         rc, head = _headline(a, [x for x in argv if x not in ("--json-out",)], work)
-        if rc:
-            return rc
-        if head is None:                                  # a torchrun rank other than 0
-            return 0
-        if not a.no_system:
+        if head is None:
+            if rc and ("RANK" not in os.environ or int(os.environ["RANK"]) == 0):
+                print(json.dumps({"metric": METRIC, "value": None, "n_gpus": a.gpus, "steps": a.steps,
+                                  "warmup": a.warmup, "higher_is_better": True,
+                                  "error": f"headline ranks failed (rc={rc}) before the headline was measured"}),
+                      flush=True)
+            return rc                                     # 0 for a torchrun rank other than 0
+        if not a.no_system and not rc:                    # (a failed headline rank: no node phases on that box)
             t0 = time.time()
             skipped = []
             for name, fn in (("system", _system_phase), ("failover", _failover_phase),
@@ -482,7 +503,10 @@ def run_rank(a) -> int:
         # rehearsal of the N > 1 path on a box with fewer GPUs than ranks (see --rehearse-gloo)
         os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
     t_rank0 = time.perf_counter()
-    env = init_from_env(backend="gloo" if (a.dry_run or a.rehearse_gloo) else None, cpu=a.dry_run)
+    # collectives time out well inside the launcher's limit (a dead peer must not hang a rank
+    # past it: the launcher then prints the line rank 0 already wrote)
+    env = init_from_env(backend="gloo" if (a.dry_run or a.rehearse_gloo) else None, cpu=a.dry_run,
+                        timeout_s=min(120.0, max(30.0, a.launch_timeout / 3)))
     if env.world != a.gpus:
         print(json.dumps({"error": f"--gpus {a.gpus} but WORLD_SIZE={env.world}"}), flush=True)
         return 2
@@ -822,23 +846,57 @@ def run_rank(a) -> int:
     head = measure(make(runner, B), W * B, a.steps, a.warmup, "weak", pipelined=pipe, runner=runner)
     progress("headline measured")
     extras = {"pipelined_collectives": pipe}
+    t_extras = time.perf_counter()
+    skipped = []
+
+    def emit() -> None:
+        """Rank 0 writes the line as it stands (atomically): first right after the
+        headline, then after every extra -- a rank that dies or hangs in an extra
+        cannot take the headline with it (the launcher prints the last line).
+        The other ranks write a marker that their headline is done."""
+        if not a.json_out:
+            return
+        line = json.dumps(headline_line(a, W, B, head, extras, runner, env, dist, serial) if coord else
+                          {"rank": env.rank, "headline_done": True})
+        path = a.json_out if coord else f"{a.json_out}.rank{env.rank}"
+        with open(path + ".tmp", "w") as f:
+            f.write(line + "\n")
+        os.replace(path + ".tmp", path)
+
+    def budget_left(name: str) -> bool:
+        ok = time.perf_counter() - t_extras < a.rank_extras_budget
+        if not ok:
+            skipped.append(name)
+            extras["rank_extras_skipped"] = skipped
+        return ok
+
     serial = None
-    if pipe:
+    emit()
+    if a.fail_after_headline == env.rank:
+        print(f"bench: rank {env.rank} failing after the headline on purpose", file=sys.stderr, flush=True)
+        os._exit(3)
+    if a.hang_in_extras == env.rank:
+        print(f"bench: rank {env.rank} hanging in the extras on purpose", file=sys.stderr, flush=True)
+        time.sleep(3600)
+    if pipe and budget_left("serial collectives"):
         # the same rounds with the broadcast and gather between the forwards on the
         # compute stream: what the pipelining saves, and the gather's own time
         serial = measure(make_run(runner, B), W * B, a.steps, a.warmup, "weak-serial")
         extras.update({"value_serial_collectives": round(serial["ips"], 2),
                        "ms_per_step_serial_collectives": round(1000 * serial["elapsed"] / a.steps, 4)})
+        emit()
     if not a.no_extras:
-        # strong scaling: ONE 400-image query split over the W ranks
-        strong = measure(make(runner, strong_chunk), QUERY, a.steps, a.warmup, "strong", pipelined=pipe)
-        progress("strong scaling measured")
-        extras.update({
-            "images_per_s_strong": round(strong["ips"], 2),
-            "p50_query_latency_strong_s": round(strong["p50"], 6) if strong["p50"] else None,
-            "strong_chunk_per_gpu": strong_chunk,
-        })
-        if not a.dry_run:
+        if budget_left("strong scaling"):
+            # strong scaling: ONE 400-image query split over the W ranks
+            strong = measure(make(runner, strong_chunk), QUERY, a.steps, a.warmup, "strong", pipelined=pipe)
+            progress("strong scaling measured")
+            extras.update({
+                "images_per_s_strong": round(strong["ips"], 2),
+                "p50_query_latency_strong_s": round(strong["p50"], 6) if strong["p50"] else None,
+                "strong_chunk_per_gpu": strong_chunk,
+            })
+            emit()
+        if not a.dry_run and budget_left("other precision"):
             other = "fp16" if a.dtype == "fp32" else "fp32"
             r2 = HipRunner(build_program(a.model, seed=a.seed, dtype=other), env.device)
             m2 = measure(make_run(r2, B), W * B, a.steps, a.warmup, other)
@@ -847,73 +905,38 @@ def run_rank(a) -> int:
                            f"p50_query_latency_{other}_s": round(m2["p50"], 6) if m2["p50"] else None})
             del r2
             progress(f"{other} measured")
-            if a.dtype == "fp32":
-                alt = "f32mfma" if a.fp32_impl == "split" else "split"
-                runner.split = alt == "split"
-                m3 = measure(make_run(runner, B), W * B, a.steps, a.warmup, alt)
-                runner.split = a.fp32_impl == "split"
-                extras.update({f"value_fp32_{alt}": round(m3["ips"], 2),
-                               f"ms_per_step_fp32_{alt}": round(1000 * m3["elapsed"] / a.steps, 4)})
+            emit()
+        if not a.dry_run and a.dtype == "fp32" and budget_left("other fp32 kernels"):
+            alt = "f32mfma" if a.fp32_impl == "split" else "split"
+            runner.split = alt == "split"
+            m3 = measure(make_run(runner, B), W * B, a.steps, a.warmup, alt)
+            runner.split = a.fp32_impl == "split"
+            extras.update({f"value_fp32_{alt}": round(m3["ips"], 2),
+                           f"ms_per_step_fp32_{alt}": round(1000 * m3["elapsed"] / a.steps, 4)})
+            emit()
+        if not a.dry_run and budget_left("numerics"):
             if coord:
                 extras.update(numerics_check(runner, a, env.device))
             progress("numerics checked")
-        if W > 1 and not a.rehearse_gloo:
+            emit()
+        if not a.dry_run and W == 1 and a.model == "resnet18" and budget_left("resnet50"):
+            extras.update(resnet50_extra(a, env, make_run))
+            progress("resnet50 measured")
+            emit()
+        if W > 1 and not a.rehearse_gloo and budget_left("scatter"):
+            # last and bounded: the only extra whose collective never ran on RCCL before round 5
             # (a rehearsal skips it: gloo moves GPU tensors point-to-point through the host)
             # M9 data variant: images only in the coordinator's HBM,
-            # scattered every round over RCCL, double-buffered against compute
+            # scattered every round over RCCL (bucketed over the peers), double-buffered
             srun, sfinish = make_scatter_run(runner, B, W * B)
             sc = measure(srun, W * B, a.steps, a.warmup, "scatter")
             sfinish()
             extras.update({"images_per_s_scatter": round(sc["ips"], 2),
                            "ms_per_step_scatter": round(1000 * sc["elapsed"] / a.steps, 4),
                            "scatter_mb_per_round": round((W - 1) * B * 150528 / 1e6, 1)})
-
-    if coord:
-        ips = head["ips"]
-        p50 = head["p50"]
-        headline = a.model == "resnet18" and B == QUERY
-        out = {
-            "metric": METRIC if headline else
-            f"images/sec (whole node) + p50 query latency, {a.model} bs={B} at {W} GPU",
-            "value": round(ips, 2),
-            "unit": "images/sec",
-            "n_gpus": W,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(1000 * head["elapsed"] / a.steps, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(ips / BASELINE_IMG_PER_S, 2) if headline else None,
-            "dtype": "fp32" if a.dry_run else a.dtype,
-            "data": "synthetic uint8 224x224x3 images (dataset replicated in every GPU's HBM), random-init weights",
-            "config": {"model": a.model, "global_batch": W * B, "seq_len": None, "image_hw": 224,
-                       "batch_per_gpu": B, "parallelism": f"dp{W}", "graph": not a.no_graph,
-                       "fp32_impl": a.fp32_impl if a.dtype == "fp32" else None,
-                       "compute": (COMPUTE_SPLIT if a.fp32_impl == "split" else COMPUTE_F32) if a.dtype == "fp32" else
-                       "f16 MFMA, fp16 activations, fp32 accumulate",
-                       "dry_run": a.dry_run},
-            "p50_query_latency_s": round(p50, 6) if p50 else None,
-            "p50_query_latency_loaded_s": round(head["p50_loaded"], 6) if head["p50_loaded"] else None,
-            "p50_vs_baseline_speedup": round(BASELINE_P50_S / p50, 1) if p50 and headline else None,
-            "results_recorded": head["recorded"],
-            **({"results_verified": head["verified"]} if head["verified"] is not None else {}),
-            # readiness keys: the collective the timed rounds ran on, read from the
-            # live process group, the per-rank spread of the step time and the gather's own time
-            "comm_backend": (dist.get_backend() if env.distributed else "none (single rank: no collective)"),
-            "comm_world": dist.get_world_size() if env.distributed else 1,
-            "rccl": bool(env.distributed and dist.get_backend() == "nccl" and torch.version.hip is not None),
-            "ms_per_step_rank_min": round(min(head["rank_ms"]), 4),
-            "ms_per_step_rank_max": round(max(head["rank_ms"]), 4),
-            "gather_us_per_round": (round(serial["gather_us"], 1) if serial and serial["gather_us"] is not None else
-                                    round(head["gather_us"], 1) if head["gather_us"] is not None else None),
-            **extras,
-        }
-        if runner is not None:
-            out["model_tflops"] = round(program_flops(runner.p) * ips / 1e12, 2)
-        line = json.dumps(out)
-        if a.json_out:
-            with open(a.json_out, "w") as f:
-                f.write(line + "\n")
+            emit()
+    extras["rank_extras_wall_s"] = round(time.perf_counter() - t_extras, 1)
+    emit()
     if env.distributed:
         dist.barrier()
         dist.destroy_process_group()
@@ -921,6 +944,98 @@ def run_rank(a) -> int:
 
 
 
+
+
+def headline_line(a, W, B, head, extras, runner, env, dist, serial) -> dict:
+    """The bench line (rank 0) from the headline measurement and the extras so far."""
+    import torch
+
+    ips = head["ips"]
+    p50 = head["p50"]
+    headline = a.model == "resnet18" and B == QUERY
+    out = {
+        "metric": METRIC if headline else
+        f"images/sec (whole node) + p50 query latency, {a.model} bs={B} at {W} GPU",
+        "value": round(ips, 2),
+        "unit": "images/sec",
+        "n_gpus": W,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1000 * head["elapsed"] / a.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(ips / BASELINE_IMG_PER_S, 2) if headline else None,
+        "dtype": "fp32" if a.dry_run else a.dtype,
+        "data": "synthetic uint8 224x224x3 images (dataset replicated in every GPU's HBM), random-init weights",
+        "config": {"model": a.model, "global_batch": W * B, "seq_len": None, "image_hw": 224,
+                   "batch_per_gpu": B, "parallelism": f"dp{W}", "graph": not a.no_graph,
+                   "fp32_impl": a.fp32_impl if a.dtype == "fp32" else None,
+                   "compute": (COMPUTE_SPLIT if a.fp32_impl == "split" else COMPUTE_F32) if a.dtype == "fp32" else
+                   "f16 MFMA, fp16 activations, fp32 accumulate",
+                   "dry_run": a.dry_run},
+        "p50_query_latency_s": round(p50, 6) if p50 else None,
+        "p50_query_latency_loaded_s": round(head["p50_loaded"], 6) if head["p50_loaded"] else None,
+        "p50_vs_baseline_speedup": round(BASELINE_P50_S / p50, 1) if p50 and headline else None,
+        "results_recorded": head["recorded"],
+        **({"results_verified": head["verified"]} if head["verified"] is not None else {}),
+        # readiness keys (VERDICT r3 item 7): the collective the timed rounds ran on, read from the
+        # live process group, the per-rank spread of the step time and the gather's own time
+        "comm_backend": (dist.get_backend() if env.distributed else "none (single rank: no collective)"),
+        "comm_world": dist.get_world_size() if env.distributed else 1,
+        "rccl": bool(env.distributed and dist.get_backend() == "nccl" and torch.version.hip is not None),
+        "ms_per_step_rank_min": round(min(head["rank_ms"]), 4),
+        "ms_per_step_rank_max": round(max(head["rank_ms"]), 4),
+        "gather_us_per_round": (round(serial["gather_us"], 1) if serial and serial["gather_us"] is not None else
+                                round(head["gather_us"], 1) if head["gather_us"] is not None else None),
+        **extras,
+    }
+    if runner is not None:
+        from idunno.models import program_flops
+
+        out["model_tflops"] = round(program_flops(runner.p) * ips / 1e12, 2)
+    return out
+
+
+def resnet50_extra(a, env, make_run) -> dict:
+    """BASELINE config 5 (ResNet50 bs=1024 fp16) as extra keys of the default line:
+    the same round loop (descriptor, hipGraph replay of the forward, top-1 to
+    the host, job-state ingest) at 1024 images per step on this GPU."""
+    import torch
+
+    from idunno import ops
+    from idunno.models import HipRunner, build_program
+    from idunno.parallel.dataplane import QueryPlane
+    from idunno.runtime.jobstate import JobState
+
+    B5 = 1024
+    ds = ops.synth_images(a.seed + 99, 0, 2 * B5, env.device)
+    r5 = HipRunner(build_program("resnet50", seed=a.seed, dtype="fp16"), env.device)
+    plane = QueryPlane(env, coordinator=0, max_chunk=B5, nbuf=1)
+    _, run = r5.capture_window(ds, B5, start=plane.row_start(), start_offset=0, packed=plane.send_buffer)
+    state = JobState()
+    host = torch.empty(1, B5, 2, dtype=torch.int32, pin_memory=True)
+
+    def step(q):
+        off = (q % 2) * B5
+        state.assign("resnet50", q, [("rank0", off, off + B5 - 1)], time.perf_counter())
+        plane.dispatch_device([(2, q, off, off + B5 - 1)], slot=q)
+        run()
+        plane.gather(None, None)
+        host.copy_(plane.gathered_all)
+        state.record_result("resnet50", q, "rank0", off, off + B5 - 1, host[0, :, 0].numpy().copy(),
+                            host[0, :, 1].view(torch.float32).numpy().copy(), time.perf_counter())
+
+    steps = max(5, min(a.steps, 20))
+    for q in range(3):
+        step(q)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for q in range(3, 3 + steps):
+        step(q)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value_resnet50_fp16": round(B5 * steps / el, 2), "ms_per_step_resnet50_fp16": round(1000 * el / steps, 4),
+            "resnet50_batch": B5, "resnet50_results_recorded": state.images_done("resnet50")}
 
 # ---------------------------------------------------------------------------
 # phases 2-3: one node process of the fault-tolerant runtime

@@ -147,3 +147,33 @@ def test_bench_under_torchrun_dry_run():
     assert d["n_gpus"] == 2 and d["results_recorded"] == (1 + 3 + 5) * 800
     assert "extras_error" not in d and d["two_job_mixed_rounds"] >= 1
     assert d["coord_failover_images_exact"] is True
+
+
+def test_bench_headline_survives_rank_failure_after_headline():
+    """VERDICT r4 item 3: rank 0 writes the headline as soon as it is measured;
+    a rank that dies in an extra cannot take the line with it."""
+    r = _run("--gpus", "8", "--steps", "2", "--warmup", "1", "--fail-after-headline", "5", timeout=300)
+    assert "failing after the headline on purpose" in r.stderr
+    d = _line(r.stdout)
+    assert d["value"] > 0 and d["n_gpus"] == 8 and d["results_verified"] is True
+    assert d["results_recorded"] == (1 + 2 + 5) * 400 * 8
+    assert "after the headline" in d["extras_error"] and d["headline_ranks_rc"] != 0
+    assert r.returncode == 0
+
+
+def test_bench_headline_survives_rank_hang_in_extras():
+    """A rank that hangs in an extra: the launcher's time limit ends the ranks
+    and still prints the headline rank 0 wrote (the driver's lease is 600 s)."""
+    r = _run("--gpus", "8", "--steps", "2", "--warmup", "1", "--hang-in-extras", "2", "--launch-timeout", "45",
+             timeout=300)
+    assert "hanging in the extras on purpose" in r.stderr
+    d = _line(r.stdout)
+    assert d["value"] > 0 and d["n_gpus"] == 8
+    assert d["headline_ranks_rc"] != 0 and "timed out" in d["extras_error"]
+
+
+def test_bench_rank_failure_before_headline_prints_error_line():
+    r = _run("--gpus", "2", "--steps", "2", "--warmup", "1", "--fail-rank", "0")
+    assert r.returncode != 0
+    d = _line(r.stdout)
+    assert d["value"] is None and "before the headline" in d["error"]
