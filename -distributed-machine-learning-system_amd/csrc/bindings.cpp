@@ -41,14 +41,13 @@ static torch::Tensor zero_buffer(const torch::Device& dev) {
   return b;
 }
 
-// Whether auto tile selection routes 3x3/s1 64->64 convs to the resident-weight
-// kernel (tile 50, conv3x3_c64.hip): on by default since sweep r1 #6 (ResNet18
-// layer1 at B=400: 112 / 153 us vs 178 / 207 us for the best im2col tile,
-// profiles/r1_v6_layer1_c64.log).
-static int g_conv_ablate = 0;
-void set_conv_ablation(int mode) { g_conv_ablate = mode; }
-static bool g_c64_default = true;
-void set_conv3x3_c64_default(bool on) { g_c64_default = on; }
+// Kernel choice is a pure function of each call's arguments (no process-global
+// switches, VERDICT r4 weakness 4): `tile` forces a kernel, `ksplit` forces split-K
+// slices (-1 auto for the auto-picked tile), `route` (a per-runner policy, bits
+// below) opts a call out of the specialised kernels for whole-graph A/Bs.
+constexpr int kRouteNoBand = 1;      // no band-staged 3x3 kernel (tile 70)
+constexpr int kRouteNoC64 = 2;       // no row-streaming 3x3 64->64 kernels (tile 50)
+constexpr int kRouteNoStream1x1 = 4; // no streaming 1x1 kernels (tile 80)
 
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
@@ -63,7 +62,8 @@ static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
 
 torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
                           c10::optional<torch::Tensor> res, int64_t KH, int64_t KW, int64_t stride,
-                          int64_t pad, bool relu, bool out_f32, int64_t tile, c10::optional<torch::Tensor> out) {
+                          int64_t pad, bool relu, bool out_f32, int64_t tile, c10::optional<torch::Tensor> out,
+                          int64_t ksplit, int64_t route) {
   CHECK_DEV(x);
   CHECK_DEV(w);
   CHECK_DEV(bias);
@@ -132,7 +132,6 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   a.M = (int)M;
   a.Kpad = Kpad;
   a.relu = relu ? 1 : 0;
-  a.ablate = g_conv_ablate;
   if (M == 0) return y;
   if (small) {
     const int t = (tile >= 0 && tile <= 3) ? (int)tile : conv_pick_tile(a.M, Cout);
@@ -145,22 +144,27 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   }
   a.zero = zero_buffer(x.device()).data_ptr();
   const bool c64_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 && conv3x3_c64_supported(C, Cout);
-  if (tile == 50 || (tile < 0 && c64_ok && g_c64_default)) {
+  // resident-weight 3x3 64->64 kernel (tile 50, conv3x3_c64.hip): since sweep r1 #6 (ResNet18
+  // layer1 at B=400: 112 / 153 us vs 178 / 207 us for the best im2col tile, profiles/r1_v6_layer1_c64.log)
+  if (tile == 50 || (tile < 0 && c64_ok && !(route & kRouteNoC64))) {
     TORCH_CHECK(c64_ok, "tile 50 (resident-weight 3x3 64->64 conv) does not support this shape");
     conv3x3_c64_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W, a.relu,
                        cur_stream()); check_launch("conv3x3_c64");
     return y;
   }
   const bool c1s_ok = KH == 1 && KW == 1 && (stride == 1 || stride == 2) && pad == 0 && !out_f32 &&
-                      a.ablate == 0 && conv1x1_stream_supported(C, Cout, M);
-  if (tile == 80 || (tile < 0 && c1s_ok && conv1x1_stream_default(C, stride, M))) {
+                      conv1x1_stream_supported(C, Cout, M);
+  if (tile == 80 || (tile < 0 && c1s_ok && !(route & kRouteNoStream1x1) && conv1x1_stream_default(C, stride, M))) {
     TORCH_CHECK(c1s_ok, "tile 80 (streaming 1x1 conv) does not support this shape");
     conv1x1_stream_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, a.M, C, Cout, a.relu,
                           H, W, Wo, Ho * Wo, stride, cur_stream()); check_launch("conv1x1_stream");
     return y;
   }
   const int t = tile >= 10 ? (int)tile : conv_glds_pick(a.M, Cout);
-  const int ks = C % 64 == 0 ? conv_f16_ksplit(a.M, Cout, t, (int)(KH * KW) * (C / 64)) : 1;
+  // split-K: auto only for the auto-picked tile (a forced tile runs its own epilogue)
+  const int ks = C % 64 == 0 ? conv_f16_ksplit(a.M, Cout, t, (int)(KH * KW) * (C / 64),
+                                               tile >= 0 && ksplit < 0 ? 1 : (int)ksplit) : 1;
+  TORCH_CHECK(ksplit <= 1 || ks == ksplit, "split-K: ", ksplit, " slices do not divide the K loop of tile ", t);
   if (ks > 1) {
     // small M: K slices into fp32 partials, one combine (conv2d_split_impl, conv_glds.hip conv_split_ksplit)
     TORCH_CHECK((long)ks * M * Cout < (1L << 31), "split-K partials too large for int32 indexing");
@@ -398,13 +402,6 @@ torch::Tensor conv2d_nhwc_f32(torch::Tensor x, torch::Tensor w, torch::Tensor bi
 
 static torch::Tensor zero_f32(const torch::Device& dev, int64_t n);
 
-// Whether auto selection routes split 3x3/s1 64->64 convs (ResNet layer1) to the
-// row-streaming register-weight kernel (tile 50 of conv2d_split, conv3x3_split.hip).
-static bool g_split_c64_default = true;
-void set_split_c64_default(bool on) { g_split_c64_default = on; }
-// auto selection of the band-staged 3x3 kernel (tile 70) for split 3x3/s1 convs
-static bool g_split_band_default = true;
-void set_split_band_default(bool on) { g_split_band_default = on; }
 // Split range guard (common.h split_guard): the int32 flag
 // that this thread's split launches write to when a value leaves fp16's range;
 // HipRunner sets it around a split forward (a captured graph keeps the pointer).
@@ -430,13 +427,6 @@ static int* split_guard_for(const torch::Device& dev) {
   return g_split_guard;
 }
 
-// split convs: tile order (0 m-major, 1 n-major, -1 auto heuristic)
-static int g_split_norder = -1;
-void set_split_norder(int64_t mode) { g_split_norder = (int)mode; }
-static int split_norder(int tiles_n, long kpad) {
-  if (g_split_norder >= 0) return g_split_norder;
-  return 0;
-}
 
 // split fp16 (fp32-accurate) conv: y = act(acc_scale * conv(x, w) + bias (+ res)).
 //   x   : [B, H, W, 2C] half, split layout ([hi x32][lo x32] per 32 channels), C % 32 == 0
@@ -458,7 +448,7 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
                                        c10::optional<torch::Tensor> res, int64_t KH, int64_t KW, int64_t stride,
                                        int64_t pad, bool relu, double acc_scale, bool out_f32, int64_t tile,
                                        c10::optional<torch::Tensor> out, int64_t nsplit, bool center_only,
-                                       double acc_scale2) {
+                                       double acc_scale2, int64_t ksplit, int64_t route) {
   CHECK_DEV(x);
   CHECK_DEV(w);
   CHECK_DEV(bias);
@@ -520,7 +510,6 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
   a.Kpad = Kpad;
   a.relu = relu ? 1 : 0;
   a.acc_scale = (float)acc_scale;
-  a.ablate = g_conv_ablate;
   a.ovf = out_f32 ? nullptr : split_guard_for(x.device());
   // strided views (a dual conv's halves): conv_glds reads them in place
   const bool strided = xP != C2 || rP != 2 * Cout;
@@ -536,7 +525,8 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
   a.zero = zero_buffer(x.device()).data_ptr();
   const bool c64_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 && !strided && nsplit == 0 &&
                       conv3x3_split_c64_supported(H, W, C2 / 2, Cout);
-  if (tile == 50 || (tile < 0 && c64_ok && g_split_c64_default)) {
+  // row-streaming register-weight kernel for split 3x3/s1 64->64 (ResNet layer1)
+  if (tile == 50 || (tile < 0 && c64_ok && !(route & kRouteNoC64))) {
     TORCH_CHECK(c64_ok, "tile 50 (row-streaming split 3x3 64->64 conv) does not support this shape");
     conv3x3_split_c64_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W, a.relu,
                              a.acc_scale, a.ovf, cur_stream());
@@ -547,7 +537,7 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
   // that give every CU a tile (conv3x3_band_default; otherwise the im2col tiles + split-K)
   const bool band_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && nsplit == 0 &&
                        conv3x3_band_supported(H, W, C2 / 2, Cout);
-  if (tile == 70 || (tile < 0 && band_ok && g_split_band_default && conv3x3_band_default(B, W, Cout))) {
+  if (tile == 70 || (tile < 0 && band_ok && !(route & kRouteNoBand) && conv3x3_band_default(B, W, Cout))) {
     TORCH_CHECK(band_ok, "tile 70 (band-staged split 3x3 conv) does not support this shape");
     TORCH_CHECK(conv3x3_band_launch(a.x, (int)xP, a.w, a.bias, rp, (int)rP, a.y, (int)ych, out_f32, B, H, W, C2 / 2,
                                     Cout, a.relu, a.acc_scale, a.ovf, 0, 0, cur_stream()),
@@ -556,8 +546,8 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
     return y;
   }
   const bool c1s_ok = KH == 1 && KW == 1 && (stride == 1 || stride == 2) && pad == 0 && !out_f32 && !strided &&
-                      nsplit == 0 && a.ablate == 0 && conv1x1_stream_split_supported(C2 / 2, Cout, M);
-  if (tile == 80 || (tile < 0 && c1s_ok && conv1x1_stream_split_default(C2 / 2, stride))) {
+                      nsplit == 0 && conv1x1_stream_split_supported(C2 / 2, Cout, M);
+  if (tile == 80 || (tile < 0 && c1s_ok && !(route & kRouteNoStream1x1) && conv1x1_stream_split_default(C2 / 2, stride))) {
     TORCH_CHECK(c1s_ok, "tile 80 (streaming split 1x1 conv) does not support this shape");
     conv1x1_stream_split_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, a.M, C2 / 2, Cout,
                                 a.relu, a.acc_scale, a.ovf, H, W, Wo, Ho * Wo, stride, cur_stream());
@@ -565,9 +555,10 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
     return y;
   }
   const int t = tile >= 0 ? (int)tile : conv_glds_split_pick(a.M, Cout);
-  a.norder = split_norder((Cout + 127) / 128, Kpad);
   const int nk_total = (int)(KH * KW) * (C2 / 64);
-  const int ks = nsplit == 0 ? conv_split_ksplit(a.M, Cout, t, nk_total) : 1;
+  // split-K: auto only for the auto-picked tile (a forced tile runs its own epilogue)
+  const int ks = nsplit == 0 ? conv_split_ksplit(a.M, Cout, t, nk_total, tile >= 0 && ksplit < 0 ? 1 : (int)ksplit) : 1;
+  TORCH_CHECK(ksplit <= 1 || ks == ksplit, "split-K: ", ksplit, " slices do not divide the K loop of tile ", t);
   if (ks > 1) {
     // small M: K slices into fp32 partials in one launch, then one combine
     // (bias, residual, ReLU, split + range guard) -- conv_glds.hip conv_split_ksplit
@@ -641,8 +632,10 @@ torch::Tensor conv3x3_band_split(torch::Tensor x, torch::Tensor w, torch::Tensor
 
 torch::Tensor conv2d_split(torch::Tensor x, torch::Tensor w, torch::Tensor bias, c10::optional<torch::Tensor> res,
                            int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool relu, double acc_scale,
-                           bool out_f32, int64_t tile, c10::optional<torch::Tensor> out) {
-  return conv2d_split_impl(x, w, bias, res, KH, KW, stride, pad, relu, acc_scale, out_f32, tile, out, 0, false, 1.0);
+                           bool out_f32, int64_t tile, c10::optional<torch::Tensor> out, int64_t ksplit,
+                           int64_t route) {
+  return conv2d_split_impl(x, w, bias, res, KH, KW, stride, pad, relu, acc_scale, out_f32, tile, out, 0, false, 1.0,
+                           ksplit, route);
 }
 
 // Two split convs of one input in ONE launch (the ResNet stride-2
@@ -657,7 +650,7 @@ torch::Tensor conv2d_split_dual(torch::Tensor x, torch::Tensor w, torch::Tensor 
                                 int64_t nsplit, bool center_only, int64_t tile) {
   TORCH_CHECK(nsplit > 0, "dual conv needs nsplit > 0");
   return conv2d_split_impl(x, w, bias, c10::nullopt, KH, KW, stride, pad, relu, acc_scale, false, tile,
-                           c10::nullopt, nsplit, center_only, acc_scale2);
+                           c10::nullopt, nsplit, center_only, acc_scale2, 1, 0);
 }
 
 // fp32-accurate FC on split fp16: y = act(acc_scale * x @ w.T + bias)
@@ -979,11 +972,6 @@ torch::Tensor conv2d_pack3_split(torch::Tensor x3, torch::Tensor w, torch::Tenso
   return y;
 }
 
-static int g_wino_ablate_host = 0;
-static void set_wino_ablation_host(int64_t mode) {
-  g_wino_ablate_host = (int)mode;
-  set_wino_ablation((int)mode);
-}
 
 // fp32 Winograd F(2x2,3x3) conv (3x3 / stride 1 / pad 1): x [B,H,W,C] f32 NHWC,
 // u [16, Cout, C] f32 (= G g G^T, models/packed.py wino_weight), y = act(conv + bias (+ res)).
@@ -1028,7 +1016,7 @@ torch::Tensor conv2d_wino_f32(torch::Tensor x, torch::Tensor u, torch::Tensor bi
   a.zero = zero_buffer(x.device()).data_ptr();
   a.B = B; a.H = H; a.W = W; a.C = C; a.Cout = Cout;
   a.relu = relu ? 1 : 0;
-  a.ablate = g_wino_ablate_host;
+  a.ablate = 0;
   TORCH_CHECK(conv_wino_f32_launch(a, (int)variant, cur_stream()), "winograd conv launch rejected the shape");
   check_launch("conv_wino_f32");
   return y;
@@ -1476,13 +1464,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_dual_split_ok", &conv1x1_dual_split_ok, "whether conv1x1_dual_split supports (K1, K2, Cout, M)");
   m.def("conv2d_nhwc", &conv2d_nhwc, "implicit-GEMM MFMA conv + bias (+res) (+relu)", py::arg("x"), py::arg("w"),
         py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
-        py::arg("relu"), py::arg("out_f32") = false, py::arg("tile") = -1, py::arg("out") = py::none());
+        py::arg("relu"), py::arg("out_f32") = false, py::arg("tile") = -1, py::arg("out") = py::none(),
+        py::arg("ksplit") = -1, py::arg("route") = 0);
   m.def("linear_splitk", &linear_splitk, "FC layer with split-K partial GEMMs + combine", py::arg("x"),
         py::arg("w"), py::arg("bias"), py::arg("relu"), py::arg("out_f32"), py::arg("splits"), py::arg("tile") = -1);
   m.def("conv2d_split", &conv2d_split, "split-fp16 (fp32-accurate) conv: 3 f16 MFMAs per 32 channels",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("acc_scale"), py::arg("out_f32") = false, py::arg("tile") = -1,
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("ksplit") = -1, py::arg("route") = 0);
   m.def("conv2d_split_dual", &conv2d_split_dual,
         "two split convs of one input in one launch (downsample as the centre tap of the 3x3/s conv)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
@@ -1508,48 +1497,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res") = py::none(), py::arg("relu") = true,
         py::arg("acc_scale") = 1.0, py::arg("out_f32") = false, py::arg("max_grid") = 0, py::arg("flags") = 0);
   m.def("conv3x3_band_tiles", &conv3x3_band_tiles, "band conv tile count for (B, W, Cout)");
-  m.def("set_split_band_default", &set_split_band_default,
-        "A/B: auto-route split 3x3/s1 convs of ResNet layers 2-4 to the band-staged kernel (tile 70)");
-  m.def("set_split_c64_default", &set_split_c64_default,
-        "A/B: route split 3x3 64->64 convs to the row-streaming kernel (tile 50; default on)");
-  m.def("set_split_norder", &set_split_norder, "A/B: split conv tile order (0 m-major, 1 n-major, -1 auto)");
-  m.def("set_stem_split_rp2", [](int64_t n) { set_stem_split_rp2((int)n); }, "A/B: split stem conv rows per pass (0/1: one, 2 default, 3)");
-  m.def("set_stem_split_reg", [](int64_t n) { set_stem_split_reg((int)n); }, "A/B: register-pooled split stem, 3 / 4 workgroups per CU (0 off)");
-  m.def("set_stem_split_niw", [](int64_t n) { set_stem_split_niw((int)n); },
-        "A/B: fused split stem, 16-cout A fragments per wave (1 default: 3 workgroups/CU; 2)");
-  m.def("set_split_wide_tile", &set_split_wide_tile, "A/B: 128x160 split tiles for M < 50000 (layer4; default on)");
-  m.def("set_conv1x1_stream", &set_conv1x1_stream,
-        "A/B: persistent streaming kernel (tile 80) as the default for eligible fp16 1x1/s1 convs");
-  m.def("set_conv1x1_stream_mask", &set_conv1x1_stream_mask,
-        "A/B: shapes that take the streaming 1x1 kernel by default (1 Cin<=128, 2 Cin 256, 4 Cin 512, 8 stride 2)");
-  m.def("set_conv1x1_stream_lio", &set_conv1x1_stream_lio, "A/B: streaming 1x1 residual / output through per-wave LDS tiles");
-  m.def("set_conv1x1_stream_lio_n2", &set_conv1x1_stream_lio_n2, "A/B: LDS-staged I/O also for the fused-next 1x1 kernels");
-  m.def("set_conv1x1_stream_wgs", [](int64_t n) { set_conv1x1_stream_wgs((int)n); }, "A/B: streaming 1x1 resident workgroups per CU (0 default)");
-  m.def("set_conv1x1_stream_split_mask", &set_conv1x1_stream_split_mask,
-        "A/B: split-path shapes that take the streaming 1x1 kernel by default (bits as set_conv1x1_stream_mask)");
-  m.def("set_conv1x1_split_wide", &set_conv1x1_split_wide, "A/B: 64 couts per wave for split Cin 64 / 128 1x1 convs");
-  m.def("set_c64_split_variant", &set_c64_split_variant,
-        "layer1 split 3x3 64->64 kernel: 0 = 16 couts per wave (2 workgroups/CU), 2 / 3 = 32 couts per wave");
-  m.def("c64_split_variant", &c64_split_variant, "current layer1 split kernel variant");
-  m.def("set_split_wide_l3", &set_split_wide_l3, "A/B: 128x160 split tiles also for 50000 <= M < 100000 (layer3)");
-  m.def("set_f16_wide_tile", &set_f16_wide_tile, "A/B: fp16 128x160 tiles for M < 50000 (layer4)");
-  m.def("set_f16_wide_all", &set_f16_wide_all, "A/B: fp16 128x160 tiles at every M (128-multiple Cout)");
-  m.def("set_conv_l2_prefetch", [](int64_t m) { set_conv_l2_prefetch((int)m); }, "A/B: conv_glds input-footprint L2 prefetch (bit 0 fp16, bit 1 split)");
-  m.def("set_split_wide_all", &set_split_wide_all, "A/B: split 128x160 tiles at every M (128-multiple Cout)");
-  m.def("set_split_mf32", &set_split_mf32, "A/B: split tiles on 32x32x16 MFMAs (bit 0: M >= 50000 -> 56, bit 1: M < 50000 -> 58)");
-  m.def("split_mf32", &split_mf32);
-  m.def("set_split_deepb", &set_split_deepb, "A/B: split M >= 50000 tile 36 -> 60 (pixel ring of 3 slots)");
-  m.def("split_deepb", &split_deepb);
-  m.def("set_split_ksplit", &set_split_ksplit, "split convs at small M: 0 off, -1 auto, k > 1 force k K-slices");
-  m.def("split_ksplit", &split_ksplit);
-  m.def("set_ksplit_cap4", &set_ksplit_cap4, "A/B: the auto split-K rule uses at most 4 K slices (default 8)");
-  m.def("set_f16_ksplit", &set_f16_ksplit, "fp16 convs at small M: 0 off, -1 auto, k > 1 force k K-slices");
-  m.def("f16_ksplit", &f16_ksplit);
-  m.def("conv_split_ksplit_for", [](int64_t M, int64_t Cout, int64_t nk) {
-    return conv_split_ksplit((int)M, (int)Cout, conv_glds_split_pick((int)M, (int)Cout), (int)nk);
-  }, "K slices the auto pick gives a split conv of M pixels x Cout with nk K stages");
-  m.def("set_f16_deepb", &set_f16_deepb, "A/B: fp16 M >= 50000 -> tile 61 (pixel ring of 3 slots)");
-  m.def("set_f16_mf32", &set_f16_mf32, "A/B: fp16 tiles on 32x32x16 MFMAs (bit 0: M >= 50000 -> 90 (92 with bit 2), bit 1: M < 50000 -> 92)");
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");
   m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),
@@ -1569,11 +1516,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("f16") = false);
   m.def("conv2d_wino_f32", &conv2d_wino_f32, "fp32 Winograd F(2x2,3x3) conv (3x3/s1/p1) + bias (+res) (+relu)",
         py::arg("x"), py::arg("u"), py::arg("bias"), py::arg("res"), py::arg("relu"), py::arg("variant") = 0);
-  m.def("set_wino_ablation", &set_wino_ablation_host,
-        "profiling only: winograd conv ablation (1 no DMA, 2 no raw/transform, 4 no U reads, 8 no stores)");
-  m.def("set_wino_pairing", &set_wino_pairing, "A/B: winograd e-GEMMs in pairs or one at a time (default)");
-  m.def("set_wino_linear", &set_wino_linear, "A/B: variant-3 consecutive-tile (LIN) blocking (default on)");
-  m.def("set_wino_rotation", &set_wino_rotation, "A/B: variant-3 rotated raw rows (default off)");
   m.def("wino_supported", &conv_wino_f32_supported, "winograd conv geometry fits (H, W, C, Cout)");
   m.def("pick_tile_f32", &pick_tile_f32, "tile id the f32 conv heuristic picks for (M, Cout, K, small)");
   m.def("preprocess", &preprocess, "uint8 HWC -> normalised fp16 (or fp32) NHWC4", py::arg("img"),
@@ -1594,12 +1536,4 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("synth_images", &synth_images, "deterministic synthetic uint8 images [n,hw,hw,3]");
   m.def("graph_launch", &graph_launch, "hipGraphLaunch(exec, current stream): a replay without any host wait");
   m.def("pick_tile", &pick_tile, "tile id the conv heuristic picks for (M, Cout)");
-  m.def("set_stem_workgroups_per_cu", &set_stem_workgroups_per_cu,
-        "fused stem: persistent workgroups per CU (1-3, default 3)");
-  m.def("set_conv_ablation", &set_conv_ablation,
-        "profiling only: conv_glds epilogue ablation (1 skip stores, 2 skip residual loads); outputs are wrong");
-  m.def("set_stem_ablation", &set_stem_ablation,
-        "profiling only: 1 skip pool, 2 skip conv MFMAs, 4 skip patch normalise (wrong outputs)");
-  m.def("set_conv3x3_c64_default", &set_conv3x3_c64_default,
-        "route auto-tiled 3x3/s1 64->64 convs to the resident-weight kernel (tile 50)");
 }

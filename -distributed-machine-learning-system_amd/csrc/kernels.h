@@ -24,14 +24,12 @@ struct ConvArgs {
   int tiles_m;  // ceil(M / BM)
   const void* zero;  // >= 16 zero bytes (DMA source for padding taps)
   int ldx;           // conv_glds: input pixel stride in halfs (0: C); a K-slice of a wider row
-  int ablate;        // profiling only (set_conv_ablation), conv_glds: 1 skip epilogue stores, 2 skip residual loads
   int nc, wp, cpk;   // conv_glds pack3 (RGB stems on packed rows, preprocess_pack3_f16): row copies,
                      // halfs per copy row, 16-byte chunks per kernel row (ceil(3*KW/8)); cpk = 0: off
   int ksplit;        // conv_glds split-K in ONE launch (FC layers, fp32 partials): block s / tiles takes
   int kslice;        // K slice s: x and w advance by s*kslice halfs, y by s*ysplit floats; 0/1: off
   long ysplit;
   float acc_scale;   // conv_glds SPLIT: accumulator multiplier (2^-e of the pre-scaled split weights)
-  int norder;        // conv_glds: 1 = n-major tile order (tn = lid / tiles_m), 0 = m-major
   int* ovf;          // conv_glds SPLIT: split range guard flag (common.h split_guard) or nullptr
   // conv_glds SPLIT dual conv (two convs of one input in one launch, outputs side
   // by side in y): output channels >= nsplit_n are the second conv -- its own
@@ -42,7 +40,6 @@ struct ConvArgs {
   int center_only;
   float acc_scale2;
   int ldr;           // residual pixel stride in halfs (0: the output width, 2*Cout split / Cout fp16)
-  int l2pf;          // conv_glds: prefetch the tile's input footprint into L2 at block start (set by the launchers)
   int kstage;        // conv split-K (small M): block s / tiles runs K stages [s*kstage, (s+1)*kstage) of the
                      // (kh, kw, cblk) loop into fp32 partials y + s*ysplit (kslice 0); 0: off
 };
@@ -102,10 +99,6 @@ struct WinoArgs {
   int ablate;          // profiling only (set_wino_ablation): 1 no DMA, 2 no raw read/transform,
                        // 4 no U reads, 8 no epilogue stores -- outputs are wrong
 };
-void set_wino_ablation(int mode);
-void set_wino_pairing(bool on);
-void set_wino_linear(bool on);
-void set_wino_rotation(bool on);
 bool conv_wino_f32_launch(WinoArgs a, int variant, hipStream_t st);   // false: shape unsupported
 bool conv_wino_f32_supported(int H, int W, int C, int Cout);
 int conv_f32_pick(int M, int Cout, int K, bool small);
@@ -141,35 +134,17 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 // ([hi x32][lo x32] per 32 channels), y fp32 with out_f32
 bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 int conv_glds_split_pick(int M, int Cout);
-void set_f16_wide_tile(bool on);     // A/B: fp16 128x160 tiles for M < 50000 (default on)
-void set_f16_wide_all(bool on);      // A/B: ... at every M
-void set_split_wide_tile(bool on);   // A/B: 128x160 tiles for small-M split convs (default on)
-void set_split_wide_l3(bool on);     // A/B: ... also for 50000 <= M < 100000 (layer3)
-void set_split_wide_all(bool on);    // A/B: ... at every M
-void set_split_mf32(int mode);       // split tiles on 32x32x16 MFMAs: bit 0 M >= 50000 (56), bit 1 M < 50000 (58)
-int split_mf32();
-void set_split_deepb(bool on);       // split tile 36 -> 60 (3-slot pixel ring, 80 KiB)
-void set_split_ksplit(int mode);     // split convs, small M: 0 off, -1 auto (fill the chip), k > 1 force k slices
-int split_ksplit();
-void set_ksplit_cap4(bool on);       // A/B: the auto split-K rule stops at 4 slices instead of 8
-int conv_split_ksplit(int M, int Cout, int tile, int nk_total);   // K slices for a split conv (1: none)
+// K slices for a conv (1: none): force < 0 auto (the default tile), 0 / 1 off, k > 1 k slices (split-K tiles 27 / 36 / 42)
+int conv_split_ksplit(int M, int Cout, int tile, int nk_total, int force);
 // fmt: 0 split residual/output, 1 split residual + fp32 output, 2 fp16 residual/output, 3 fp16 residual + fp32 output
 void splitk_reduce_res_launch(const float* part, int S, long MN, int N, const float* bias, const half_t* res,
                               int ldr, int relu, void* y, int ldy, int fmt, int* ovf, hipStream_t st);
-void set_f16_ksplit(int mode);       // fp16 convs at small M: 0 off, -1 auto, k > 1 force
-int f16_ksplit();
-int conv_f16_ksplit(int M, int Cout, int tile, int nk_total);
-void set_f16_deepb(bool on);         // fp16 M >= 50000, Cout % 128 == 0 -> tile 61 (3-slot pixel ring)
-bool split_deepb();
-void set_f16_mf32(int mode);        // fp16 tiles on 32x32x16 MFMAs: bit 0 M >= 50000 (90, or 92 with bit 2), bit 1 M < 50000 (92)
-void set_conv_l2_prefetch(int mode);  // A/B: conv_glds input-footprint L2 prefetch (bit 0 fp16, bit 1 split)
+int conv_f16_ksplit(int M, int Cout, int tile, int nk_total, int force);
 // persistent streaming 1x1 fp16 conv, stride 1 or 2 (conv1x1_stream.hip): shapes in conv1x1_stream_supported
 bool conv1x1_stream_supported(int C, int Cout, long M);
 bool conv1x1_stream_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
                            const void* zero, int M, int C, int Cout, int relu, int H, int W, int Wo, int HWo,
                            int stride, hipStream_t st);
-void set_conv1x1_stream(bool on);   // default choice for eligible fp16 1x1 convs (A/B)
-void set_conv1x1_stream_mask(int mask);  // default shapes: 1 Cin<=128, 2 Cin 256, 4 Cin 512, 8 stride 2
 bool conv1x1_stream_default(int C, int stride, long M);
 bool conv1x1_stream_split_supported(int C, int Cout, long M);    // split fp16 (fp32-accurate) 1x1 convs
 bool conv1x1_stream_split_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
@@ -188,14 +163,7 @@ bool conv1x1_fused_next_launch(const half_t* x1, const half_t* x2, const half_t*
                                const half_t* res, half_t* y, const half_t* w2, const float* b2, half_t* z,
                                const void* zero, int M, int K1, int K2, int N, int N2, int relu, int H, int W, int Wo,
                                int HWo, int stride, hipStream_t st);
-void set_conv1x1_stream_split_mask(int mask);
-void set_conv1x1_split_wide(bool on);   // A/B: 64 couts per wave for split Cin 64 / 128, Cout % 256 == 0   // default shapes of the split path (bits as the fp16 mask)
 bool conv1x1_stream_split_default(int C, int stride);
-void set_conv1x1_stream_wgs(int n);   // A/B: resident workgroups per CU (0: two waves per SIMD)
-void set_conv1x1_stream_lio(bool on);  // A/B: residual / output through per-wave LDS tiles
-void set_conv1x1_stream_lio_n2(bool on);  // A/B: ... also for the fused-next kernels
-void set_c64_split_variant(int v);  // layer1 split kernel: 0 = 16 couts/wave, 2/3 = 32 couts/wave (read ring depth)
-int c64_split_variant();
 // split 3x3/s1/p1 64 -> 64 conv, weights in registers, input rows streamed through an LDS ring
 bool conv3x3_split_c64_supported(int H, int W, int C, int Cout);
 void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
@@ -212,17 +180,12 @@ bool conv3x3_band_launch(const half_t* x, int ldx, const half_t* w, const float*
 // split-fp16 RGB stem on packed rows (a.cpk > 0, x from preprocess_pack3_split): fp32 output
 bool conv_glds_split_p3_launch(ConvArgs a, int tile, hipStream_t st);   // a.cpk > 0: pack3 stem
 bool conv3x3_c64_supported(int C, int Cout);
-void set_stem_ablation(int mode);
-void set_stem_workgroups_per_cu(int n);
 void conv3x3_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
                         const void* zero, int B, int H, int W, int relu, hipStream_t st);
 int conv_glds_pick(int M, int Cout);
 // split-fp16 (fp32-accurate) fused stem, exact-u8 form: w = [2][64][7*32] hi/lo of
 // w * s_c (pre-scaled by 1/acc_scale), bias = folded bias + full sum of w * c_c,
 // psum = [8][8][64] 2D prefix sums of w * c_c over (kh, kw); y = split [B][Hp][Wp][128]
-void set_stem_split_niw(int n);   // A/B: 16-cout fragments per wave (1 default, 2)
-void set_stem_split_rp2(int rows); // A/B: conv rows per pass (0/1: one, 2 default, 3; interleaved MFMA chains)
-void set_stem_split_reg(int wgs);   // A/B: register-pooled split stem, 3 / 4 workgroups per CU (0 off)
 void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
                        half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,
                        long long max_start, long long sub, int* ovf, hipStream_t st);

@@ -596,17 +596,11 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   c1_vmcnt<0>();
 }
 
-// resident workgroups per CU of the streaming 1x1 kernels (A/B knob; default
-// 8 / NW = two waves per SIMD; more only where registers and LDS allow)
-static int g_c1s_wgs = 0;
-void set_conv1x1_stream_wgs(int n) { g_c1s_wgs = n; }
-// residual / output through per-wave LDS tiles (the LIO kernels): ResNet50 b1024
-// fp16 +4.2 %, split +5.7 %, ResNet18 split +0.2 % (profiles/r3_ab_lio.md)
-static bool g_c1s_lio = true;
-void set_conv1x1_stream_lio(bool on) { g_c1s_lio = on; }
-static bool g_c1s_lio_n2 = true;       // ... also for the fused-next (N2) kernels: ResNet50 fp16 +3.5 %
-void set_conv1x1_stream_lio_n2(bool on) { g_c1s_lio_n2 = on; }
-
+// Residual / output through per-wave LDS tiles (the LIO kernels) wherever the
+// shape allows: ResNet50 b1024 fp16 +4.2 %, split +5.7 %, ResNet18 split +0.2 %,
+// fused-next (N2) kernels ResNet50 fp16 +3.5 % (profiles/r3_ab_lio.md).  Two
+// waves per SIMD (more resident workgroups measured no gain for fp16, +1 % split:
+// not kept).
 template <int K, int NW, int BM, int CW, bool R, bool SPLIT = false, int K1 = 0, int N2 = 0, bool LIO = false>
 static void c1s_cfg(C1sArgs a, hipStream_t st) {
   constexpr int RT = BM * CW * 2 * (SPLIT ? 2 : 1), CPRW = RT / BM / 16;
@@ -616,10 +610,8 @@ static void c1s_cfg(C1sArgs a, hipStream_t st) {
   // (not K = 512: those tails are not addresser-bound, and the LDS round trip
   // spilled and cost 3-15 %: 258 -> 295 us, profiles/r3_resnet50_b1024_fp16_kernels_v2.md)
   if constexpr (!LIO && K != 512 && N2OK && RT % 1024 == 0 && (!SPLIT || CW % 32 == 0) && (CPRW & (CPRW - 1)) == 0) {
-    if (g_c1s_lio && (N2 == 0 || g_c1s_lio_n2)) {
-      c1s_cfg<K, NW, BM, CW, R, SPLIT, K1, N2, true>(a, st);
-      return;
-    }
+    c1s_cfg<K, NW, BM, CW, R, SPLIT, K1, N2, true>(a, st);
+    return;
   }
   a.nslab = a.N / (NW * CW);
   constexpr int TILE = (SPLIT ? 2 : 1) * (K / 64) * BM * 128;
@@ -627,14 +619,7 @@ static void c1s_cfg(C1sArgs a, hipStream_t st) {
   a.ntiles = (a.M + BM - 1) / BM;
   auto kern = conv1x1_stream_kernel<K, NW, BM, CW, R, SPLIT, K1, N2, LIO>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), LDSB);
-  int per_cu = 8 / NW;                              // two waves per SIMD
-  if (g_c1s_wgs > per_cu) {
-    // more resident workgroups (more loads in flight), as many as registers and LDS allow
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kern), 64 * NW, LDSB) ==
-            hipSuccess && occ > per_cu)
-      per_cu = occ < g_c1s_wgs ? occ : g_c1s_wgs;
-  }
+  const int per_cu = 8 / NW;                        // two waves per SIMD
   int G = per_cu * device_cu_count();
   G -= G % a.nslab;
   const long items = (long)a.ntiles * a.nslab;
@@ -651,22 +636,14 @@ bool conv1x1_stream_supported(int C, int Cout, long M) {
   return shape && M > 0 && M * Cout * 2 < (1L << 31);
 }
 
-// default on: ResNet50 b1024 fp16 whole forward 19.21 -> 17.80 ms (+7.9 %),
-// profiles/r3_conv1x1_stream.md
-static bool g_c1s_default = true;
-// which eligible shapes take it by default: bit 0 Cin <= 128, bit 1 Cin 256
-// (+3.7 % whole forward on top of bit 0), bit 2 Cin 512 (+1.7 %), bit 3 stride 2
-// (+1.0 %): profiles/r3_conv1x1_stream.md
-static int g_c1s_mask = 15;
-void set_conv1x1_stream(bool on) { g_c1s_default = on; }
-void set_conv1x1_stream_mask(int mask) { g_c1s_mask = mask; }
+// Default for every eligible fp16 shape: ResNet50 b1024 fp16 whole forward 19.21 ->
+// 17.80 ms (+7.9 %; Cin 256 +3.7 %, Cin 512 +1.7 %, stride 2 +1.0 % on top),
+// profiles/r3_conv1x1_stream.md -- except fp16 stride 2 below ~100k output pixels
+// (ResNet18's downsamples at B = 400: -0.4 % whole forward), which stay on the
+// implicit-GEMM tiles.
 bool conv1x1_stream_default(int C, int stride, long M) {
-  if (!g_c1s_default || (stride != 1 && !(g_c1s_mask & 8))) return false;
-  // fp16 stride 2 below ~100k output pixels (ResNet18's downsamples at B = 400):
-  // -0.4 % whole forward, so those stay on the implicit-GEMM tiles
-  if (stride != 1 && M < 100000) return false;
-  const int bit = C <= 128 ? 1 : C == 256 ? 2 : C == 512 ? 4 : 0;
-  return (g_c1s_mask & bit) != 0;
+  (void)C;
+  return stride == 1 || M >= 100000;
 }
 
 bool conv1x1_stream_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
@@ -714,17 +691,13 @@ bool conv1x1_stream_split_supported(int C, int Cout, long M) {
   return shape && M > 0 && (M + 64) * Cout * 4 < (1L << 32);
 }
 
-// default shapes of the split path: bit 0 Cin <= 128, bit 1 Cin 256, bit 2 Cin 512, bit 3 stride 2
-// (all on: ResNet50 b1024 split +9.4 %, ResNet18 b400 split +0.5 %, profiles/r3_conv1x1_stream.md)
-static int g_c1s_split_mask = 15;
-// on: ResNet50 b1024 split +2.5 % (profiles/r3_conv1x1_stream_ab_split.log)
-static bool g_c1s_split_wide = true;
-void set_conv1x1_split_wide(bool on) { g_c1s_split_wide = on; }
-void set_conv1x1_stream_split_mask(int mask) { g_c1s_split_mask = mask; }
+// Default for every eligible split shape (ResNet50 b1024 split +9.4 %, ResNet18 b400
+// split +0.5 %, profiles/r3_conv1x1_stream.md); Cin 64 / 128 with Cout % 256 == 0 use
+// 64 couts per wave (ResNet50 b1024 split +2.5 %, profiles/r3_conv1x1_stream_ab_split.log).
 bool conv1x1_stream_split_default(int C, int stride) {
-  if (stride != 1 && !(g_c1s_split_mask & 8)) return false;
-  const int bit = C <= 128 ? 1 : C == 256 ? 2 : C == 512 ? 4 : 0;
-  return (g_c1s_split_mask & bit) != 0;
+  (void)C;
+  (void)stride;
+  return true;
 }
 
 bool conv1x1_stream_split_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
@@ -752,7 +725,7 @@ bool conv1x1_stream_split_launch(const half_t* x, const half_t* w, const float* 
   const bool narrow = C == 512 || Cout == 64;
   // wide: 64 couts per wave (256-channel slabs: 4x the bytes per item, the input
   // tile read once per 256 outputs) for Cin 64 / 128
-  const bool wide = g_c1s_split_wide && Cout % 256 == 0;
+  const bool wide = Cout % 256 == 0;
   switch (C) {
     case 64:
       if (narrow) r ? c1s_cfg<64, 4, 32, 16, true, true>(a, st) : c1s_cfg<64, 4, 32, 16, false, true>(a, st);
@@ -832,7 +805,7 @@ bool conv1x1_dual_split_launch(const half_t* x1, const half_t* x2, const half_t*
   a.stride = stride;
   a.acc_scale = acc_scale;
   a.ovf = ovf;
-  if (K1 == 64 && g_c1s_split_wide && Cout % 256 == 0) c1s_cfg<128, 4, 16, 64, false, true, 64>(a, st);
+  if (K1 == 64 && Cout % 256 == 0) c1s_cfg<128, 4, 16, 64, false, true, 64>(a, st);
   else if (K1 == 64) c1s_cfg<128, 4, 32, 32, false, true, 64>(a, st);
   else c1s_cfg<384, 4, 16, 16, false, true, 128>(a, st);
   return true;

@@ -241,386 +241,6 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// lgkmcnt wait for "at most 4n LDS reads of this wave in flight" (n = groups
-// still in flight behind the current one; a constant after unrolling)
-template <int D>
-__device__ __forceinline__ void c64w_wait_groups(int n) {
-  if (D >= 4 && n >= 3) { lds_waitcnt<12>(); return; }
-  if (D >= 3 && n >= 2) { lds_waitcnt<8>(); return; }
-  if (n >= 1) { lds_waitcnt<4>(); return; }
-  lds_waitcnt<0>();
-}
-
-// 32-couts-per-wave variant ("W32").  The kernel above gives every wave 16
-// couts x all 4 pixel fragments of a row: each B fragment read (hi or lo)
-// feeds 1.5 MFMAs, and with two waves per SIMD the ds_read / waitcnt /
-// address issue of a 3-MFMA group nearly fills the 48 cycles those MFMAs
-// leave (mfma_busy 0.46-0.53, profiles/r2_v32_pmc_split_forward.md).  Here a
-// wave owns 32 couts (cout group cg = wave & 1) x 2 pixel fragments (pixel
-// half ph = wave >> 1) of the row: per (tap, channel block) it reads the hi
-// and lo B fragments of its 2 pixel fragments (4 ds_read_b128) and issues 12
-// MFMAs, 3 per read.  The 2 x 9 x 2 x (hi, lo) A fragments take 288 of the
-// 512 registers a lone wave per SIMD may use (one 4-wave workgroup per CU);
-// the MFMAs read them straight from AGPRs.  Same LDS row ring, DMA, slot
-// swizzle, task loop and epilogue stores (NST per wave and row) as above.
-template <bool HAS_RES, int D>
-__global__ void __launch_bounds__(256, 1) conv3x3_split_c64w_kernel(const C64sArgs a) {
-  using namespace c64s;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cg = wave & 1, ph = wave >> 1;
-  const int frow = lane & 15, q = lane >> 4;
-  if ((int)blockIdx.x >= a.ntasks) return;   // uniform
-
-  // ---- A fragments of this wave's 32 couts: [cout frag][tap][block][hi|lo] ----
-  half8v fa[2][9][2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const half_t* wr = a.w + (size_t)(cg * 32 + i * 16 + frow) * (9 * PIX) + q * 8;
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) fa[i][t][cb][p] = *reinterpret_cast<const half8v*>(wr + t * PIX + cb * 64 + p * 32);
-  }
-  int n0[2];
-  float4v bv[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    n0[i] = cg * 32 + i * 16 + 4 * q;            // this lane's 4 output channels of cout fragment i
-    bv[i] = *reinterpret_cast<const float4v*>(a.bias + n0[i]);
-  }
-  const uint32_t ring = lds_addr(smem);
-  // as above, plus this wave's pixel half: fragments 2*ph, 2*ph+1 start 8192*ph
-  // bytes into the row (bits 13+, untouched by the (2cb+p) << 6 XOR)
-  uint32_t loff[3];
-#pragma unroll
-  for (int kw = 0; kw < 3; ++kw) {
-    const int col = frow + kw, x = (2 * col) & 15;
-    loff[kw] = (uint32_t)(col * 256 + (((x >> 2) & 3) << 6) + (((q ^ x) & 3) << 4) + 8192 * ph);
-  }
-
-  for (int task = blockIdx.x; task < a.ntasks; task += gridDim.x) {
-    const int b = task / a.nbands;
-    const int y0 = (task - b * a.nbands) * a.band;
-    const int y1 = min(y0 + a.band, a.H);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();              // previous item's ring reads are done
-    c64s_load_row(a, smem, b, y0 - 1, (y0 + 3) & 3, tid);
-    c64s_load_row(a, smem, b, y0, y0 & 3, tid);
-    c64s_load_row(a, smem, b, y0 + 1, (y0 + 1) & 3, tid);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (int y = y0; y < y1; ++y) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
-      __builtin_amdgcn_s_barrier();
-      if (y + 2 <= y1) c64s_load_row(a, smem, b, y + 2, (y + 2) & 3, tid);
-      const size_t rowpix = ((size_t)b * a.H + y) * a.W;
-      half4v rh[HAS_RES ? 2 : 1][HAS_RES ? 2 : 1], rl[HAS_RES ? 2 : 1][HAS_RES ? 2 : 1];
-      if constexpr (HAS_RES) {
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          const int ox = min(16 * (2 * ph + f) + frow, a.W - 1);
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const size_t off = (rowpix + ox) * PIX + split_off(n0[i]);
-            rh[f][i] = gload_b64_untracked(a.res + off);
-            rl[f][i] = gload_b64_untracked(a.res + off + 32);
-          }
-        }
-      }
-      float4v acc[2][2];
-#pragma unroll
-      for (int f = 0; f < 2; ++f)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) acc[f][i] = float4v{0.f, 0.f, 0.f, 0.f};
-      // 18 groups g = (tap t, block cb): 4 B reads ((hi, lo) x 2 pixel
-      // fragments), 12 MFMAs; a D-deep register ring of read groups
-      half8v bf[D][2][2];
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) asm volatile("" : "+v"(loff[kw]));
-      uint32_t rowb[3];
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) rowb[kh] = ring + (uint32_t)(((y - 1 + kh) & 3) * RB);
-      auto issue = [&](int g, int buf) {
-        const int t = g >> 1, cb = g & 1;
-        const int kh = t / 3, kw = t - 3 * kh;
-#pragma unroll
-        for (int f = 0; f < 2; ++f)
-#pragma unroll
-          for (int p = 0; p < 2; ++p)
-            bf[buf][f][p] = lds_read_frag(rowb[kh] + (loff[kw] ^ (uint32_t)((2 * cb + p) << 6)), f);
-      };
-#pragma unroll
-      for (int p = 0; p < D - 1; ++p) issue(p, p);
-#pragma unroll
-      for (int g = 0; g < 18; ++g) {
-        const int buf = g % D;
-        if (g + D - 1 < 18) issue(g + D - 1, (g + D - 1) % D);
-        c64w_wait_groups<D>(min(D - 1, 17 - g));
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          lds_tie(bf[buf][f][0]);
-          lds_tie(bf[buf][f][1]);
-        }
-        const int t = g >> 1, cb = g & 1;
-        // hi*hi of all four accumulators first, then the cross terms: no
-        // accumulator is written by two MFMAs in a row
-#pragma unroll
-        for (int f = 0; f < 2; ++f)
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-            acc[f][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][t][cb][0], bf[buf][f][0], acc[f][i], 0, 0, 0);
-#pragma unroll
-        for (int f = 0; f < 2; ++f)
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-            acc[f][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][t][cb][0], bf[buf][f][1], acc[f][i], 0, 0, 0);
-#pragma unroll
-        for (int f = 0; f < 2; ++f)
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-            acc[f][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][t][cb][1], bf[buf][f][0], acc[f][i], 0, 0, 0);
-      }
-      // ---- epilogue: scale, bias (+ residual), ReLU, split store ----
-      if constexpr (HAS_RES) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int f = 0; f < 2; ++f)
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            reg_tie(rh[f][i]);
-            reg_tie(rl[f][i]);
-          }
-      }
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        const int ox = 16 * (2 * ph + f) + frow;
-        if (ox >= a.W) continue;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const size_t off = (rowpix + ox) * PIX + split_off(n0[i]);
-          float4v v = acc[f][i] * a.acc_scale + bv[i];
-          if constexpr (HAS_RES) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += (float)rh[f][i][e] + (float)rl[f][i][e];
-          }
-          if (a.relu) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-          }
-          split_guard(a.ovf, v);
-          half4v h, l;
-          split_f16x4(v, h, l);
-          *reinterpret_cast<half4v*>(a.y + off) = h;
-          *reinterpret_cast<half4v*>(a.y + off + 32) = l;
-        }
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// lgkmcnt wait for "at most 2n LDS reads in flight" (n groups of 2 reads)
-template <int D>
-__device__ __forceinline__ void c64k_wait_groups(int n) {
-  if (D >= 4 && n >= 3) { lds_waitcnt<6>(); return; }
-  if (D >= 3 && n >= 2) { lds_waitcnt<4>(); return; }
-  if (n >= 1) { lds_waitcnt<2>(); return; }
-  lds_waitcnt<0>();
-}
-
-// K-split pairs variant ("KS"): 32 couts per wave at 2 waves per SIMD.  The
-// W32 kernel above holds all 64 input channels' A fragments (288 registers)
-// and runs one wave per SIMD with the compiler shuttling A between AGPRs and
-// VGPRs (-2.3 % whole graph).  Here wave w owns cout group cg = w & 1 (32
-// couts) and input-channel block cb = w >> 1 (32 channels): 2 x 9 x (hi, lo) A
-// fragments = 144 VGPRs, and each of its B reads ((hi, lo) of one pixel
-// fragment, only its channel block) feeds 6 MFMAs' worth of 3-term products
-// over 2 cout fragments -- 3 MFMAs per read, as W32, half the reads per MFMA
-// of the 16-cout kernel.  The two waves of a cout group hold partial sums of
-// the same 32 couts x 64 pixels; after the row's MFMAs they exchange halves
-// through the ring slot of row y-1 (read by this row's kh = 0 taps, not
-// rewritten before the next row's DMA): wave cb finalises pixel fragments
-// 2cb, 2cb+1.  Two workgroups per CU as in the 16-cout kernel.
-template <bool HAS_RES, int D>
-__global__ void __launch_bounds__(256, 2) conv3x3_split_c64k_kernel(const C64sArgs a) {
-  using namespace c64s;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cg = wave & 1, cb = wave >> 1;
-  const int frow = lane & 15, q = lane >> 4;
-  if ((int)blockIdx.x >= a.ntasks) return;   // uniform
-
-  // ---- A fragments: [cout frag][tap][hi|lo] of channel block cb ----
-  half8v fa[2][9][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const half_t* wr = a.w + (size_t)(cg * 32 + i * 16 + frow) * (9 * PIX) + cb * 64 + q * 8;
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) fa[i][t][p] = *reinterpret_cast<const half8v*>(wr + t * PIX + p * 32);
-  }
-  int n0[2];
-  float4v bv[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    n0[i] = cg * 32 + i * 16 + 4 * q;
-    bv[i] = *reinterpret_cast<const float4v*>(a.bias + n0[i]);
-  }
-  const uint32_t ring = lds_addr(smem);
-  // LDS offset of column frow + kw, 64-byte group 2*cb (hi) -- lo is group 2*cb+1
-  uint32_t loff[3];
-#pragma unroll
-  for (int kw = 0; kw < 3; ++kw) {
-    const int col = frow + kw, x = (2 * col) & 15;
-    loff[kw] = (uint32_t)(col * 256 + (((x >> 2) & 3) << 6) + (((q ^ x) & 3) << 4)) ^ (uint32_t)((2 * cb) << 6);
-  }
-  // partial-sum exchange: wave w's lane writes float4 slots [(w*2 + f)*2 + i] x 64 lanes
-  // (f = the partner's pixel fragment index 0/1, i = cout fragment): 4 KiB per wave
-  auto xoff = [&](int w, int f, int i) { return (uint32_t)((((w * 2 + f) * 2 + i) * 64 + lane) * 16); };
-
-  for (int task = blockIdx.x; task < a.ntasks; task += gridDim.x) {
-    const int b = task / a.nbands;
-    const int y0 = (task - b * a.nbands) * a.band;
-    const int y1 = min(y0 + a.band, a.H);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    c64s_load_row(a, smem, b, y0 - 1, (y0 + 3) & 3, tid);
-    c64s_load_row(a, smem, b, y0, y0 & 3, tid);
-    c64s_load_row(a, smem, b, y0 + 1, (y0 + 1) & 3, tid);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (int y = y0; y < y1; ++y) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
-      __builtin_amdgcn_s_barrier();
-      if (y + 2 <= y1) c64s_load_row(a, smem, b, y + 2, (y + 2) & 3, tid);
-      const size_t rowpix = ((size_t)b * a.H + y) * a.W;
-      float4v acc[4][2];
-#pragma unroll
-      for (int F = 0; F < 4; ++F)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) acc[F][i] = float4v{0.f, 0.f, 0.f, 0.f};
-      // 36 groups g = (tap t, pixel fragment F): 2 B reads (hi, lo), 6 MFMAs
-      half8v bf[D][2];
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) asm volatile("" : "+v"(loff[kw]));
-      uint32_t rowb[3];
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) rowb[kh] = ring + (uint32_t)(((y - 1 + kh) & 3) * RB);
-      auto issue = [&](int g, int buf) {
-        const int t = g >> 2, F = g & 3;
-        const int kh = t / 3, kw = t - 3 * kh;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) bf[buf][p] = lds_read_frag(rowb[kh] + (loff[kw] ^ (uint32_t)(p << 6)), F);
-      };
-#pragma unroll
-      for (int p = 0; p < D - 1; ++p) issue(p, p);
-#pragma unroll
-      for (int g = 0; g < 36; ++g) {
-        const int buf = g % D;
-        if (g + D - 1 < 36) issue(g + D - 1, (g + D - 1) % D);
-        c64k_wait_groups<D>(min(D - 1, 35 - g));
-        lds_tie(bf[buf][0]);
-        lds_tie(bf[buf][1]);
-        const int t = g >> 2, F = g & 3;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc[F][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][t][0], bf[buf][0], acc[F][i], 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc[F][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][t][0], bf[buf][1], acc[F][i], 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc[F][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][t][1], bf[buf][0], acc[F][i], 0, 0, 0);
-      }
-      // ---- partial-sum exchange through the ring slot of row y-1 ----
-      __builtin_amdgcn_s_barrier();              // every wave's reads of row y-1 are done
-      const uint32_t xb = ring + (uint32_t)(((y - 1) & 3) * RB);
-#pragma unroll
-      for (int f = 0; f < 2; ++f)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)               // the partner's half: pixel fragments 2(1-cb)+f
-          *reinterpret_cast<float4v*>(smem + (xb - ring) + xoff(wave, f, i)) = acc[2 * (1 - cb) + f][i];
-      // residual of this wave's output half (pixel fragments 2cb, 2cb+1): issued
-      // once the partner's partials are out of registers (held across the MFMAs
-      // it spilled at two waves per SIMD); its latency hides behind the exchange
-      half4v rh[HAS_RES ? 2 : 1][HAS_RES ? 2 : 1], rl[HAS_RES ? 2 : 1][HAS_RES ? 2 : 1];
-      if constexpr (HAS_RES) {
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          const int ox = min(16 * (2 * cb + f) + frow, a.W - 1);
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const size_t off = (rowpix + ox) * PIX + split_off(n0[i]);
-            rh[f][i] = gload_b64_untracked(a.res + off);
-            rl[f][i] = gload_b64_untracked(a.res + off + 32);
-          }
-        }
-      }
-      lds_waitcnt<0>();
-      __builtin_amdgcn_s_barrier();
-      float4v part[2][2];
-#pragma unroll
-      for (int f = 0; f < 2; ++f)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          part[f][i] = __builtin_bit_cast(float4v, lds_read_b128(xb + xoff(wave ^ 2, f, i)));
-      lds_waitcnt<0>();
-      // ---- epilogue on pixel fragments 2cb, 2cb+1 ----
-      if constexpr (HAS_RES) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int f = 0; f < 2; ++f)
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            reg_tie(rh[f][i]);
-            reg_tie(rl[f][i]);
-          }
-      }
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        const int ox = 16 * (2 * cb + f) + frow;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          lds_tie(part[f][i]);
-          if (ox >= a.W) continue;
-          const size_t off = (rowpix + ox) * PIX + split_off(n0[i]);
-          float4v v = (acc[2 * cb + f][i] + part[f][i]) * a.acc_scale + bv[i];
-          if constexpr (HAS_RES) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += (float)rh[f][i][e] + (float)rl[f][i][e];
-          }
-          if (a.relu) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-          }
-          split_guard(a.ovf, v);
-          half4v h, l;
-          split_f16x4(v, h, l);
-          *reinterpret_cast<half4v*>(a.y + off) = h;
-          *reinterpret_cast<half4v*>(a.y + off + 32) = l;
-        }
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <int D>
-static void c64k_launch(const C64sArgs& a, bool res, int grid, hipStream_t st) {
-  using namespace c64s;
-  if (res) {
-    ensure_lds_attr(reinterpret_cast<const void*>(conv3x3_split_c64k_kernel<true, D>), LDS);
-    hipLaunchKernelGGL((conv3x3_split_c64k_kernel<true, D>), dim3(grid), dim3(256), LDS, st, a);
-  } else {
-    ensure_lds_attr(reinterpret_cast<const void*>(conv3x3_split_c64k_kernel<false, D>), LDS);
-    hipLaunchKernelGGL((conv3x3_split_c64k_kernel<false, D>), dim3(grid), dim3(256), LDS, st, a);
-  }
-}
-
 // W in [49, 62]: every one of the 4 pixel fragments has a valid column, so
 // each wave issues exactly NST epilogue stores per row (counted vmcnt above)
 template <int D>
@@ -635,25 +255,9 @@ static void c64s_launch(const C64sArgs& a, bool res, int grid, hipStream_t st) {
   }
 }
 
-template <int D>
-static void c64w_launch(const C64sArgs& a, bool res, int grid, hipStream_t st) {
-  using namespace c64s;
-  if (res) {
-    ensure_lds_attr(reinterpret_cast<const void*>(conv3x3_split_c64w_kernel<true, D>), LDS);
-    hipLaunchKernelGGL((conv3x3_split_c64w_kernel<true, D>), dim3(grid), dim3(256), LDS, st, a);
-  } else {
-    ensure_lds_attr(reinterpret_cast<const void*>(conv3x3_split_c64w_kernel<false, D>), LDS);
-    hipLaunchKernelGGL((conv3x3_split_c64w_kernel<false, D>), dim3(grid), dim3(256), LDS, st, a);
-  }
-}
-
-// layer1 split kernel choice: 0 = 16 couts / wave (2 workgroups per CU),
-// 2 / 3 = 32 couts / wave with a 2- / 3-deep read ring (1 workgroup per CU),
-// 4 / 5 = K-split pairs, 32 couts per wave, 3- / 4-deep read ring (2 per CU)
-static int g_c64_split_variant = 0;
-void set_c64_split_variant(int v) { g_c64_split_variant = (v >= 2 && v <= 5) ? v : 0; }
-int c64_split_variant() { return g_c64_split_variant; }
-
+// Measured and dropped (round 3, profiles/r3_c64_split_variants.md, deleted in round 5):
+// 32 couts per wave as one wave per SIMD holding all 64 input channels' A fragments
+// (W32, -2.3 %) or as K-split wave pairs exchanging partial sums through LDS (-2.7 %).
 bool conv3x3_split_c64_supported(int H, int W, int C, int Cout) {
   return C == 64 && Cout == 64 && W >= 49 && W <= 62 && H >= 1;
 }
@@ -675,8 +279,7 @@ void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bia
   a.W = W;
   a.relu = relu;
   a.acc_scale = acc_scale;
-  const int variant = g_c64_split_variant;
-  const int per = (variant == 2 || variant == 3 ? 1 : 2) * device_cu_count();
+  const int per = 2 * device_cu_count();
   // rows per work item: BAND, or fewer so that a small batch still makes ~2
   // work items per resident workgroup (each item re-reads 2 halo rows)
   int band = BAND;
@@ -685,14 +288,9 @@ void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bia
   a.nbands = (H + band - 1) / band;
   a.ntasks = B * a.nbands;
   const int grid = a.ntasks < per ? a.ntasks : per;
-  // depth 4 only without the residual: with it the kernel spills (256 VGPRs at depth 3 already)
   // ring depth 3: a 4th group of reads spills the residual variant (256 VGPRs at
   // depth 3), and without a residual it measured +0.09 % (profiles/r3_ab_c64_depth.log)
-  if (variant == 2) c64w_launch<2>(a, res != nullptr, grid, st);
-  else if (variant == 3) c64w_launch<3>(a, res != nullptr, grid, st);
-  else if (variant == 4) c64k_launch<3>(a, res != nullptr, grid, st);
-  else if (variant == 5) c64k_launch<4>(a, res != nullptr, grid, st);
-  else c64s_launch<3>(a, res != nullptr, grid, st);
+  c64s_launch<3>(a, res != nullptr, grid, st);
 }
 
 }  // namespace idunno

@@ -43,172 +43,6 @@ __device__ __forceinline__ void wait_stages(int pending_stages) {
   wait_vmcnt<0>();
 }
 
-typedef float float16v __attribute__((ext_vector_type(16)));
-
-// Main loop + epilogue of the MF32 tiles (see conv_glds_kernel): the caller
-// has issued the ring's first NS-1 stages; ``issue(buf)`` issues the next
-// stage's DMA into ring slot ``buf``.  SPLIT: a stage row is 32 channels x
-// (hi, lo), products hi*hi (first wait) then hi*lo + lo*hi; fp16: a stage row
-// is 64 channels = 4 k-steps of 16, k-steps 0-1 after the first wait, 2-3
-// after the second.
-template <int BN, int BM, int WN, int WM, int NS, int G, int STAGE, int A_BYTES, bool HAS_RES, bool OUT_F32,
-          bool SPLIT, typename Issue>
-__device__ __forceinline__ void conv_glds_mf32_body(const ConvArgs& a, char* smem, int wave, int lane, int nK, int n0,
-                                                    int m0, bool second, Issue& issue) {
-  constexpr int RB = 128;                                   // 64 halfs per row (32 channels x hi, lo)
-  constexpr int TN = BN / WN, TM = BM / WM;
-  constexpr int F32N = TN / 32, F32M = TM / 32;
-  const int wn = wave / WM, wm = wave % WM;
-  float16v acc[F32N][F32M];
-#pragma unroll
-  for (int i = 0; i < F32N; ++i)
-#pragma unroll
-    for (int j = 0; j < F32M; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  // per-lane byte offsets (within a stage) of fragment 0 for (k-step t, plane p):
-  // chunk 4p + 2t + (lane >> 5) of row (lane & 31); fragments 32 rows apart share
-  // the row swizzle (period 16), so fragment i is + i * 32 rows (an immediate)
-  const int hl = lane >> 5, r32 = lane & 31;
-  uint32_t fa[2][2], fb[2][2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int ch = 4 * p + 2 * t + hl;
-      const int ra = wn * TN + r32, rb = wm * TM + r32;
-      fa[t][p] = (uint32_t)(ra * RB + ((ch ^ swz_r(ra, 8)) << 4));
-      fb[t][p] = (uint32_t)(A_BYTES + rb * RB + ((ch ^ swz_r(rb, 8)) << 4));
-    }
-  static_assert(32 * RB * (F32N > F32M ? F32N : F32M) <= 65536, "fragment offsets must fit the ds immediate");
-
-  for (int s = 0; s < nK; ++s) {
-    const int ahead = min(NS - 2, nK - 1 - s);
-    wait_stages<G, NS>(ahead);
-    __builtin_amdgcn_s_barrier();
-    if (s + NS - 1 < nK) issue((s + NS - 1) % NS);
-
-    const uint32_t base = lds_addr(smem) + (s % NS) * STAGE;
-    half8v ah[2][F32N], al[2][F32N], bh[2][F32M], bl[2][F32M];
-    // hi planes first (both k-steps), then lo: hi*hi issues as soon as they land
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int i = 0; i < F32N; ++i) ah[t][i] = lds_read_b128_step<32 * RB>(base + fa[t][0], i);
-#pragma unroll
-      for (int j = 0; j < F32M; ++j) bh[t][j] = lds_read_b128_step<32 * RB>(base + fb[t][0], j);
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int i = 0; i < F32N; ++i) al[t][i] = lds_read_b128_step<32 * RB>(base + fa[t][1], i);
-#pragma unroll
-      for (int j = 0; j < F32M; ++j) bl[t][j] = lds_read_b128_step<32 * RB>(base + fb[t][1], j);
-    }
-    constexpr int NLO = 2 * (F32N + F32M);
-    lds_waitcnt<NLO>();
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int i = 0; i < F32N; ++i) lds_tie(ah[t][i]);
-#pragma unroll
-      for (int j = 0; j < F32M; ++j) lds_tie(bh[t][j]);
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < F32N; ++i)
-#pragma unroll
-        for (int j = 0; j < F32M; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t][i], bh[t][j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);          // hi*hi stays above the second wait
-    lds_waitcnt<0>();
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int i = 0; i < F32N; ++i) lds_tie(al[t][i]);
-#pragma unroll
-      for (int j = 0; j < F32M; ++j) lds_tie(bl[t][j]);
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < F32N; ++i)
-#pragma unroll
-        for (int j = 0; j < F32M; ++j) {
-          if constexpr (SPLIT) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t][i], bl[t][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t][i], bh[t][j], acc[i][j], 0, 0, 0);
-          } else {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t][i], bl[t][j], acc[i][j], 0, 0, 0);
-          }
-        }
-  }
-
-  // ---- epilogue: x 2^-e, +bias (+split residual) (+ReLU), split (or fp32) NHWC store ----
-  // the ring is drained (last wait vmcnt(0)): ordinary loads; one cout fragment at a time
-  const float acc_scale = SPLIT ? (second ? a.acc_scale2 : a.acc_scale) : 1.f;
-  const bool relu = a.relu && !second;
-#pragma unroll
-  for (int i = 0; i < F32N; ++i) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int n = n0 + wn * TN + i * 32 + 8 * g + 4 * hl;
-      if (n >= a.Cout) continue;
-      const float4v bv = *reinterpret_cast<const float4v*>(a.bias + n);
-      half4v rh[F32M], rl[F32M];
-      if constexpr (HAS_RES) {
-#pragma unroll
-        for (int j = 0; j < F32M; ++j) {
-          const int m = m0 + wm * TM + j * 32 + r32;
-          if constexpr (SPLIT) {
-            const size_t off = m < a.M ? (size_t)m * (a.ldr ? a.ldr : 2 * a.Cout) + split_off(n) : 0;
-            rh[j] = *reinterpret_cast<const half4v*>(a.res + off);
-            rl[j] = *reinterpret_cast<const half4v*>(a.res + off + 32);
-          } else {
-            const size_t off = m < a.M ? (size_t)m * (a.ldr ? a.ldr : a.Cout) + n : 0;
-            rh[j] = *reinterpret_cast<const half4v*>(a.res + off);
-            rl[j] = half4v{0, 0, 0, 0};
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < F32M; ++j) {
-        const int m = m0 + wm * TM + j * 32 + r32;
-        if (m >= a.M) continue;
-        float4v v;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = acc[i][j][4 * g + q] * acc_scale + bv[q];
-        if constexpr (HAS_RES) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] += (float)rh[j][q] + (float)rl[j][q];
-        }
-        if (relu) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-        }
-        if constexpr (OUT_F32) {
-          *reinterpret_cast<float4v*>(static_cast<float*>(a.y) + (size_t)m * a.ldy + n) = v;
-        } else if constexpr (!SPLIT) {
-          half4v o;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = (half_t)v[q];
-          *reinterpret_cast<half4v*>(static_cast<half_t*>(a.y) + (size_t)m * a.ldy + n) = o;
-        } else {
-          split_guard(a.ovf, v);
-          half4v h, l;
-          split_f16x4(v, h, l);
-          half_t* yp = static_cast<half_t*>(a.y) + (size_t)m * a.ldy + split_off(n);
-          *reinterpret_cast<half4v*>(yp) = h;
-          *reinterpret_cast<half4v*>(yp + 32) = l;
-        }
-      }
-    }
-  }
-}
-
-
 // P3: RGB stem on packed rows (preprocess_pack3_f16, x = [B][H][nc][wp] halfs):
 // the 3*KW halfs of one kernel row are contiguous in the row copy in which
 // they start 16-byte aligned; K = (kh, 16-byte chunk), ceil(3*KW/8) chunks per
@@ -225,28 +59,19 @@ __device__ __forceinline__ void conv_glds_mf32_body(const ConvArgs& a, char* sme
 // the epilogue multiplies by a.acc_scale = 2^-e (exact).  Residual in, output
 // out in the same split layout (or fp32 with OUT_F32).
 //
-// MF32: the split product on v_mfma_f32_32x32x16_f16 instead of 16x16x32 --
-// half the MFMA instructions per stage (12 instead of 24 for a 64x32 wave
-// tile), so the stage's DMA issue, fragment reads, waits and barrier fit in
-// the longer gaps (a 32x32x16 MFMA leaves 24 of its 32 issue cycles, a
-// 16x16x32 one 8 of 16; the split loop was issue-bound, docs/KERNELS.md).
-// Same LDS image and swizzle: a 32x32x16 operand fragment is 32 rows x 16 k,
-// lane l reads row l & 31, chunk 2t + (l >> 5) of k-step t (+4 for the lo
-// plane); the row XOR is conflict-free for these lane groups too.  C/D
-// layout: register r of a 32x32 accumulator is row 8(r/4) + 4(l>>5) + r%4,
-// column l & 31, so each lane still stores 4 consecutive output channels.
+// KS: conv split-K (small M) -- block s / tiles runs its own contiguous run of
+// a.kstage K stages into fp32 partials; without it the prologue has no
+// kstage / mid-tap start code (the B = 400 launches compile the plain loop).
 template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false,
-          bool SPLIT = false, bool MF32 = false, bool DEEPB = false>
+          bool SPLIT = false, bool KS = false>
 __global__ void __launch_bounds__(64 * WN * WM, (BM % 64 != 0 && WN * WM == 8) ? 4 : 1)   // 2nd: min waves per SIMD
 conv_glds_kernel(const ConvArgs a) {
   static_assert(!SPLIT || BK == 64, "split stages are 32 channels x (hi, lo)");
-  static_assert(!DEEPB || (!P3 && !MF32 && NS == 2 && BK == 64), "deep-B ring: BK-64 NHWC tiles, A ring of 2");
-  static_assert(!MF32 || (BK == 64 && !P3), "32x32x16 tiles: BK 64, NHWC convs");
+  static_assert(!KS || (OUT_F32 && !HAS_RES && !P3), "split-K writes fp32 partials");
   constexpr int NW = WN * WM;
   constexpr int NT = 64 * NW;
   constexpr int TN = BN / WN, TM = BM / WM;
-  static_assert(!MF32 || (TN % 32 == 0 && TM % 32 == 0), "32x32 wave fragments");
-  constexpr int FN = MF32 ? 1 : TN / 16, FM = MF32 ? 1 : TM / 16;
+  constexpr int FN = TN / 16, FM = TM / 16;
   constexpr int CPR = BK / 8;                 // 16-byte chunks per row
   constexpr int RB = BK * 2;                  // bytes per row
   constexpr int RPI = 64 / CPR;               // rows per DMA instruction (1 KiB)
@@ -269,10 +94,9 @@ conv_glds_kernel(const ConvArgs a) {
   const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
   const int lid_all = xcd_remap(blockIdx.x, nwg * nsplit);
   const int split = lid_all / nwg, lid = lid_all - split * nwg;
-  // norder: n-major tile order (an XCD's resident blocks share one weight
-  // panel, pixel panels stream) instead of m-major (they share pixel panels)
-  const int tm = a.norder ? lid % a.tiles_m : lid / a.tiles_n;
-  const int tn = a.norder ? lid / a.tiles_m : lid % a.tiles_n;
+  // m-major: an XCD's consecutive blocks share one pixel panel (n-major, sharing a
+  // weight panel, was 0-6 % slower: profiles/r2_v26_split_tile_order.md)
+  const int tm = lid / a.tiles_n, tn = lid - tm * a.tiles_n;
   const int n0 = tn * BN, m0 = tm * BM;
   // dual conv: this tile belongs to the second conv (see ConvArgs::nsplit_n)
   const bool second = a.nsplit_n > 0 && n0 >= a.nsplit_n;
@@ -332,7 +156,7 @@ conv_glds_kernel(const ConvArgs a) {
     i_s = (i_kh * a.KW + i_kw) * a.cblk;
     nK = a.cblk;
   }
-  if (a.kstage > 0) {                          // conv split-K: this block's contiguous run of K stages
+  if constexpr (KS) {                          // conv split-K: this block's contiguous run of K stages
     i_s = split * a.kstage;
     i_cb = i_s % a.cblk;
     const int tap = i_s / a.cblk;
@@ -365,7 +189,9 @@ conv_glds_kernel(const ConvArgs a) {
       b_voff[j] = ok ? (uint32_t)((b_base[j] + (ih * a.W + iw) * ldx) * 2) : OOR;
     }
   };
-  if (i_cb != 0) set_tap();                    // a split-K slice that starts inside a tap
+  if constexpr (KS) {
+    if (i_cb != 0) set_tap();                  // a split-K slice that starts inside a tap
+  }
   auto issue_buf = [&](int buf) {
     char* base = smem + buf * STAGE;
     if (i_cb == 0) set_tap();
@@ -444,39 +270,6 @@ conv_glds_kernel(const ConvArgs a) {
     else issue_buf(buf);
   };
 
-  // L2 prefetch of the tile's input footprint (the contiguous NHWC pixel range
-  // from its first input row, halo included, to its last): one 4-byte LDS-DMA
-  // per 128-byte line into ring slot NS-1, which no real DMA writes before stage
-  // 0's wait (these are older than every ring DMA) and barrier.  The taps' first
-  // touches of the input rows then go to HBM together at block start instead of
-  // stalling the early stages one after another.
-  if constexpr (!P3 && !DEEPB) {
-    if (a.l2pf && !(second && a.center_only)) {
-      const int hw = a.Ho * a.Wo;
-      const int mlo = m0, mhi = min(m0 + BM, a.M) - 1;
-      const int b0 = mlo / hw, oh0 = (mlo - b0 * hw) / a.Wo;
-      const int b1 = mhi / hw, oh1 = (mhi - b1 * hw) / a.Wo;
-      const int ih_lo = max(oh0 * a.stride - a.pad, 0), ih_hi = min(oh1 * a.stride - a.pad + a.KH - 1, a.H - 1);
-      const long long lo = ((long long)b0 * a.H + ih_lo) * a.W * ldx * 2;
-      const long long hi = ((long long)b1 * a.H + ih_hi + 1) * a.W * ldx * 2;
-      const int nl = (int)min((hi - lo + 127) >> 7, 2048LL);       // 128-byte lines, at most 256 KiB
-      char* dummy = smem + (NS - 1) * STAGE + wave * 256;
-      for (int i = wave * 64; i < nl; i += NW * 64) {
-        const int line = i + lane;
-        dma_buf4(x_rsrc, dummy, line < nl ? (uint32_t)(lo + ((long long)line << 7)) : OOR);
-      }
-    }
-  }
-
-  if constexpr (MF32) {
-#pragma unroll
-    for (int p = 0; p < NS - 1; ++p)
-      if (p < nK) issue(p);
-    conv_glds_mf32_body<BN, BM, WN, WM, NS, G, STAGE, A_BYTES, HAS_RES, OUT_F32, SPLIT>(a, smem, wave, lane, nK, n0, m0,
-                                                                                 second, issue);
-    return;
-  }
-
   float4v acc[FN][FM];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
@@ -506,109 +299,12 @@ conv_glds_kernel(const ConvArgs a) {
       for (int j = 0; j < FM; ++j) {
         const int m = m0 + wm * TM + j * 16 + (lane & 15);
         const size_t off = (m < a.M && n < a.Cout) ? (size_t)m * (a.ldr ? a.ldr : a.Cout) + n : 0;
-        rv[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : gload_b64_untracked(a.res + off);
+        rv[i][j] = gload_b64_untracked(a.res + off);
       }
     }
   }
 
   const int frow = lane & 15, fch = lane >> 4;
-  if constexpr (DEEPB) {
-    // Deep-B ring (split tiles, round 4): A (weights, L2-resident: every block of a
-    // layer reads the same panel) keeps a 2-slot ring, B (pixels, whose first
-    // touches miss L2) gets 3 slots, so a B stage is issued TWO stages ahead and
-    // its miss latency has two stages of MFMAs to hide under.  LDS: 2 A + 3 B
-    // slots = 80 KiB (two blocks per CU, as tile 42).  Issue order per stage:
-    // A(s+1), B(s+2); at the top of stage s, vmcnt(GB) leaves only B(s+1) in flight
-    // (vmcnt retires in order), i.e. A(s) and B(s) have landed.
-    constexpr int B_BYTES = BMD * RB;
-    char* const a_ring = smem;
-    char* const b_ring = smem + 2 * A_BYTES;
-    int ia_s = i_s;                            // A's own stage counter (B uses i_s / i_cb / i_kw / i_kh)
-    auto issue_a = [&](int slot) {
-      char* base = a_ring + slot * A_BYTES;
-      const int koff = ia_s * BK * 2;
-#pragma unroll
-      for (int j = 0; j < GA; ++j) dma_buf16(w_rsrc, base + (wave + NW * j) * 1024, a_voff[j], koff);
-      ++ia_s;
-    };
-    auto issue_b = [&](int slot) {
-      char* base = b_ring + slot * B_BYTES;
-      if (i_cb == 0) set_tap();
-      const int coff = i_cb * BK * 2;
-#pragma unroll
-      for (int j = 0; j < GB; ++j) dma_buf16(x_rsrc, base + (wave + NW * j) * 1024, b_voff[j], coff);
-      ++i_s;
-      if (++i_cb == a.cblk) {
-        i_cb = 0;
-        if (++i_kw == a.KW) {
-          i_kw = 0;
-          ++i_kh;
-        }
-      }
-    };
-    issue_a(0);
-    issue_b(0);
-    if (nK > 1) issue_b(1);
-    uint32_t fa_off[2], fb_off[2];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int ch = fch + 4 * kk;
-      const int ra = wn * TN + frow, rb = wm * TM + frow;
-      fa_off[kk] = (uint32_t)(ra * RB + ((ch ^ swz_r(ra, CPR)) << 4));
-      fb_off[kk] = (uint32_t)(rb * RB + ((ch ^ swz_r(rb, CPR)) << 4));
-    }
-    const uint32_t lds0 = lds_addr(smem);
-    int as = 0, bs = 0;                        // ring slots of stage s
-    for (int s = 0; s < nK; ++s) {
-      if (s + 1 < nK) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      // slots (s+1)%2 and (s+2)%3 were last read in stage s-1: free after the barrier
-      if (s + 1 < nK) issue_a(as ^ 1);
-      if (s + 2 < nK) issue_b(bs == 0 ? 2 : bs - 1);
-      const uint32_t abase = lds0 + as * A_BYTES, bbase = lds0 + 2 * A_BYTES + bs * B_BYTES;
-      constexpr int NR = FN + FM;
-      half8v fa[2][FN], fb[2][FM];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-        for (int i = 0; i < FN; ++i) fa[kk][i] = lds_read_b128_step<16 * RB>(abase + fa_off[kk], i);
-#pragma unroll
-        for (int j = 0; j < FM; ++j) fb[kk][j] = lds_read_b128_step<16 * RB>(bbase + fb_off[kk], j);
-      }
-      // chunk 0 (SPLIT: the hi planes) as soon as its fragments land, then chunk 1
-      // (SPLIT: hi*lo + lo*hi; fp16: the stage's second 32 channels)
-      lds_waitcnt<NR>();
-#pragma unroll
-      for (int i = 0; i < FN; ++i) lds_tie(fa[0][i]);
-#pragma unroll
-      for (int j = 0; j < FM; ++j) lds_tie(fb[0][j]);
-#pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      lds_waitcnt<0>();
-#pragma unroll
-      for (int i = 0; i < FN; ++i) lds_tie(fa[1][i]);
-#pragma unroll
-      for (int j = 0; j < FM; ++j) lds_tie(fb[1][j]);
-#pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j) {
-          if constexpr (SPLIT) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[0][i], fb[1][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[1][i], fb[0][j], acc[i][j], 0, 0, 0);
-          } else {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
-          }
-        }
-      as ^= 1;
-      bs = bs == 2 ? 0 : bs + 1;
-    }
-  } else {
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < nK) issue(p);
@@ -699,7 +395,6 @@ conv_glds_kernel(const ConvArgs a) {
     lds_waitcnt<0>();
     mfma_chunk(KK - 1);
   }
-  }   // !DEEPB
 
   // ---- epilogue: bias (+residual) (+ReLU), NHWC store --------------------
   // late residual: the ring is drained (last wait was vmcnt(0)), so ordinary
@@ -714,16 +409,11 @@ conv_glds_kernel(const ConvArgs a) {
       const bool ok = m < a.M && n < a.Cout;
       if constexpr (SPLIT) {
         const size_t off = ok ? (size_t)m * (a.ldr ? a.ldr : 2 * a.Cout) + split_off(n) : 0;
-        if (a.ablate & 2) {
-          rv[i][j] = half4v{0, 0, 0, 0};
-          rl[i][j] = half4v{0, 0, 0, 0};
-        } else {
-          rv[i][j] = *reinterpret_cast<const half4v*>(a.res + off);
-          rl[i][j] = *reinterpret_cast<const half4v*>(a.res + off + 32);
-        }
+        rv[i][j] = *reinterpret_cast<const half4v*>(a.res + off);
+        rl[i][j] = *reinterpret_cast<const half4v*>(a.res + off + 32);
       } else {
         const size_t off = ok ? (size_t)m * (a.ldr ? a.ldr : a.Cout) + n : 0;
-        rv[i][j] = (a.ablate & 2) ? half4v{0, 0, 0, 0} : *reinterpret_cast<const half4v*>(a.res + off);
+        rv[i][j] = *reinterpret_cast<const half4v*>(a.res + off);
       }
     }
   };
@@ -773,9 +463,7 @@ conv_glds_kernel(const ConvArgs a) {
         v[2] = fmaxf(v[2], 0.f);
         v[3] = fmaxf(v[3], 0.f);
       }
-      if (a.ablate & 1) {
-        if (v[0] == 12345.f) *reinterpret_cast<float*>(a.y) = v[1] + v[2] + v[3];   // keep the math alive
-      } else if constexpr (OUT_F32) {
+      if constexpr (OUT_F32) {
         *reinterpret_cast<float4v*>(static_cast<float*>(a.y) + (size_t)split * a.ysplit + (size_t)m * a.ldy + n) = v;
       } else if constexpr (SPLIT) {
         split_guard(a.ovf, v);
@@ -802,11 +490,8 @@ static bool glds_fits(const ConvArgs& a) {
   return xb < (1L << 31) && wb < (1L << 31);
 }
 
-static int g_l2pf = 0;   // conv_glds input-footprint L2 prefetch: bit 0 fp16 convs, bit 1 split convs
-void set_conv_l2_prefetch(int mode) { g_l2pf = mode; }
-
 template <int BN, int BM, int BK, int WN, int WM, int NS, bool HAS_RES, bool OUT_F32, bool P3 = false,
-          bool SPLIT = false, bool MF32 = false, bool DEEPB = false>
+          bool SPLIT = false, bool KS = false>
 static void glds_cfg(ConvArgs a, hipStream_t st) {
   a.tiles_n = (a.Cout + BN - 1) / BN;
   a.tiles_m = (a.M + BM - 1) / BM;
@@ -821,8 +506,8 @@ static void glds_cfg(ConvArgs a, hipStream_t st) {
   const int grid = a.tiles_n * a.tiles_m * (a.ksplit > 1 ? a.ksplit : 1);
   constexpr int RPI_ = 64 / (BK / 8), NW_ = WN * WM;
   constexpr int BMD = (BM + RPI_ * NW_ - 1) / (RPI_ * NW_) * (RPI_ * NW_);
-  const size_t lds = DEEPB ? (size_t)(2 * BN + 3 * BMD) * BK * 2 : (size_t)NS * (BN + BMD) * BK * 2;
-  auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32, P3, SPLIT, MF32, DEEPB>;
+  const size_t lds = (size_t)NS * (BN + BMD) * BK * 2;
+  auto kern = conv_glds_kernel<BN, BM, BK, WN, WM, NS, HAS_RES, OUT_F32, P3, SPLIT, KS>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), (int)lds);   // per (kernel, device), launch_util.h
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WN * WM), lds, st, a);
 }
@@ -839,6 +524,9 @@ static void glds_cfg(ConvArgs a, hipStream_t st) {
 //   18: 128x128, BK 32, 4 waves, 3 stages 48 KiB   19: 128x64, BK 32, 4 stages 48 KiB
 //   20: 64x128,  BK 32, 4 stages 48 KiB            21: 256x128, BK 32, 8 waves, 4 stages 96 KiB
 //   22: 128x256, BK 32, 8 waves, 4 stages 96 KiB   23: 64x64, BK 64, 4 waves (2x2), 3 stages 48 KiB
+// The measured-and-dropped variants (32x32x16 MFMA tiles 55-59 / 90-92, deep pixel ring
+// 60 / 61, input-footprint L2 prefetch) were deleted in round 5 (docs/KERNELS.md keeps
+// their numbers; the code is in git history before commit "prune dropped conv variants").
 template <bool R, bool F>
 static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
   switch (tile) {
@@ -873,11 +561,17 @@ static bool glds_dispatch(ConvArgs a, int tile, hipStream_t st) {
     case 38: glds_cfg<128, 64, 64, 2, 4, 2, R, F>(a, st); return true;    // 8 waves (32x16 wave tile)
     case 39: glds_cfg<128, 128, 32, 2, 4, 4, R, F>(a, st); return true;   // 8 waves, 64 KiB, 3 stages in flight
     case 42: glds_cfg<128, 160, 64, 4, 2, 2, R, F>(a, st); return true;   // 8 waves, B as 192 rows, 80 KiB (small M)
-    case 61: glds_cfg<128, 128, 64, 2, 4, 2, R, F, false, false, false, true>(a, st); return true;   // deep-B ring, 80 KiB
-    // 32x32x16 MFMA (MF32) fp16 tiles: the shapes of split 56 / 57 / 58
-    case 90: glds_cfg<128, 128, 64, 2, 4, 2, R, F, false, false, true>(a, st); return true;
-    case 91: glds_cfg<128, 128, 64, 2, 2, 2, R, F, false, false, true>(a, st); return true;
-    case 92: glds_cfg<128, 192, 64, 4, 2, 2, R, F, false, false, true>(a, st); return true;
+    default: return false;
+  }
+}
+
+// split-K instantiations (fp32 partials, no residual): the auto-pickable BK-64 tiles
+template <bool SPLIT>
+static bool glds_dispatch_ks(ConvArgs a, int tile, hipStream_t st) {
+  switch (tile) {
+    case 27: glds_cfg<64, 128, 64, 1, 4, 2, false, true, false, SPLIT, true>(a, st); return true;
+    case 36: glds_cfg<128, 128, 64, 2, 4, 2, false, true, false, SPLIT, true>(a, st); return true;
+    case 42: glds_cfg<128, 160, 64, 4, 2, 2, false, true, false, SPLIT, true>(a, st); return true;
     default: return false;
   }
 }
@@ -895,16 +589,11 @@ static bool glds_dispatch_p3(ConvArgs a, int tile, hipStream_t st) {
   }
 }
 
-// split fp16 (fp32-accurate) tiles: the BK = 64 shapes of the fp16 table
-// The tiles below are the measured-useful ones: 36 / 42 / 27 are the defaults
-// (conv_glds_split_pick), 26 / 34 / 38 near-equal alternatives kept for A/B.
-// Measured and dropped (profiles/r2_v24..v29): 14/17/25/30 (256-wide), 15/16/41
-// (3-stage rings), 24, 33, 35, 37, 43 -- 5-45 % slower on every ResNet layer (15/16/24
-// re-measured after the round-3 buffer-DMA rewrite: still 5-30 % slower, profiles/r3_split_resweep.log);
-// 192 x 128 for AlexNet conv2 (Cout 192): 8 % slower than 64 x 128.  Round 3
-// (profiles/r3_split_stagger_layers.md): half the waves issuing the next stage's
-// DMA behind their first MFMA chunk (0-13 % slower), 128 x 256 with a 3-stage
-// ring at one block per CU (10-35 % slower).
+// split fp16 (fp32-accurate) tiles: the BK = 64 shapes of the fp16 table that were
+// measured useful: 36 / 42 / 27 are the defaults (conv_glds_split_pick), 26 / 34 / 38
+// near-equal alternatives.  Measured and dropped (profiles/r2_v24..v29, r3, r4): 14/17/25/30
+// (256-wide), 15/16/41 (3-stage rings), 24, 33, 35, 37, 43, 32x32x16 MFMA tiles, deep
+// pixel ring -- 5-45 % slower on every ResNet layer.
 template <bool R, bool F>
 static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
   switch (tile) {
@@ -916,102 +605,60 @@ static bool glds_dispatch_split(ConvArgs a, int tile, hipStream_t st) {
     // 128 x 160 (B staged as 192 rows): 0.96 waves of blocks on ResNet layer4
     // at B = 400 where 128 x 64 tiles make 1.6 (the partial last wave idles)
     case 42: glds_cfg<128, 160, 64, 4, 2, 2, R, F, false, true>(a, st); return true;    // 8 waves, 80 KiB
-    // 32x32x16 MFMA tiles (MF32): 56 = tile 36's shape (64x32 wave tiles), 57 = 128 x 128 on 4 waves
-    // (64x64 wave tiles), 58 = 128 x 192 on 8 waves (32x96 wave tiles, the layer4-sized GEMMs)
-    case 56: glds_cfg<128, 128, 64, 2, 4, 2, R, F, false, true, true>(a, st); return true;
-    case 57: glds_cfg<128, 128, 64, 2, 2, 2, R, F, false, true, true>(a, st); return true;
-    case 58: glds_cfg<128, 192, 64, 4, 2, 2, R, F, false, true, true>(a, st); return true;
-    // Cout 64 (ResNet layer1): 55 = 64 x 256 on 8 waves, 59 = 64 x 128 on 4 waves (64x32 wave tiles)
-    // deep-B ring (2 weight slots, 3 pixel slots, 80 KiB): tile 36's shape
-    case 60: glds_cfg<128, 128, 64, 2, 4, 2, R, F, false, true, false, true>(a, st); return true;
-    case 55: glds_cfg<64, 256, 64, 1, 8, 2, R, F, false, true, true>(a, st); return true;
-    case 59: glds_cfg<64, 128, 64, 1, 4, 2, R, F, false, true, true>(a, st); return true;
     default: return false;
   }
 }
 
 bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
-  a.l2pf = (g_l2pf >> 1) & 1;
   if (!glds_fits(a)) return false;
+  if (a.kstage > 0) return out_f32 && a.res == nullptr && glds_dispatch_ks<true>(a, tile, st);
   const bool res = a.res != nullptr;
   if (res) return out_f32 ? glds_dispatch_split<true, true>(a, tile, st) : glds_dispatch_split<true, false>(a, tile, st);
   return out_f32 ? glds_dispatch_split<false, true>(a, tile, st) : glds_dispatch_split<false, false>(a, tile, st);
 }
 
-// Default split tile: same shape logic as the fp16 pick (a stage is 32 channels
-// instead of 64, so a tile does 3x the MFMAs per byte staged).
-static bool g_split_wide = true;
-void set_split_wide_tile(bool on) { g_split_wide = on; }
-static bool g_split_wide_l3 = false;
-void set_split_wide_l3(bool on) { g_split_wide_l3 = on; }
-static bool g_split_wide_all = false;
-void set_split_wide_all(bool on) { g_split_wide_all = on; }
-static int g_split_mf32 = 0;
-void set_split_mf32(int mode) { g_split_mf32 = mode; }
-int split_mf32() { return g_split_mf32; }
-static bool g_split_deepb = false;
-void set_split_deepb(bool on) { g_split_deepb = on; }
-bool split_deepb() { return g_split_deepb; }
-// conv split-K for small M (strong scaling: a 400-image query over 8 GPUs is 50
+// Conv split-K for small M (strong scaling: a 400-image query over 8 GPUs is 50
 // images per GPU, and ResNet layer4 then makes 64 blocks of tile 42 on 256 CUs):
 // K slices of whole (kh, kw, cblk) stage runs in ONE launch into fp32 partials,
 // then splitk_reduce_res adds bias (+ residual), ReLU and re-splits.
-static int g_split_ksplit = -1;
-void set_split_ksplit(int mode) { g_split_ksplit = mode; }
-static int g_ksplit_cap = 8;             // most K slices the auto rule uses
-void set_ksplit_cap4(bool on) { g_ksplit_cap = on ? 4 : 8; }
-int split_ksplit() { return g_split_ksplit; }
-static void split_tile_dims(int tile, int& bn, int& bm) {
+//   force < 0: auto (only for the auto-picked tile); 0 / 1: off; k > 1: k slices
+//   (k must divide the K loop: 1 is returned otherwise).
+static void ks_tile_dims(int tile, int& bn, int& bm) {
   switch (tile) {
     case 42: bn = 128; bm = 160; return;
-    case 27: case 59: bn = 64; bm = 128; return;
-    case 34: case 38: bn = 128; bm = 64; return;
-    case 55: bn = 64; bm = 256; return;
-    case 58: bn = 128; bm = 192; return;
-    default: bn = 128; bm = 128; return;
+    case 27: bn = 64; bm = 128; return;
+    default: bn = 128; bm = 128; return;        // 36
   }
 }
-static int ksplit_rule(int mode, int M, int Cout, int tile, int nk_total) {
-  // the 32x32x16 tiles (55-59) have their own epilogue without split-K partial slices
-  if (mode == 0 || nk_total < 8 || (tile >= 55 && tile <= 59)) return 1;
+static int ksplit_rule(int force, int M, int Cout, int tile, int nk_total) {
+  if (tile != 27 && tile != 36 && tile != 42) return 1;   // split-K instantiations (glds_dispatch_ks)
+  if (force == 0 || force == 1) return 1;
+  if (force > 1) return nk_total % force == 0 ? force : 1;
+  if (nk_total < 8) return 1;
   int bn, bm;
-  split_tile_dims(tile, bn, bm);
+  ks_tile_dims(tile, bn, bm);
   const long blocks = (long)((M + bm - 1) / bm) * ((Cout + bn - 1) / bn);
-  if (mode > 1) return nk_total % mode == 0 ? mode : 1;   // forced (tests, A/B)
   const long target = 2L * device_cu_count();  // two blocks per CU
   int s = 1;
   // double the slices while the grid stays within one wave of two blocks per CU,
-  // each slice keeps >= 4 stages and the slices divide the K loop evenly
-  while (s < g_ksplit_cap && blocks * s * 2 <= target && nk_total % (s * 2) == 0 && nk_total / (s * 2) >= 4) s *= 2;
+  // each slice keeps >= 4 stages and the slices divide the K loop evenly (at most 8:
+  // capping at 4 lost 11 % at B = 8, profiles/r4_ab_ksplit_cap4_b8.log)
+  while (s < 8 && blocks * s * 2 <= target && nk_total % (s * 2) == 0 && nk_total / (s * 2) >= 4) s *= 2;
   return s;
 }
-int conv_split_ksplit(int M, int Cout, int tile, int nk_total) {
-  return ksplit_rule(g_split_ksplit, M, Cout, tile, nk_total);
+int conv_split_ksplit(int M, int Cout, int tile, int nk_total, int force) {
+  return ksplit_rule(force, M, Cout, tile, nk_total);
+}
+int conv_f16_ksplit(int M, int Cout, int tile, int nk_total, int force) {
+  return ksplit_rule(force, M, Cout, tile, nk_total);     // same rule: fp16's BK-64 tiles 27 / 42
 }
 
-static int g_f16_ksplit = -1;
-void set_f16_ksplit(int mode) { g_f16_ksplit = mode; }
-int f16_ksplit() { return g_f16_ksplit; }
-int conv_f16_ksplit(int M, int Cout, int tile, int nk_total) {
-  if (tile >= 90) return 1;                      // 32x32x16 fp16 tiles: no partial slices in their epilogue
-  switch (tile) {                                // BK = 32 tiles: nk_total (counted in 64-channel stages) differs
-    case 11: case 13: case 18: case 19: case 20: case 21: case 22: case 28: case 31: case 32: case 39: return 1;
-    default: break;
-  }
-  return ksplit_rule(g_f16_ksplit, M, Cout, tile, nk_total);   // same rule, the fp16 switch
-}
-
+// Default split tile (a stage is 32 channels instead of 64, so a tile does 3x the
+// MFMAs per byte staged): 128 x 128 8-wave tiles where M is large, 128 x 160 for
+// layer4-sized GEMMs (~1 full wave of blocks where 128 x 64 made 1.6; whole-graph
+// A/B profiles/r2_v29_split_wide_tile.md; 128 x 160 at every M: ResNet18 -2.9 %).
 int conv_glds_split_pick(int M, int Cout) {
-  if (Cout % 128 == 0) {
-    if ((g_split_mf32 & 1) && M >= 50000) return 56;
-    if ((g_split_mf32 & 2) && M < 50000) return 58;
-    if (g_split_wide && g_split_wide_all) return 42;
-    if (g_split_wide && g_split_wide_l3 && M >= 50000 && M < 100000) return 42;   // layer3: 1.91 vs 2.39 waves
-    if (M >= 50000) return g_split_deepb ? 60 : 36;
-    // layer4-sized GEMMs: 128 x 160 tiles make ~1 full wave of blocks where
-    // 128 x 64 made 1.6 (whole-graph A/B: profiles/r2_v29_split_wide_tile.md)
-    return g_split_wide ? 42 : 34;
-  }
+  if (Cout % 128 == 0) return M >= 50000 ? 36 : 42;
   return 27;
 }
 
@@ -1028,41 +675,23 @@ bool conv_glds_split_p3_launch(ConvArgs a, int tile, hipStream_t st) {
 }
 
 bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st) {
-  a.l2pf = g_l2pf & 1;
   const bool res = a.res != nullptr;
   if (a.cpk > 0) {
     if (res) return false;
     return out_f32 ? glds_dispatch_p3<true>(a, tile, st) : glds_dispatch_p3<false>(a, tile, st);
   }
   if (!glds_fits(a)) return false;
+  if (a.kstage > 0) return out_f32 && !res && glds_dispatch_ks<false>(a, tile, st);
   if (res) return out_f32 ? glds_dispatch<true, true>(a, tile, st) : glds_dispatch<true, false>(a, tile, st);
   return out_f32 ? glds_dispatch<false, true>(a, tile, st) : glds_dispatch<false, false>(a, tile, st);
 }
 
-// Default tile per shape, from the per-layer sweep on MI355X (tools/bench_layers.py,
-// profiles/r1_layer_sweep.md): 2 blocks/CU with a 4-deep BK=32 ring wins where
-// M is large; 128x64 tiles keep >= 2 waves of blocks when M is small (layer4).
-static bool g_f16_wide = true;   // whole fp16 graph +3.6 % (profiles/r2_v31_wide_tiles.md)
-void set_f16_wide_tile(bool on) { g_f16_wide = on; }
-// fp16 A/B after the buffer-DMA rewrite: 42 at every M, ResNet18 b400 +4.2 %, ResNet50 b1024
-// +3.4 % (profiles/r3_ab_f16_wide_all.md; per-layer: profiles/r3_f16_big_tiles.log)
-static bool g_f16_wide_all = true;
-void set_f16_wide_all(bool on) { g_f16_wide_all = on; }
-static int g_f16_mf32 = 0;
-void set_f16_mf32(int mode) { g_f16_mf32 = mode; }
-static bool g_f16_deepb = false;
-void set_f16_deepb(bool on) { g_f16_deepb = on; }
+// Default fp16 tile: 128 x 160 (8 waves, BK 64) for every 128-multiple Cout (after the
+// buffer-DMA rewrite: ResNet18 b400 +4.2 %, ResNet50 b1024 +3.4 %, profiles/r3_ab_f16_wide_all.md),
+// 64 x 128 otherwise.
 int conv_glds_pick(int M, int Cout) {
-  // sweeps r1 #3/#4: BK=64 double buffering with 2-3 workgroups/CU beats deeper
-  // rings; 8 waves per 128x128 tile (4 waves/SIMD) best where M is large
-  if (Cout % 128 == 0) {
-    if (g_f16_deepb && M >= 50000) return 61;
-    if ((g_f16_mf32 & 1) && M >= 50000) return (g_f16_mf32 & 4) ? 92 : 90;
-    if ((g_f16_mf32 & 2) && M < 50000) return 92;
-    if (g_f16_wide && g_f16_wide_all) return 42;
-    return M >= 50000 ? 36 : (g_f16_wide ? 42 : 34);   // 128x128 8-wave | 128x64
-  }
-  return 27;                                           // 64x128, 48 KiB
+  (void)M;
+  return Cout % 128 == 0 ? 42 : 27;
 }
 
 }  // namespace idunno

@@ -53,8 +53,6 @@ constexpr int kRaw3 = 40 * 1024;
 
 __device__ __forceinline__ int raw_swz(int p) { return wino_raw_swz(p); }   // tile_math.h
 
-int g_wino_ablate = 0;
-
 template <bool ASM>
 __device__ __forceinline__ float4v ldsr(uint32_t addr) {
   if constexpr (ASM) return lds_read_f4(addr);
@@ -71,9 +69,6 @@ __device__ __forceinline__ void ldst(float4v& r) {
 
 }  // namespace
 
-void set_wino_ablation(int mode) { g_wino_ablate = mode; }
-extern bool g_wino_pair;
-void set_wino_pairing(bool on) { g_wino_pair = on; }
 
 // SINGLE: one LDS stage of 40 KiB raw + 32 KiB U (72 KiB) instead of two of
 // 40 + 32 KiB, so TWO 4-wave blocks share a CU: each block's DMA wait,
@@ -797,21 +792,14 @@ bool conv_wino_f32_supported(int H, int W, int C, int Cout) {
   return C % 16 == 0 && Cout % 32 == 0 && wino_geometry(a, 4, kRaw2);
 }
 
-bool g_wino_lin = true;    // A/B switch (set_wino_linear): LIN blocking in variant 3
-void set_wino_linear(bool on) { g_wino_lin = on; }
-// A/B switch (set_wino_rotation): rotated raw rows in variant 3.  Off: the
-// rotation removes the simulated 2-way raw-read bank conflicts (PMC lds_conf
-// 0.21-0.23) but measured 0.99-1.00x at 56/28/14 and 1.02x (slower) at 7x7
-// (profiles/r2_v11_wino_rotation.md) -- the conflicts are not on the critical path
-bool g_wino_rot = false;
-void set_wino_rotation(bool on) { g_wino_rot = on; }
-bool g_wino_pair = false;  // A/B switch (set_wino_pairing): e-GEMMs in pairs (4w: -4 %, 8w: +13 % time, same box)
-
+// Variant 3 uses LIN blocking (consecutive tiles, virtual rows: 40.3k vs 39.4k img/s,
+// profiles/r2_v8_wino_linear_40k.md) without rotated raw rows (the rotation removed the
+// simulated 2-way raw-read bank conflicts but measured 0.99-1.02x, profiles/r2_v11_wino_rotation.md);
+// e-GEMMs in pairs measured 4w -4 %, 8w +13 % time.  Those A/B switches were folded in round 5.
 template <int NW, bool R>
 static void wino_cfg(WinoArgs a, hipStream_t st) {
   const int lds = 2 * kStage;
-  auto kern = a.ablate ? conv_wino_f32_kernel<NW, R, false, false, true>
-              : g_wino_pair ? conv_wino_f32_kernel<NW, R, true> : conv_wino_f32_kernel<NW, R, false>;
+  auto kern = conv_wino_f32_kernel<NW, R, false>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), lds);
   hipLaunchKernelGGL(kern, dim3(a.nblk_t * a.nblk_n), dim3(64 * NW), lds, st, a);
 }
@@ -821,13 +809,10 @@ static void wino_cfg(WinoArgs a, hipStream_t st) {
 //          3 = 4 waves, one 58-KiB stage, two blocks per CU
 bool conv_wino_f32_launch(WinoArgs a, int variant, hipStream_t st) {
   if (variant == 3) {
-    if (a.C % 16 || a.Cout % 32 || !wino_geometry(a, 4, kRaw3, g_wino_lin, g_wino_rot)) return false;
+    if (a.C % 16 || a.Cout % 32 || !wino_geometry(a, 4, kRaw3, true, false)) return false;
     const int lds = kRaw3 + kUBytes;
     const bool r = a.res != nullptr;
-    auto kern = a.ablate ? (r ? conv_wino_f32_kernel<4, true, false, true, true>
-                              : conv_wino_f32_kernel<4, false, false, true, true>)
-                : g_wino_pair ? (r ? conv_wino_f32_kernel<4, true, true, true> : conv_wino_f32_kernel<4, false, true, true>)
-                              : (r ? conv_wino_f32_kernel<4, true, false, true> : conv_wino_f32_kernel<4, false, false, true>);
+    auto kern = r ? conv_wino_f32_kernel<4, true, false, true> : conv_wino_f32_kernel<4, false, false, true>;
     ensure_lds_attr(reinterpret_cast<const void*>(kern), lds);
     hipLaunchKernelGGL(kern, dim3(a.nblk_t * a.nblk_n), dim3(256), lds, st, a);
     return true;

@@ -74,15 +74,13 @@ __device__ __forceinline__ int hp_off(int r, int px, int c) { return (r * stem::
 
 struct StemGeom {
   int B, H, W, Hc, Wc, Hp, Wp, tiles_x, tiles_y, ntiles;
-  int ablate;   // profiling only (set_stem_ablation): skip 1 pool, 2 MFMAs, 4 patch normalise, 8 conv epilogue, 16 patch loads
   int* ovf;     // stem_split: split range guard flag or nullptr (common.h split_guard)
 };
 
-static int g_stem_ablate = 0;
-void set_stem_ablation(int mode) { g_stem_ablate = mode; }
+// Round-1/2 ablation switches (tools/stem_ablate.py measurements, docs/KERNELS.md) are
+// compiled out: the bit tests below fold to "no ablation".
+constexpr int kStemAblate = 0;
 // persistent workgroups per CU (A/B knob)
-static int g_stem_wgs = stem::WGS_MAX;
-void set_stem_workgroups_per_cu(int n) { g_stem_wgs = n < 1 ? 1 : (n > stem::WGS_MAX ? stem::WGS_MAX : n); }
 
 struct Quads {
   uint32_t d[stem::QPT][3];
@@ -244,7 +242,7 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
       float4v acc[NIW];
 #pragma unroll
       for (int i = 0; i < NIW; ++i) acc[i] = float4v{0.f, 0.f, 0.f, 0.f};
-      if (!(g.ablate & 2)) {
+      if (!(kStemAblate & 2)) {
 #pragma unroll
         for (int kh = 0; kh < KH; ++kh) {
           const half8v fb = *reinterpret_cast<const half8v*>(pb + kh * IPC * 8);
@@ -256,7 +254,7 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
       // conv output is the pool's -inf padding (-65504); the 3-wide horizontal
       // max takes lanes cx+1, cx+2 of the same DPP row, on packed fp16 pairs
       // (VALU issue is this phase's cost: 4 cycles per wave instruction).
-      if (g.ablate & 8) continue;
+      if (kStemAblate & 8) continue;
       half4v o[NIW];
       if ((unsigned)(oy0 + f) < (unsigned)g.Hc) {          // wave-uniform
 #pragma unroll
@@ -285,13 +283,13 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
 
     const int tnext = tn;
     if (tnext < g.ntiles) {
-      if (!(g.ablate & 4)) store_patch(patch, g, tnext, tid, q);   // uses the quads prefetched one tile ago
+      if (!(kStemAblate & 4)) store_patch(patch, g, tnext, tid, q);   // uses the quads prefetched one tile ago
       tn = tnext + gridDim.x;
-      if (tn < g.ntiles && !(g.ablate & 16)) load_quads(img, g, tn, tid, q);
+      if (tn < g.ntiles && !(kStemAblate & 16)) load_quads(img, g, tn, tid, q);
     }
 
     // ---- vertical 3-max over conv rows 4*vpy2 .. 4*vpy2+4 -> 2 pooled rows ----
-    if (tid < NVP && !(g.ablate & 1)) {
+    if (tid < NVP && !(kStemAblate & 1)) {
       const int r0 = 4 * vpy2;
       const half8v a0 = *reinterpret_cast<const half8v*>(hp + hp_off(r0 + 0, vpx, c8));
       const half8v a1 = *reinterpret_cast<const half8v*>(hp + hp_off(r0 + 1, vpx, c8));
@@ -331,9 +329,8 @@ void stem_fused_launch(const uint8_t* img, const half_t* w, const float* bias, h
   g.tiles_x = (g.Wp + PTX - 1) / PTX;
   g.tiles_y = (g.Hp + PTY - 1) / PTY;
   g.ntiles = B * g.tiles_x * g.tiles_y;
-  g.ablate = g_stem_ablate;
   const int ncu = device_cu_count();   // per device (launch_util.h)
-  const int per = g_stem_wgs * ncu;   // persistent: g_stem_wgs workgroups per CU
+  const int per = stem::WGS_MAX * ncu;   // persistent: WGS_MAX workgroups per CU
   const int grid = g.ntiles < per ? g.ntiles : per;
   hipLaunchKernelGGL(stem_fused_kernel, dim3(grid), dim3(256), LDS, st, img, w, bias, y, g, start_idx, start_off,
                      max_start, sub);
@@ -358,12 +355,10 @@ namespace stem_s {
 constexpr int HP_BYTES = stem::CRY * stem::PTX * 256;     // [conv row][pooled col][64 ch] f32 = 30464
 constexpr int LDS = stem::PATCH_BYTES + HP_BYTES;         // 44816
 }  // namespace stem_s
-static int g_stem_split_niw = 1;   // measured: 399 vs 461 us at B = 400 (profiles/r2_v28_stem_split_u8.md)
-void set_stem_split_niw(int n) { g_stem_split_niw = n == 1 ? 1 : 2; }
-static int g_stem_split_rp2 = 2;   // conv rows per pass: 2 whole graph +0.86 % (profiles/r3_stem_split_rp2.md)
-void set_stem_split_rp2(int rows) { g_stem_split_rp2 = rows == 3 ? 3 : rows >= 2 ? 2 : 0; }
-static int g_stem_split_reg = 0;       // register-pooled kernel with 3 / 4 workgroups per CU (0: off)
-void set_stem_split_reg(int wgs) { g_stem_split_reg = wgs == 3 || wgs == 4 ? wgs : 0; }
+// Stem variants measured and dropped (deleted in round 5): two 16-cout fragments per
+// wave (461 vs 399 us at B = 400, profiles/r2_v28_stem_split_u8.md), one / three conv
+// rows per pass (-0.86 % / -0.7 % whole graph vs two, profiles/r3_stem_split_rp2.md),
+// a register-pooled kernel (-0.1 ... -0.5 %).
 
 // f32 tile offset of 4-channel chunk c (0..15) of (conv row r, pooled col px),
 // chunk XOR-swizzled by px
@@ -551,7 +546,7 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
         for (int r = 0; r < RP; ++r) acc[r][0] = float4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kh = 0; kh < KH; ++kh) {
-          if (g.ablate & 2) break;
+          if (kStemAblate & 2) break;
           half8v bq[RP];
 #pragma unroll
           for (int r = 0; r < RP; ++r) bq[r] = *reinterpret_cast<const half8v*>(pa + (r * 2 * IPC + kh * IPC) * 8);
@@ -561,7 +556,7 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
           for (int r = 0; r < RP; ++r)
             if constexpr (!F16) acc[r][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh][0], bq[r], acc[r][0], 0, 0, 0);
         }
-        if (g.ablate & 8) continue;
+        if (kStemAblate & 8) continue;
         row_epi(f, acc[0]);
 #pragma unroll
         for (int r = 1; r < RP; ++r)
@@ -575,7 +570,7 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
         for (int i = 0; i < NIW; ++i) acc[i] = float4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kh = 0; kh < KH; ++kh) {
-          if (g.ablate & 2) break;
+          if (kStemAblate & 2) break;
           const half8v bu = *reinterpret_cast<const half8v*>(pb + kh * IPC * 8);
 #pragma unroll
           for (int i = 0; i < NIW; ++i) {
@@ -583,7 +578,7 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
             if constexpr (!F16) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh][i], bu, acc[i], 0, 0, 0);
           }
         }
-        if (g.ablate & 8) continue;
+        if (kStemAblate & 8) continue;
         row_epi(f, acc);
       }
     }
@@ -591,13 +586,13 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
 
     const int tnext = tn;
     if (tnext < g.ntiles) {
-      if (!(g.ablate & 4)) store_patch_u8(patch, g, tnext, tid, q);
+      if (!(kStemAblate & 4)) store_patch_u8(patch, g, tnext, tid, q);
       tn = tnext + gridDim.x;
-      if (tn < g.ntiles && !(g.ablate & 16)) load_quads(img, g, tn, tid, q);
+      if (tn < g.ntiles && !(kStemAblate & 16)) load_quads(img, g, tn, tid, q);
     }
 
     // ---- vertical 3-max over conv rows 4*vpy2 .. 4*vpy2+4 -> 2 pooled rows ----
-    if (tid < NVP && !(g.ablate & 1)) {
+    if (tid < NVP && !(kStemAblate & 1)) {
       const int r0 = 4 * vpy2;
       float4v a[5][2];
 #pragma unroll
@@ -646,162 +641,6 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
   }
 }
 
-// Register-pooled split stem (round 3): one 16-cout fragment per wave over all
-// CRY conv rows, two rows per pass (interleaved MFMA chains); the vertical
-// 3-max runs in registers as the rows go by (pooled row p = rows 2p..2p+2) and
-// each pooled row is scaled, biased, ReLU'd, split and stored straight from the
-// lanes of its even conv columns -- no f32 pooling tile in LDS and no pooling
-// phase.  The input patch is double-buffered (2 x 14 KiB), so a tile costs one
-// barrier: tile t+1's patch is stored from the quads loaded one tile earlier
-// while tile t computes.  Same arithmetic, bit for bit, as stem_split_kernel.
-namespace stem_r {
-constexpr int LDS = 2 * stem::PATCH_BYTES + 1024;   // + slack for the dropped row's reads
-}  // namespace stem_r
-
-template <int WGS>
-__global__ void __launch_bounds__(256, WGS)
-stem_split_rp_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w, const float* __restrict__ bias,
-                     const float* __restrict__ psum, float acc_scale, half_t* __restrict__ y, const StemGeom g,
-                     const long long* __restrict__ start_idx, long long start_off, long long max_start,
-                     long long sub) {
-  using namespace stem;
-  static_assert(((2 * CRY + KH - 1) * IPC + 2 * 15 + 2 * 3 + PCO) * 8 + 16 + PATCH_BYTES <= stem_r::LDS,
-                "the dropped row's patch reads stay inside the LDS allocation");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (start_idx != nullptr) {
-    long long s = *start_idx - start_off;
-    s = (s < 0 ? 0 : (s > max_start ? max_start : s)) + sub;
-    img += (size_t)s * g.H * g.W * 3;
-  }
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int t = blockIdx.x;
-  if (t >= g.ntiles) return;   // whole workgroup exits together (uniform)
-
-  Quads q;
-  load_quads(img, g, t, tid, q);
-  const int frow = lane & 15, fch = lane >> 4, cx = frow;
-  const int co = wave * 16 + fch * 4;                  // this lane's 4 couts
-  half8v fah[KH], fal[KH];
-#pragma unroll
-  for (int kh = 0; kh < KH; ++kh) {
-    const size_t o = (size_t)(wave * 16 + frow) * (KH * 32) + kh * 32 + fch * 8;
-    fah[kh] = *reinterpret_cast<const half8v*>(w + o);
-    fal[kh] = *reinterpret_cast<const half8v*>(w + 64 * KH * 32 + o);
-  }
-  const float4v bias4 = *reinterpret_cast<const float4v*>(bias + co);
-  const float inv_scale = 1.f / acc_scale;
-  const float4v s_ff = *reinterpret_cast<const float4v*>(psum + (7 * 8 + 7) * 64 + co);
-
-  store_patch_u8(smem, g, t, tid, q);
-  int tn = t + gridDim.x;
-  if (tn < g.ntiles) load_quads(img, g, tn, tid, q);
-  __syncthreads();
-  int buf = 0;
-
-  while (true) {
-    // the next tile's patch into the other buffer (its quads landed a tile ago)
-    const int tnext = tn;
-    if (tnext < g.ntiles) {
-      if (!(g.ablate & 4)) store_patch_u8(smem + (buf ^ 1) * PATCH_BYTES, g, tnext, tid, q);
-      tn = tnext + gridDim.x;
-      if (tn < g.ntiles && !(g.ablate & 16)) load_quads(img, g, tn, tid, q);
-    }
-    const char* patch = smem + buf * PATCH_BYTES;
-    int b, py0, px0;
-    tile_coords(g, t, b, py0, px0);
-    const int oy0 = py0 * PS - PP, ox0 = px0 * PS - PP;
-    const bool colv = cx < CRX && (unsigned)(ox0 + cx) < (unsigned)g.Wc;
-    const bool interior = ox0 >= 0 && ox0 + CRX <= g.Wc;
-    int wlo, whi;
-    tap_range(ox0 + cx, g.W, wlo, whi);
-    const bool colb = wlo > 0 || whi < KH;
-    float4v colcorr = float4v{0.f, 0.f, 0.f, 0.f};
-    if (colb) {
-      const float4v s_h = *reinterpret_cast<const float4v*>(psum + (7 * 8 + whi) * 64 + co);
-      const float4v s_l = *reinterpret_cast<const float4v*>(psum + (7 * 8 + wlo) * 64 + co);
-      colcorr = (s_h - s_l - s_ff) * inv_scale;
-    }
-    // pooled output of this lane (even conv column cx = 2 * pooled column)
-    const int ox = px0 + (cx >> 1);
-    const bool outc = !(cx & 1) && cx < 2 * PTX && ox < g.Wp;
-    half_t* ydst = y + (((size_t)b * g.Hp + py0) * g.Wp + ox) * 128 + split_off(co);
-
-    // border delta + horizontal 3-max of conv row f
-    auto row_h = [&](int f, float4v acc) -> float4v {
-      const int oy = oy0 + f;
-      const bool rowv = (unsigned)oy < (unsigned)g.Hc;    // wave-uniform
-      int hlo, hhi;
-      tap_range(oy, g.H, hlo, hhi);
-      const bool rowb = hlo > 0 || hhi < KH;              // wave-uniform
-      if (rowv && !rowb && colb) {
-        acc += colcorr;
-      } else if (rowv && rowb) {
-        const float4v s_hh = *reinterpret_cast<const float4v*>(psum + (hhi * 8 + whi) * 64 + co);
-        const float4v s_lh = *reinterpret_cast<const float4v*>(psum + (hlo * 8 + whi) * 64 + co);
-        const float4v s_hl = *reinterpret_cast<const float4v*>(psum + (hhi * 8 + wlo) * 64 + co);
-        const float4v s_ll = *reinterpret_cast<const float4v*>(psum + (hlo * 8 + wlo) * 64 + co);
-        acc += (s_hh - s_lh - s_hl + s_ll - s_ff) * inv_scale;
-      }
-      float4v o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v = acc[e];
-        if (!rowv || (!interior && !colv)) v = -INFINITY;
-        o[e] = fmaxf(v, fmaxf(row_shl_f32<1>(v), row_shl_f32<2>(v)));
-      }
-      return o;
-    };
-    // pooled row p = max of conv rows 2p .. 2p+2 -> scale, bias, ReLU, split store
-    auto emit = [&](int p, float4v m) {
-      if (!outc || py0 + p >= g.Hp || (g.ablate & 1)) return;
-      float4v v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(m[e] * acc_scale + bias4[e], 0.f);
-      split_guard(g.ovf, v);
-      half4v h, l;
-      split_f16x4(v, h, l);
-      half_t* dst = ydst + (size_t)p * g.Wp * 128;
-      *reinterpret_cast<half4v*>(dst) = h;
-      *reinterpret_cast<half4v*>(dst + 32) = l;
-    };
-    float4v run = float4v{0.f, 0.f, 0.f, 0.f};
-    for (int f = 0; f < CRY; f += 2) {
-      // rows f and f+1, MFMA chains interleaved; row CRY (past the tile) is computed and dropped
-      const char* pa = patch + ((2 * f) * IPC + 2 * cx + 2 * fch + PCO) * 8;
-      const char* pc = pa + 2 * IPC * 8;
-      float4v a0 = float4v{0.f, 0.f, 0.f, 0.f}, a1 = a0;
-#pragma unroll
-      for (int kh = 0; kh < KH; ++kh) {
-        if (g.ablate & 2) break;
-        const half8v b0 = *reinterpret_cast<const half8v*>(pa + kh * IPC * 8);
-        const half8v b1 = *reinterpret_cast<const half8v*>(pc + kh * IPC * 8);
-        a0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[kh], b0, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[kh], b1, a1, 0, 0, 0);
-        a0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh], b0, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[kh], b1, a1, 0, 0, 0);
-      }
-      if (g.ablate & 8) continue;
-      const float4v h0 = row_h(f, a0);
-      if (f > 0) {                           // f even: closes pooled row f/2 - 1
-        float4v m;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) m[e] = fmaxf(run[e], h0[e]);
-        emit(f / 2 - 1, m);
-      }
-      run = h0;
-      if (f + 1 < CRY) {
-        const float4v h1 = row_h(f + 1, a1);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) run[e] = fmaxf(run[e], h1[e]);
-      }
-    }
-    __syncthreads();   // the next patch is complete; this one's reads are done
-    if (tnext >= g.ntiles) break;
-    t = tnext;
-    buf ^= 1;
-  }
-}
-
 void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
                        half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,
                        long long max_start, long long sub, int* ovf, hipStream_t st) {
@@ -818,31 +657,10 @@ void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, c
   g.tiles_x = (g.Wp + PTX - 1) / PTX;
   g.tiles_y = (g.Hp + PTY - 1) / PTY;
   g.ntiles = B * g.tiles_x * g.tiles_y;
-  g.ablate = g_stem_ablate;
-  const int wgs = g_stem_split_niw == 1 ? 3 : 2;
-  const int per = wgs * device_cu_count();
+  const int per = 3 * device_cu_count();
   const int grid = g.ntiles < per ? g.ntiles : per;
-  if (g_stem_split_reg) {
-    const int per_r = g_stem_split_reg * device_cu_count();
-    const int grid_r = g.ntiles < per_r ? g.ntiles : per_r;
-    if (g_stem_split_reg == 4)
-      hipLaunchKernelGGL(stem_split_rp_kernel<4>, dim3(grid_r), dim3(256), stem_r::LDS, st, img, w, bias, psum,
-                         acc_scale, y, g, start_idx, start_off, max_start, sub);
-    else
-      hipLaunchKernelGGL(stem_split_rp_kernel<3>, dim3(grid_r), dim3(256), stem_r::LDS, st, img, w, bias, psum,
-                         acc_scale, y, g, start_idx, start_off, max_start, sub);
-  } else if (g_stem_split_niw == 1 && g_stem_split_rp2 == 3)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_split_kernel<1, 3>), dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias,
-                       psum, acc_scale, y, g, start_idx, start_off, max_start, sub);
-  else if (g_stem_split_niw == 1 && g_stem_split_rp2)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_split_kernel<1, 2>), dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias,
-                       psum, acc_scale, y, g, start_idx, start_off, max_start, sub);
-  else if (g_stem_split_niw == 1)
-    hipLaunchKernelGGL(stem_split_kernel<1>, dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias, psum, acc_scale,
-                       y, g, start_idx, start_off, max_start, sub);
-  else
-    hipLaunchKernelGGL(stem_split_kernel<2>, dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias, psum, acc_scale,
-                       y, g, start_idx, start_off, max_start, sub);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_split_kernel<1, 2>), dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias,
+                     psum, acc_scale, y, g, start_idx, start_off, max_start, sub);
 }
 
 // fp16 programs: the exact-u8 stem, hi MFMA only, fp16 [B][Hp][Wp][64] out
@@ -862,7 +680,6 @@ void stem_u8_f16_launch(const uint8_t* img, const half_t* w, const float* bias, 
   g.tiles_x = (g.Wp + PTX - 1) / PTX;
   g.tiles_y = (g.Hp + PTY - 1) / PTY;
   g.ntiles = B * g.tiles_x * g.tiles_y;
-  g.ablate = g_stem_ablate;
   const int per = 3 * device_cu_count();
   const int grid = g.ntiles < per ? g.ntiles : per;
   hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_split_kernel<1, 2, true>), dim3(grid), dim3(256), stem_s::LDS, st, img, w,

@@ -18,12 +18,16 @@ __all__ = [
 
 
 def conv2d_split(x, w, bias, acc_scale: float, kh: int, kw: int, stride: int, pad: int, relu: bool,
-                 residual=None, out_f32: bool = False, tile: int = -1, out=None):
+                 residual=None, out_f32: bool = False, tile: int = -1, out=None, ksplit: int = -1, route: int = 0):
     """fp32-accurate conv on split-fp16 activations ([.., 2C] halfs, hi/lo per
     32 channels; models.packed.to_split) and weights (pack_split_weight):
     hi*hi + hi*lo + lo*hi on the f16 MFMA.  Output split (or fp32 with
-    ``out_f32``)."""
-    return load().conv2d_split(x, w, bias, residual, kh, kw, stride, pad, relu, acc_scale, out_f32, tile, out)
+    ``out_f32``).  ``tile`` forces a kernel (-1: the shape's default), ``ksplit``
+    forces split-K slices (-1: auto for the default tile), ``route`` opts out of
+    the specialised kernels (bit 0 band 3x3, bit 1 row-streaming 64->64, bit 2
+    streaming 1x1) -- kernel choice depends on these arguments only."""
+    return load().conv2d_split(x, w, bias, residual, kh, kw, stride, pad, relu, acc_scale, out_f32, tile, out,
+                               ksplit, route)
 
 
 def conv2d_split_dual(x, w, bias, acc_scale: float, acc_scale2: float, nsplit: int, kh: int, kw: int,
@@ -106,7 +110,7 @@ def pick_tile_split(m: int, cout: int) -> int:
 
 
 def conv2d(x, w, bias, kh: int, kw: int, stride: int, pad: int, relu: bool,
-           residual=None, out_f32: bool = False, tile: int = -1, out=None):
+           residual=None, out_f32: bool = False, tile: int = -1, out=None, ksplit: int = -1, route: int = 0):
     """Implicit-GEMM MFMA convolution with fused bias / residual / ReLU
     (into ``out`` when given: a contiguous NHWC tensor, e.g. a batch slice).
 
@@ -116,7 +120,7 @@ def conv2d(x, w, bias, kh: int, kw: int, stride: int, pad: int, relu: bool,
 
     if x.dtype == torch.float32:
         return load().conv2d_nhwc_f32(x, w, bias, residual, kh, kw, stride, pad, relu, tile, out)
-    return load().conv2d_nhwc(x, w, bias, residual, kh, kw, stride, pad, relu, out_f32, tile, out)
+    return load().conv2d_nhwc(x, w, bias, residual, kh, kw, stride, pad, relu, out_f32, tile, out, ksplit, route)
 
 
 def conv1x1_dual(x1, x2, w, bias, stride: int, relu: bool):

@@ -211,8 +211,7 @@ def test_conv_split_default_tile(ops, B, H, Cin, Cout, k, s, p):
     (2, 56, 64, 256, 1, True), (2, 56, 64, 64, 1, False), (3, 28, 128, 512, 1, True), (2, 14, 256, 1024, 1, True),
     (2, 56, 256, 64, 1, False), (1, 13, 256, 384, 1, False), (2, 28, 512, 128, 1, False), (2, 7, 512, 2048, 1, True),
     (2, 56, 64, 128, 2, False), (2, 28, 256, 512, 2, False), (3, 14, 512, 1024, 2, False), (1, 9, 128, 256, 2, True)])
-@pytest.mark.parametrize("lio", [False, True])
-def test_conv_split_1x1_stream(ops, B, H, Cin, Cout, s, res, lio):
+def test_conv_split_1x1_stream(ops, B, H, Cin, Cout, s, res):
     torch.manual_seed(B * 100 + H + Cin + Cout + s + res)
     x = torch.randn(B, H, H, Cin, device=DEV)
     w = torch.randn(Cout, Cin, 1, 1) / Cin ** 0.5
@@ -221,12 +220,8 @@ def test_conv_split_1x1_stream(ops, B, H, Cin, Cout, s, res, lio):
     r = torch.randn(B, ho, ho, Cout, device=DEV) if res else None
     sw, scale = P.pack_split_weight(w)
     for relu in (True, False):
-        ops.load().set_conv1x1_stream_lio(lio)
-        try:
-            y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, 1, 1, s, 0, relu,
-                                 residual=None if r is None else ops.split_from_f32(r), tile=80)
-        finally:
-            ops.load().set_conv1x1_stream_lio(True)
+        y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, 1, 1, s, 0, relu,
+                             residual=None if r is None else ops.split_from_f32(r), tile=80)
         assert y.shape == (B, ho, ho, 2 * Cout)
         _check(P.from_split(y), _ref64(x, w, b, s, 0, relu, r))
 
@@ -234,8 +229,7 @@ def test_conv_split_1x1_stream(ops, B, H, Cin, Cout, s, res, lio):
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,Ho,K1,K2,Cout,s", [(2, 56, 64, 64, 256, 1), (3, 28, 128, 256, 512, 2), (1, 9, 64, 64, 128, 1),
                                                (2, 13, 128, 256, 64, 2)])
-@pytest.mark.parametrize("lio", [False, True])
-def test_conv1x1_dual_split(ops, B, Ho, K1, K2, Cout, s, lio):
+def test_conv1x1_dual_split(ops, B, Ho, K1, K2, Cout, s):
     """Split bottleneck tail: expansion 1x1 + (strided) 1x1 downsample as one GEMM, vs fp64."""
     torch.manual_seed(B + Ho + K1 + K2 + Cout + s)
     H = (Ho - 1) * s + 1 + (s - 1)
@@ -245,12 +239,8 @@ def test_conv1x1_dual_split(ops, B, Ho, K1, K2, Cout, s, lio):
     wd = torch.randn(Cout, K2, 1, 1) / K2 ** 0.5 * 0.1       # different magnitudes: one shared scale
     b3, bd = torch.randn(Cout) * 0.1, torch.randn(Cout) * 0.1
     sw, scale = P.pack_split_weight(torch.cat([w3, wd], 1))
-    ops.load().set_conv1x1_stream_lio(lio)
-    try:
-        out = ops.conv1x1_dual_split(ops.split_from_f32(y), ops.split_from_f32(x), sw.to(DEV), (b3 + bd).to(DEV),
-                                     scale, s, True)
-    finally:
-        ops.load().set_conv1x1_stream_lio(True)
+    out = ops.conv1x1_dual_split(ops.split_from_f32(y), ops.split_from_f32(x), sw.to(DEV), (b3 + bd).to(DEV),
+                                 scale, s, True)
     assert out.shape == (B, Ho, Ho, 2 * Cout)
     ref = torch.relu(_ref64(y, w3, b3, 1, 0, False) + _ref64(x, wd, bd, s, 0, False))
     _check(P.from_split(out), ref)
@@ -271,23 +261,15 @@ def test_resnet50_split_fused_downsample_matches_unfused(ops):
     assert (outs[True] - outs[False]).abs().max().item() <= 2e-5 * scale
 
 
-SPLIT_TILES = [26, 27, 34, 36, 38, 42, 55, 56, 57, 58, 59, 60]   # 55-59: 32x32x16 MFMA (MF32); 60: deep-B ring
+SPLIT_TILES = [26, 27, 34, 36, 38, 42]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,H,W", [(2, 56, 56), (3, 13, 49), (1, 9, 62)])
 @pytest.mark.parametrize("res", [False, True])
-@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5])
-def test_conv_split_c64_rows(ops, B, H, W, res, variant):
-    """Row-streaming register-weight 3x3 64->64 kernel (tile 50): 16 couts per
-    wave (variant 0) and 32 couts per wave with a 2- / 3-deep read ring."""
-    ext = ops.load()
-    keep = ext.c64_split_variant()
-    ext.set_c64_split_variant(variant)
-    try:
-        _c64_rows_case(ops, B, H, W, res)
-    finally:
-        ext.set_c64_split_variant(keep)
+def test_conv_split_c64_rows(ops, B, H, W, res):
+    """Row-streaming register-weight 3x3 64->64 kernel (tile 50, 16 couts per wave)."""
+    _c64_rows_case(ops, B, H, W, res)
 
 
 def _c64_rows_case(ops, B, H, W, res):
@@ -330,43 +312,17 @@ def test_conv_split_ksplit(ops, B, H, cin, cout, k, s, ks, res, out_f32):
     """Small-M split-K (K slices of whole stage runs into fp32 partials, one
     combine with bias / residual / ReLU / re-split): forced k slices (k = 8 over
     72 stages starts slices inside a tap) and the auto pick (-1) at M = 49."""
-    ext = ops.load()
-    keep = ext.split_ksplit()
-    ext.set_split_ksplit(ks)
-    try:
-        torch.manual_seed(B + H + cin + ks)
-        x = torch.randn(B, H, H, cin, device=DEV)
-        w = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
-        b = torch.randn(cout) * 0.1
-        pad = k // 2
-        ho = (H + 2 * pad - k) // s + 1
-        r = torch.randn(B, ho, ho, cout, device=DEV) if res else None
-        sw, scale = P.pack_split_weight(w)
-        y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, k, k, s, pad, True,
-                             residual=None if r is None else ops.split_from_f32(r), out_f32=out_f32)
-        _check(y if out_f32 else P.from_split(y), _ref64(x, w, b, s, pad, True, r))
-        if ks == -1:
-            assert ext.conv_split_ksplit_for(B * ho * ho, cout, k * k * (2 * cin // 64)) > 1
-    finally:
-        ext.set_split_ksplit(keep)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("cin,k", [(32, 1), (64, 1), (96, 1), (32, 3)])
-@pytest.mark.parametrize("res", [False, True])
-def test_conv_split_deepb_short_k(ops, cin, k, res):
-    """Tile 60 (deep-B ring) at 1, 2, 3 and 9 stages: the prologue and the
-    last-stage vmcnt(0) paths of the 3-slot pixel ring."""
-    torch.manual_seed(cin + k + res)
-    B, H, Cout = 2, 17, 256
+    torch.manual_seed(B + H + cin + ks)
     x = torch.randn(B, H, H, cin, device=DEV)
-    w = torch.randn(Cout, cin, k, k) / (cin * k * k) ** 0.5
-    b = torch.randn(Cout) * 0.1
-    r = torch.randn(B, H, H, Cout, device=DEV) if res else None
+    w = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
+    b = torch.randn(cout) * 0.1
+    pad = k // 2
+    ho = (H + 2 * pad - k) // s + 1
+    r = torch.randn(B, ho, ho, cout, device=DEV) if res else None
     sw, scale = P.pack_split_weight(w)
-    y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, k, k, 1, k // 2, True,
-                         residual=None if r is None else ops.split_from_f32(r), tile=60)
-    _check(P.from_split(y), _ref64(x, w, b, 1, k // 2, True, r))
+    y = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, k, k, s, pad, True,
+                         residual=None if r is None else ops.split_from_f32(r), out_f32=out_f32, ksplit=ks)
+    _check(y if out_f32 else P.from_split(y), _ref64(x, w, b, s, pad, True, r))
 
 
 @pytest.mark.gpu
@@ -389,11 +345,9 @@ def test_stem_pack3_split(ops, kh, stride, pad, B, tile):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,hw", [(3, 224), (2, 100), (1, 37)])
-@pytest.mark.parametrize("niw", [2, 1, "rp2", "rp3", "reg3", "reg4"])
-def test_stem_split_fused(ops, B, hw, niw):
+def test_stem_split_fused(ops, B, hw):
     """uint8 -> normalise -> conv7x7/2 -> +bias -> ReLU -> maxpool3x3/2, split out
-    (niw "rpN": one cout fragment per wave, N conv rows per pass; "regN": the
-    register-pooled kernel at N workgroups per CU)."""
+    (one cout fragment per wave, two conv rows per pass)."""
     from idunno.models import reference as ref
 
     torch.manual_seed(B + hw)
@@ -401,16 +355,7 @@ def test_stem_split_fused(ops, B, hw, niw):
     w = torch.randn(64, 3, 7, 7) / (3 * 49) ** 0.5
     b = torch.randn(64) * 0.1
     fs, scale, bias, psum = P.pack_stem_split(w, b)
-    ext = ops.load()
-    ext.set_stem_split_niw(2 if niw == 2 else 1)
-    ext.set_stem_split_rp2(int(niw[2:]) if str(niw).startswith("rp") else 1)
-    ext.set_stem_split_reg(int(niw[3:]) if str(niw).startswith("reg") else 0)
-    try:
-        y = ops.stem_split(img, fs.to(DEV), bias.to(DEV), psum.to(DEV), scale)
-    finally:
-        ext.set_stem_split_niw(1)
-        ext.set_stem_split_rp2(2)
-        ext.set_stem_split_reg(0)
+    y = ops.stem_split(img, fs.to(DEV), bias.to(DEV), psum.to(DEV), scale)
     x = ref.preprocess_u8(img).permute(0, 2, 3, 1)
     want = _ref64(x, w, b, 2, 3, True).permute(0, 3, 1, 2)
     want = F.max_pool2d(want, 3, 2, 1).permute(0, 2, 3, 1)
@@ -618,37 +563,3 @@ def test_resnet18_fused_downsample_same_logits(ops):
     plain = r.logits(img).double()
     scale = plain.abs().max().item()
     assert (fused - plain).abs().max().item() <= 1e-6 * scale
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("tile", [26, 27, 36, 42])
-@pytest.mark.parametrize("B,H,C,Cout,k,s", [(3, 28, 128, 128, 3, 1), (2, 56, 64, 128, 3, 2), (2, 14, 256, 256, 3, 1),
-                                            (4, 7, 512, 512, 3, 1), (2, 28, 128, 256, 1, 2)])
-def test_conv_l2_prefetch_identical(ops, tile, B, H, C, Cout, k, s):
-    """conv_glds input-footprint L2 prefetch (set_conv_l2_prefetch) leaves every output bit unchanged,
-    split and fp16, with and without the residual."""
-    from idunno.models.packed import pack_conv_weight
-
-    torch.manual_seed(B + H + C + Cout + k + s + tile)
-    ext = ops.load()
-    x = torch.randn(B, H, H, C, device=DEV)
-    w = torch.randn(Cout, C, k, k) / (C * k * k) ** 0.5
-    b = torch.randn(Cout) * 0.1
-    pad = k // 2
-    ho = (H + 2 * pad - k) // s + 1
-    r = torch.randn(B, ho, ho, Cout, device=DEV)
-    sw, scale = P.pack_split_weight(w)
-    pw, _ = pack_conv_weight(w)
-    outs = []
-    for mode in (0, 3):
-        ext.set_conv_l2_prefetch(mode)
-        try:
-            ys = ops.conv2d_split(ops.split_from_f32(x), sw.to(DEV), b.to(DEV), scale, k, k, s, pad, True,
-                                  residual=ops.split_from_f32(r), tile=tile)
-            yh = ops.conv2d(x.half(), pw.to(DEV), b.to(DEV), k, k, s, pad, True, residual=r.half(), tile=tile)
-            torch.cuda.synchronize()
-        finally:
-            ext.set_conv_l2_prefetch(0)
-        outs.append((ys, yh))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    _check(P.from_split(outs[1][0]), _ref64(x, w, b, s, pad, True, r))

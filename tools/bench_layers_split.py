@@ -26,13 +26,11 @@ def main():
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--tiles", default="26,27,34,36,38,42")
     ap.add_argument("--json", default=None)
-    ap.add_argument("--norder", type=int, default=-1, help="split conv tile order: 0 m-major, 1 n-major, -1 auto")
     a = ap.parse_args()
     from idunno import ops
     from idunno.models.packed import pack_conv_weight, pack_split_weight, split_eligible, wino_weight
 
     ops.load()
-    ops.load().set_split_norder(a.norder)
     dev = "cuda"
     tiles = [int(t) for t in a.tiles.split(",")]
     rows = []
