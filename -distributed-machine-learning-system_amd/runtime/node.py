@@ -312,7 +312,8 @@ class Node:
         if qnum is None:
             qnum = self.state.new_query_number(model)
         self.sched.active_jobs = self.state.active_models() | {model}
-        plan = self.sched.assign(model, start, end, alive)
+        # a query boundary with nothing in flight: the fair-time split may follow the EMA
+        plan = self.sched.assign(model, start, end, alive, drained=self.state.pending_count() == 0)
         now = self.clock()
         self.state.assign(model, qnum, plan, now)
         self.tracer.instant("query.submit", model=model, q=qnum, start=start, end=end, workers=len(plan))

@@ -119,11 +119,13 @@ class FairTimeScheduler:
     seed: int | None = None
     avg_time: dict = field(default_factory=lambda: {"alexnet": 1.0, "resnet18": 1.0})
     active_jobs: set = field(default_factory=set)
+    hysteresis: float = 0.1          # workers past the rounding point before a drained re-split
 
     def __post_init__(self):
         self._rng = random.Random(self.seed)
         self._seen: set = set()
         self._part: dict = {}
+        self.repartitions = 0        # drained-boundary re-splits of the current (active, workers) key
 
     def effective_avg(self, models) -> dict[str, float]:
         """Per-model average query time for the split: a model with no
@@ -134,20 +136,37 @@ class FairTimeScheduler:
         fill = sum(seen) / len(seen) if seen else 1.0
         return {m: (self.avg_time[m] if m in self._seen else fill) for m in models}
 
-    def subsets(self, active, workers: list) -> dict[str, list]:
-        """``partition`` of ``workers`` over the ``active`` models, fixed while
-        the same jobs run on the same workers: the split is computed when the
-        active set (a job starts or ends), the worker set (a failure / join)
-        or the set of measured models changes, and kept otherwise, so EMA
-        jitter never moves a job's GPUs mid-job (a moved subset collides with
-        the other job's in-flight queries; report Fig 2 keeps 5/5, 4/6
-        splits per query pair)."""
+    def subsets(self, active, workers: list, drained: bool = False) -> dict[str, list]:
+        """``partition`` of ``workers`` over the ``active`` models.
+
+        The split is computed when the active set (a job starts or ends), the
+        worker set (a failure / join) or the set of measured models changes,
+        and kept while queries are in flight, so EMA jitter never moves a job's
+        GPUs under its running queries (a moved subset would collide with the
+        other job's in-flight chunks).  At a DRAINED query boundary (no query of
+        any job in flight, ``drained``) it follows the measured averages again,
+        like the reference, which re-plans every query from the current averages
+        (mp4_machinelearning.py:501-521; report Fig 2: 5/5 -> 4/6): the split
+        moves when some model's exact share (t_i / sum(t) x workers) is more than
+        ``hysteresis`` workers past the half-way point of its current count."""
         active = frozenset(active)
         key = (active, tuple(workers), frozenset(self._seen & active))
         cur = self._part.get(key)
         if cur is None:
             cur = partition(self.effective_avg(active), active, list(workers), self.budget)
             self._part = {key: cur}
+            self.repartitions = 0
+        elif drained and len(active) > 1:
+            avg = self.effective_avg(active)
+            eff = max(1, min(self.budget, len(workers)))
+            sh = time_shares(avg, active)
+            moved = any(abs(sh[m] * eff - len(cur[m])) > 0.5 + self.hysteresis for m in active)
+            if moved:
+                new = partition(avg, active, list(workers), self.budget)
+                if {m: len(v) for m, v in new.items()} != {m: len(v) for m, v in cur.items()}:
+                    cur = new
+                    self._part = {key: cur}
+                    self.repartitions += 1
         return cur
 
     def observe(self, model: str, normalized_query_time: float) -> None:
@@ -174,19 +193,20 @@ class FairTimeScheduler:
         return max(1, fair_share(self.effective_avg(act), model, self.budget, len(alive), act))
 
     def assign(self, model: str, start: int, end: int, alive: list,
-               n: int | None = None, shuffle: bool = True) -> list[tuple]:
+               n: int | None = None, shuffle: bool = True, drained: bool = False) -> list[tuple]:
         """Returns [(worker, s, e), ...] for the inclusive query range.
 
         A single active job gets the whole budget (a random sample of the
         alive workers when the budget is smaller, as the reference samples,
         :520-521).  With several active jobs each gets its own disjoint,
         fair-time-sized subset (``partition``), so concurrent jobs share the
-        node in space instead of queueing on the same GPUs."""
+        node in space instead of queueing on the same GPUs; ``drained`` (no
+        query in flight) lets that split follow the measured averages."""
         if not alive:
             return []
         active = set(self.active_jobs) | {model}
         if n is None and len(active) > 1:
-            workers = self.subsets(active, list(alive))[model]
+            workers = self.subsets(active, list(alive), drained=drained)[model]
         else:
             n = self.n_workers(model, alive) if n is None else max(1, min(n, len(alive)))
             workers = self._rng.sample(list(alive), n) if shuffle else list(alive)[:n]

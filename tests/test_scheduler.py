@@ -96,3 +96,45 @@ def test_adopted_averages_count_as_measurements():
     s.adopt({"alexnet": 2.0, "resnet18": 6.0})
     p = s.subsets({"alexnet", "resnet18"}, [f"r{i}" for i in range(8)])
     assert (len(p["alexnet"]), len(p["resnet18"])) == (2, 6)
+
+
+def test_split_follows_ema_only_at_drained_boundaries():
+    """with fake EMA drift, the fair-time split moves (5/5 ->
+    4/6 like report Fig 2) only at a query boundary where nothing is in flight,
+    and the two jobs' subsets never overlap -- before, at, or after the move."""
+    s = FairTimeScheduler(budget=10, seed=0)
+    ws = [f"rank{i}" for i in range(10)]
+    both = {"alexnet", "resnet18"}
+    s.adopt({"alexnet": 5.0, "resnet18": 5.0})
+    sizes = lambda p: (len(p["alexnet"]), len(p["resnet18"]))      # noqa: E731
+    p0 = s.subsets(both, ws)
+    assert sizes(p0) == (5, 5)
+    # EMA drifts: resnet18 slows to 6/4 of alexnet's time -> exact share 4 / 6
+    for _ in range(30):
+        s.observe("alexnet", 4.0)
+        s.observe("resnet18", 6.0)
+        assert s.subsets(both, ws, drained=False) == p0             # queries in flight: frozen
+    p1 = s.subsets(both, ws, drained=True)                           # drained boundary: moves
+    assert sizes(p1) == (4, 6) and s.repartitions == 1
+    assert set(p1["alexnet"]).isdisjoint(p1["resnet18"])
+    assert sorted(p1["alexnet"] + p1["resnet18"]) == sorted(ws)
+    # kept afterwards while queries run, and assign() lands on the new subsets
+    s.active_jobs = both
+    for m in both:
+        assert [w for w, _, _ in s.assign(m, 0, 399, ws)] == p1[m]
+    # jitter inside the hysteresis band never re-splits, drained or not
+    import random
+    rng = random.Random(3)
+    for _ in range(100):
+        s.observe("alexnet", 4.0 * rng.uniform(0.97, 1.03))
+        s.observe("resnet18", 6.0 * rng.uniform(0.97, 1.03))
+        assert s.subsets(both, ws, drained=rng.random() < 0.5) == p1
+    assert s.repartitions == 1
+    # drift back: follows again only once drained
+    for _ in range(30):
+        s.observe("alexnet", 5.0)
+        s.observe("resnet18", 5.0)
+    assert s.subsets(both, ws) == p1
+    p2 = s.assign("alexnet", 0, 399, ws, drained=True)
+    assert len(p2) == 5 and s.repartitions == 2
+
