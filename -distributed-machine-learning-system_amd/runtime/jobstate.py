@@ -391,7 +391,7 @@ class JobState:
         key = (model, qnum)
         ents = self.worker_set[key]
         pos = {(x[0], x[1], x[2]): i for i, x in enumerate(ents) if x[3] == "w"}
-        bs = self.batchsize.get(model, 1)
+        bsz = self.batchsize.get(model)             # None: per-chunk time, as record_result
         tot = 0
         res = self.results[f"{model} {qnum}"]
         chunks = []
@@ -414,7 +414,7 @@ class JobState:
             done.add((model, qnum, s, e))
             n = e - s + 1
             tot += n
-            pw.append((now, (now - t_start) / n * bs))
+            pw.append((now, (now - t_start) / n * (n if bsz is None else bsz)))
             res.append(ChunkResult(s, e, c if type(c) is np.ndarray and c.dtype == np.int32 else
                                    np.asarray(c, dtype=np.int32),
                                    p if type(p) is np.ndarray and p.dtype == np.float32 else

@@ -134,3 +134,32 @@ def test_bulk_round_ingest_matches_per_chunk_and_replicates():
     assert any(op == "results" for _, op, _ in a._log)
     assert standby.apply_deltas(a.deltas_since(0))
     assert standby.pending_count() == 0 and standby.cq() == a.cq() and standby.cvm() == a.cvm()
+
+
+def test_bulk_and_per_chunk_same_c2_without_configured_batchsize():
+    """a model with no configured batch size gets the same c2 window
+    (per-chunk time) whether a round takes the bulk or the per-chunk path."""
+    import numpy as np
+
+    from idunno.runtime.jobstate import JobState
+
+    a, b = (JobState(batchsize={}, clock=lambda: 5.0) for _ in range(2))
+    sizes = [30, 50, 20, 70]
+    for q in range(1, 4):
+        plan, s0 = [], q * 1000
+        for r, n in enumerate(sizes):
+            plan.append((f"node{r:02d}", s0, s0 + n - 1))
+            s0 += n
+        for st in (a, b):
+            st.assign("vgg", q, plan, now=float(q))
+        recs = [("vgg", q, w, s, e, np.zeros(e - s + 1, np.int32), np.zeros(e - s + 1, np.float32))
+                for w, s, e in plan]
+        assert a.record_results(recs, now=q + 0.5) == len(plan)
+        for r in recs:
+            b.record_result(*r, now=q + 0.5)
+    assert list(a._ptime_win["vgg"]) == list(b._ptime_win["vgg"])
+    assert a.c2() == b.c2() and "average 0.5" in a.c2()
+    sa, sb = a.snapshot(), b.snapshot()
+    for k in sa:
+        if k != "seq":
+            assert sa[k] == sb[k], k
