@@ -269,10 +269,11 @@ class ElasticGroup:
         outs = self._gather_outs[slot] if self.rank == 0 else []
         return pg.gather(outs, [self._send[slot]], opts)
 
-    def wait(self, work, check=None) -> None:
+    def wait(self, work, check=None, spin_s: float = 0.001) -> None:
         """Poll ``work`` until it completes; ``check()`` raises RoundAbandoned
-        (liveness) between polls.  Spins ~1 ms, then sleeps ``poll_s``,
-        backing off to 4x after 10 ms and 20x after 1 s."""
+        (liveness) between polls.  Spins ``spin_s`` (the coordinator's gather:
+        on the critical path), then sleeps ``poll_s``, backing off to 4x after
+        10 ms and 20x after 1 s."""
         if work is None:
             return
         t0 = time.perf_counter()
@@ -282,7 +283,7 @@ class ElasticGroup:
             if self.pg is None:
                 raise RoundAbandoned("epoch torn down")
             waited = time.perf_counter() - t0
-            if waited > 0.001:
+            if waited >= spin_s:
                 time.sleep(self.poll_s * (1 if waited < 0.01 else 4 if waited < 1.0 else 20))
         work.wait()
 
@@ -296,7 +297,9 @@ class ElasticGroup:
         if self.device.type == "cuda":
             work.wait()
         else:
-            self.wait(work, check)
+            # off the critical path (the slot is reused depth rounds later): sleep
+            # between polls instead of spinning a core the coordinator needs
+            self.wait(work, check, spin_s=0.0)
 
     def collect(self, seq: int, work, check=None) -> np.ndarray:
         """Rank 0: wait for round ``seq``'s gather and return the whole round

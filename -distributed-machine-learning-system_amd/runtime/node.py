@@ -198,6 +198,8 @@ class Node:
             self._ingest_result(msg)
             return None
         if t == Type.RESULTS:                   # one finished round, mirrored to the standby
+            if "rows" in msg:
+                self._ingest_mirrored_round(msg)
             for r in msg.get("results", []):
                 self._ingest_result(dict(r, src=msg.get("src")))
             return None
@@ -431,6 +433,22 @@ class Node:
             with self._progress:
                 self._progress.notify_all()
         return new
+
+    def _ingest_mirrored_round(self, msg: dict) -> int:
+        """Standby: a round the coordinator mirrored as one frame (rounds.py
+        ``_mirror``): row table + concatenated class / probability planes."""
+        cls = np.frombuffer(msg["cls"], dtype=np.int32)
+        prob = np.frombuffer(msg["prob"], dtype=np.float32)
+        recs, o = [], 0
+        for m, q, w, s, e in msg["rows"]:
+            k = e - s + 1
+            recs.append((m, q, w, s, e, cls[o:o + k], prob[o:o + k]))
+            o += k
+        if o != cls.size or o != prob.size:
+            self.logger.error("mirrored round from %s: %d rows cover %d images, planes hold %d / %d",
+                              msg.get("src"), len(recs), o, cls.size, prob.size)
+            return 0
+        return self._ingest_round(recs, self.state.clock())
 
     MAX_CHUNK_RETRIES = 3
 

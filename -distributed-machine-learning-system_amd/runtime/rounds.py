@@ -78,6 +78,8 @@ class _Round:
 
 class RoundPlane:
     HDR_RING = 4        # pinned header buffers (> depth: a slot is rewritten only after its gather)
+    CHECK_PERIOD_S = 0.002   # liveness re-check period inside a coordinator's poll loops
+    ANNOUNCE_ROUNDS = 4      # rounds whose descriptors share one multicast frame (backlog only)
 
     def __init__(self, node, device):
         self.node = node
@@ -113,7 +115,11 @@ class RoundPlane:
         self._mirror_q = None                 # coordinator: rounds waiting for the standby mirror thread
         # coordinator host time: building / posting rounds and ingesting them (host_s), and
         # blocked on a gather (host_wait_s); bench.py reports host_s per round
+        self._built_for = None                # member set of the last _build (stale sweep on change)
+        self._announced: deque = deque()      # coordinator: rounds multicast but not yet posted
+        self.announce_frames = 0              # descriptor frames sent (<= rounds posted)
         self.host_s = 0.0
+        self.host_cpu_s = 0.0                 # the same spans in driver-thread CPU time (no preemption)
         self.host_wait_s = 0.0
         self.launch_cpu_s = 0.0               # thread CPU time of this node's chunk launches
         self.host_post_s = 0.0                # of host_s: posting (descriptors, own chunk, gather)
@@ -169,12 +175,18 @@ class RoundPlane:
         self._wake.set()
 
     def on_round(self, msg: dict) -> None:
-        """Member: a ROUND descriptor (or STOP) from the coordinator."""
+        """Member: a ROUND descriptor (or STOP, or a batch of consecutive
+        rounds' descriptors) from the coordinator."""
         with self.cv:
             ep = int(msg["epoch"])
             if ep < self.epoch:
                 return
-            self._round_msgs[(ep, int(msg["seq"]))] = msg
+            batch = msg.get("batch")
+            if batch is not None:
+                for seq, rows in batch:
+                    self._round_msgs[(ep, int(seq))] = {"t": msg["t"], "epoch": ep, "seq": int(seq), "rows": rows}
+            else:
+                self._round_msgs[(ep, int(msg["seq"]))] = msg
             self.cv.notify_all()
 
     def try_enqueue(self, model: str, qnum, plan) -> bool:
@@ -205,8 +217,8 @@ class RoundPlane:
                 "mixed_rounds": self.mixed_rounds, "mixed_splits": dict(self.mixed_splits),
                 "max_queries_per_round": self.max_queries_per_round,
                 "parked": self.parked, "pending_collectives": self.pending_collectives(),
-                "host_s": self.host_s, "host_wait_s": self.host_wait_s, "host_post_s": self.host_post_s,
-                "host_send_s": self.host_send_s, "launch_cpu_s": self.launch_cpu_s,
+                "host_s": self.host_s, "host_cpu_s": self.host_cpu_s, "host_wait_s": self.host_wait_s, "host_post_s": self.host_post_s,
+                "host_send_s": self.host_send_s, "announce_frames": self.announce_frames, "launch_cpu_s": self.launch_cpu_s,
                 "queued": len(self._queue)}
 
     def pending_collectives(self) -> int:
@@ -218,14 +230,23 @@ class RoundPlane:
     def _check_coordinator(self, members: list[str]):
         n = self.node
 
+        others = [m for m in members if m != n.name]
+        last = [0.0]
+
         def check():
             if not n.alive_flag:
                 raise RoundAbandoned("node stopping")
             if not n.is_coordinator:
                 raise RoundAbandoned("no longer coordinator")
+            # the detector's verdicts move on a heartbeat period (>= 0.1 s): a poll
+            # loop re-reads the member table at most every CHECK_PERIOD_S, not per spin
+            t = time.perf_counter()
+            if t - last[0] < self.CHECK_PERIOD_S:
+                return
+            last[0] = t
             # ANY member the detector now marks dead (a member that dies
             # during the round must count, not only one already dead at its start)
-            dead = [m for m in members if m != n.name and not n.membership.is_alive(m)]
+            dead = [m for m in others if not n.membership.is_alive(m)]
             if dead:
                 raise RoundAbandoned(f"member(s) {dead} failed")
         return check
@@ -315,7 +336,9 @@ class RoundPlane:
             return
         import cProfile
 
-        pr = cProfile.Profile()
+        # IDUNNO_PROFILE_DRIVER_CPU=1: the thread's CPU clock (preemption and GIL
+        # waits under host contention do not count)
+        pr = cProfile.Profile(time.thread_time) if os.environ.get("IDUNNO_PROFILE_DRIVER_CPU") else cProfile.Profile()
         pr.enable()
         try:
             self._drive()
@@ -379,63 +402,89 @@ class RoundPlane:
         workers are all still free joins; a query that does not fit reserves
         its workers (no starvation).  Queued queries are first re-split onto
         the current fair-time partition (``_replan``).  Returns (queries,
-        stale) where stale queries were planned for another member set (-> TCP)."""
+        stale) where stale queries were planned for another member set (-> TCP).
+
+        The scan stops once every member is taken or reserved (nothing further
+        back can join this round), so a deep backlog costs O(members) per
+        round, not O(queue); the unscanned tail keeps its order.  Stale queries
+        exist only after a member-set change: the first build of an epoch
+        sweeps the whole queue for them."""
         with self.cv:
-            qs, self._queue = list(self._queue), deque()
-        if not qs:
+            rest, self._queue = self._queue, deque()
+        if not rest:
             return [], []
         take, stale, keep = [], [], []
-        live = [q for q in qs if q.members == members]
-        stale = [q for q in qs if q.members != members]
-        self._replan(live, members)
+        if self._built_for != members:
+            self._built_for = members
+            stale = [q for q in rest if q.members != members]
+            if stale:
+                rest = deque(q for q in rest if q.members == members)
+        part = self._replan_part(members)
         used, reserved = set(), set()
-        for q in live:
+        nm = len(members)
+        while rest and len(used) + len(reserved) < nm:
+            q = rest.popleft()
+            if q.members != members:
+                stale.append(q)
+                continue
+            if part is not None:
+                self._replan_one(q, part)
             ws = set(q.rows)
-            if ws & used or ws & reserved or len(used) >= len(members):
-                reserved |= ws
+            if ws & used or ws & reserved:
+                reserved |= ws - used
                 keep.append(q)
             else:
                 used |= ws
                 take.append(q)
+        rest.extendleft(reversed(keep))
         with self.cv:
-            keep.extend(self._queue)               # queued while we were packing
-            self._queue = deque(keep)
+            rest.extend(self._queue)               # queued while we were packing
+            self._queue = rest
         return take, stale
 
-    def _replan(self, qs: list, members: tuple) -> None:
-        """Move queued (not yet posted) queries onto the current partition.
+    def _replan_part(self, members: tuple):
+        """The fair-time partition queued queries move onto (``_replan_one``),
+        or None while fewer than two jobs are active."""
+        n = self.node
+        active = n.state.active_models()
+        if len(active) < 2:
+            return None
+        alive = set(n.membership.alive())
+        return n.sched.subsets(active, [w for w in sorted(members) if w in alive])
+
+    def _replan_one(self, q, part: dict) -> None:
+        """Move a queued (not yet posted) query onto the current partition.
         A query planned while its job ran alone holds every GPU; once a second
         job is active it is re-split onto its own fair-time subset, so the two
         jobs share the very next round instead of after the first job's backlog
         drains.  The change is a replicated job-state op (the standby sees it)."""
-        n = self.node
-        if not qs:
+        tgt = part.get(q.model)
+        if not tgt or set(tgt) == set(q.rows):
             return
-        active = n.state.active_models()
-        if len(active) < 2:
+        s0 = min(s for s, _ in q.rows.values())
+        e0 = max(e for _, e in q.rows.values())
+        new = [(w, s, e) for w, (s, e) in zip(tgt, split_range(s0, e0, len(tgt)))]
+        if any(e - s + 1 > self.cfg.max_chunk for _, s, e in new):
             return
-        alive = set(n.membership.alive())
-        part = n.sched.subsets(active, [w for w in sorted(members) if w in alive])
-        for q in qs:
-            tgt = part.get(q.model)
-            if not tgt or set(tgt) == set(q.rows):
-                continue
-            s0 = min(s for s, _ in q.rows.values())
-            e0 = max(e for _, e in q.rows.values())
-            new = [(w, s, e) for w, (s, e) in zip(tgt, split_range(s0, e0, len(tgt)))]
-            if any(e - s + 1 > self.cfg.max_chunk for _, s, e in new):
-                continue
-            old = [(w, s, e) for w, (s, e) in q.rows.items()]
-            if n.state.replan(q.model, q.qnum, old, new):
-                q.rows = {w: (s, e) for w, s, e in new}
+        old = [(w, s, e) for w, (s, e) in q.rows.items()]
+        if self.node.state.replan(q.model, q.qnum, old, new):
+            q.rows = {w: (s, e) for w, s, e in new}
 
     def _serve(self) -> None:
         """Run rounds of the current epoch until the queue is drained and a
-        re-form / release / role change asks to stop (coordinator)."""
+        re-form / release / role change asks to stop (coordinator).
+
+        With a backlog, up to ``ANNOUNCE_ROUNDS`` rounds are built at once and
+        their descriptor tables go to the members in ONE multicast frame (the
+        per-member send is the coordinator's largest per-round cost that grows
+        with the group); each is then posted when its slot frees.  A lone query
+        is announced and posted at once, as before."""
         n, g = self.node, self.group
         members = tuple(g.members)
         check = self._check_coordinator(list(members))
         inflight = self._inflight
+        announced: deque = deque()              # multicast, not yet posted (members expect them)
+        self._announced = announced
         idle_since = time.monotonic()
         try:
             while n.alive_flag and n.is_coordinator and not self._reform_due():
@@ -445,12 +494,15 @@ class RoundPlane:
                     self._finalize_oldest(members, check)
                 while inflight and inflight[0].work.is_completed():
                     self._finalize_oldest(members, check)
-                tb = time.perf_counter()
-                qs, stale = self._build(members)
-                self.host_s += time.perf_counter() - tb
-                for q in stale:
-                    self._fallback_query(q)
-                if not qs:
+                if not announced:
+                    tb, cb = time.perf_counter(), time.thread_time()
+                    rounds = self._build_rounds(members)
+                    if rounds:
+                        self._announce(rounds, members)
+                        announced.extend(rounds)
+                    self.host_s += time.perf_counter() - tb
+                    self.host_cpu_s += time.thread_time() - cb
+                if not announced:
                     if inflight:
                         # the next query (a job's window refills on ingest) may arrive
                         # while the oldest round still computes: post it as soon as it
@@ -466,14 +518,12 @@ class RoundPlane:
                         return        # hand back to the driver loop now and then (cheap)
                     continue
                 idle_since = time.monotonic()
-                tp = time.perf_counter()
-                r = _Round(self._next_seq, qs, self._table(members, qs))
-                self._next_seq += 1
-                inflight.append(r)
-                self._post(r, members)
-                dt = time.perf_counter() - tp
-                self.host_s += dt
-                self.host_post_s += dt
+                self._post_next(announced, members)
+            # rounds already announced are owed to the members (they wait for each seq)
+            while announced:
+                while len(inflight) >= g.depth:
+                    self._finalize_oldest(members, check)
+                self._post_next(announced, members)
             while inflight:
                 self._finalize_oldest(members, check)
             self._stop_epoch()
@@ -483,7 +533,8 @@ class RoundPlane:
             self.rounds_failed += 1
             log.warning("%s: round failed in epoch %d (%s); falling back to TCP", n.name, g.epoch, e)
             n.tracer.instant("round.failed", epoch=g.epoch)
-            lost = list(inflight)
+            lost = list(inflight) + list(announced)
+            announced.clear()
             self._drop_group(abandoned=True)
             for r in lost:
                 for q in r.queries:
@@ -495,6 +546,54 @@ class RoundPlane:
             # the failure detector re-forms on a death; re-form anyway in case it was
             # transient -- after the detector had time to drop a dead member
             self.schedule_reform("round failure", delay=self.cfg.failure_timeout_s * 1.2)
+
+    def _build_rounds(self, members: tuple) -> list:
+        """Up to ANNOUNCE_ROUNDS consecutive rounds from the queue (stale
+        queries go to the TCP path).  Rounds after the first are committed
+        ahead only when they occupy every member: a partial round stays queued,
+        so a query arriving meanwhile (the other job's, two-job sharing) can
+        still join it."""
+        out = []
+        for k in range(self.ANNOUNCE_ROUNDS):
+            qs, stale = self._build(members)
+            for q in stale:
+                self._fallback_query(q)
+            if not qs:
+                break
+            if k and sum(len(q.rows) for q in qs) < len(members):
+                with self.cv:
+                    self._queue.extendleft(reversed(qs))
+                break
+            out.append(_Round(self._next_seq, qs, self._table(members, qs)))
+            self._next_seq += 1
+        return out
+
+    def _announce(self, rounds: list, members: tuple) -> None:
+        """ONE frame with the descriptor tables of ``rounds`` (member i reads
+        row i of each), encoded once and written to every member's link."""
+        n, g = self.node, self.group
+        ts = time.perf_counter()
+        rows = lambda r: [list(row) if row else None for row in r.table]      # noqa: E731
+        if len(rounds) == 1:
+            msg = {"t": Type.ROUND, "epoch": g.epoch, "seq": rounds[0].seq, "rows": rows(rounds[0])}
+        else:
+            msg = {"t": Type.ROUND, "epoch": g.epoch, "seq": rounds[0].seq,
+                   "batch": [[r.seq, rows(r)] for r in rounds]}
+        lost = n.transport.multicast(members[1:], msg)
+        if lost:
+            raise RoundAbandoned(f"ROUND {rounds[0].seq}..{rounds[-1].seq} to {lost} not delivered")
+        self.host_send_s += time.perf_counter() - ts
+        self.announce_frames += 1
+
+    def _post_next(self, announced: deque, members: tuple) -> None:
+        tp, cp = time.perf_counter(), time.thread_time()
+        r = announced.popleft()
+        self._inflight.append(r)
+        self._post(r, members)
+        dt = time.perf_counter() - tp
+        self.host_s += dt
+        self.host_post_s += dt
+        self.host_cpu_s += time.thread_time() - cp
 
     def _wait_queue_or(self, work, check) -> None:
         t0 = time.perf_counter()
@@ -516,16 +615,9 @@ class RoundPlane:
         return table
 
     def _post(self, r: _Round, members: tuple) -> None:
-        n, g = self.node, self.group
-        ts = time.perf_counter()
-        # ONE frame with the whole descriptor table (member i reads row i), encoded
-        # once and written to every member's link
-        msg = {"t": Type.ROUND, "epoch": g.epoch, "seq": r.seq,
-               "rows": [list(row) if row else None for row in r.table]}
-        lost = n.transport.multicast(members[1:], msg)
-        if lost:
-            raise RoundAbandoned(f"ROUND {r.seq} to {lost} not delivered")
-        self.host_send_s += time.perf_counter() - ts
+        """Run the coordinator's own chunk of announced round ``r`` and post
+        its gather."""
+        g = self.group
         if r.table[0] is not None:
             self._run_chunk(r.table[0], r.seq)
         self._write_header(r.seq)
@@ -556,7 +648,7 @@ class RoundPlane:
         n, g = self.node, self.group
         t_wait = time.perf_counter()
         arr = g.collect(r.seq, r.work, check)
-        t0 = time.perf_counter()
+        t0, c0 = time.perf_counter(), time.thread_time()
         self.host_wait_s += t0 - t_wait
         mc = g.max_chunk
         now = time.time()
@@ -601,6 +693,7 @@ class RoundPlane:
         if recs and n.standby != n.name and n.membership.is_alive(n.standby):
             self._mirror(recs, now)
         self.host_s += time.perf_counter() - t0
+        self.host_cpu_s += time.thread_time() - c0
 
     def _mirror(self, recs: list, now: float) -> None:
         """Queue a finished round for the standby (RESULTS message built and
@@ -618,11 +711,15 @@ class RoundPlane:
                     if item is None:
                         return
                     rs, t = item
-                    batch = [{"t": Type.RESULT, "model": m, "qnum": q, "start": s, "end": e, "worker": w,
-                              "cls": c.tobytes(), "prob": p.tobytes(), "epoch": n.membership.epoch, "t_done": t}
-                             for m, q, w, s, e, c, p in rs]
+                    # the whole round as ONE frame: a row table plus two concatenated
+                    # planes (not a dict + two byte strings per chunk), ingested by the
+                    # standby with one record_results call
+                    msg = {"t": Type.RESULTS, "rows": [[m, q, w, s, e] for m, q, w, s, e, _, _ in rs],
+                           "cls": np.concatenate([r[5] for r in rs]).astype(np.int32, copy=False).tobytes(),
+                           "prob": np.concatenate([r[6] for r in rs]).astype(np.float32, copy=False).tobytes(),
+                           "epoch": n.membership.epoch, "t_done": t}
                     if n.standby != n.name and n.membership.is_alive(n.standby):
-                        n.transport.send(n.standby, {"t": Type.RESULTS, "results": batch})
+                        n.transport.send(n.standby, msg)
 
             threading.Thread(target=run, name=f"{self.node.name}-mirror", daemon=True).start()
         self._mirror_q.put((recs, now))

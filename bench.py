@@ -1214,6 +1214,7 @@ def _drive_system(a, node, W: int, B: int) -> dict:
         # the coordinator's own host work per round (plan, post, ingest; not the gather wait)
         nr = rb["rounds_done"] - ra["rounds_done"]
         out["system_host_ms_per_round"] = round(1000 * (rb["host_s"] - ra["host_s"]) / nr, 4)
+        out["system_host_cpu_ms_per_round"] = round(1000 * (rb["host_cpu_s"] - ra["host_cpu_s"]) / nr, 4)
         out["system_host_wait_ms_per_round"] = round(1000 * (rb["host_wait_s"] - ra["host_wait_s"]) / nr, 4)
         out["system_rounds"] = nr
         out["system_host_post_ms_per_round"] = round(1000 * (rb["host_post_s"] - ra["host_post_s"]) / nr, 4)

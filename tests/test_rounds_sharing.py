@@ -173,31 +173,29 @@ def test_two_jobs_share_the_rounds_on_8_ranks():
         done = {"alexnet": 0, "resnet18": 0}
 
         def run_jobs(models, base_img):
-            t0 = time.monotonic()
+            t0, r0 = time.monotonic(), cl.view("rounds")["rounds_done"]
             for m in models:
                 cl.submit_job(base_img, base_img + Q * bs[m] - 1, m)
                 done[m] += Q * bs[m]
             s = cl.wait_idle(60, dict(done))
             assert all(s["done"].get(m, 0) == done[m] for m in done), s
-            return time.monotonic() - t0
+            return time.monotonic() - t0, cl.view("rounds")["rounds_done"] - r0
 
-        t_r = run_jobs(["resnet18"], 0)
-        t_a = run_jobs(["alexnet"], 0)
+        t_r, n_r = run_jobs(["resnet18"], 0)
+        t_a, n_a = run_jobs(["alexnet"], 0)
         before = cl.view("rounds")
-        t_both = run_jobs(["alexnet", "resnet18"], 10_000)
+        t_both, n_both = run_jobs(["alexnet", "resnet18"], 10_000)
         after = cl.view("rounds")
+        print(f"alone: alexnet {t_a:.2f}s / {n_a} rounds, resnet18 {t_r:.2f}s / {n_r} rounds; "
+              f"together {t_both:.2f}s / {n_both} rounds; rounds {before} -> {after}")
         # both models' chunks in the same round tables, on disjoint worker subsets
         assert after["mixed_rounds"] - before["mixed_rounds"] >= Q - 3, (before, after)
         assert after["max_queries_per_round"] >= 2
-        print(f"alone: alexnet {t_a:.2f}s resnet18 {t_r:.2f}s; together {t_both:.2f}s; rounds {before} -> {after}")
-        # space sharing: about the slower job alone, well under the time-sliced sum
-        # (1.2x held in quiet runs; 1.25x seen with the whole CPU suite loading the
-        # 8 processes, hence the margin).  Under pytest-xdist the other workers
-        # starve these 8 processes unevenly (6.4 s vs 4.8/3.0 s alone seen at -n 4), so
-        # the wall-clock bound is enforced in serial runs only; the round-table
-        # checks above hold either way.
-        if not os.environ.get("PYTEST_XDIST_WORKER"):
-            assert t_both <= 1.35 * max(t_a, t_r) and t_both <= 0.8 * (t_a + t_r), (t_a, t_r, t_both)
+        # space sharing, counted in rounds (each round costs one per-chunk delay on
+        # every member, whatever the host load): the two jobs together take about
+        # as many rounds as the longer job alone, well under the time-sliced sum.
+        # A wall-clock bound here failed under CPU contention.
+        assert n_both <= max(n_a, n_r) + 3 and n_both <= 0.75 * (n_a + n_r), (n_a, n_r, n_both)
 
         # idle gap longer than the collective-op timeout: nothing is posted while idle,
         # so the epoch survives and the next query runs as a round in it

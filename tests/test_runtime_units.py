@@ -229,7 +229,7 @@ def test_round_finalize_reruns_range_guard_rows_only():
         membership=types.SimpleNamespace(is_alive=lambda n: True))
     rp = RoundPlane.__new__(RoundPlane)
     rp.node, rp.group, rp.cfg = node, G(), ClusterConfig()
-    rp.host_s = rp.host_wait_s = 0.0
+    rp.host_s = rp.host_wait_s = rp.host_cpu_s = 0.0
     rp.rounds_done = 0
     table = [(mid, 7, 0, 3), (mid, 7, 4, 7), (mid, 7, 8, 13)]
     rp._finalize(_Round(1, [], table), ("node00", "node01", "node02"), None)
@@ -267,3 +267,49 @@ def test_send_frame_falls_back_when_the_socket_buffer_is_full():
         for _ in range(64):                         # the peer is gone: EPIPE / ECONNRESET
             _send_frame(a, data[:1 << 16])
     a.close()
+
+
+def test_round_batch_announce_and_member_unpack():
+    """Coordinator: with a backlog of full rounds, up to ANNOUNCE_ROUNDS
+    descriptor tables share ONE multicast frame; a partial round after the
+    first stays queued (another job's query may still join it).  Member: a
+    batch frame is unpacked into per-seq descriptors."""
+    import threading as th
+    from collections import deque
+
+    from idunno.config import ClusterConfig
+    from idunno.runtime.rounds import RoundPlane, _Query
+
+    members = ("node00", "node01", "node02", "node03")
+    frames = []
+    node = types.SimpleNamespace(
+        name="node00", transport=types.SimpleNamespace(multicast=lambda d, m: frames.append((list(d), m)) or []),
+        state=types.SimpleNamespace(active_models=lambda: {"resnet18"}),
+        membership=types.SimpleNamespace(alive=lambda: list(members)))
+    rp = RoundPlane.__new__(RoundPlane)
+    rp.node, rp.cfg, rp.cv = node, ClusterConfig(), th.Condition()
+    rp.group = types.SimpleNamespace(epoch=5)
+    rp._queue, rp._built_for, rp._next_seq = deque(), None, 0
+    rp.host_send_s, rp.announce_frames = 0.0, 0
+    full = lambda q: _Query("resnet18", q, {m: (100 * q + i, 100 * q + i) for i, m in enumerate(members)}, members)  # noqa: E731
+    half = _Query("alexnet", 9, {"node00": (0, 0), "node01": (1, 1)}, members)
+    rp._queue.extend([full(1), full(2), half, full(3)])
+    rounds = rp._build_rounds(members)
+    assert [r.seq for r in rounds] == [0, 1]                  # the partial 3rd round is not committed
+    assert [q.qnum for q in rp._queue] == [9, 3]              # ... and keeps its queue position
+    rp._announce(rounds, members)
+    assert len(frames) == 1 and frames[0][0] == list(members[1:])
+    msg = frames[0][1]
+    from idunno.parallel.elastic import MODEL_IDS
+    rid = MODEL_IDS["resnet18"]
+    assert [s for s, _ in msg["batch"]] == [0, 1] and msg["batch"][1][1][2] == [rid, 2, 202, 202]
+    # a partial FIRST round is built as before (posted at once); a full one may follow it
+    rounds = rp._build_rounds(members)
+    assert [r.seq for r in rounds] == [2, 3] and [q.qnum for q in rounds[0].queries] == [9]
+    assert not rp._queue
+    # member side
+    mem = RoundPlane.__new__(RoundPlane)
+    mem.cv, mem.epoch, mem._round_msgs = th.Condition(), 5, {}
+    mem.on_round(dict(msg, src="node00"))
+    assert sorted(mem._round_msgs) == [(5, 0), (5, 1)]
+    assert mem._round_msgs[(5, 1)]["rows"][3] == [rid, 2, 203, 203]
