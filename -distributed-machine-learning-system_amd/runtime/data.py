@@ -91,13 +91,22 @@ class HbmStager:
     READ_THREADS = 8
 
     def stage_file(self, path: str, shape: tuple) -> torch.Tensor:
+        """``_stage_file`` with the current stream ordered after the copy."""
+        t, ev = self._stage_file(path, shape)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+        return t
+
+    def _stage_file(self, path: str, shape: tuple):
         """Stage a file's bytes into a new device tensor of ``shape`` (uint8)
         without a host copy of the file: each piece is read with ``os.preadv``
         by up to READ_THREADS threads straight into a pinned ping-pong buffer (the
         reads release the GIL), then DMA'd on the side stream while the next
         piece is read into the other buffer.  A bytes object of a large file
         costs fresh page faults on every read (~1.5 GB/s on these hosts); the
-        pinned buffers are faulted in once."""
+        pinned buffers are faulted in once.  Returns (tensor, event of its last
+        copy); the tensor is allocated on the side stream (hand-outs to other
+        streams call ``record_stream``, see SdfsSource._shard)."""
         nbytes = int(np.prod(shape))
         fd = os.open(path, os.O_RDONLY)
         try:
@@ -107,8 +116,9 @@ class HbmStager:
                 buf = np.empty(nbytes, np.uint8)
                 self._pread(fd, memoryview(buf), 0)
                 self.bytes_staged += nbytes
-                return torch.from_numpy(buf).view(*shape)
-            out = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+                return torch.from_numpy(buf).view(*shape), None
+            with torch.cuda.stream(self.stream):
+                out = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
             step = self.pinned[0].numel()
             nb = len(self.pinned)
             with self.lock:
@@ -135,9 +145,7 @@ class HbmStager:
                 self.bytes_staged += nbytes
         finally:
             os.close(fd)
-        if ev is not None:
-            torch.cuda.current_stream(self.device).wait_event(ev)
-        return out.view(*shape)
+        return out.view(*shape), ev
 
     def _pread(self, fd: int, dst: memoryview, off: int) -> None:
         """Fill ``dst`` from file offset ``off`` with parallel preadv calls."""
@@ -169,12 +177,21 @@ class HbmStager:
         """Copy host bytes to a new device tensor of ``shape`` (uint8).  The
         current stream is made to wait for the copy; nothing blocks the host
         beyond the ping-pong buffer reuse."""
+        t, ev = self._stage(data, shape)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+        return t
+
+    def _stage(self, data, shape: tuple):
+        """``stage`` without the current-stream wait: (tensor, event of its
+        last copy), the tensor allocated on the side stream."""
         src = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) \
             else np.ascontiguousarray(data).reshape(-1).view(np.uint8)
         if not self.gpu:
             self.bytes_staged += src.size
-            return torch.from_numpy(src.copy()).view(*shape)
-        out = torch.empty(src.size, dtype=torch.uint8, device=self.device)
+            return torch.from_numpy(src.copy()).view(*shape), None
+        with torch.cuda.stream(self.stream):
+            out = torch.empty(src.size, dtype=torch.uint8, device=self.device)
         step = self.pinned[0].numel()
         nb = len(self.pinned)
         with self.lock:
@@ -199,9 +216,7 @@ class HbmStager:
                 ev1.record(self.stream)
                 tl.append(("h2d", ev0, ev1, src.size))
             self.bytes_staged += src.size
-        if ev is not None:
-            torch.cuda.current_stream(self.device).wait_event(ev)
-        return out.view(*shape)
+        return out.view(*shape), ev
 
 
 def shard_name(k: int) -> str:
@@ -233,7 +248,11 @@ class SdfsSource:
         # a background thread, so its SDFS read and H2D copy (side stream) run while the
         # current chunk computes instead of in front of the next one
         self.readahead = int(readahead)
+        self.max_queued = max(2, 2 * self.readahead)   # background fetches queued or running at most
         self._inflight: dict[int, object] = {}     # shard -> Future of a background fetch
+        self._ready: dict[int, object] = {}        # shard -> event of its last H2D copy (side stream)
+        self._rec: set = set()                    # (shard, stream) pairs already record_stream'ed
+        self._ahead: set = set()                  # shards a background fetch put in the cache
         self._absent: set = set()                 # shards a readahead found missing (past the dataset's end)
         self._pool = None
         self.readahead_hits = 0
@@ -256,15 +275,24 @@ class SdfsSource:
             t = self.cache.get(k) if k is not None else None
             if t is not None and ver is not None and self.ver.get(k) != int(ver):
                 t = None
+            ev = self._ready.get(k) if t is not None else None
         if t is None:
             return None
-        torch.cuda.current_stream(self.device).synchronize()     # staged bytes have landed
+        if ev is not None:
+            ev.synchronize()                                      # its staged bytes have landed
+        else:
+            torch.cuda.current_stream(self.device).synchronize()
         return export_tensor(t, consumer_pid)
 
-    def _prefetch(self, k: int) -> None:
-        """Start fetching shard k in the background unless cached or in flight."""
+    def _prefetch(self, k: int, requested: bool = False) -> None:
+        """Start fetching shard k in the background unless cached or in flight.
+        One worker, FIFO, so shards stage in request order.  Speculative
+        readahead (past a request) is bounded to ``max_queued`` background
+        fetches; a shard an announced chunk needs (``requested``) always queues."""
         with self.lock:
             if k in self.cache or k in self._inflight or k in self._absent:
+                return
+            if not requested and len(self._inflight) >= self.max_queued:
                 return
             if self._pool is None:
                 from concurrent.futures import ThreadPoolExecutor
@@ -278,7 +306,10 @@ class SdfsSource:
                 ctx = torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()
                 try:
                     with ctx:
-                        return self._fetch(k)
+                        t = self._fetch(k)
+                    with self.lock:
+                        self._ahead.add(k)
+                    return t
                 except KeyError:
                     with self.lock:
                         self._absent.add(k)              # not asked again by readahead
@@ -292,26 +323,42 @@ class SdfsSource:
         """Start staging every shard of images [start, end] in the background
         (in request order, behind shards already queued)."""
         for k in range(start // self.S, end // self.S + 1):
-            self._prefetch(k)
+            self._prefetch(k, requested=True)
 
     def _shard(self, k: int) -> torch.Tensor:
         with self.lock:
             t = self.cache.get(k)
             if t is not None:
                 self.cache.move_to_end(k)
-                return t
-            fut = self._inflight.get(k)
-        if fut is not None:
+            fut = self._inflight.get(k) if t is None else None
+        if t is None and fut is not None:
             try:
                 t = fut.result()
-                self.readahead_hits += 1
-                if self.device.type == "cuda":
-                    # its H2D ran on the stager's side stream: order the consumer after it
-                    torch.cuda.current_stream(self.device).wait_stream(self.stager.stream)
-                return t
             except Exception:  # noqa: BLE001  (fetch again below; a missing shard raises there)
-                pass
-        return self._fetch(k)
+                t = None
+        if t is None:
+            t = self._fetch(k)
+        return self._hand_out(k, t)
+
+    def _hand_out(self, k: int, t: torch.Tensor) -> torch.Tensor:
+        """Order the caller's current stream after shard k's own H2D copy (its
+        event, not the whole side stream, which may hold later readahead), and
+        record that stream on the tensor so the allocator keeps the block until
+        the consumer's work is done if the shard is evicted."""
+        with self.lock:
+            if k in self._ahead:
+                self._ahead.discard(k)
+                self.readahead_hits += 1
+            ev = self._ready.get(k)
+        if self.device.type == "cuda":
+            cs = torch.cuda.current_stream(self.device)
+            if ev is not None:
+                cs.wait_event(ev)
+            key = (k, cs.cuda_stream)
+            if key not in self._rec:
+                t.record_stream(cs)
+                self._rec.add(key)
+        return t
 
     def _fetch(self, k: int) -> torch.Tensor:
         with self.lock:
@@ -320,6 +367,7 @@ class SdfsSource:
                 return t
         name = shard_name(k)
         got = self.sdfs.fetch_hbm(name, self.device) if self.peer_copy else None
+        ev = None
         if got is not None:
             t, ver = got
             self.peer_fetches += 1
@@ -331,7 +379,7 @@ class SdfsSource:
                 path, ver = loc
                 try:
                     n = os.path.getsize(path) // IMG_BYTES
-                    t = self.stager.stage_file(path, (n, HW, HW, 3))
+                    t, ev = self.stager._stage_file(path, (n, HW, HW, 3))
                     self.local_reads += 1
                 except OSError:                   # replaced by a newer version meanwhile
                     loc = None
@@ -341,16 +389,20 @@ class SdfsSource:
                     raise KeyError(f"missing SDFS shard {name}")
                 data, ver = got
                 n = len(data) // IMG_BYTES
-                t = self.stager.stage(data, (n, HW, HW, 3))
+                t, ev = self.stager._stage(data, (n, HW, HW, 3))
         dropped = []
         with self.lock:
             self.fetches += 1
             self.cache[k] = t
             self.ver[k] = ver
+            self._ready[k] = ev
             tot = sum(v.numel() for v in self.cache.values())
             while tot > self.cache_bytes and len(self.cache) > 1:
                 ko, old = self.cache.popitem(last=False)
                 self.ver.pop(ko, None)
+                self._ready.pop(ko, None)
+                self._ahead.discard(ko)
+                self._rec = {x for x in self._rec if x[0] != ko}
                 tot -= old.numel()
                 dropped.append(ko)
         if self.device.type == "cuda":

@@ -188,6 +188,21 @@ class RoundPlane:
             else:
                 self._round_msgs[(ep, int(msg["seq"]))] = msg
             self.cv.notify_all()
+            me = self.members.index(self.node.name) if ep == self.epoch and self.node.name in self.members else -1
+        if me >= 0:
+            # the images of this member's announced chunks start staging now (SDFS
+            # readahead in request order), not when the round loop reaches them
+            for rows in ([r for _, r in batch] if batch is not None else [msg.get("rows")]):
+                if rows is not None and me < len(rows) and rows[me] is not None:
+                    self._readahead(rows[me][2], rows[me][3])
+
+    def _readahead(self, s: int, e: int) -> None:
+        pre = getattr(self.node.source, "prefetch", None)
+        if pre is not None:
+            try:
+                pre(int(s), int(e))
+            except Exception:  # noqa: BLE001  (best effort: the round's own get() fetches)
+                log.debug("%s: readahead of [%s, %s] failed", self.node.name, s, e, exc_info=True)
 
     def try_enqueue(self, model: str, qnum, plan) -> bool:
         """Coordinator: queue a query for the round path if the group covers its
@@ -208,6 +223,9 @@ class RoundPlane:
             self._queue.append(q)
             self.cv.notify_all()
         self._wake.set()
+        own = q.rows.get(self.node.name)
+        if own is not None:
+            self._readahead(*own)
         return True
 
     def stats(self) -> dict:

@@ -309,7 +309,10 @@ def test_round_batch_announce_and_member_unpack():
     assert not rp._queue
     # member side
     mem = RoundPlane.__new__(RoundPlane)
-    mem.cv, mem.epoch, mem._round_msgs = th.Condition(), 5, {}
+    mem.cv, mem.epoch, mem._round_msgs, mem.members = th.Condition(), 5, {}, list(members)
+    staged = []
+    mem.node = types.SimpleNamespace(name="node02", source=types.SimpleNamespace(prefetch=lambda s, e: staged.append((s, e))))
     mem.on_round(dict(msg, src="node00"))
+    assert staged == [(102, 102), (202, 202)]          # its announced chunks start staging at once
     assert sorted(mem._round_msgs) == [(5, 0), (5, 1)]
     assert mem._round_msgs[(5, 1)]["rows"][3] == [rid, 2, 203, 203]
