@@ -101,6 +101,12 @@ class QueryPlane:
             self._packs = [torch.zeros(max_chunk, 2, dtype=torch.int32, device=dev) for _ in range(nbuf)]
         self._pack = self._packs[0]
         self._desc_host = None
+        # scatter buckets: each peer's shard goes as SCATTER_BUCKET_BYTES pieces posted
+        # round-robin over the peers in one group, so all 7 xGMI links of the root
+        # carry data from the first piece on and a peer's receive completes piecewise
+        self.scatter_bucket_bytes = self.SCATTER_BUCKET_BYTES
+
+    SCATTER_BUCKET_BYTES = 4 << 20
 
     # -- M9 ---------------------------------------------------------------------
     def dispatch(self, table: list[tuple[int, int, int, int]] | None) -> tuple[int, int, int, int]:
@@ -218,8 +224,10 @@ class QueryPlane:
         n = 0 if e == NO_WORK else e - s + 1
         if self.env.rank == self.coord:
             base = min(r[2] for r in table if r[3] != NO_WORK)
-            ops = [dist.P2POp(dist.isend, images[r[2] - base:r[3] - base + 1].contiguous(), peer, self.group)
-                   for peer, r in enumerate(table) if peer != self.coord and r[3] != NO_WORK]
+            src = images.contiguous()
+            shards = {peer: (r[2] - base, r[3] - base) for peer, r in enumerate(table)
+                      if peer != self.coord and r[3] != NO_WORK}
+            ops = self._send_ops(src, shards)
             if ops and self.env.distributed:
                 for req in dist.batch_isend_irecv(ops):
                     req.wait()
@@ -229,16 +237,40 @@ class QueryPlane:
         if getattr(self, "_recv", None) is None or tuple(self._recv.shape[1:]) != tuple(img_shape):
             self._recv = torch.empty((self.max_chunk, *img_shape), dtype=torch.uint8, device=self.env.device)
         buf = self._recv[:n]
-        for req in dist.batch_isend_irecv([dist.P2POp(dist.irecv, buf, self.coord, self.group)]):
+        for req in dist.batch_isend_irecv(self._recv_ops(buf)):
             req.wait()
         return buf
+
+    def _bucket_rows(self, row_bytes: int) -> int:
+        b = int(self.scatter_bucket_bytes)
+        return max(1, b // max(1, row_bytes)) if b > 0 else 1 << 62
+
+    def _send_ops(self, images: torch.Tensor, shards: dict) -> list:
+        """Root: isend ops of every peer's rows [a, b] of ``images`` in buckets
+        of ``scatter_bucket_bytes``, interleaved round-robin over the peers
+        (bucket 0 of every peer, then bucket 1, ...).  P2P between one pair of
+        ranks matches in posting order, so ``_recv_ops`` mirrors the split."""
+        step = self._bucket_rows(images[0].numel() * images.element_size()) if images.numel() else 1
+        pieces = {p: [(i, min(i + step - 1, b)) for i in range(a, b + 1, step)] for p, (a, b) in shards.items()}
+        ops = []
+        for k in range(max((len(v) for v in pieces.values()), default=0)):
+            for p, v in pieces.items():
+                if k < len(v):
+                    ops.append(dist.P2POp(dist.isend, images[v[k][0]:v[k][1] + 1], p, self.group))
+        return ops
+
+    def _recv_ops(self, buf: torch.Tensor) -> list:
+        """Member: irecv ops of its shard ``buf`` in the root's bucket split."""
+        step = self._bucket_rows(buf[0].numel() * buf.element_size()) if buf.numel() else 1
+        return [dist.P2POp(dist.irecv, buf[i:i + step], self.coord, self.group) for i in range(0, buf.shape[0], step)]
 
     def scatter_async(self, images: torch.Tensor | None, chunks, out: torch.Tensor) -> list:
         """Non-blocking fixed-size scatter into ``out`` (every rank's receive
         buffer, [n, ...]): the coordinator sends rank r the rows
-        ``images[chunks[r][0]:chunks[r][1] + 1]`` (one grouped P2P op per peer:
-        the root's 7 xGMI links carry the shards concurrently) and copies its
-        own chunk into ``out``.  Returns the requests; ``wait_scatter`` makes
+        ``images[chunks[r][0]:chunks[r][1] + 1]`` (one group of P2P ops, every
+        peer's shard in ``scatter_bucket_bytes`` buckets posted round-robin over
+        the peers: the root's 7 xGMI links carry the shards concurrently) and
+        copies its own chunk into ``out``.  Returns the requests; ``wait_scatter`` makes
         the CURRENT stream wait for them (RCCL) -- the host does not block.
 
         Ordering on RCCL: the communication stream waits for the work queued
@@ -248,11 +280,10 @@ class QueryPlane:
         if self.env.rank == self.coord:
             s0, e0 = chunks[self.coord]
             out[: e0 - s0 + 1].copy_(images[s0:e0 + 1], non_blocking=True)
-            ops = [dist.P2POp(dist.isend, images[s:e + 1], peer, self.group)
-                   for peer, (s, e) in enumerate(chunks) if peer != self.coord]
+            ops = self._send_ops(images, {peer: (s, e) for peer, (s, e) in enumerate(chunks) if peer != self.coord})
         else:
             s, e = chunks[self.env.rank]
-            ops = [dist.P2POp(dist.irecv, out[: e - s + 1], self.coord, self.group)]
+            ops = self._recv_ops(out[: e - s + 1])
         if not ops or not self.env.distributed:
             return []
         return dist.batch_isend_irecv(ops)

@@ -287,3 +287,86 @@ def test_double_buffered_rounds_over_gloo(world):
         p.join(60)
         assert p.exitcode == 0
     assert ok is True
+
+
+def _bucketed_scatter_worker(rank, world, port, q):
+    """Bucketed scatter (1 MiB buckets = 6 images, round-robin over the peers):
+    every rank's shard arrives byte-exact, uneven shard sizes included, for the
+    async double-buffered path and the synchronous path."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import numpy as np
+    import torch.distributed as dist
+
+    from idunno.parallel.dataplane import NO_WORK, QueryPlane, init_from_env
+    from idunno.runtime.data import synth_images_cpu
+    from idunno.runtime.scheduler import split_range
+
+    env = init_from_env(backend="gloo")
+    plane = QueryPlane(env, coordinator=0, max_chunk=20)
+    plane.scatter_bucket_bytes = 1 << 20
+    assert plane._bucket_rows(224 * 224 * 3) == 6
+    B = 20
+    src = torch.from_numpy(synth_images_cpu(11, 0, world * B + 13)) if rank == 0 else None
+    ok = True
+    bufs = [torch.zeros(B, 224, 224, 3, dtype=torch.uint8) for _ in range(2)]
+    rounds = [split_range(0, world * B - 1, world), split_range(13, 13 + world * B - 8, world)]
+    posted = [plane.scatter_async(src, ch, bufs[i]) for i, ch in enumerate(rounds)]
+    for i, ch in enumerate(rounds):
+        plane.wait_scatter(posted[i])
+        s, e = ch[rank]
+        ok &= np.array_equal(bufs[i][:e - s + 1].numpy(), synth_images_cpu(11, s, e - s + 1))
+    # synchronous scatter, one idle rank
+    table = None
+    if rank == 0:
+        chunks = split_range(100, 100 + 7 * (world - 1) + 4, world - 1) if world > 1 else [(100, 104)]
+        table = [(1, 0, s, e) for s, e in chunks] + [(1, 0, 0, NO_WORK)] * (world - len(chunks))
+        imgs = torch.from_numpy(synth_images_cpu(11, 100, chunks[-1][1] - 99))
+    row = plane.dispatch(table)
+    got = plane.scatter(imgs if rank == 0 else None, table, row)
+    if row[3] == NO_WORK:
+        ok &= got is None
+    else:
+        ok &= np.array_equal(got.numpy(), synth_images_cpu(11, row[2], row[3] - row[2] + 1))
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_bucketed_scatter_byte_exact_over_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_bucketed_scatter_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res == {r: True for r in range(world)}
+
+
+def test_scatter_bucket_split_round_robin():
+    """The root's op list: bucket k of every peer before bucket k+1 of any, and
+    each peer's pieces tile its rows exactly (CPU, no process group)."""
+    import types
+
+    from idunno.parallel.dataplane import QueryPlane
+
+    plane = QueryPlane.__new__(QueryPlane)
+    plane.coord, plane.group, plane.scatter_bucket_bytes = 0, None, 3 * 10
+    imgs = torch.arange(40 * 10, dtype=torch.uint8).view(40, 10)
+    seen = []
+    import idunno.parallel.dataplane as dp
+    real = dp.dist.P2POp
+    dp.dist.P2POp = lambda op, t, peer, group: types.SimpleNamespace(t=t, peer=peer)
+    try:
+        ops = plane._send_ops(imgs, {1: (0, 6), 2: (7, 8), 3: (9, 17)})
+        rops = plane._recv_ops(torch.zeros(7, 10, dtype=torch.uint8))
+    finally:
+        dp.dist.P2POp = real
+    seen = [(o.peer, o.t.shape[0]) for o in ops]
+    assert seen == [(1, 3), (2, 2), (3, 3), (1, 3), (3, 3), (1, 1), (3, 3)]
+    assert [o.t.shape[0] for o in rops] == [3, 3, 1]
