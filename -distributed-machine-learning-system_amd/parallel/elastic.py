@@ -73,6 +73,21 @@ class _Solo:
         pass
 
 
+class _PairWork:
+    """Both gathers of a round (coordinator root, standby root) as one handle."""
+
+    def __init__(self, *works):
+        self.works = works
+
+    def is_completed(self) -> bool:
+        return all(w.is_completed() for w in self.works)
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        return True
+
+
 class _EventWork:
     """Work-like handle of a solo round: complete once the round's kernels
     (recorded event) have finished; nothing to wait for on the CPU."""
@@ -119,6 +134,7 @@ class ElasticGroup:
         self._store = None
         self._aborters: list[threading.Thread] = []
         self.poll_s = 0.0005
+        self.standby_rank = -1                # second gather root (the hot standby), -1: none
         self._send = self._gathered = self._host = None
         self._d2h = None
 
@@ -188,15 +204,22 @@ class ElasticGroup:
         self._aborters = [t for t in self._aborters if t.is_alive()]
         return not self._aborters
 
-    def form(self, me: str, members: list[str], epoch: int, host: str, port: int) -> bool:
+    def form(self, me: str, members: list[str], epoch: int, host: str, port: int,
+             standby: str | None = None) -> bool:
         """Join epoch ``epoch`` (blocking rendezvous of all ``members``; rank 0
-        = members[0] hosts the TCPStore).  Returns False on failure."""
+        = members[0] hosts the TCPStore).  With ``standby`` (a member other
+        than rank 0) every round is gathered to it as well (the
+        reference sends every RESULT to the standby too,
+        mp4_machinelearning.py:603-613), so a promoted standby already holds
+        the rounds that completed before the coordinator died.  Every member
+        must be given the same ``standby``.  Returns False on failure."""
         with self.lock:
             self.teardown()
             if me not in members:
                 return False
             rank = members.index(me)
             world = len(members)
+            self.standby_rank = members.index(standby) if standby in members[1:] else -1
             if world == 1:
                 self.pg = _Solo()
                 self.epoch, self.members, self.rank = epoch, list(members), 0
@@ -231,13 +254,14 @@ class ElasticGroup:
     def _alloc(self, world: int) -> None:
         dev, rows, D = self.device, self.max_chunk + HDR_ROWS, self.depth
         self._send = [torch.zeros(rows, 2, dtype=torch.int32, device=dev) for _ in range(D)]
+        root = self.rank == 0 or self.rank == self.standby_rank
         if self.rank == 0 and world == 1:
             self._gathered = [s.unsqueeze(0) for s in self._send]       # the send buffer IS the round
-        elif self.rank == 0:
+        elif root:
             self._gathered = [torch.zeros(world, rows, 2, dtype=torch.int32, device=dev) for _ in range(D)]
             # per-slot gather output lists, built once (not one unbind per round)
             self._gather_outs = [[list(g.unbind(0))] for g in self._gathered]
-        if self.rank == 0:
+        if root:
             gpu = dev.type == "cuda"
             self._host = [torch.zeros(world, rows, 2, dtype=torch.int32, pin_memory=gpu) for _ in range(D)]
             if gpu and self._d2h is None:
@@ -267,7 +291,13 @@ class ElasticGroup:
         opts.rootRank = 0
         slot = seq % self.depth
         outs = self._gather_outs[slot] if self.rank == 0 else []
-        return pg.gather(outs, [self._send[slot]], opts)
+        work = pg.gather(outs, [self._send[slot]], opts)
+        sb = self.standby_rank
+        if sb <= 0:
+            return work
+        o2 = dist.GatherOptions()
+        o2.rootRank = sb
+        return _PairWork(work, pg.gather(self._gather_outs[slot] if self.rank == sb else [], [self._send[slot]], o2))
 
     def wait(self, work, check=None, spin_s: float = 0.001) -> None:
         """Poll ``work`` until it completes; ``check()`` raises RoundAbandoned
@@ -302,7 +332,8 @@ class ElasticGroup:
             self.wait(work, check, spin_s=0.0)
 
     def collect(self, seq: int, work, check=None) -> np.ndarray:
-        """Rank 0: wait for round ``seq``'s gather and return the whole round
+        """A gather root (rank 0, or the standby): wait for round ``seq``'s
+        gather and return the whole round
         as host int32 [world, max_chunk + HDR_ROWS, 2] (one device->host copy
         on a side stream: compute queued on the current stream is not waited
         for)."""

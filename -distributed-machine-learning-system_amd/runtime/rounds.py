@@ -118,6 +118,7 @@ class RoundPlane:
         self._built_for = None                # member set of the last _build (stale sweep on change)
         self._announced: deque = deque()      # coordinator: rounds multicast but not yet posted
         self.announce_frames = 0              # descriptor frames sent (<= rounds posted)
+        self.standby_rounds = 0               # standby: rounds ingested from its own gather copy
         self.host_s = 0.0
         self.host_cpu_s = 0.0                 # the same spans in driver-thread CPU time (no preemption)
         self.host_wait_s = 0.0
@@ -236,7 +237,7 @@ class RoundPlane:
                 "max_queries_per_round": self.max_queries_per_round,
                 "parked": self.parked, "pending_collectives": self.pending_collectives(),
                 "host_s": self.host_s, "host_cpu_s": self.host_cpu_s, "host_wait_s": self.host_wait_s, "host_post_s": self.host_post_s,
-                "host_send_s": self.host_send_s, "announce_frames": self.announce_frames, "launch_cpu_s": self.launch_cpu_s,
+                "host_send_s": self.host_send_s, "announce_frames": self.announce_frames, "standby_rounds": self.standby_rounds, "launch_cpu_s": self.launch_cpu_s,
                 "queued": len(self._queue)}
 
     def pending_collectives(self) -> int:
@@ -708,7 +709,9 @@ class RoundPlane:
             recs.append((MODEL_NAMES[mid], qnum, members[i], s, e, cls, prob))
         n._ingest_round(recs, now, seq=r.seq)
         self.rounds_done += 1
-        if recs and n.standby != n.name and n.membership.is_alive(n.standby):
+        sb = g.standby_rank
+        gathered_by_standby = sb > 0 and members[sb] == n.standby
+        if recs and not gathered_by_standby and n.standby != n.name and n.membership.is_alive(n.standby):
             self._mirror(recs, now)
         self.host_s += time.perf_counter() - t0
         self.host_cpu_s += time.thread_time() - c0
@@ -766,9 +769,13 @@ class RoundPlane:
         port = self.cfg.base_port + self.cfg.collective_port_offset + epoch % 100
         log.warning("%s: forming collective epoch %d over %s", n.name, epoch, members)
         n.tracer.instant("round.form", epoch=epoch, members=len(members))
+        # the standby is the rounds' second gather root (it holds every finished round
+        # itself, no mirror needed); every member posts the same pair of gathers
+        standby = n.standby if n.standby in members[1:] else None
         for m in members[1:]:
-            n.transport.send(m, {"t": Type.GROUP_FORM, "epoch": epoch, "members": members, "port": port})
-        ok = self.group.form(n.name, members, epoch, self.cfg.host, port)
+            n.transport.send(m, {"t": Type.GROUP_FORM, "epoch": epoch, "members": members, "port": port,
+                                 "standby": standby})
+        ok = self.group.form(n.name, members, epoch, self.cfg.host, port, standby=standby)
         self._next_seq = 0
         with self.cv:
             self.healthy = ok and self._reform_at is None and epoch == self.epoch
@@ -804,21 +811,24 @@ class RoundPlane:
                 return
             self.epoch, self.members = epoch, members
             self._round_msgs = {k: v for k, v in self._round_msgs.items() if k[0] >= epoch}
-        if not self.group.form(n.name, members, epoch, self.cfg.host, port):
+        if not self.group.form(n.name, members, epoch, self.cfg.host, port, standby=msg.get("standby")):
             return
         self._follow(epoch, members)
         if self._pending_form is not None:
             self._wake.set()
 
-    def _await_round(self, epoch: int, seq: int, check) -> dict:
+    def _await_round(self, epoch: int, seq: int, check, idle=None) -> dict:
         """Member: wait on the control plane (nothing posted on the GPU) for
-        the coordinator's descriptor of round ``seq``."""
+        the coordinator's descriptor of round ``seq``.  ``idle()`` (the
+        standby's drain of finished gathers) runs between waits; while it
+        reports rounds still pending the wait is short."""
         while True:
+            busy = idle() if idle is not None else False
             with self.cv:
                 msg = self._round_msgs.pop((epoch, seq), None)
                 if msg is None:
                     self.parked = True
-                    self.cv.wait(0.05)
+                    self.cv.wait(0.001 if busy else 0.05)
                     msg = self._round_msgs.pop((epoch, seq), None)
                 if msg is not None:
                     self.parked = False
@@ -830,26 +840,79 @@ class RoundPlane:
         check = self._check_member(members[0])
         inflight = self._inflight
         me = members.index(self.node.name)
+        standby = g.standby_rank == me          # this member is the rounds' second gather root
         abandoned = False
         seq = 0
         try:
             while True:
-                msg = self._await_round(epoch, seq, check)
+                msg = self._await_round(epoch, seq, check,
+                                        (lambda: self._standby_drain(members, check)) if standby else None)
                 if msg.get("stop"):
                     while inflight:
-                        g.wait(inflight.popleft()[1], check)
+                        x = inflight.popleft()
+                        g.wait(x[1], check)
+                        if standby:
+                            self._standby_ingest(x, members, check)
                     break
                 while inflight and inflight[0][0] <= seq - g.depth:
-                    g.release(inflight.popleft()[1], check)
+                    x = inflight.popleft()
+                    g.release(x[1], check)
+                    if standby:
+                        self._standby_ingest(x, members, check)
                 rows = msg.get("rows")
                 row = rows[me] if rows is not None else msg.get("row")
                 if row is not None:
                     self._run_chunk(row, seq)
                 self._write_header(seq)
-                inflight.append((seq, g.post_gather(seq)))
+                inflight.append([seq, g.post_gather(seq), rows, False])
                 self.rounds_done += 1
                 seq += 1
         except Exception as e:  # noqa: BLE001
             log.info("%s: left epoch %d (%s)", self.node.name, epoch, e)
             abandoned = True
+            if standby:
+                # rounds whose gather reached this standby before the coordinator (or a
+                # member) failed are kept: the promoted standby does not recompute them
+                for x in list(inflight):
+                    try:
+                        if x[1] is not None and x[1].is_completed():
+                            self._standby_ingest(x, members, None)
+                    except Exception:  # noqa: BLE001
+                        log.debug("standby ingest of round %s failed", x[0], exc_info=True)
         self._drop_group(abandoned=abandoned)
+
+    def _standby_drain(self, members, check) -> bool:
+        """Standby: ingest every in-flight round whose gather has completed
+        (kept in flight until its slot is released).  True while some round
+        is not ingested yet."""
+        pending = False
+        for x in self._inflight:
+            if not x[3]:
+                if x[1] is not None and x[1].is_completed():
+                    self._standby_ingest(x, members, check)
+                else:
+                    pending = True
+        return pending
+
+    def _standby_ingest(self, x: list, members, check) -> None:
+        """Standby: record round x = [seq, work, rows, ingested] from its own
+        copy of the gathered results (rows: the coordinator's descriptor
+        table).  A row that left fp16's range (class < 0) is skipped: the
+        coordinator reruns it and its RESULT reaches the standby too."""
+        seq, work, rows, done = x
+        if done or rows is None:
+            return
+        x[3] = True
+        arr = self.group.collect(seq, work, check)
+        recs = []
+        for i, row in enumerate(rows):
+            if row is None:
+                continue
+            mid, qnum, s, e = (int(v) for v in row)
+            k = e - s + 1
+            cls = arr[i, :k, 0].copy()
+            if cls.min() < 0:
+                continue
+            recs.append((MODEL_NAMES[mid], qnum, members[i], s, e, cls, arr[i, :k, 1].copy().view(np.float32)))
+        self.node._ingest_round(recs, time.time(), seq=seq)
+        self.standby_rounds += 1

@@ -67,6 +67,10 @@ def test_collective_rounds_with_failures():
         s = cl.wait_idle(20, {"resnet18": 1200})
         assert s["done"]["resnet18"] == 1200, s
         assert me.rounds.rounds_done >= 3              # served as collective rounds, not TCP JOBs
+        # this node is the standby: every round is gathered to it as well (second root),
+        # so it holds the results itself instead of waiting for a mirror from rank 0
+        assert me.name == me.standby and me.rounds.group.standby_rank == me.rounds.group.rank
+        assert wait_for(lambda: me.rounds.standby_rounds >= 3, 5), me.rounds.standby_rounds
 
         # idle for longer than the collective timeout: the epoch survives, rounds go on
         time.sleep(3.0)
@@ -95,6 +99,13 @@ def test_collective_rounds_with_failures():
         assert s["done"]["resnet18"] == 2000, s
         assert me.rounds.rounds_done > before
 
+        # a round the standby gathered itself survives the coordinator's death: once
+        # it holds the query, SIGKILL the coordinator; the query is not run again
+        sr = me.rounds.standby_rounds
+        cl.inference(2400, 2799, "alexnet")
+        assert wait_for(lambda: me.state.images_done("alexnet") >= 800, 10)
+        assert wait_for(lambda: me.rounds.standby_rounds > sr, 5)
+
         # SIGKILL the coordinator: this standby promotes itself and re-forms as rank 0
         procs[0].send_signal(signal.SIGKILL)
         assert wait_for(lambda: me.is_coordinator, 10)
@@ -107,7 +118,8 @@ def test_collective_rounds_with_failures():
         s = cl.wait_idle(20, {"resnet18": 2400})
         assert s["done"]["resnet18"] == 2400, s
         assert me.rounds.rounds_done > before
-        assert _indices(cl) == set(range(2400))
+        assert _indices(cl) == set(range(2800))
+        assert me.state.images_done("alexnet") == 800
     finally:
         me.stop()
         for p in procs.values():

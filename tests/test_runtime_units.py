@@ -218,6 +218,7 @@ def test_round_finalize_reruns_range_guard_rows_only():
 
     class G:
         max_chunk = mc
+        standby_rank = -1
 
         def collect(self, seq, work, check):
             return arr
