@@ -336,7 +336,10 @@ class ElasticGroup:
         gather and return the whole round
         as host int32 [world, max_chunk + HDR_ROWS, 2] (one device->host copy
         on a side stream: compute queued on the current stream is not waited
-        for)."""
+        for).  Of a gather pair only this root's own gather is waited for; the
+        caller releases the pair before the slot is rewritten."""
+        if isinstance(work, _PairWork):
+            work = work.works[0 if self.rank == 0 else 1]
         self.wait(work, check)
         slot = seq % self.depth
         host = self._host[slot]

@@ -710,6 +710,8 @@ class RoundPlane:
         n._ingest_round(recs, now, seq=r.seq)
         self.rounds_done += 1
         sb = g.standby_rank
+        if sb > 0:
+            g.release(r.work, check)        # the standby's gather of this slot too, before reuse
         gathered_by_standby = sb > 0 and members[sb] == n.standby
         if recs and not gathered_by_standby and n.standby != n.name and n.membership.is_alive(n.standby):
             self._mirror(recs, now)
