@@ -152,6 +152,17 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
                        cur_stream()); check_launch("conv3x3_c64");
     return y;
   }
+  // band-staged 3x3 kernel in fp16 (conv3x3_band.hip, tile 70): ResNet layers 2-4
+  const bool band_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 &&
+                       conv3x3_band_supported(H, W, C, Cout);
+  if (tile == 70 || (tile < 0 && band_ok && !(route & kRouteNoBand) && conv3x3_band_f16_default(B, W, Cout))) {
+    TORCH_CHECK(band_ok, "tile 70 (band-staged 3x3 conv) does not support this shape");
+    TORCH_CHECK(conv3x3_band_launch(a.x, C, a.w, a.bias, rp, Cout, a.y, Cout, false, B, H, W, C, Cout, a.relu, 1.0f,
+                                    nullptr, 0, 0, cur_stream(), true),
+                "band conv: tensor too large for 32-bit buffer offsets");
+    check_launch("conv3x3_band (fp16)");
+    return y;
+  }
   const bool c1s_ok = KH == 1 && KW == 1 && (stride == 1 || stride == 2) && pad == 0 && !out_f32 &&
                       conv1x1_stream_supported(C, Cout, M);
   if (tile == 80 || (tile < 0 && c1s_ok && !(route & kRouteNoStream1x1) && conv1x1_stream_default(C, stride, M))) {
@@ -627,6 +638,36 @@ torch::Tensor conv3x3_band_split(torch::Tensor x, torch::Tensor w, torch::Tensor
                                   cur_stream()),
               "band conv: tensor too large for 32-bit buffer offsets");
   check_launch("conv3x3_band");
+  return y;
+}
+
+// fp16 band-staged 3x3/s1/p1 conv with a persistent-grid cap (tests)
+torch::Tensor conv3x3_band_f16(torch::Tensor x, torch::Tensor w, torch::Tensor bias, c10::optional<torch::Tensor> res,
+                               bool relu, int64_t max_grid) {
+  CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(bias);
+  CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(bias);
+  CHECK_DT(x, torch::kHalf); CHECK_DT(w, torch::kHalf); CHECK_DT(bias, torch::kFloat);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "bad ranks");
+  const int B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), Cout = w.size(0);
+  TORCH_CHECK(w.size(1) == 9 * C && bias.numel() == Cout, "fp16 weight must be [Cout, 9*C]");
+  TORCH_CHECK(w.device() == x.device() && bias.device() == x.device(), "operands on different devices");
+  TORCH_CHECK(conv3x3_band_supported(H, W, C, Cout), "band conv: unsupported shape");
+  auto y = torch::empty({B, H, W, Cout}, x.options());
+  const half_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    auto& r = *res;
+    CHECK_DEV(r); CHECK_CONTIG(r); CHECK_DT(r, torch::kHalf);
+    TORCH_CHECK(r.device() == x.device() && r.dim() == 4 && r.size(0) == B && r.size(1) == H && r.size(2) == W &&
+                r.size(3) == Cout, "residual shape mismatch");
+    rp = reinterpret_cast<const half_t*>(r.data_ptr());
+  }
+  if (B == 0) return y;
+  TORCH_CHECK(conv3x3_band_launch(reinterpret_cast<const half_t*>(x.data_ptr()), C,
+                                  reinterpret_cast<const half_t*>(w.data_ptr()), bias.data_ptr<float>(), rp, Cout,
+                                  y.data_ptr(), Cout, false, B, H, W, C, Cout, relu ? 1 : 0, 1.0f, nullptr,
+                                  (int)max_grid, 0, cur_stream(), true),
+              "band conv: tensor too large for 32-bit buffer offsets");
+  check_launch("conv3x3_band (fp16)");
   return y;
 }
 
@@ -1496,6 +1537,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "band-staged split 3x3/s1/p1 conv (tile 70) with a persistent-grid cap (0: one workgroup per CU)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res") = py::none(), py::arg("relu") = true,
         py::arg("acc_scale") = 1.0, py::arg("out_f32") = false, py::arg("max_grid") = 0, py::arg("flags") = 0);
+  m.def("conv3x3_band_f16", &conv3x3_band_f16,
+        "band-staged fp16 3x3/s1/p1 conv (tile 70) with a persistent-grid cap (0: one workgroup per CU)",
+        py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("relu"), py::arg("max_grid") = 0);
   m.def("conv3x3_band_tiles", &conv3x3_band_tiles, "band conv tile count for (B, W, Cout)");
   m.def("split_from_f32", &split_from_f32, "fp32 NHWC -> split-fp16 layout");
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");

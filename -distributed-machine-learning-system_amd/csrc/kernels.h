@@ -169,14 +169,16 @@ bool conv3x3_split_c64_supported(int H, int W, int C, int Cout);
 void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
                               const void* zero, int B, int H, int W, int relu, float acc_scale, int* ovf,
                               hipStream_t st);
-// band-staged split 3x3/s1/p1 conv (conv3x3_band.hip): ResNet layers 2-4 (W 28 / 14 / 7,
-// C % 64 == 0, Cout % 128 == 0); x / res read in place at pixel strides ldx / ldr (halfs)
+// band-staged 3x3/s1/p1 conv (conv3x3_band.hip): ResNet layers 2-4 (W 28 / 14 / 7,
+// C % 64 == 0, Cout % 128 == 0); x / res read in place at pixel strides ldx / ldr (halfs).
+// Split operands by default; f16: plain fp16 operands, weights [Cout][9*C], fp16 output.
 bool conv3x3_band_supported(int H, int W, int C, int Cout);
 int conv3x3_band_tiles(int B, int W, int Cout);
-bool conv3x3_band_default(int B, int W, int Cout);   // auto-selection rule for conv2d_split
+bool conv3x3_band_default(int B, int W, int Cout);       // auto-selection rule for conv2d_split
+bool conv3x3_band_f16_default(int B, int W, int Cout);   // auto-selection rule for conv2d_nhwc (fp16)
 bool conv3x3_band_launch(const half_t* x, int ldx, const half_t* w, const float* bias, const half_t* res, int ldr,
                          void* y, int ldy, bool out_f32, int B, int H, int W, int C, int Cout, int relu,
-                         float acc_scale, int* ovf, int max_grid, int flags, hipStream_t st);
+                         float acc_scale, int* ovf, int max_grid, int flags, hipStream_t st, bool f16 = false);
 // split-fp16 RGB stem on packed rows (a.cpk > 0, x from preprocess_pack3_split): fp32 output
 bool conv_glds_split_p3_launch(ConvArgs a, int tile, hipStream_t st);   // a.cpk > 0: pack3 stem
 bool conv3x3_c64_supported(int C, int Cout);

@@ -59,6 +59,7 @@ struct BandArgs {
   int B, C, Cout, M;
   int ldx, ldr, ldy;
   int relu, ncb, tiles_n, ntiles;
+  uint32_t wrow, wtap;  // weight row / one tap's bytes (split: 36C / 4C, fp16: 18C / 2C)
   float acc_scale;
   int* ovf;             // split range guard flag or nullptr
   int flags;            // bit 0: waves 4-7 at s_setprio 1 (MI355X_MICROARCH.md, two waves per SIMD item 4)
@@ -197,7 +198,7 @@ __device__ __forceinline__ void band_vmcnt() {
 // Epilogue of one tile: x 2^-e, + bias (+ split residual), ReLU, split (or fp32)
 // buffer stores -- exactly FN*FM*(OUT_F32 ? 1 : 2) store instructions per wave
 // (rows past M get an offset past the descriptor and are dropped); clears acc.
-template <int FM, bool HAS_RES, bool OUT_F32, typename Rsrc>
+template <int FM, bool HAS_RES, bool OUT_F32, bool F16, typename Rsrc>
 __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile& cur, float4v (&acc)[bnd::FN][FM],
                                               int wn, int wm, int frow, int q, Rsrc y_rsrc, bool& bad) {
   using namespace bnd;
@@ -210,13 +211,13 @@ __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile&
 #pragma unroll
         for (int i = 0; i < FN; ++i) {
           const int n = cur.n0 + wn * 32 + 16 * i + 4 * q;
-          const half_t* p = a.res + (size_t)m * a.ldr + split_off(n);
+          const half_t* p = a.res + (size_t)m * a.ldr + (F16 ? n : split_off(n));
           if (a.flags & 4) {
             rh[i][j] = half4v{0, 0, 0, 0};
             rl[i][j] = half4v{0, 0, 0, 0};
           } else {
             rh[i][j] = gload_b64_untracked(p);
-            rl[i][j] = gload_b64_untracked(p + 32);
+            if constexpr (!F16) rl[i][j] = gload_b64_untracked(p + 32);
           }
         }
       }
@@ -231,7 +232,7 @@ __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile&
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
           reg_tie(rh[i][j]);
-          reg_tie(rl[i][j]);
+          if constexpr (!F16) reg_tie(rl[i][j]);
         }
     }
 #pragma unroll
@@ -244,7 +245,7 @@ __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile&
         float4v v = acc[i][j] * a.acc_scale + bv[i];
         if constexpr (HAS_RES) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (float)rh[i][j][e] + (float)rl[i][j][e];
+          for (int e = 0; e < 4; ++e) v[e] += F16 ? (float)rh[i][j][e] : (float)rh[i][j][e] + (float)rl[i][j][e];
         }
         if (a.relu) {
 #pragma unroll
@@ -252,6 +253,12 @@ __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile&
         }
         if (a.flags & 2) {
           if (v[0] == 12345.f) bad = true;           // keep the math alive
+        } else if constexpr (F16) {
+          half4v h;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) h[e] = (half_t)v[e];
+          const uint32_t off = mok ? ((uint32_t)m * (uint32_t)a.ldy + (uint32_t)n) * 2u : OOR;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_bd, h), y_rsrc, (int)off, 0, 0);
         } else if constexpr (OUT_F32) {
           const uint32_t off = mok ? ((uint32_t)m * (uint32_t)a.ldy + (uint32_t)n) * 4u : OOR;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_bd, v), y_rsrc, (int)off, 0, 0);
@@ -269,14 +276,17 @@ __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile&
     }
   }
 
-template <int W, int FM, int WM, bool HAS_RES, bool OUT_F32>
+// F16: plain fp16 operands (a 128-byte LDS row = 64 channels, two K = 32 halves:
+// 2 MFMAs per fragment pair instead of the split's 3) and an fp16 epilogue.
+template <int W, int FM, int WM, bool HAS_RES, bool OUT_F32, bool F16>
 __global__ void __launch_bounds__(256 * WM, WM) conv3x3_band_kernel(const BandArgs a) {
   using G = BandGeom<W, FM, WM>;
   using namespace bnd;
   constexpr int NW = G::NW, GW = G::GW;
   constexpr int NPI = G::NPI;
-  constexpr int NEPI = OUT_F32 ? FN * FM : 2 * FN * FM;   // epilogue stores per wave and tile
+  constexpr int NEPI = (OUT_F32 || F16) ? FN * FM : 2 * FN * FM;   // epilogue stores per wave and tile
   static_assert(NEPI < 64 && NPI <= 8, "vmcnt immediates; patch chunks go out at taps 0 .. NPI-1");
+  static_assert(!(F16 && OUT_F32), "fp16 band conv stores fp16");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -293,8 +303,8 @@ __global__ void __launch_bounds__(256 * WM, WM) conv3x3_band_kernel(const BandAr
   const auto x_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, 0x7fffffff, 0x00020000);
   const uint32_t ybytes = (uint32_t)a.M * (uint32_t)a.ldy * (OUT_F32 ? 4u : 2u);
   const auto y_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)ybytes, 0x00020000);
-  const uint32_t wrow = 36u * (uint32_t)a.C;        // weight row bytes (9 taps x 2C halfs)
-  const uint32_t wtap = 4u * (uint32_t)a.C;         // one tap's bytes
+  const uint32_t wrow = a.wrow;                     // weight row bytes (9 taps x K-row halfs)
+  const uint32_t wtap = a.wtap;                     // one tap's bytes
 
   // weight DMA: instruction j of this wave fills rows (wave + 8j)*8 .. +7 of a slot
   uint32_t wv[GW];
@@ -442,15 +452,25 @@ __global__ void __launch_bounds__(256 * WM, WM) conv3x3_band_kernel(const BandAr
               aC[i][1] = aN[i][1];
             }
           }
+          if constexpr (F16) {
+            // channels 0-31 (chunks 0-3) and 32-63 (chunks 4-7) of the 64-channel block
 #pragma unroll
-          for (int i = 0; i < FN; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aC[i][0], bR[rg][0], acc[i][j], 0, 0, 0);
+            for (int i = 0; i < FN; ++i)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aC[i][0], bR[rg][0], acc[i][j], 0, 0, 0);
 #pragma unroll
-          for (int i = 0; i < FN; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aC[i][0], bR[rg][1], acc[i][j], 0, 0, 0);
+            for (int i = 0; i < FN; ++i)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aC[i][1], bR[rg][1], acc[i][j], 0, 0, 0);
+          } else {
 #pragma unroll
-          for (int i = 0; i < FN; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aC[i][1], bR[rg][0], acc[i][j], 0, 0, 0);
+            for (int i = 0; i < FN; ++i)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aC[i][0], bR[rg][0], acc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aC[i][0], bR[rg][1], acc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aC[i][1], bR[rg][0], acc[i][j], 0, 0, 0);
+          }
         }
       }
       // the next stage's A and first B groups are in flight and cross the loop
@@ -468,7 +488,7 @@ __global__ void __launch_bounds__(256 * WM, WM) conv3x3_band_kernel(const BandAr
       }
     }
 
-    band_epilogue<FM, HAS_RES, OUT_F32>(a, cur, acc, wn, wm, frow, q, y_rsrc, bad);
+    band_epilogue<FM, HAS_RES, OUT_F32, F16>(a, cur, acc, wn, wm, frow, q, y_rsrc, bad);
     if (!have_nxt) break;
     first_tile = false;
     T += GS;
@@ -512,8 +532,8 @@ __global__ void __launch_bounds__(1024, 4) conv3x3_band16_kernel(const BandArgs 
   const auto x_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, 0x7fffffff, 0x00020000);
   const uint32_t ybytes = (uint32_t)a.M * (uint32_t)a.ldy * (OUT_F32 ? 4u : 2u);
   const auto y_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)ybytes, 0x00020000);
-  const uint32_t wrow = 36u * (uint32_t)a.C;
-  const uint32_t wtap = 4u * (uint32_t)a.C;
+  const uint32_t wrow = a.wrow;
+  const uint32_t wtap = a.wtap;
   const int wrow_i = wave * 8 + (lane >> 3);
   const uint32_t wv = (uint32_t)wrow_i * wrow + (uint32_t)((((lane & 7) ^ swz_r(wrow_i, 8))) << 4);
   const int arow = wn * 32 + frow;
@@ -633,7 +653,7 @@ __global__ void __launch_bounds__(1024, 4) conv3x3_band16_kernel(const BandArgs 
         }
       }
     }
-    band_epilogue<FM, HAS_RES, OUT_F32>(a, cur, acc, wn, wm, frow, q, y_rsrc, bad);
+    band_epilogue<FM, HAS_RES, OUT_F32, false>(a, cur, acc, wn, wm, frow, q, y_rsrc, bad);
     if (!have_nxt) break;
     first_tile = false;
     T += GS;
@@ -677,6 +697,13 @@ bool conv3x3_band_default(int B, int W, int Cout) {
   return conv3x3_band_tiles(B, W, Cout) >= device_cu_count();
 }
 
+// fp16 (ResNet50 b1024 / ResNet18 fp16): 2 MFMAs per 128-byte K block make the
+// im2col tiles' per-tap pixel DMA the larger share of their time, so every
+// supported W takes the band kernel once each CU has a tile
+bool conv3x3_band_f16_default(int B, int W, int Cout) {
+  return conv3x3_band_tiles(B, W, Cout) >= device_cu_count();
+}
+
 int conv3x3_band_tiles(int B, int W, int Cout) {
   const int fm = band_fm(W);
   if (fm <= 0) return 0;
@@ -685,21 +712,24 @@ int conv3x3_band_tiles(int B, int W, int Cout) {
   return (int)((M + bm - 1) / bm) * (Cout / bnd::BN);
 }
 
-template <int W, int FM, int WM, bool R, bool F>
+template <int W, int FM, int WM, bool R, bool F, bool H>
 static void band_cfg(const BandArgs& a, int grid, hipStream_t st) {
-  auto kern = conv3x3_band_kernel<W, FM, WM, R, F>;
+  auto kern = conv3x3_band_kernel<W, FM, WM, R, F, H>;
   ensure_lds_attr(reinterpret_cast<const void*>(kern), bnd::LDS);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256 * WM), bnd::LDS, st, a);
 }
 
 template <int W, int FM, int WM>
-static bool band_dispatch(const BandArgs& a, bool res, bool out_f32, int grid, hipStream_t st) {
-  if (res) {
-    if (out_f32) band_cfg<W, FM, WM, true, true>(a, grid, st);
-    else band_cfg<W, FM, WM, true, false>(a, grid, st);
+static bool band_dispatch(const BandArgs& a, bool res, bool out_f32, bool f16, int grid, hipStream_t st) {
+  if (f16) {
+    if (res) band_cfg<W, FM, WM, true, false, true>(a, grid, st);
+    else band_cfg<W, FM, WM, false, false, true>(a, grid, st);
+  } else if (res) {
+    if (out_f32) band_cfg<W, FM, WM, true, true, false>(a, grid, st);
+    else band_cfg<W, FM, WM, true, false, false>(a, grid, st);
   } else {
-    if (out_f32) band_cfg<W, FM, WM, false, true>(a, grid, st);
-    else band_cfg<W, FM, WM, false, false>(a, grid, st);
+    if (out_f32) band_cfg<W, FM, WM, false, true, false>(a, grid, st);
+    else band_cfg<W, FM, WM, false, false, false>(a, grid, st);
   }
   return true;
 }
@@ -725,8 +755,9 @@ static bool band16_dispatch(const BandArgs& a, bool res, bool out_f32, int grid,
 
 bool conv3x3_band_launch(const half_t* x, int ldx, const half_t* w, const float* bias, const half_t* res, int ldr,
                          void* y, int ldy, bool out_f32, int B, int H, int W, int C, int Cout, int relu,
-                         float acc_scale, int* ovf, int max_grid, int flags, hipStream_t st) {
+                         float acc_scale, int* ovf, int max_grid, int flags, hipStream_t st, bool f16) {
   if (!conv3x3_band_supported(H, W, C, Cout)) return false;
+  if (f16 && (out_f32 || (flags & 8))) return false;
   BandArgs a;
   a.x = x;
   a.w = w;
@@ -741,14 +772,17 @@ bool conv3x3_band_launch(const half_t* x, int ldx, const half_t* w, const float*
   a.ldr = ldr;
   a.ldy = ldy;
   a.relu = relu;
-  a.ncb = C / 32;
+  // one 128-byte K block per stage: 32 split channels (hi, lo) or 64 fp16 channels
+  a.ncb = f16 ? C / 64 : C / 32;
+  a.wrow = (f16 ? 18u : 36u) * (uint32_t)C;
+  a.wtap = (f16 ? 2u : 4u) * (uint32_t)C;
   a.tiles_n = Cout / bnd::BN;
   a.ntiles = conv3x3_band_tiles(B, W, Cout);
   a.acc_scale = acc_scale;
   a.ovf = ovf;
   a.flags = flags;
   // 32-bit buffer offsets: input pixels x stride, weights, output
-  if ((long)B * H * W * ldx * 2 >= (1L << 31) || (long)Cout * 36 * C >= (1L << 31) ||
+  if ((long)B * H * W * ldx * 2 >= (1L << 31) || (long)Cout * (f16 ? 18 : 36) * C >= (1L << 31) ||
       (long)a.M * ldy * (out_f32 ? 4 : 2) >= (1L << 31))
     return false;
   if (a.ntiles <= 0) return true;
@@ -758,9 +792,9 @@ bool conv3x3_band_launch(const half_t* x, int ldx, const half_t* w, const float*
   switch (W) {
     case 28:
       if (flags & 8) return band16_dispatch<28, 4>(a, res != nullptr, out_f32, grid, st);   // 16 waves
-      return band_dispatch<28, 8, 2>(a, res != nullptr, out_f32, grid, st);
-    case 14: return band_dispatch<14, 5, 2>(a, res != nullptr, out_f32, grid, st);
-    case 7: return band_dispatch<7, 5, 2>(a, res != nullptr, out_f32, grid, st);
+      return band_dispatch<28, 8, 2>(a, res != nullptr, out_f32, f16, grid, st);
+    case 14: return band_dispatch<14, 5, 2>(a, res != nullptr, out_f32, f16, grid, st);
+    case 7: return band_dispatch<7, 5, 2>(a, res != nullptr, out_f32, f16, grid, st);
     default: return false;
   }
 }

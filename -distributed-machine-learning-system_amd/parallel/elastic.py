@@ -118,8 +118,11 @@ def _shutdown_backend(pg, abort: bool) -> None:
 class ElasticGroup:
     def __init__(self, device: torch.device, backend: str | None = None, timeout_s: float = 30.0,
                  max_chunk: int = 1024, op_timeout_s: float = 120.0, abort_join_s: float = 5.0,
-                 depth: int = 2):
+                 depth: int = 2, solo: bool = True):
         self.device = torch.device(device)
+        # solo: a one-member epoch runs without a backend (_Solo); False builds the
+        # real one even then (the GPU test of the RCCL path on a one-GPU box)
+        self.solo = solo
         self.backend = backend or ("nccl" if self.device.type == "cuda" else "gloo")
         self.timeout_s = timeout_s            # rendezvous (store + backend construction)
         self.op_timeout_s = op_timeout_s      # backstop for one collective; liveness comes from check()
@@ -220,7 +223,7 @@ class ElasticGroup:
             rank = members.index(me)
             world = len(members)
             self.standby_rank = members.index(standby) if standby in members[1:] else -1
-            if world == 1:
+            if world == 1 and self.solo:
                 self.pg = _Solo()
                 self.epoch, self.members, self.rank = epoch, list(members), 0
                 self._alloc(1)
@@ -255,7 +258,7 @@ class ElasticGroup:
         dev, rows, D = self.device, self.max_chunk + HDR_ROWS, self.depth
         self._send = [torch.zeros(rows, 2, dtype=torch.int32, device=dev) for _ in range(D)]
         root = self.rank == 0 or self.rank == self.standby_rank
-        if self.rank == 0 and world == 1:
+        if isinstance(self.pg, _Solo):
             self._gathered = [s.unsqueeze(0) for s in self._send]       # the send buffer IS the round
         elif root:
             self._gathered = [torch.zeros(world, rows, 2, dtype=torch.int32, device=dev) for _ in range(D)]

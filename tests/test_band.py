@@ -176,3 +176,52 @@ def test_band_conv_range_guard(ops):
         assert flag.item() == 1
     finally:
         ext.set_split_guard(None)
+
+
+# ---------------------------------------------------------------------------
+# fp16 operands (ResNet50 b1024 / ResNet18 fp16 layers 2-4)
+# ---------------------------------------------------------------------------
+
+def _ref32_f16(x, w, b, relu, res=None):
+    """fp32 oracle of the fp16 conv: the fp16 input / weight / residual values
+    themselves, fp32 arithmetic."""
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), w.half().float().to(x.device), b.float().to(x.device), 1, 1)
+    if res is not None:
+        y = y + res.float().permute(0, 3, 1, 2)
+    if relu:
+        y = F.relu(y)
+    return y.permute(0, 2, 3, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,Cin,Cout", BAND_CASES + [(3, 14, 512, 256)])
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("max_grid", [0, 3])
+def test_band_conv_f16_vs_fp32(ops, B, H, Cin, Cout, res, max_grid):
+    torch.manual_seed(B * 17 + H + Cin + Cout + res)
+    x = torch.randn(B, H, H, Cin, device=DEV).half()
+    w = torch.randn(Cout, Cin, 3, 3) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    r = torch.randn(B, H, H, Cout, device=DEV).half() if res else None
+    pw, small = P.pack_conv_weight(w, "fp16")
+    assert not small
+    ext = ops.load()
+    for relu in (True, False):
+        y = ext.conv3x3_band_f16(x, pw.to(DEV), b.to(DEV), r, relu, max_grid)
+        assert y.dtype == torch.float16 and y.shape == (B, H, H, Cout)
+        _check(y, _ref32_f16(x, w, b, relu, r).double(), rel=2e-3)
+
+
+@pytest.mark.gpu
+def test_band_conv_f16_matches_im2col_tile(ops):
+    """fp16 conv2d through tile 70 (band) and the default im2col tile agree to fp16 rounding."""
+    torch.manual_seed(5)
+    B, H, C = 4, 28, 128
+    x = torch.randn(B, H, H, C, device=DEV).half()
+    w = torch.randn(C, C, 3, 3) / (C * 9) ** 0.5
+    pw, _ = P.pack_conv_weight(w, "fp16")
+    b = (torch.randn(C) * 0.1).to(DEV)
+    r = torch.randn(B, H, H, C, device=DEV).half()
+    y70 = ops.conv2d(x, pw.to(DEV), b, 3, 3, 1, 1, True, residual=r, tile=70).float()
+    y42 = ops.conv2d(x, pw.to(DEV), b, 3, 3, 1, 1, True, residual=r, tile=36).float()
+    assert (y70 - y42).abs().max().item() <= 2e-3 * y42.abs().max().item()
