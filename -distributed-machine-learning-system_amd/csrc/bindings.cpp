@@ -155,7 +155,7 @@ torch::Tensor conv2d_nhwc(torch::Tensor x, torch::Tensor w, torch::Tensor bias,
   // band-staged 3x3 kernel in fp16 (conv3x3_band.hip, tile 70): ResNet layers 2-4
   const bool band_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && !out_f32 &&
                        conv3x3_band_supported(H, W, C, Cout);
-  if (tile == 70 || (tile < 0 && band_ok && !(route & kRouteNoBand) && conv3x3_band_f16_default(B, W, Cout))) {
+  if (tile == 70 || (tile < 0 && band_ok && !(route & kRouteNoBand) && conv3x3_band_f16_default(B, W, Cout, rp != nullptr))) {
     TORCH_CHECK(band_ok, "tile 70 (band-staged 3x3 conv) does not support this shape");
     TORCH_CHECK(conv3x3_band_launch(a.x, C, a.w, a.bias, rp, Cout, a.y, Cout, false, B, H, W, C, Cout, a.relu, 1.0f,
                                     nullptr, 0, 0, cur_stream(), true),
@@ -539,8 +539,9 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
   // row-streaming register-weight kernel for split 3x3/s1 64->64 (ResNet layer1)
   if (tile == 50 || (tile < 0 && c64_ok && !(route & kRouteNoC64))) {
     TORCH_CHECK(c64_ok, "tile 50 (row-streaming split 3x3 64->64 conv) does not support this shape");
-    conv3x3_split_c64_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W, a.relu,
-                             a.acc_scale, a.ovf, cur_stream());
+    TORCH_CHECK(conv3x3_split_c64_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W,
+                                         a.relu, a.acc_scale, a.ovf, cur_stream()),
+                "row-streaming split conv: tensor too large for 32-bit offsets");
     check_launch("conv3x3_split_c64");
     return y;
   }

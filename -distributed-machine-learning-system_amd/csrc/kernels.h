@@ -166,7 +166,7 @@ bool conv1x1_fused_next_launch(const half_t* x1, const half_t* x2, const half_t*
 bool conv1x1_stream_split_default(int C, int stride);
 // split 3x3/s1/p1 64 -> 64 conv, weights in registers, input rows streamed through an LDS ring
 bool conv3x3_split_c64_supported(int H, int W, int C, int Cout);
-void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
+bool conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
                               const void* zero, int B, int H, int W, int relu, float acc_scale, int* ovf,
                               hipStream_t st);
 // band-staged 3x3/s1/p1 conv (conv3x3_band.hip): ResNet layers 2-4 (W 28 / 14 / 7,
@@ -175,7 +175,7 @@ void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bia
 bool conv3x3_band_supported(int H, int W, int C, int Cout);
 int conv3x3_band_tiles(int B, int W, int Cout);
 bool conv3x3_band_default(int B, int W, int Cout);       // auto-selection rule for conv2d_split
-bool conv3x3_band_f16_default(int B, int W, int Cout);   // auto-selection rule for conv2d_nhwc (fp16)
+bool conv3x3_band_f16_default(int B, int W, int Cout, bool res);   // auto rule for conv2d_nhwc (fp16)
 bool conv3x3_band_launch(const half_t* x, int ldx, const half_t* w, const float* bias, const half_t* res, int ldr,
                          void* y, int ldy, bool out_f32, int B, int H, int W, int C, int Cout, int relu,
                          float acc_scale, int* ovf, int max_grid, int flags, hipStream_t st, bool f16 = false);

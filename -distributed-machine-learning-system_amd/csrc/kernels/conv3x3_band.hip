@@ -697,11 +697,12 @@ bool conv3x3_band_default(int B, int W, int Cout) {
   return conv3x3_band_tiles(B, W, Cout) >= device_cu_count();
 }
 
-// fp16 (ResNet50 b1024 / ResNet18 fp16): 2 MFMAs per 128-byte K block make the
-// im2col tiles' per-tap pixel DMA the larger share of their time, so every
-// supported W takes the band kernel once each CU has a tile
-bool conv3x3_band_f16_default(int B, int W, int Cout) {
-  return conv3x3_band_tiles(B, W, Cout) >= device_cu_count();
+// fp16 (round-5 per-layer A/B, profiles/r5_band_f16_layers.log): 2 MFMAs per
+// 128-byte K block leave the band kernel ahead of the im2col tiles only at W 28
+// without a residual (ResNet50 layer2 -2.4 %, ResNet18 layer2 c0 -7 %); with the
+// all-W rule the whole graph lost 1.1 % (ResNet50 b1024) / 2.6 % (ResNet18 b400)
+bool conv3x3_band_f16_default(int B, int W, int Cout, bool res) {
+  return W == 28 && !res && conv3x3_band_tiles(B, W, Cout) >= device_cu_count();
 }
 
 int conv3x3_band_tiles(int B, int W, int Cout) {

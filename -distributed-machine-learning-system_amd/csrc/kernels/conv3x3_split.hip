@@ -7,19 +7,22 @@
 //   * the weights live in REGISTERS: wave w owns output channels 16w..16w+15
 //     and holds their 9 taps x 2 channel blocks x (hi, lo) A fragments
 //     (36 x half8v = 144 VGPRs) for the whole launch;
-//   * the input streams through LDS one image row at a time: a 4-row ring
-//     (rows y-1, y, y+1 in use, row y+2 landing by LDS-DMA while row y
+//   * the input streams through LDS one image row at a time: a 5-row ring
+//     (rows y-2 .. y+1 in use, row y+2 landing by LDS-DMA while row y
 //     computes), so each input row is fetched once per band of rows instead
 //     of 9 times;
-//   * an output row is 4 pixel fragments of 16 (49 <= W <= 62); per (tap,
-//     channel block, fragment) a wave reads the hi and lo B fragments and
-//     issues 3 MFMAs (hi*hi + hi*lo + lo*hi), the reads of the next two such
-//     groups in flight behind them (3-deep register ring, counted lgkmcnt);
+//   * an output row is 3 pixel fragments of 16 (columns 0..47) and every
+//     second row adds one tail fragment with columns 48..W-1 of both rows of
+//     the pair (49 <= W <= 56); per (tap, channel block, fragment) a wave reads
+//     the hi and lo B fragments and issues 3 MFMAs (hi*hi + hi*lo + lo*hi),
+//     the reads of the next two such groups in flight behind them (3-deep
+//     register ring, counted lgkmcnt);
 //   * the residual of the row is loaded into registers when the row starts.
 // LDS pixel rows are 256 B (64 channels x (hi, lo) halfs: 16 chunks of 16 B);
 // chunk c of LDS column col sits in slot c ^ ((2*col) & 15), which makes the
 // B-fragment reads (lane = pixel col + 16 * k-group) conflict-free for every
-// tap shift (exhaustive check in tests/test_split.py).
+// tap shift, the tail fragment's two-row lane split included (exhaustive
+// checks in tests/test_split.py).
 // Persistent: a work item is a band of BAND output rows of one image.
 #include "../kernels.h"
 #include "../launch_util.h"
@@ -29,13 +32,14 @@ namespace idunno {
 namespace c64s {
 constexpr int C = 64;              // channels in and out
 constexpr int PIX = 2 * C;         // halfs per pixel (split)
-constexpr int RC = 66;             // LDS columns per ring row (W + 2 <= 64 read + 2 of masked lanes)
+constexpr int RC = 60;             // LDS columns per ring row (W + 2 <= 58 read; 60 = 3.75 whole DMA instructions)
 constexpr int RB = RC * 256;       // bytes per ring row
-constexpr int RING = 4;
-constexpr int LDS = RING * RB;     // 67,584 B: 2 workgroups per CU
+constexpr int RING = 5;            // rows y-2 .. y+1 in use (a row pair's tail fragment) + row y+2 landing
+constexpr int BIAS = RING * RB;    // the 64 biases (fp32), read by the epilogue: no VGPRs held for them
+constexpr int LDS = BIAS + 256;    // 77,056 B: 2 workgroups per CU
 constexpr int BAND = 8;            // output rows per work item (at most; fewer for small batches)
-constexpr int NF = 4;              // pixel fragments per row (49 <= W <= 62: all 4 store)
-constexpr int NST = 2 * NF;        // epilogue store instructions per wave and row
+constexpr int WMAX = 56;           // 3 full fragments + an 8-column tail per row
+constexpr int NST = 6;             // epilogue stores per wave and row, at least (3 fragments x hi, lo)
 }  // namespace c64s
 
 struct C64sArgs {
@@ -44,7 +48,7 @@ struct C64sArgs {
   const float* bias;    // [64]
   const half_t* res;    // split [B][H][W][128] or nullptr
   half_t* y;            // split [B][H][W][128]
-  const void* zero;     // >= 16 zero bytes
+  const void* zero;     // unused (padding comes from out-of-range buffer offsets)
   int B, H, W, relu, band, nbands, ntasks;
   float acc_scale;
   int* ovf;             // split range guard flag or nullptr (common.h split_guard)
@@ -61,34 +65,46 @@ __device__ __forceinline__ half8v lds_read_b128_off(uint32_t addr) {
   return v;
 }
 
-// fragment f's read (f = 0..3, constant after unrolling): immediate offset 4096 * f
+// fragment f's read (f = 0..2 of the row: immediate offset 4096 * f; f = 3: the
+// tail fragment, whose lanes carry their own row base)
 __device__ __forceinline__ half8v lds_read_frag(uint32_t addr, int f) {
   switch (f) {
     case 0: return lds_read_b128_off<0>(addr);
     case 1: return lds_read_b128_off<4096>(addr);
     case 2: return lds_read_b128_off<8192>(addr);
-    default: return lds_read_b128_off<12288>(addr);
+    default: return lds_read_b128_off<0>(addr);
   }
 }
 
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void glb_void_t;
-
-// DMA input row iy of image b into ring slot rs (zeros outside the image);
-// every wave issues exactly 4 DMA instructions
-__device__ __forceinline__ void c64s_load_row(const C64sArgs& a, char* ring, int b, int iy, int rs, int tid) {
+// Per-lane buffer offsets of the row DMA (constant for the launch): chunk
+// i = r * 256 + tid of an LDS ring row is column i / 16, slot i % 16, which holds
+// global chunk c64s_slot(slot, col) of pixel col - 1; padding columns get an
+// offset past the descriptor (zeros).
+__device__ __forceinline__ void c64s_row_offsets(const C64sArgs& a, int tid, uint32_t (&voff)[4]) {
   using namespace c64s;
-  const bool rowv = (unsigned)iy < (unsigned)a.H;
-  const half_t* zero = static_cast<const half_t*>(a.zero);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int i = r * 256 + tid;                // 16-byte chunk of the LDS row (lane-linear)
+    const int i = r * 256 + tid;
     const int col = i >> 4, slot = i & 15;
     const int ix = col - 1;
-    const bool ok = rowv && (unsigned)ix < (unsigned)a.W;
-    const half_t* src = ok ? a.x + (((size_t)b * a.H + iy) * a.W + ix) * PIX + (c64s_slot(slot, col) << 3) : zero;
-    __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(ring + rs * RB + (r * 256 + (tid & ~63)) * 16),
-                                     16, 0, 0);
+    voff[r] = (unsigned)ix < (unsigned)a.W ? (uint32_t)(ix * 256 + (c64s_slot(slot, col) << 4)) : 0x80000000u;
+  }
+}
+
+// DMA input row iy of image b into ring slot rs (zeros outside the image):
+// RC * 16 = 960 chunks, so waves 0-2 issue 4 DMA instructions and wave 3 issues 3
+// (a wave-uniform split: the counted waits below only need each wave's own DMAs
+// to be older than its epilogue stores).  The row's base is the uniform soffset.
+template <typename Rsrc>
+__device__ __forceinline__ void c64s_load_row(const C64sArgs& a, char* ring, Rsrc x_rsrc, const uint32_t (&voff)[4],
+                                              int b, int iy, int rs, int tid) {
+  using namespace c64s;
+  const bool rowv = (unsigned)iy < (unsigned)a.H;
+  const int soff = rowv ? (b * a.H + iy) * a.W * 256 : 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (r == 3 && (tid >> 6) == 3) break;       // chunks 960..1023: past the row (wave-uniform)
+    dma_buf16(x_rsrc, ring + rs * RB + (r * 256 + (tid & ~63)) * 16, rowv ? voff[r] : 0x80000000u, soff);
   }
 }
 
@@ -99,6 +115,18 @@ __device__ __forceinline__ void c64s_wait_groups() {
   lds_waitcnt<2 * N>();
 }
 
+template <int N>
+struct c64s_nf {
+  static constexpr int value = N;
+};
+
+// Output row y is fragments 0-2 (columns 0..47) plus, every second row, one
+// TAIL fragment holding columns 48..W-1 of BOTH rows of the pair (lanes 0-7:
+// row y-1, lanes 8-15: row y): 7 fragments per row pair instead of 8, so no
+// MFMA work on the 8 columns past W = 56 (12.5 % of the round-4 kernel's).  A
+// band's last row when the band has an odd count gets a tail of its own (lanes
+// 8-15 masked).  The tail of the pair (y-1, y) reads input rows y-2 .. y+1: a
+// 5-row ring holds them while row y+2 lands.
 template <bool HAS_RES, int D>
 __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArgs a) {
   using namespace c64s;
@@ -120,17 +148,27 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
         for (int p = 0; p < 2; ++p) fa[t][cb][p] = *reinterpret_cast<const half8v*>(wr + t * PIX + cb * 64 + p * 32);
   }
   const int n0 = wave * 16 + 4 * q;            // this lane's 4 output channels (C/D layout)
-  const float4v bv = *reinterpret_cast<const float4v*>(a.bias + n0);
+  if (tid < 16) *reinterpret_cast<float4v*>(smem + BIAS + 16 * tid) = *reinterpret_cast<const float4v*>(a.bias + 4 * tid);
   const uint32_t ring = lds_addr(smem);
-  // per-lane LDS byte offset of column frow + kw, chunk 4c + q:
+  const auto x_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, 0x7fffffff, 0x00020000);
+  uint32_t voff[4];
+  c64s_row_offsets(a, tid, voff);
+  // per-lane LDS byte offset of column col0 + kw, chunk 4c + q:
   //   col*256 + (slot << 4), slot = (4c + q) ^ x, x = (2*col) & 15
-  // = loff[kw] ^ (c << 6): bits 6-7 hold c ^ (x >> 2), bits 4-5 q ^ (x & 3)
+  // = off ^ (c << 6): bits 6-7 hold c ^ (x >> 2), bits 4-5 q ^ (x & 3)
+  auto col_off = [&](int col) {
+    const int x = (2 * col) & 15;
+    return (uint32_t)(col * 256 + (((x >> 2) & 3) << 6) + (((q ^ x) & 3) << 4));
+  };
+  // fragments 0-2 read column frow + kw (+ 16 f by immediate offset); the tail
+  // reads column 48 + frow % 8 + kw = frow + kw + (48 or 40), the same swizzle
+  // (2 * col mod 16 does not change by a multiple of 8 columns): loff + tshift
   uint32_t loff[3];
 #pragma unroll
-  for (int kw = 0; kw < 3; ++kw) {
-    const int col = frow + kw, x = (2 * col) & 15;
-    loff[kw] = (uint32_t)(col * 256 + (((x >> 2) & 3) << 6) + (((q ^ x) & 3) << 4));
-  }
+  for (int kw = 0; kw < 3; ++kw) loff[kw] = col_off(frow + kw);
+  const uint32_t tshift = frow < 8 ? 48u * 256u : 40u * 256u;
+  const int tcol = 48 + (frow & 7);            // the tail fragment's output column
+  const int tailn = a.W - 48;                  // valid tail columns per row (1..8)
 
   for (int task = blockIdx.x; task < a.ntasks; task += gridDim.x) {
     const int b = task / a.nbands;
@@ -138,111 +176,132 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
     const int y1 = min(y0 + a.band, a.H);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();              // previous item's ring reads are done
-    c64s_load_row(a, smem, b, y0 - 1, (y0 + 3) & 3, tid);
-    c64s_load_row(a, smem, b, y0, y0 & 3, tid);
-    c64s_load_row(a, smem, b, y0 + 1, (y0 + 1) & 3, tid);
+    c64s_load_row(a, smem, x_rsrc, voff, b, y0 - 1, (y0 + 4) % RING, tid);
+    c64s_load_row(a, smem, x_rsrc, voff, b, y0, y0 % RING, tid);
+    c64s_load_row(a, smem, x_rsrc, voff, b, y0 + 1, (y0 + 1) % RING, tid);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int y = y0; y < y1; ++y) {
       // row y+1 landed: its DMA (issued one row ago) is older than this wave's
-      // last NST epilogue stores; then the barrier publishes everyone's DMA
-      // and ends every wave's reads of row y-2, whose slot row y+2 now takes
+      // last >= NST epilogue stores; then the barrier publishes everyone's DMA
+      // and ends every wave's reads of row y-3, whose slot row y+2 now takes
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
       __builtin_amdgcn_s_barrier();
-      if (y + 2 <= y1) c64s_load_row(a, smem, b, y + 2, (y + 2) & 3, tid);
-      // residual of row y -> registers now (untracked loads, retired by the
-      // epilogue's vmcnt(0)): a load issued in the epilogue exposed a full
-      // memory latency per row (+25 % on the residual variant)
-      const size_t rowpix = ((size_t)b * a.H + y) * a.W;
-      half4v rh[HAS_RES ? NF : 1], rl[HAS_RES ? NF : 1];
-      if constexpr (HAS_RES) {
+      if (y + 2 <= y1) c64s_load_row(a, smem, x_rsrc, voff, b, y + 2, (y + 2) % RING, tid);
+      const bool pair = ((y - y0) & 1) != 0;           // tail of rows (y-1, y)
+      const bool single = !pair && y == y1 - 1;        // odd band: tail of row y alone
+      // the tail's rows per lane: lanes 0-7 the pair's first row, 8-15 the second
+      const int trow = (pair && frow < 8) ? y - 1 : y;
+      const bool tok = (frow & 7) < tailn && (pair || frow < 8);
+      // pixel indices: B*H*W*128 < 2^31 (checked by the launcher), 32-bit offsets
+      const uint32_t rowpix = (uint32_t)((b * a.H + y) * a.W);
+      const uint32_t tpix = (uint32_t)((b * a.H + trow) * a.W + min(tcol, a.W - 1));
+      // ring rows of input rows y-2 .. y+1 (uniform); the tail's lanes 0-7 of a
+      // pair read output row y-1's taps (rb4[kh]), every other lane row y's (rb4[kh + 1])
+      uint32_t rb4[4];
 #pragma unroll
-        for (int f = 0; f < NF; ++f) {
-          const int ox = min(16 * f + frow, a.W - 1);
-          const size_t off = (rowpix + ox) * PIX + split_off(n0);
-          rh[f] = gload_b64_untracked(a.res + off);
-          rl[f] = gload_b64_untracked(a.res + off + 32);
-        }
-      }
-      float4v acc[NF];
-#pragma unroll
-      for (int f = 0; f < NF; ++f) acc[f] = float4v{0.f, 0.f, 0.f, 0.f};
-      // 72 groups g = (tap t, block cb, pixel fragment F): 2 B reads (hi, lo),
-      // 3 MFMAs; a D-deep register ring keeps the reads of groups g+1 .. g+D-1
-      // in flight behind group g's MFMAs (counted lgkmcnt)
-      half8v bf[D][2];
+      for (int i = 0; i < 4; ++i) rb4[i] = ring + (uint32_t)(((y - 2 + i + RING) % RING) * RB);
+      const bool tprev = pair && frow < 8;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) asm volatile("" : "+v"(loff[kw]));
-      uint32_t rowb[3];
+
+      auto body = [&](auto nft) {
+        constexpr int NF = decltype(nft)::value;       // 3: fragments 0-2; 4: + the tail
+        constexpr int NG = 18 * NF;                    // groups (tap, block, fragment)
+        half4v rh[HAS_RES ? NF : 1], rl[HAS_RES ? NF : 1];
+        // residual of the row's fragments -> registers when the row starts
+        // (untracked loads, retired by the epilogue's vmcnt(0)): a load issued in
+        // the epilogue exposed a full memory latency per row (+25 % on the residual
+        // variant)
+        auto load_res = [&]() {
+          if constexpr (HAS_RES) {
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh) rowb[kh] = ring + (uint32_t)(((y - 1 + kh) & 3) * RB);
-      auto issue = [&](int g, int buf) {
-        const int t = g >> 3, cb = (g >> 2) & 1, F = g & 3;
-        const int kh = t / 3, kw = t - 3 * kh;
+            for (int f = 0; f < NF; ++f) {
+              const uint32_t off = (f < 3 ? rowpix + 16 * f + frow : tpix) * PIX + split_off(n0);
+              rh[f] = gload_b64_untracked(a.res + off);
+              rl[f] = gload_b64_untracked(a.res + off + 32);
+            }
+          }
+        };
+        load_res();
+        float4v acc[NF];
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
-          bf[buf][p] = lds_read_frag(rowb[kh] + (loff[kw] ^ (uint32_t)((2 * cb + p) << 6)), F);
-      };
+        for (int f = 0; f < NF; ++f) acc[f] = float4v{0.f, 0.f, 0.f, 0.f};
+        // groups g = (tap t, block cb, pixel fragment F): 2 B reads (hi, lo), 3 MFMAs;
+        // a D-deep register ring keeps the reads of groups g+1 .. g+D-1 in flight
+        // behind group g's MFMAs (counted lgkmcnt)
+        half8v bf[D][2];
+        auto issue = [&](int g, int buf) {
+          const int t = g / (2 * NF), cb = (g / NF) & 1, F = g % NF;
+          const int kh = t / 3, kw = t - 3 * kh;
+          uint32_t base;
+          if (F < 3) {
+            base = rb4[kh + 1] + loff[kw];
+          } else {
+            // opaque per read: the 9 tail addresses are not hoisted into live registers
+            uint32_t ts = tshift;
+            asm volatile("" : "+v"(ts));
+            base = (tprev ? rb4[kh] : rb4[kh + 1]) + ts + loff[kw];
+          }
 #pragma unroll
-      for (int p = 0; p < D - 1; ++p) issue(p, p);
+          for (int p = 0; p < 2; ++p) bf[buf][p] = lds_read_frag(base ^ (uint32_t)((2 * cb + p) << 6), F);
+        };
 #pragma unroll
-      for (int g = 0; g < 72; ++g) {
-        const int buf = g % D;
-        if (g + D - 1 < 72) {
-          issue(g + D - 1, (g + D - 1) % D);
-          c64s_wait_groups<D - 1>();
-        } else if (g == 72 - 4) {
-          c64s_wait_groups<3>();
-        } else if (g == 72 - 3) {
-          c64s_wait_groups<2>();
-        } else if (g == 72 - 2) {
-          c64s_wait_groups<1>();
-        } else {
-          c64s_wait_groups<0>();
+        for (int p = 0; p < D - 1; ++p) issue(p, p);
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          const int buf = g % D;
+          if (g + D - 1 < NG) {
+            issue(g + D - 1, (g + D - 1) % D);
+            c64s_wait_groups<D - 1>();
+          } else {
+            c64s_wait_groups<0>();
+          }
+          lds_tie(bf[buf][0]);
+          lds_tie(bf[buf][1]);
+          const int t = g / (2 * NF), cb = (g / NF) & 1, F = g % NF;
+          float4v& c = acc[F];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][cb][0], bf[buf][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][cb][0], bf[buf][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][cb][1], bf[buf][0], c, 0, 0, 0);
         }
-        lds_tie(bf[buf][0]);
-        lds_tie(bf[buf][1]);
-        const int t = g >> 3, cb = (g >> 2) & 1, F = g & 3;
-        float4v& c = acc[F];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][cb][0], bf[buf][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][cb][0], bf[buf][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t][cb][1], bf[buf][0], c, 0, 0, 0);
-      }
-      // ---- epilogue: scale, bias (+ residual), ReLU, split store ----
-      if constexpr (HAS_RES) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // ---- epilogue: scale, bias (+ residual), ReLU, split store ----
+        if constexpr (HAS_RES) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int f = 0; f < NF; ++f) {
+            reg_tie(rh[f]);
+            reg_tie(rl[f]);
+          }
+        }
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
-          reg_tie(rh[f]);
-          reg_tie(rl[f]);
-        }
-      }
+          // fragments 0-2: columns 0..47 < W, every lane stores; the tail: lane 0
+          // (column 48 < W) always does, so every store instruction issues
+          if (f == 3 && !tok) continue;
+          const uint32_t off = (f < 3 ? rowpix + 16 * f + frow : tpix) * PIX + split_off(n0);
+          float4v v = acc[f] * a.acc_scale + *reinterpret_cast<const float4v*>(smem + BIAS + 4 * n0);
+          if constexpr (HAS_RES) {
 #pragma unroll
-      for (int f = 0; f < NF; ++f) {
-        const int ox = 16 * f + frow;
-        if (ox >= a.W) continue;
-        const size_t off = (rowpix + ox) * PIX + split_off(n0);
-        float4v v = acc[f] * a.acc_scale + bv;
-        if constexpr (HAS_RES) {
+            for (int e = 0; e < 4; ++e) v[e] += (float)rh[f][e] + (float)rl[f][e];
+          }
+          if (a.relu) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (float)rh[f][e] + (float)rl[f][e];
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          split_guard(a.ovf, v);
+          half4v h, l;
+          split_f16x4(v, h, l);
+          *reinterpret_cast<half4v*>(a.y + off) = h;
+          *reinterpret_cast<half4v*>(a.y + off + 32) = l;
         }
-        if (a.relu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        split_guard(a.ovf, v);
-        half4v h, l;
-        split_f16x4(v, h, l);
-        *reinterpret_cast<half4v*>(a.y + off) = h;
-        *reinterpret_cast<half4v*>(a.y + off + 32) = l;
-      }
+      };
+      if (pair || single) body(c64s_nf<4>{});
+      else body(c64s_nf<3>{});
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// W in [49, 62]: every one of the 4 pixel fragments has a valid column, so
-// each wave issues exactly NST epilogue stores per row (counted vmcnt above)
 template <int D>
 static void c64s_launch(const C64sArgs& a, bool res, int grid, hipStream_t st) {
   using namespace c64s;
@@ -258,11 +317,13 @@ static void c64s_launch(const C64sArgs& a, bool res, int grid, hipStream_t st) {
 // Measured and dropped (round 3, profiles/r3_c64_split_variants.md, deleted in round 5):
 // 32 couts per wave as one wave per SIMD holding all 64 input channels' A fragments
 // (W32, -2.3 %) or as K-split wave pairs exchanging partial sums through LDS (-2.7 %).
+// Round 5: W in [49, 56] (three full fragments and a tail of at most 8 columns per
+// row; the round-4 kernel's fourth fragment per row also took W up to 62).
 bool conv3x3_split_c64_supported(int H, int W, int C, int Cout) {
-  return C == 64 && Cout == 64 && W >= 49 && W <= 62 && H >= 1;
+  return C == 64 && Cout == 64 && W >= 49 && W <= c64s::WMAX && H >= 1;
 }
 
-void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
+bool conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
                               const void* zero, int B, int H, int W, int relu, float acc_scale, int* ovf,
                               hipStream_t st) {
   using namespace c64s;
@@ -279,6 +340,7 @@ void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bia
   a.W = W;
   a.relu = relu;
   a.acc_scale = acc_scale;
+  if ((long)B * H * W * c64s::PIX * 2 >= (1L << 31)) return false;   // 32-bit byte offsets
   const int per = 2 * device_cu_count();
   // rows per work item: BAND, or fewer so that a small batch still makes ~2
   // work items per resident workgroup (each item re-reads 2 halo rows)
@@ -291,6 +353,7 @@ void conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bia
   // ring depth 3: a 4th group of reads spills the residual variant (256 VGPRs at
   // depth 3), and without a residual it measured +0.09 % (profiles/r3_ab_c64_depth.log)
   c64s_launch<3>(a, res != nullptr, grid, st);
+  return true;
 }
 
 }  // namespace idunno

@@ -61,6 +61,28 @@ def test_c64_split_lds_swizzle_conflict_free_cpu():
                 assert len(slots) == 16, (base, c0, g)
 
 
+def test_c64_split_tail_fragment_conflict_free_cpu():
+    """The tail fragment of a row pair: lanes 0-7 read columns 48.. of one ring
+    row, lanes 8-15 the same columns of another (ring rows 60 * 256 B apart, a
+    multiple of 16 slots): still 16 distinct 16-byte slots per lane group for
+    every tap shift and chunk base."""
+    groups = [[*range(0, 4), *range(12, 16), *range(20, 28)], [*range(4, 12), *range(16, 20), *range(28, 32)]]
+    groups += [[lane + 32 for lane in g] for g in groups]
+    rb = 60 * 256
+    for kw in range(3):
+        for c0 in range(0, 16, 4):
+            for ra, rbw in ((0, 1), (3, 4), (4, 0), (2, 2)):
+                for g in groups:
+                    addr = set()
+                    for lane in g:
+                        fr = lane & 15
+                        col = 48 + (fr & 7) + kw
+                        row = ra if fr < 8 else rbw
+                        chunk = (c0 + (lane >> 4)) ^ ((2 * col) & 15)
+                        addr.add(((row * rb + col * 256 + chunk * 16) // 16) % 16)
+                    assert len(addr) == 16, (kw, c0, ra, rbw, g)
+
+
 def _unpack_split_p3(sp3, scale, cout, kh, kw):
     cpk = (3 * kw + 7) // 8
     v = sp3.double().reshape(cout, -1, 2, 32)
@@ -265,10 +287,14 @@ SPLIT_TILES = [26, 27, 34, 36, 38, 42]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,H,W", [(2, 56, 56), (3, 13, 49), (1, 9, 62)])
+@pytest.mark.parametrize("B,H,W", [(2, 56, 56), (3, 13, 49), (1, 9, 52), (160, 56, 56), (40, 56, 56),
+                                   (150, 13, 52)])
 @pytest.mark.parametrize("res", [False, True])
 def test_conv_split_c64_rows(ops, B, H, W, res):
-    """Row-streaming register-weight 3x3 64->64 kernel (tile 50, 16 couts per wave)."""
+    """Row-streaming register-weight 3x3 64->64 kernel (tile 50, 16 couts per wave).
+    Small batches run one-row bands (every row's tail fragment alone); B = 160 / 40
+    at H = 56 run bands of 8 / 2 rows (tails of row pairs); B = 150 at H = 13 runs
+    two-row bands whose last band has one row."""
     _c64_rows_case(ops, B, H, W, res)
 
 

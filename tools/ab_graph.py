@@ -5,7 +5,7 @@ interleaved rounds on one device (cdna_hip_programming §5.4 rule 24; boxes of
 the pool differ by several % in wall time, so cross-call numbers do not rank
 builds).
 
-usage: python tools/ab_graph.py --alt-so ab/_C_base.so [--model resnet18] [--batch 400]
+usage: python tools/ab_graph.py --alt-so ab/_C_base.so [--model resnet18] [--batch 400] [--dtype fp32]
 """
 import argparse
 import importlib.util
@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--batch", type=int, default=400)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--dtype", default="fp32", help="fp32 (split fp16, the headline) or fp16")
     a = ap.parse_args()
     from idunno import ops
     from idunno.models import HipRunner, build_program
@@ -40,7 +41,7 @@ def main():
     dev = torch.device("cuda")
     main_mod = ops.load()
     alt_mod = load_alt(a.alt_so)
-    prog = build_program(a.model)
+    prog = build_program(a.model, dtype=a.dtype)
     shard = ops.synth_images(1234, 0, a.batch, dev)
     runs, outs, keep = {}, {}, []
     for name, mod in (("main", main_mod), ("alt", alt_mod)):
