@@ -23,7 +23,10 @@
 // B-fragment reads (lane = pixel col + 16 * k-group) conflict-free for every
 // tap shift, the tail fragment's two-row lane split included (exhaustive
 // checks in tests/test_split.py).
-// Persistent: a work item is a band of BAND output rows of one image.
+// Persistent: workgroup g takes the g-th equal share of the B * H output rows
+// (flattened image-major), as one band per image it touches, so every
+// workgroup finishes within a row of the others (round 4: 8-row bands, 2800
+// items over 512 workgroups = 5.47 rounds, the last one half empty).
 #include "../kernels.h"
 #include "../launch_util.h"
 
@@ -37,7 +40,6 @@ constexpr int RB = RC * 256;       // bytes per ring row
 constexpr int RING = 5;            // rows y-2 .. y+1 in use (a row pair's tail fragment) + row y+2 landing
 constexpr int BIAS = RING * RB;    // the 64 biases (fp32), read by the epilogue: no VGPRs held for them
 constexpr int LDS = BIAS + 256;    // 77,056 B: 2 workgroups per CU
-constexpr int BAND = 8;            // output rows per work item (at most; fewer for small batches)
 constexpr int WMAX = 56;           // 3 full fragments + an 8-column tail per row
 constexpr int NST = 6;             // epilogue stores per wave and row, at least (3 fragments x hi, lo)
 }  // namespace c64s
@@ -49,7 +51,7 @@ struct C64sArgs {
   const half_t* res;    // split [B][H][W][128] or nullptr
   half_t* y;            // split [B][H][W][128]
   const void* zero;     // unused (padding comes from out-of-range buffer offsets)
-  int B, H, W, relu, band, nbands, ntasks;
+  int B, H, W, relu, nrows;
   float acc_scale;
   int* ovf;             // split range guard flag or nullptr (common.h split_guard)
 };
@@ -134,7 +136,10 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int frow = lane & 15, q = lane >> 4;
-  if ((int)blockIdx.x >= a.ntasks) return;   // uniform
+  // this workgroup's rows [r_begin, r_end) of the B * H output rows
+  const int r_begin = (int)((long long)blockIdx.x * a.nrows / gridDim.x);
+  const int r_end = (int)((long long)(blockIdx.x + 1) * a.nrows / gridDim.x);
+  if (r_begin >= r_end) return;              // uniform
 
   // ---- A fragments of this wave's 16 couts: [tap][block][hi|lo] ----
   half8v fa[9][2][2];
@@ -170,10 +175,11 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
   const int tcol = 48 + (frow & 7);            // the tail fragment's output column
   const int tailn = a.W - 48;                  // valid tail columns per row (1..8)
 
-  for (int task = blockIdx.x; task < a.ntasks; task += gridDim.x) {
-    const int b = task / a.nbands;
-    const int y0 = (task - b * a.nbands) * a.band;
-    const int y1 = min(y0 + a.band, a.H);
+  for (int r = r_begin; r < r_end;) {           // one band per image the range touches
+    const int b = r / a.H;
+    const int y0 = r - b * a.H;
+    const int y1 = min(a.H, y0 + (r_end - r));
+    r += y1 - y0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();              // previous item's ring reads are done
     c64s_load_row(a, smem, x_rsrc, voff, b, y0 - 1, (y0 + 4) % RING, tid);
@@ -342,16 +348,11 @@ bool conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bia
   a.acc_scale = acc_scale;
   if ((long)B * H * W * c64s::PIX * 2 >= (1L << 31)) return false;   // 32-bit byte offsets
   const int per = 2 * device_cu_count();
-  // rows per work item: BAND, or fewer so that a small batch still makes ~2
-  // work items per resident workgroup (each item re-reads 2 halo rows)
-  int band = BAND;
-  while (band > 1 && (long)B * ((H + band - 1) / band) < 2L * per) band /= 2;
-  a.band = band;
-  a.nbands = (H + band - 1) / band;
-  a.ntasks = B * a.nbands;
-  const int grid = a.ntasks < per ? a.ntasks : per;
-  // ring depth 3: a 4th group of reads spills the residual variant (256 VGPRs at
-  // depth 3), and without a residual it measured +0.09 % (profiles/r3_ab_c64_depth.log)
+  // equal row shares over the resident workgroups, at least 4 rows each (a band
+  // loads 2 halo rows and waits for its first 3 rows before computing)
+  a.nrows = B * H;
+  int grid = (a.nrows + 3) / 4;
+  if (grid > per) grid = per;
   c64s_launch<3>(a, res != nullptr, grid, st);
   return true;
 }
