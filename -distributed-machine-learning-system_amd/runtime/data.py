@@ -257,6 +257,7 @@ class SdfsSource:
         self._pool = None
         self.readahead_hits = 0
         self.local_reads = 0                      # shards streamed from this node's own replica file
+        self.tracer = None                        # optional utils.tracing.Tracer: "sdfs.fetch" spans
         if self.device.type == "cuda":
             sdfs.hbm_provider = self.export_shard
 
@@ -361,6 +362,12 @@ class SdfsSource:
         return t
 
     def _fetch(self, k: int) -> torch.Tensor:
+        if self.tracer is None:
+            return self._fetch_body(k)
+        with self.tracer.span("sdfs.fetch", shard=k):
+            return self._fetch_body(k)
+
+    def _fetch_body(self, k: int) -> torch.Tensor:
         with self.lock:
             t = self.cache.get(k)
             if t is not None:

@@ -1384,7 +1384,11 @@ def _sdfs_pass(a, node, per_q: int) -> dict:
         src.stager.timeline = tl
         node.gpu_timeline = tl
         b0 = src.stager.bytes_staged
+        src.tracer = node.tracer
+        th0 = time.time()
         cold = run_pass("cold")
+        th1 = time.time()
+        src.tracer = None
         node.gpu_timeline = src.stager.timeline = None
         staged = src.stager.bytes_staged - b0
         if gpu:
@@ -1404,6 +1408,10 @@ def _sdfs_pass(a, node, per_q: int) -> dict:
         if a.sdfs_trace and iv:
             ev = [{"name": k, "ph": "X", "ts": 1000.0 * t0, "dur": 1000.0 * (t1 - t0), "pid": 0,
                    "tid": 1 if k == "h2d" else 0, "args": {"n": n}} for k, t0, t1, n in iv]
+            # host spans of the cold pass (node thread activity: query submit, chunk staging
+            # waits, launches, SDFS fetches), on their own clock (pid 1)
+            ev += [dict(e, pid=1, ts=e["ts"] - th0 * 1e6) for e in node.tracer.export()
+                   if e["ph"] in ("X", "i") and th0 * 1e6 <= e["ts"] <= th1 * 1e6]
             with open(a.sdfs_trace, "w") as f:
                 json.dump({"traceEvents": ev, "displayTimeUnit": "ms"}, f)
     finally:
