@@ -1492,6 +1492,11 @@ torch::Tensor synth_images(int64_t seed, int64_t start, int64_t n, int64_t hw, t
 
 int64_t pick_tile(int64_t M, int64_t Cout) { return conv_glds_pick((int)M, (int)Cout); }
 
+namespace idunno {
+void stage_file_native(const std::string& path, torch::Tensor out, std::vector<torch::Tensor> pinned, int64_t stream,
+                       int64_t nthreads);
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "IDunno-MI355X native HIP kernels (gfx950)";
   m.def("conv1x1_dual", &conv1x1_dual, "bottleneck expansion 1x1 + 1x1 downsample as one GEMM (fp16)",
@@ -1579,6 +1584,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "split range guard flag (int32 device tensor) for this thread's split launches; None = off",
         py::arg("flag") = py::none());
   m.def("synth_images", &synth_images, "deterministic synthetic uint8 images [n,hw,hw,3]");
+  m.def("stage_file_native", &idunno::stage_file_native,
+        "host -> HBM staging of a file's bytes into `out` through pinned ping-pong buffers on `stream`, "
+        "parallel pread(2) with the GIL released (runtime/staging.cpp)",
+        py::arg("path"), py::arg("out"), py::arg("pinned"), py::arg("stream"), py::arg("nthreads") = 8);
   m.def("graph_launch", &graph_launch, "hipGraphLaunch(exec, current stream): a replay without any host wait");
   m.def("pick_tile", &pick_tile, "tile id the conv heuristic picks for (M, Cout)");
 }

@@ -90,6 +90,17 @@ class HbmStager:
 
     READ_THREADS = 8
 
+    def _native(self):
+        """The extension's GIL-free file stager (None: the Python preadv path)."""
+        if not self.gpu or os.environ.get("IDUNNO_PY_STAGING") == "1":
+            return None
+        try:
+            from .. import ops
+
+            return getattr(ops.load(), "stage_file_native", None)
+        except Exception:  # noqa: BLE001  (no extension: the Python path)
+            return None
+
     def stage_file(self, path: str, shape: tuple) -> torch.Tensor:
         """``_stage_file`` with the current stream ordered after the copy."""
         t, ev = self._stage_file(path, shape)
@@ -121,13 +132,28 @@ class HbmStager:
                 out = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
             step = self.pinned[0].numel()
             nb = len(self.pinned)
+            native = self._native()
             with self.lock:
                 ev = None
                 tl = self.timeline
                 if tl is not None:
                     ev0 = torch.cuda.Event(enable_timing=True)
                     ev0.record(self.stream)
-                for i, off in enumerate(range(0, nbytes, step)):
+                if native is not None:
+                    # the whole file with the GIL released (csrc/runtime/staging.cpp); it
+                    # returns once the pinned buffers are free again
+                    for b in range(nb):
+                        if self._done[b] is not None:
+                            self._done[b].synchronize()
+                            self._done[b] = None
+                    native(path, out, self.pinned, self.stream.cuda_stream, self.READ_THREADS)
+                    with torch.cuda.stream(self.stream):
+                        ev = torch.cuda.Event()
+                        ev.record(self.stream)
+                    nbytes_left = 0
+                else:
+                    nbytes_left = nbytes
+                for i, off in enumerate(range(0, nbytes_left, step)):
                     b = i % nb
                     n = min(step, nbytes - off)
                     if self._done[b] is not None:
@@ -232,11 +258,17 @@ class SdfsSource:
     announced to the SDFS master so peers can do the same (``peer_copy``)."""
 
     def __init__(self, sdfs, device, shard_images: int = 500, cache_bytes: int = 32 << 30, peer_copy: bool = True,
-                 readahead: int = 1):
+                 readahead: int = 1, stage_streams: int = 1):
         self.sdfs = sdfs
         self.device = torch.device(device)
         self.S = int(shard_images)
-        self.stager = HbmStager(self.device)
+        # shards stage on `stage_streams` side streams at once (one stager, pinned pair and
+        # background worker each).  Two measured no faster than one on the cold SDFS pass
+        # (0.70 vs 0.74 cold/warm): the copies themselves run at ~45 GB/s beside the
+        # forwards (tools/overlap_probe.py under rocprofv3); the host reads set the pace
+        self.nstage = max(1, int(stage_streams)) if self.device.type == "cuda" else 1
+        self.stagers = [HbmStager(self.device) for _ in range(self.nstage)]
+        self.stager = self.stagers[0]
         self.cache: OrderedDict[int, torch.Tensor] = OrderedDict()
         self.ver: dict[int, int] = {}             # SDFS version of each cached shard
         self.cache_bytes = cache_bytes
@@ -287,7 +319,7 @@ class SdfsSource:
 
     def _prefetch(self, k: int, requested: bool = False) -> None:
         """Start fetching shard k in the background unless cached or in flight.
-        One worker, FIFO, so shards stage in request order.  Speculative
+        ``stage_streams`` workers, FIFO, so shards start staging in request order.  Speculative
         readahead (past a request) is bounded to ``max_queued`` background
         fetches; a shard an announced chunk needs (``requested``) always queues."""
         with self.lock:
@@ -298,7 +330,7 @@ class SdfsSource:
             if self._pool is None:
                 from concurrent.futures import ThreadPoolExecutor
 
-                self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="sdfs-readahead")
+                self._pool = ThreadPoolExecutor(max_workers=self.nstage, thread_name_prefix="sdfs-readahead")
             dev = self.device
 
             def run():
@@ -386,7 +418,7 @@ class SdfsSource:
                 path, ver = loc
                 try:
                     n = os.path.getsize(path) // IMG_BYTES
-                    t, ev = self.stager._stage_file(path, (n, HW, HW, 3))
+                    t, ev = self.stagers[k % self.nstage]._stage_file(path, (n, HW, HW, 3))
                     self.local_reads += 1
                 except OSError:                   # replaced by a newer version meanwhile
                     loc = None
@@ -396,7 +428,7 @@ class SdfsSource:
                     raise KeyError(f"missing SDFS shard {name}")
                 data, ver = got
                 n = len(data) // IMG_BYTES
-                t, ev = self.stager._stage(data, (n, HW, HW, 3))
+                t, ev = self.stagers[k % self.nstage]._stage(data, (n, HW, HW, 3))
         dropped = []
         with self.lock:
             self.fetches += 1
@@ -435,7 +467,19 @@ class SdfsSource:
         # took the stager first would put a whole shard in front of the one needed now
         for r in range(1, self.readahead + 1):
             self._prefetch(last + r)
-        return parts[0] if len(parts) == 1 else torch.cat(parts, 0)
+        if len(parts) == 1:
+            return parts[0]
+        # joined with async copies, not torch.cat: the first cat of a process loads
+        # its kernel's code object, which waited for the in-flight H2D staging to
+        # drain and held the round thread 14-25 ms in the cold SDFS pass
+        # (profiles/r5_sdfs_trace_before.json, tools/alloc_probe.py)
+        out = torch.empty((sum(p.shape[0] for p in parts), *parts[0].shape[1:]), dtype=parts[0].dtype,
+                          device=parts[0].device)
+        i = 0
+        for p in parts:
+            out[i:i + p.shape[0]].copy_(p, non_blocking=True)
+            i += p.shape[0]
+        return out
 
 
 def load_image_u8(data: bytes, resize: int = 256, crop: int = 224) -> np.ndarray:

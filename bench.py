@@ -1381,21 +1381,29 @@ def _sdfs_pass(a, node, per_q: int) -> dict:
             return time.perf_counter() - t0
 
         tl = [] if gpu else None
-        src.stager.timeline = tl
+        for sg in src.stagers:
+            sg.timeline = tl
         node.gpu_timeline = tl
-        b0 = src.stager.bytes_staged
+        b0 = sum(sg.bytes_staged for sg in src.stagers)
         src.tracer = node.tracer
         th0 = time.time()
         cold = run_pass("cold")
         th1 = time.time()
         src.tracer = None
-        node.gpu_timeline = src.stager.timeline = None
-        staged = src.stager.bytes_staged - b0
+        node.gpu_timeline = None
+        for sg in src.stagers:
+            sg.timeline = None
+        staged = sum(sg.bytes_staged for sg in src.stagers) - b0
         if gpu:
             torch.cuda.synchronize(src.device)
         ovl, iv = _timeline_overlap(tl) if gpu else (None, [])
         warm = run_pass("warm")
-        h2d_ms = sum(t1 - t0 for k, t0, t1, _ in iv if k == "h2d")
+        # wall time with at least one H2D in flight (the union: stagers overlap each other)
+        h2d_ms, end = 0.0, float("-inf")
+        for t0, t1 in sorted((t0, t1) for k, t0, t1, _ in iv if k == "h2d"):
+            if t1 > end:
+                h2d_ms += t1 - max(t0, end)
+                end = t1
         out = {"value_system_sdfs_cold": round(n_img / cold, 2), "value_system_sdfs_warm": round(n_img / warm, 2),
                "sdfs_cold_to_warm": round(warm / cold, 4), "sdfs_images": n_img, "sdfs_shards": shards,
                "sdfs_put_gb_per_s": round(n_img * 150528 / put_s / 1e9, 3),
@@ -1404,7 +1412,7 @@ def _sdfs_pass(a, node, per_q: int) -> dict:
                "sdfs_h2d_overlap_frac": round(ovl, 4) if ovl is not None else None,
                "sdfs_local_file_reads": src.local_reads, "sdfs_readahead_hits": src.readahead_hits,
                "sdfs_path": "SDFS store (local replica file) -> parallel preadv into pinned ping-pong buffers -> "
-                            "hipMemcpyAsync on a side stream -> HBM shard cache -> rounds (4-shard readahead)"}
+                            f"hipMemcpyAsync on {src.nstage} side stream(s) -> HBM shard cache -> rounds (4-shard readahead)"}
         if a.sdfs_trace and iv:
             ev = [{"name": k, "ph": "X", "ts": 1000.0 * t0, "dur": 1000.0 * (t1 - t0), "pid": 0,
                    "tid": 1 if k == "h2d" else 0, "args": {"n": n}} for k, t0, t1, n in iv]

@@ -29,6 +29,40 @@ def test_hbm_stager_roundtrip():
     assert t.is_cuda and np.array_equal(t.cpu().numpy().reshape(-1), data)
 
 
+@pytest.mark.parametrize("pinned_mb,threads", [(1, 8), (64, 8), (3, 1)])
+def test_hbm_stager_file_native(tmp_path, pinned_mb, threads):
+    """HbmStager.stage_file through the extension's GIL-free stager
+    (csrc/runtime/staging.cpp): byte-exact against the file for sizes that are
+    not a multiple of the pinned pieces, then the pinned buffers are reusable by
+    the Python byte path; the Python preadv path gives the same bytes."""
+    from idunno import ops
+    from idunno.runtime.data import HbmStager
+
+    assert hasattr(ops.load(), "stage_file_native")
+    rng = np.random.default_rng(pinned_mb + threads)
+    data = rng.integers(0, 256, size=(9 << 20) + 4099, dtype=np.uint8)
+    p = tmp_path / "shard.bin"
+    p.write_bytes(data.tobytes())
+    st = HbmStager(torch.device("cuda"), pinned_bytes=pinned_mb << 20)
+    st.READ_THREADS = threads
+    assert st._native() is not None
+    t = st.stage_file(str(p), (data.size,))
+    assert t.is_cuda and np.array_equal(t.cpu().numpy(), data)
+    t2 = st.stage(data[:1000].tobytes(), (1000,))
+    assert np.array_equal(t2.cpu().numpy(), data[:1000])
+    with pytest.raises(Exception):
+        st.stage_file(str(tmp_path / "missing.bin"), (10,))
+    import os
+
+    os.environ["IDUNNO_PY_STAGING"] = "1"
+    try:
+        assert st._native() is None
+        t3 = st.stage_file(str(p), (data.size,))
+        assert np.array_equal(t3.cpu().numpy(), data)
+    finally:
+        os.environ.pop("IDUNNO_PY_STAGING")
+
+
 def _cluster(source_kind):
     from idunno.runtime.cluster import LocalCluster
     from idunno.runtime.data import SdfsSource, SyntheticSource

@@ -75,3 +75,24 @@ def test_elastic_group_rccl_standby_pair_one_rank():
     assert g.standby_rank == -1
     _rounds(g, range(4), 7)
     g.teardown()
+
+
+def test_two_rccl_ranks_on_one_gpu():
+    """World 2 over RCCL on a one-GPU box (tools/rccl_two_rank.py: per-rank
+    NCCL_HOSTID, socket transport on loopback): QueryPlane broadcast / gather /
+    bucketed scatter byte-exact, ElasticGroup gather rounds to the coordinator
+    and the standby, and abort() of a communicator whose peer died."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "rccl_two_rank.py")], capture_output=True,
+                       text=True, timeout=300, cwd=root)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and lines, (r.returncode, r.stdout[-3000:], r.stderr[-3000:])
+    res = json.loads(lines[-1])
+    assert res["backend"] == "nccl" and res["epoch_backend"] == "nccl", res
+    assert res["gather_ok"] and res["scatter_ok"] and res["rounds_ok"], res
+    assert res["abandoned"] and res["abort_returned"] and res["reformed_world"] == 1, res
