@@ -23,9 +23,9 @@ without a GPU).
 """
 from __future__ import annotations
 
-import os
-
+import contextlib
 import math
+import os
 import threading
 from dataclasses import dataclass, field
 
@@ -479,6 +479,27 @@ def emulate(p: Program, img_u8: torch.Tensor) -> torch.Tensor:
 # ---------------------------------------------------------------------------
 
 _CAPTURE_LOCK = threading.Lock()
+
+
+@contextlib.contextmanager
+def _capture_nosync(g, device):
+    """``torch.cuda.graph(g, capture_error_mode="thread_local")`` without the
+    device-wide synchronize (and gc / empty_cache) that context manager does
+    first: a runtime that captures a graph for a new send slot while an RCCL
+    collective of an earlier round is pending on a paused or dead member would
+    wait for that collective -- until the backend's timeout (120 s) when the
+    member was killed (bench --rehearse-rccl worker failover, round 5).  Work
+    queued on the current stream is ordered before the capture by a stream
+    dependency instead."""
+    s = torch.cuda.Stream(device=device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        g.capture_begin(capture_error_mode="thread_local")
+        try:
+            yield
+        finally:
+            g.capture_end()
+    torch.cuda.current_stream(device).wait_stream(s)
 
 
 def x_is_cuda(t: torch.Tensor) -> bool:
@@ -1128,7 +1149,7 @@ class HipRunner:
             g = torch.cuda.CUDAGraph()
             self._capturing = True
             try:
-                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                with _capture_nosync(g, self.device):
                     sout = self.forward(shard, start, batch, start_offset, packed)
             finally:
                 self._capturing = False
@@ -1192,7 +1213,7 @@ class HipRunner:
             g = torch.cuda.CUDAGraph()
             self._capturing = True
             try:
-                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                with _capture_nosync(g, self.device):
                     sout = self.forward(sin, packed=packed)
             finally:
                 self._capturing = False

@@ -252,7 +252,30 @@ class ElasticGroup:
             self.pg = pg
             self.epoch, self.members, self.rank = epoch, list(members), rank
             self._alloc(world)
+            if self.backend == "nccl" and not self._warm_up():
+                log.error("%s: epoch %d: warm-up gather did not complete", me, epoch)
+                self.abort_async()
+                return False
             return True
+
+    def _warm_up(self) -> bool:
+        """One gather (pair) of every member while all of them are still in
+        ``form()``: RCCL sets up a pair's point-to-point connection at the pair's
+        first operation, and that handshake blocks the POSTING thread until the
+        peer posts too.  Without it the coordinator's first post of an epoch
+        waited on a member paused in its chunk, and when that member was killed,
+        for the backend's whole timeout (120 s) instead of the failure detector's
+        2 s (bench --rehearse-rccl worker failover, round 5)."""
+        work = self.post_gather(0)
+        end = time.monotonic() + self.timeout_s
+        while not work.is_completed():
+            if time.monotonic() > end:
+                return False
+            time.sleep(0.001)
+        work.wait()
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        return True
 
     def _alloc(self, world: int) -> None:
         dev, rows, D = self.device, self.max_chunk + HDR_ROWS, self.depth

@@ -104,11 +104,18 @@ def parse(argv=None):
     ap.add_argument("--rehearse-gloo", action="store_true",
                     help="N > 1 on a box with fewer GPUs: gloo collectives on GPU tensors, ranks share "
                          "cuda:(local_rank %% device_count) -- exercises the multi-rank GPU path, not RCCL")
+    ap.add_argument("--rehearse-rccl", action="store_true",
+                    help="N > 1 on a box with fewer GPUs over RCCL itself: every process gets its own "
+                         "NCCL_HOSTID (RCCL then treats the ranks sharing a GPU as separate hosts and "
+                         "connects them over its socket transport on loopback); ranks share "
+                         "cuda:(local_rank %% device_count) -- the RCCL code paths of the N-GPU run, not xGMI")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N > 1: keep the descriptor broadcast and result gather between the forwards "
                          "(default: double-buffered, overlapped with the next round's forward)")
     ap.add_argument("--no-extras", action="store_true", help="skip the strong-scaling / fp16 / numerics extras")
     ap.add_argument("--no-system", action="store_true", help="skip phases 2-3 (system + failover)")
+    ap.add_argument("--node-phases", default="system,failover,worker",
+                    help="node phases to run after the headline (comma list of system, failover, worker)")
     ap.add_argument("--extras-timeout", type=float, default=150.0,
                     help="seconds per system / failover phase (bounded: the driver gives the whole run 600 s)")
     ap.add_argument("--extras-budget", type=float, default=240.0,
@@ -314,6 +321,7 @@ def _kill_phase(a, work: str, phase: str, tag: str, extra: list, driver: int) ->
             state["done"] = True
 
     drv = procs[driver % n]
+    t_phase = time.time()
     deadline = min(time.time() + a.extras_timeout, getattr(a, "phase_deadline", float("inf")))
     try:
         while time.time() < deadline:
@@ -325,6 +333,8 @@ def _kill_phase(a, work: str, phase: str, tag: str, extra: list, driver: int) ->
             time.sleep(0.02)
     finally:
         _stop_all(procs)
+    print(f"bench: {tag} phase {time.time() - t_phase:.1f} s (driver rc={drv.returncode})", file=sys.stderr,
+          flush=True)
     d = _read_json(out)
     if d is None:
         return {"extras_error": f"{tag} phase failed (driver rc={drv.returncode})"}
@@ -363,7 +373,10 @@ def _worker_failover_phase(a, work: str) -> dict:
             break                                         # out of extras budget: report what ran
         d = _kill_phase(a, work, "worker", f"worker_k{k}", ["--kill-chunks", str(k)], driver=0)
         if "extras_error" in d:
-            return d
+            if not rec:
+                return d
+            out["extras_error"] = d["extras_error"]         # report the k that ran, and the failure
+            break
         rec[str(k)] = d
     if not rec:
         return {"extras_error": "worker failover: out of extras budget"}
@@ -392,6 +405,8 @@ def _phase_argv(a, phase: str, out: str, work: str) -> list:
         argv.append("--dry-run")
     if a.rehearse_gloo:
         argv.append("--rehearse-gloo")
+    if a.rehearse_rccl:
+        argv.append("--rehearse-rccl")
     return argv
 
 
@@ -417,17 +432,22 @@ def launcher(a, argv) -> int:
         if not a.no_system and not rc:                    # (a failed headline rank: no node phases on that box)
             t0 = time.time()
             skipped = []
-            for name, fn in (("system", _system_phase), ("failover", _failover_phase),
-                             ("worker failover", _worker_failover_phase)):
+            want = set(a.node_phases.split(","))
+            for key, name, fn in (("system", "system", _system_phase), ("failover", "failover", _failover_phase),
+                                  ("worker", "worker failover", _worker_failover_phase)):
+                if key not in want:
+                    continue
                 left = a.extras_budget - (time.time() - t0)
                 if left < 20.0:
                     skipped.append(name)
                     continue
                 a.phase_deadline = time.time() + left
+                tp = time.time()
                 try:
                     d = fn(a, work)
                 except Exception as e:  # noqa: BLE001
                     d = {"extras_error": f"{name}: {type(e).__name__}: {e}"}
+                head.setdefault("phase_wall_s", {})[name] = round(time.time() - tp, 1)
                 err = d.pop("extras_error", None)
                 if err:
                     head["extras_error"] = (head.get("extras_error", "") + "; " + err).lstrip("; ")
@@ -449,6 +469,10 @@ def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else argv
     a = parse(argv)
     role = os.environ.get(ROLE)
+    if a.rehearse_rccl and role in ("rank", "node"):
+        # before any RCCL communicator: a host id of this process's own (see --rehearse-rccl)
+        os.environ["NCCL_HOSTID"] = f"idunno-rehearse-{os.getpid()}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     if role == "rank":
         return run_rank(a)
     if role == "node":
@@ -499,8 +523,8 @@ def run_rank(a) -> int:
     from idunno.runtime.jobstate import JobState
     from idunno.runtime.scheduler import split_range
 
-    if a.rehearse_gloo and not a.dry_run:
-        # rehearsal of the N > 1 path on a box with fewer GPUs than ranks (see --rehearse-gloo)
+    if (a.rehearse_gloo or a.rehearse_rccl) and not a.dry_run:
+        # rehearsal of the N > 1 path on a box with fewer GPUs than ranks (see --rehearse-gloo/-rccl)
         os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
     t_rank0 = time.perf_counter()
     # collectives time out well inside the launcher's limit (a dead peer must not hang a rank
@@ -1052,6 +1076,12 @@ def run_node(a) -> int:
     from idunno.runtime.node import Node
     from idunno.runtime.transport import TcpTransport
 
+    if os.environ.get("IDUNNO_BENCH_STACKS"):
+        # debugging a stuck phase: every node process dumps all its threads' stacks
+        # to stderr every IDUNNO_BENCH_STACKS seconds
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["IDUNNO_BENCH_STACKS"]), repeat=True)
     rank = int(os.environ.get("RANK", "0"))
     n = int(os.environ.get("WORLD_SIZE", "1"))           # node processes (failover: >= 2)
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -1059,8 +1089,8 @@ def run_node(a) -> int:
     if not a.dry_run and not gpu:
         print(json.dumps({"error": "bench.py phases 2-3 need a GPU (MI355X); use --dry-run on CPU"}), flush=True)
         return 2
-    if gpu and a.rehearse_gloo:
-        local %= max(1, torch.cuda.device_count())       # N nodes on fewer GPUs, gloo rounds
+    if gpu and (a.rehearse_gloo or a.rehearse_rccl):
+        local %= max(1, torch.cuda.device_count())       # N nodes on fewer GPUs (gloo / RCCL-socket rounds)
     dev = torch.device("cuda", local) if gpu else torch.device("cpu")
     if gpu:
         torch.cuda.set_device(dev)
@@ -1083,6 +1113,10 @@ def run_node(a) -> int:
             cfg.update(heartbeat_period_s=0.1, failure_timeout_s=1.0, metadata_period_s=0.2)
         else:
             cfg.update(heartbeat_period_s=0.3, failure_timeout_s=2.0, metadata_period_s=0.2)
+    if os.environ.get("IDUNNO_BENCH_LOG_DIR"):
+        # node logs of every phase kept (debugging a rehearsal): <dir>/<phase tag>/nodeNN.log
+        cfg.update(log_dir=os.path.join(os.environ["IDUNNO_BENCH_LOG_DIR"],
+                                        os.path.basename((a.work_dir or a.phase).rstrip("/"))))
     name = cfg.node_name(rank)
     ex = FakeExecutor() if a.dry_run else HipExecutor(dev, seed=a.seed, dtype=a.dtype, fp32_impl=a.fp32_impl)
     node = Node(cfg, name, TcpTransport(name, cfg.address, cfg.address(name)), ex)

@@ -81,7 +81,7 @@ def rank_main(rank: int, port: int, eport: int, marker: str) -> int:
     dist.destroy_process_group()
 
     # 2. ElasticGroup epoch over RCCL, gather pairs to coordinator + standby
-    grp = ElasticGroup(dev, backend="nccl", timeout_s=60, op_timeout_s=60, max_chunk=256)
+    grp = ElasticGroup(dev, backend="nccl", timeout_s=60, op_timeout_s=40, max_chunk=256)
     me = f"node{rank}"
     assert grp.form(me, ["node0", "node1"], 1, "127.0.0.1", eport, standby="node1")
     res["epoch_backend"] = grp.describe().get("backend")
@@ -118,9 +118,18 @@ def rank_main(rank: int, port: int, eport: int, marker: str) -> int:
         res["abandoned"] = False
     except RoundAbandoned:
         res["abandoned"] = True
+    if os.environ.get("RCCL2_STREAM_DEP") == "1":
+        work.wait()                                 # the compute stream now depends on the dead gather
     grp.abort_async()
     res["abort_returned"] = grp.join_aborters(60)
     res["abort_s"] = round(time.perf_counter() - t0, 3)
+    # GPU work queued on the compute stream after the abort must run: the aborted
+    # collective may not hold the stream (a stream dependency on it would stall
+    # every later forward until the backend's timeout)
+    t1 = time.perf_counter()
+    x = torch.ones(1 << 20, device=dev)
+    res["after_abort_sum"] = float((x * 2).sum().item())
+    res["after_abort_s"] = round(time.perf_counter() - t1, 3)
     assert grp.form(me, ["node0"], 2, "127.0.0.1", _port())      # survivors re-form (solo)
     res["reformed_world"] = grp.world
     print(json.dumps(res), flush=True)
