@@ -1493,8 +1493,8 @@ torch::Tensor synth_images(int64_t seed, int64_t start, int64_t n, int64_t hw, t
 int64_t pick_tile(int64_t M, int64_t Cout) { return conv_glds_pick((int)M, (int)Cout); }
 
 namespace idunno {
-void stage_file_native(const std::string& path, torch::Tensor out, std::vector<torch::Tensor> pinned, int64_t stream,
-                       int64_t nthreads);
+std::vector<double> stage_file_native(const std::string& path, torch::Tensor out, std::vector<torch::Tensor> pinned,
+                                      int64_t stream, int64_t nthreads);
 }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cerrno>
 #include <cstring>
 #include <string>
@@ -71,8 +72,10 @@ bool pread_parallel(int fd, char* dst, size_t n, size_t off, int nthreads, int* 
 // out: contiguous uint8 device tensor of the file's first out.numel() bytes;
 // pinned: >= 1 pinned host uint8 buffers (ping-pong); stream: the side stream
 // (hipStream_t as an integer, torch.cuda.Stream.cuda_stream)
-void stage_file_native(const std::string& path, torch::Tensor out, std::vector<torch::Tensor> pinned, int64_t stream,
-                       int64_t nthreads) {
+// Returns (seconds in pread, seconds waiting for a pinned buffer's previous copy,
+// seconds waiting for the last copies at the end).
+std::vector<double> stage_file_native(const std::string& path, torch::Tensor out, std::vector<torch::Tensor> pinned,
+                                      int64_t stream, int64_t nthreads) {
   TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.scalar_type() == torch::kUInt8, "out: contiguous uint8 GPU");
   TORCH_CHECK(!pinned.empty(), "no pinned buffers");
   size_t step = (size_t)-1;
@@ -95,12 +98,21 @@ void stage_file_native(const std::string& path, torch::Tensor out, std::vector<t
   TORCH_CHECK(fd >= 0, "open ", path, ": ", std::strerror(errno));
   std::vector<hipEvent_t> done(nb, nullptr);
   std::string fail;
+  using clk = std::chrono::steady_clock;
+  double t_read = 0, t_wait = 0, t_tail = 0;
+  auto secs = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); };
   for (size_t off = 0, i = 0; off < nbytes; off += step, ++i) {
     const int b = (int)(i % nb);
     const size_t n = std::min(step, nbytes - off);
+    auto t0 = clk::now();
     if (done[b] != nullptr) check_hip(hipEventSynchronize(done[b]), "hipEventSynchronize");
+    auto t1 = clk::now();
     int err = 0;
-    if (!pread_parallel(fd, pb[b], n, off, (int)nthreads, &err)) {
+    const bool ok = pread_parallel(fd, pb[b], n, off, (int)nthreads, &err);
+    auto t2 = clk::now();
+    t_wait += secs(t0, t1);
+    t_read += secs(t1, t2);
+    if (!ok) {
       fail = std::string("read ") + path + ": " + std::strerror(err);
       break;
     }
@@ -109,13 +121,16 @@ void stage_file_native(const std::string& path, torch::Tensor out, std::vector<t
     check_hip(hipEventRecord(done[b], st), "hipEventRecord");
   }
   ::close(fd);
+  auto t3 = clk::now();
   for (auto e : done) {
     if (e != nullptr) {
       (void)hipEventSynchronize(e);       // the pinned buffers are free for the next call
       (void)hipEventDestroy(e);
     }
   }
+  t_tail = secs(t3, clk::now());
   TORCH_CHECK(fail.empty(), fail);
+  return {t_read, t_wait, t_tail};
 }
 
 }  // namespace idunno

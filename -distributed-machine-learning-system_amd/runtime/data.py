@@ -87,6 +87,8 @@ class HbmStager:
         # on the side stream (bench.py lines it up against the forwards' events)
         self.timeline: list | None = None
         self._readers = None              # preadv thread pool of stage_file (lazy)
+        self.native_read_s = 0.0          # native stager: time in pread / waiting for the DMA engine
+        self.native_wait_s = 0.0
 
     READ_THREADS = 8
 
@@ -146,7 +148,9 @@ class HbmStager:
                         if self._done[b] is not None:
                             self._done[b].synchronize()
                             self._done[b] = None
-                    native(path, out, self.pinned, self.stream.cuda_stream, self.READ_THREADS)
+                    tr, tw, tt = native(path, out, self.pinned, self.stream.cuda_stream, self.READ_THREADS)
+                    self.native_read_s += tr
+                    self.native_wait_s += tw + tt
                     with torch.cuda.stream(self.stream):
                         ev = torch.cuda.Event()
                         ev.record(self.stream)

@@ -1419,6 +1419,8 @@ def _sdfs_pass(a, node, per_q: int) -> dict:
             sg.timeline = tl
         node.gpu_timeline = tl
         b0 = sum(sg.bytes_staged for sg in src.stagers)
+        r0 = sum(sg.native_read_s for sg in src.stagers)
+        w0 = sum(sg.native_wait_s for sg in src.stagers)
         src.tracer = node.tracer
         th0 = time.time()
         cold = run_pass("cold")
@@ -1428,6 +1430,8 @@ def _sdfs_pass(a, node, per_q: int) -> dict:
         for sg in src.stagers:
             sg.timeline = None
         staged = sum(sg.bytes_staged for sg in src.stagers) - b0
+        read_s = sum(sg.native_read_s for sg in src.stagers) - r0
+        dma_wait_s = sum(sg.native_wait_s for sg in src.stagers) - w0
         if gpu:
             torch.cuda.synchronize(src.device)
         ovl, iv = _timeline_overlap(tl) if gpu else (None, [])
@@ -1442,6 +1446,8 @@ def _sdfs_pass(a, node, per_q: int) -> dict:
                "sdfs_cold_to_warm": round(warm / cold, 4), "sdfs_images": n_img, "sdfs_shards": shards,
                "sdfs_put_gb_per_s": round(n_img * 150528 / put_s / 1e9, 3),
                "sdfs_bytes_staged": staged,
+               "sdfs_host_read_gb_per_s": round(staged / read_s / 1e9, 2) if read_s > 0 else None,
+               "sdfs_stager_dma_wait_ms": round(dma_wait_s * 1e3, 2),
                "hbm_stage_gb_per_s": round(staged / (h2d_ms * 1e-3) / 1e9, 2) if h2d_ms > 0 else None,
                "sdfs_h2d_overlap_frac": round(ovl, 4) if ovl is not None else None,
                "sdfs_local_file_reads": src.local_reads, "sdfs_readahead_hits": src.readahead_hits,

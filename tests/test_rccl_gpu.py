@@ -96,3 +96,27 @@ def test_two_rccl_ranks_on_one_gpu():
     assert res["backend"] == "nccl" and res["epoch_backend"] == "nccl", res
     assert res["gather_ok"] and res["scatter_ok"] and res["rounds_ok"], res
     assert res["abandoned"] and res["abort_returned"] and res["reformed_world"] == 1, res
+
+
+def test_bench_worker_failover_rehearsal_over_rccl(tmp_path):
+    """bench.py --gpus 2 --rehearse-rccl, worker-failover phase only: a member
+    paused with its chunk in flight is SIGKILLed and the coordinator recovers on
+    the failure detector's clock (~2 s), not on RCCL's 120 s backend timeout
+    (regressions of the epoch warm-up gather and the sync-free graph capture)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "line.json"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--rehearse-rccl",
+                        "--steps", "3", "--warmup", "1", "--no-extras", "--node-phases", "worker",
+                        "--worker-kill-chunks", "1", "--json-out", str(out)],
+                       capture_output=True, text=True, timeout=240, cwd=root)
+    assert r.returncode == 0 and out.exists(), (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+    d = json.loads(out.read_text().strip().splitlines()[-1])
+    assert d["rccl"] and d["comm_world"] == 2, d
+    assert d.get("extras_error") is None, d.get("extras_error")
+    assert d["worker_failover_rounds"] and d["worker_failover_survivor_world"]["1"] == 1, d
+    assert d["worker_failover_recovery_s"]["1"] < 10.0, d["worker_failover_recovery_s"]
