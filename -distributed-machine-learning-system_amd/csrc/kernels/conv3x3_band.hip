@@ -62,8 +62,8 @@ struct BandArgs {
   uint32_t wrow, wtap;  // weight row / one tap's bytes (split: 36C / 4C, fp16: 18C / 2C)
   float acc_scale;
   int* ovf;             // split range guard flag or nullptr
-  int flags;            // bit 0: waves 4-7 at s_setprio 1 (MI355X_MICROARCH.md, two waves per SIMD item 4)
-                        // profiling ablations (outputs wrong): bit 1 no epilogue stores, bit 2 no residual loads
+  int flags;            // profiling ablations (outputs wrong; tools/band_ab.py, tools/gpu/pmc_band.sh):
+                        // bit 1 no epilogue stores, bit 2 no residual loads
 };
 
 namespace bnd {
@@ -294,7 +294,6 @@ __global__ void __launch_bounds__(256 * WM, WM) conv3x3_band_kernel(const BandAr
   const int frow = lane & 15, q = lane >> 4;
   int T = blockIdx.x;
   if (T >= a.ntiles) return;                  // uniform
-  if ((a.flags & 1) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   const int GS = gridDim.x;
   const int ncb = a.ncb;
   const uint32_t lds0 = lds_addr(smem);
@@ -502,170 +501,6 @@ __global__ void __launch_bounds__(256 * WM, WM) conv3x3_band_kernel(const BandAr
 }
 
 
-// 16-wave variant (4 waves per SIMD, same 128 x 256 tile: wave (wn, wm) owns 32
-// couts x 64 pixels): the other waves of a SIMD hide the LDS and barrier latency
-// that the 8-wave loop above exposes, so the pipeline is plain -- the barrier of
-// stage s at its start, its A fragments read there, B reads R groups ahead
-// inside the stage only (nothing in flight crosses a stage).
-template <int W, int FM, bool HAS_RES, bool OUT_F32>
-__global__ void __launch_bounds__(1024, 4) conv3x3_band16_kernel(const BandArgs a) {
-  constexpr int WM = 4;
-  using G = BandGeom<W, FM, WM>;
-  using namespace bnd;
-  constexpr int NW = G::NW, GW = G::GW, NPI = G::NPI;
-  constexpr int NEPI = OUT_F32 ? FN * FM : 2 * FN * FM;
-  constexpr int RR = FM >= 3 ? 2 : FM - 1;            // B read groups ahead of the MFMAs
-  static_assert(NEPI < 64 && NPI <= 8 && GW == 1, "counted waits");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave / WM, wm = wave % WM;
-  const int frow = lane & 15, q = lane >> 4;
-  int T = blockIdx.x;
-  if (T >= a.ntiles) return;                  // uniform
-  if ((a.flags & 1) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-  const int GS = gridDim.x;
-  const int ncb = a.ncb;
-  const uint32_t lds0 = lds_addr(smem);
-
-  const auto w_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
-  const auto x_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, 0x7fffffff, 0x00020000);
-  const uint32_t ybytes = (uint32_t)a.M * (uint32_t)a.ldy * (OUT_F32 ? 4u : 2u);
-  const auto y_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)ybytes, 0x00020000);
-  const uint32_t wrow = a.wrow;
-  const uint32_t wtap = a.wtap;
-  const int wrow_i = wave * 8 + (lane >> 3);
-  const uint32_t wv = (uint32_t)wrow_i * wrow + (uint32_t)((((lane & 7) ^ swz_r(wrow_i, 8))) << 4);
-  const int arow = wn * 32 + frow;
-  const uint32_t fa = lds0 + WB + (uint32_t)(arow * 128 + ((q ^ swz_r(arow, 8)) << 4));
-
-  BandTile cur = band_tile<W, FM, WM>(a, T);
-  bool have_nxt = T + GS < a.ntiles;
-  BandTile nxt = band_tile<W, FM, WM>(a, have_nxt ? T + GS : T);
-  uint32_t pv[NPI];
-  uint32_t bq[FM], kb[FM];
-  band_patch_offsets<W, FM, WM>(a, cur, true, wave, lane, pv);
-  band_read_bases<W, FM, WM>(a, cur, wm, frow, q, lds0, bq, kb);
-
-  auto issue_w = [&](uint32_t slot, uint32_t soff) {
-    dma_buf16(w_rsrc, smem + WB + slot + wave * 1024, wv, (int)soff);
-  };
-  float4v acc[FN][FM];
-#pragma unroll
-  for (int i = 0; i < FN; ++i)
-#pragma unroll
-    for (int j = 0; j < FM; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
-  bool bad = false;
-
-  // prologue: the whole first patch and stage 0's weights
-#pragma unroll
-  for (int i = 0; i < NPI; ++i) dma_buf16(x_rsrc, smem + (wave + NW * i) * 1024, pv[i], 0);
-  issue_w(0u, (uint32_t)cur.n0 * wrow);
-  bool first_tile = true;
-  bool after_epi = false;
-
-  for (;;) {
-    for (int cb = 0; cb < ncb; ++cb) {
-#pragma unroll
-      for (int j = 0; j < FM; ++j) asm volatile("" : "+v"(bq[j]), "+v"(kb[j]));
-      const bool last_cb = cb == ncb - 1;
-      const uint32_t pbit = (uint32_t)(cb & 1) << 16;
-      const uint32_t slot0 = (uint32_t)(cb & 1) * WS1;
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const uint32_t slot = (tap & 1) ? (slot0 ^ WS1) : slot0;
-        // ---- barrier of stage s: w(s) landed (younger: the patch chunk issued
-        // at the previous barrier, or the previous tile's epilogue stores) ----
-        if (first_tile && cb == 0 && tap == 0) band_vmcnt<0>();
-        else if (tap == 0 && cb == 0) band_vmcnt<NEPI>();
-        else if (tap >= 1 && tap <= NPI) band_vmcnt<1>();
-        else band_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();
-        {
-          // w(s+1) into the other slot (stage s-1's A reads are done everywhere)
-          int t1 = tap + 1, cbn = cb;
-          bool nt1 = false;
-          if (t1 == 9) {
-            t1 = 0;
-            if (++cbn == ncb) {
-              cbn = 0;
-              nt1 = true;
-            }
-          }
-          if (!nt1 || have_nxt) {
-            const int n0 = nt1 ? nxt.n0 : cur.n0;
-            issue_w(slot ^ WS1, (uint32_t)n0 * wrow + (uint32_t)t1 * wtap + (uint32_t)cbn * 128u);
-          }
-        }
-        if (tap < NPI) {
-          // chunk `tap` of the next channel block's patch (or the next tile's first)
-          if (last_cb && tap == 0) band_patch_offsets<W, FM, WM>(a, nxt, have_nxt, wave, lane, pv);
-          dma_buf16(x_rsrc, smem + (pbit ^ PB1) + (wave + NW * tap) * 1024, pv[tap], last_cb ? 0 : (cb + 1) * 128);
-        }
-        // opaque per stage: the 9 taps' B addresses are computed next to their reads
-#pragma unroll
-        for (int j = 0; j < FM; ++j) asm volatile("" : "+v"(bq[j]), "+v"(kb[j]));
-        // A of this stage, then the B groups R ahead
-        half8v aC[FN][2];
-        {
-          const uint32_t base = fa ^ slot;
-          aC[0][0] = lds_read_b128_imm<0>(base);
-          aC[1][0] = lds_read_b128_imm<2048>(base);
-          aC[0][1] = lds_read_b128_imm<0>(base ^ 64u);
-          aC[1][1] = lds_read_b128_imm<2048>(base ^ 64u);
-        }
-        const int kh = tap / 3, kw = tap - 3 * kh;
-        const uint32_t dk16 = (uint32_t)(((kh * G::KS + kw) & 7) << 4);
-        half8v bR[RR + 1][2];
-        auto read_b = [&](int j) {
-          const uint32_t ah = bq[j] ^ (((kb[j] + dk16) & 0x70u) | pbit);
-          bR[j % (RR + 1)][0] = band_read<W>(ah, tap);
-          bR[j % (RR + 1)][1] = band_read<W>(ah ^ 64u, tap);
-        };
-#pragma unroll
-        for (int j = 0; j < RR; ++j) read_b(j);
-#pragma unroll
-        for (int j = 0; j < FM; ++j) {
-          if (j + RR < FM) read_b(j + RR);
-          const int ahead = (FM - 1 - j) < RR ? (FM - 1 - j) : RR;   // groups issued after group j
-          if (ahead == 2) lds_waitcnt<4>();
-          else if (ahead == 1) lds_waitcnt<2>();
-          else lds_waitcnt<0>();
-          const int rg = j % (RR + 1);
-          lds_tie(bR[rg][0]);
-          lds_tie(bR[rg][1]);
-          if (j == 0) {
-#pragma unroll
-            for (int i = 0; i < FN; ++i) {
-              lds_tie(aC[i][0]);
-              lds_tie(aC[i][1]);
-            }
-          }
-#pragma unroll
-          for (int i = 0; i < FN; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aC[i][0], bR[rg][0], acc[i][j], 0, 0, 0);
-#pragma unroll
-          for (int i = 0; i < FN; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aC[i][0], bR[rg][1], acc[i][j], 0, 0, 0);
-#pragma unroll
-          for (int i = 0; i < FN; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aC[i][1], bR[rg][0], acc[i][j], 0, 0, 0);
-        }
-      }
-    }
-    band_epilogue<FM, HAS_RES, OUT_F32, false>(a, cur, acc, wn, wm, frow, q, y_rsrc, bad);
-    if (!have_nxt) break;
-    first_tile = false;
-    T += GS;
-    cur = nxt;
-    have_nxt = T + GS < a.ntiles;
-    nxt = band_tile<W, FM, WM>(a, have_nxt ? T + GS : T);
-    band_read_bases<W, FM, WM>(a, cur, wm, frow, q, lds0, bq, kb);
-  }
-  band_vmcnt<0>();
-  if (bad && a.ovf != nullptr) *a.ovf = 1;
-}
-
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -735,30 +570,11 @@ static bool band_dispatch(const BandArgs& a, bool res, bool out_f32, bool f16, i
   return true;
 }
 
-template <int W, int FM, bool R, bool F>
-static void band16_cfg(const BandArgs& a, int grid, hipStream_t st) {
-  auto kern = conv3x3_band16_kernel<W, FM, R, F>;
-  ensure_lds_attr(reinterpret_cast<const void*>(kern), bnd::LDS);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), bnd::LDS, st, a);
-}
-
-template <int W, int FM>
-static bool band16_dispatch(const BandArgs& a, bool res, bool out_f32, int grid, hipStream_t st) {
-  if (res) {
-    if (out_f32) band16_cfg<W, FM, true, true>(a, grid, st);
-    else band16_cfg<W, FM, true, false>(a, grid, st);
-  } else {
-    if (out_f32) band16_cfg<W, FM, false, true>(a, grid, st);
-    else band16_cfg<W, FM, false, false>(a, grid, st);
-  }
-  return true;
-}
-
 bool conv3x3_band_launch(const half_t* x, int ldx, const half_t* w, const float* bias, const half_t* res, int ldr,
                          void* y, int ldy, bool out_f32, int B, int H, int W, int C, int Cout, int relu,
                          float acc_scale, int* ovf, int max_grid, int flags, hipStream_t st, bool f16) {
   if (!conv3x3_band_supported(H, W, C, Cout)) return false;
-  if (f16 && (out_f32 || (flags & 8))) return false;
+  if (f16 && out_f32) return false;
   BandArgs a;
   a.x = x;
   a.w = w;
@@ -792,7 +608,6 @@ bool conv3x3_band_launch(const half_t* x, int ldx, const half_t* w, const float*
   if (max_grid > 0 && grid > max_grid) grid = max_grid;
   switch (W) {
     case 28:
-      if (flags & 8) return band16_dispatch<28, 4>(a, res != nullptr, out_f32, grid, st);   // 16 waves
       return band_dispatch<28, 8, 2>(a, res != nullptr, out_f32, f16, grid, st);
     case 14: return band_dispatch<14, 5, 2>(a, res != nullptr, out_f32, f16, grid, st);
     case 7: return band_dispatch<7, 5, 2>(a, res != nullptr, out_f32, f16, grid, st);

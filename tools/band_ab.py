@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--batch", type=int, default=400)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--flags", default="0,1,3,5,7")
+    ap.add_argument("--flags", default="0,2,4,6", help="conv3x3_band.hip profiling ablations: 2 no stores, 4 no residual loads")
     ap.add_argument("--tiles", default="36,42")
     a = ap.parse_args()
     from idunno import ops
