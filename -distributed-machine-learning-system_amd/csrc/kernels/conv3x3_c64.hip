@@ -21,7 +21,12 @@
 // chunks XOR-swizzled by (row & 6) make every such read, at any row offset,
 // conflict-free for ds_read_b128's lane groups (searched exhaustively; the
 // (row >> 1) & 7 swizzle of the im2col kernels is 2-way conflicted here).
-// W = 56 wastes 8 of every 64 columns; that buys the conflict-free layout.
+// W = 56 leaves 8 of the second x-tile's 32 columns empty.  That tile (valid
+// width 17..24) runs in PAIRED mode: 8 full fragments (row r, columns 0..15)
+// plus 4 fragments that each take columns 16..23 of a row PAIR (lanes 0..7 row
+// 2j, lanes 8..15 row 2j+1 at columns rotated by 6, which keeps every
+// ds_read_b128 lane group on 8 distinct row residues, i.e. conflict-free):
+// 12 fragments, 3 per wave, instead of 16 (-25 % MFMAs on half the tiles).
 //
 // Workgroup = 8 waves (2 x 4, two per SIMD): wave = 32 output channels (2 A
 // frags) x 64 pixels (4 B frags) -> 8 MFMAs per K-chunk of 32, 144 per tile;
@@ -64,7 +69,29 @@ struct C64Args {
   int B, H, W;
   int tiles_x, tiles_y, ntiles;
   int relu;
+  int pair_tx;         // x-tile run in paired mode (valid width 17..24), -1: none
 };
+
+// Tile-local pixel of lane `frow` of fragment f of wave wm: 4 fragments per
+// wave (one row of 16 columns each), or (FMX 3) the paired map of the header.
+template <int FMX>
+__device__ __forceinline__ void c64_pix(int wm, int f, int frow, int& py, int& px) {
+  using namespace c64;
+  if constexpr (FMX == FM) {
+    const int p = (wm * FM + f) * 16 + frow;
+    py = p / TW;
+    px = p % TW;
+  } else {
+    const int k = wm * FMX + f;
+    if (k < TH) {
+      py = k;
+      px = frow;
+    } else {
+      py = 2 * (k - TH) + (frow >> 3);
+      px = 16 + (frow < 8 ? frow : ((frow + 6) & 7));
+    }
+  }
+}
 
 
 // Patch DMA of tile t into dst: 8 patch rows per instruction, rows past the
@@ -95,6 +122,12 @@ __device__ __forceinline__ void c64_issue_patch(const C64Args& a, int t, char* _
 // (or of its first use) while the patch DMA of tile t+1 is in flight, and that
 // prefetch would never overlap tile t's MFMAs.
 // Residual of tile t -> registers (untracked asm loads; masked pixels read row 0).
+// Branch-free over the tile's mode: an untracked load issued inside a branch
+// has its result copied into the merged register at the join, before it lands.
+__device__ __forceinline__ bool c64_paired(const C64Args& a, int t) {
+  return (t % (a.tiles_x * a.tiles_y)) % a.tiles_x == a.pair_tx;
+}
+
 __device__ __forceinline__ void c64_load_res(const C64Args& a, int t, half4v (&rv)[c64::FN][c64::FM], int wn,
                                              int wm, int lane) {
   using namespace c64;
@@ -102,26 +135,29 @@ __device__ __forceinline__ void c64_load_res(const C64Args& a, int t, half4v (&r
   const int per = a.tiles_x * a.tiles_y;
   const int b = t / per, r = t - b * per;
   const int oh0 = (r / a.tiles_x) * TH, ow0 = (r % a.tiles_x) * TW;
+  const bool paired = (r % a.tiles_x) == a.pair_tx;
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
     for (int f = 0; f < FM; ++f) {
       const int n = wn * (FN * 16) + i * 16 + fch * 4;
-      const int p = (wm * FM + f) * 16 + frow;
-      const int oh = oh0 + p / TW, ow = ow0 + p % TW;
+      int py, px, qy = TH, qx = 0;                 // paired mode has FM - 1 fragments
+      c64_pix<FM>(wm, f, frow, py, px);
+      if (f < FM - 1) c64_pix<FM - 1>(wm, f, frow, qy, qx);
+      const int oh = oh0 + (paired ? qy : py), ow = ow0 + (paired ? qx : px);
       const size_t m = (oh < a.H && ow < a.W) ? (((size_t)b * a.H + oh) * a.W + ow) : 0;
       rv[i][f] = gload_b64_untracked(a.res + m * CO + n);
     }
 }
 
+// Head of one tile: the barrier, then the patch DMA and residual of tile t+1.
+// Kept out of the mode branch below (the untracked residual loads must not be
+// merged at a join).
 template <bool HAS_RES>
-__device__ __forceinline__ void c64_tile(const C64Args& a, int t, bool prefetch, const char* __restrict__ wl,
-                                         const char* __restrict__ cur, char* __restrict__ nxt, const float4v* bvr,
-                                         const int* pbase, half4v (&rv)[c64::FN][c64::FM],
-                                         half4v (&rv_next)[c64::FN][c64::FM], int wave, int wn, int wm, int lane) {
-  using namespace c64;
+__device__ __forceinline__ void c64_tile_head(const C64Args& a, int t, bool prefetch, char* __restrict__ nxt,
+                                              half4v (&rv_next)[c64::FN][c64::FM], int wave, int wn, int wm,
+                                              int lane) {
   const int lrow = lane >> 3, lslot = lane & 7;
-  const int frow = lane & 15, fch = lane >> 4;
   // One barrier per tile.  Every wave reaches it after (a) its MFMAs of tile
   // t-1 (so `nxt`, tile t-1's patch, is free) and (b) its `vmcnt(0)` behind
   // those MFMAs (so its DMAs of tile t's patch, issued a whole tile earlier,
@@ -133,27 +169,36 @@ __device__ __forceinline__ void c64_tile(const C64Args& a, int t, bool prefetch,
     c64_issue_patch(a, t + 1, nxt, wave, lrow, lslot);
     if constexpr (HAS_RES) c64_load_res(a, t + 1, rv_next, wn, wm, lane);
   }
+}
 
-  float4v acc[FN][FM];
+// MFMAs and epilogue of one tile, FMX pixel fragments per wave (4, or 3 in the
+// paired mode).
+template <bool HAS_RES, int FMX>
+__device__ __forceinline__ void c64_tile(const C64Args& a, int t, const char* __restrict__ wl,
+                                         const char* __restrict__ cur, const float4v* bvr, const int* pbase,
+                                         const half4v (&rv)[c64::FN][c64::FM], int wn, int wm, int lane) {
+  using namespace c64;
+  const int frow = lane & 15, fch = lane >> 4;
+  float4v acc[FN][FMX];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int f = 0; f < FM; ++f) acc[i][f] = float4v{0.f, 0.f, 0.f, 0.f};
+    for (int f = 0; f < FMX; ++f) acc[i][f] = float4v{0.f, 0.f, 0.f, 0.f};
 
   // 18 K-chunks (9 taps x 2 halves of 64 channels); fragments of chunk q+1 are
   // read (inline-asm ds_read_b128, common.h) into the other register set before
   // chunk q's MFMAs are issued; a counted lgkmcnt wait retires exactly chunk q
-  constexpr int NR = FN + FM;                    // ds_reads per chunk
+  constexpr int NR = FN + FMX;                   // ds_reads per chunk
   const uint32_t wl_a = lds_addr(wl), cur_a = lds_addr(cur);
   // keep the 72 per-(fragment, tap) B addresses from being hoisted out of the tile
   // loop into registers (they spill at 2 waves/SIMD); recomputing them is 3 VALU
-  int pb[FM];
+  int pb[FMX];
 #pragma unroll
-  for (int f = 0; f < FM; ++f) {
+  for (int f = 0; f < FMX; ++f) {
     pb[f] = pbase[f];
     asm volatile("" : "+v"(pb[f]));
   }
-  half8v fa[2][FN], fb[2][FM];
+  half8v fa[2][FN], fb[2][FMX];
   auto load_frags = [&](int q, half8v* a_, half8v* b_) {
     const int tap = q >> 1, kk = q & 1;
     const int toff = (tap / 3) * PW + (tap % 3);
@@ -165,7 +210,7 @@ __device__ __forceinline__ void c64_tile(const C64Args& a, int t, bool prefetch,
       a_[i] = lds_read_b128(wt + row * 128 + ((ch ^ c64_swz(row)) << 4));
     }
 #pragma unroll
-    for (int f = 0; f < FM; ++f) {
+    for (int f = 0; f < FMX; ++f) {
       const int row = pb[f] + toff;
       b_[f] = lds_read_b128(cur_a + row * 128 + ((ch ^ c64_swz(row)) << 4));
     }
@@ -184,11 +229,11 @@ __device__ __forceinline__ void c64_tile(const C64Args& a, int t, bool prefetch,
 #pragma unroll
     for (int i = 0; i < FN; ++i) lds_tie(ca[i]);
 #pragma unroll
-    for (int f = 0; f < FM; ++f) lds_tie(cb[f]);
+    for (int f = 0; f < FMX; ++f) lds_tie(cb[f]);
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
-      for (int f = 0; f < FM; ++f)
+      for (int f = 0; f < FMX; ++f)
         acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ca[i], cb[f], acc[i][f], 0, 0, 0);
   }
   __builtin_amdgcn_sched_barrier(0);
@@ -204,9 +249,10 @@ __device__ __forceinline__ void c64_tile(const C64Args& a, int t, bool prefetch,
   for (int i = 0; i < FN; ++i) {
     const int n = wn * (FN * 16) + i * 16 + fch * 4;
 #pragma unroll
-    for (int f = 0; f < FM; ++f) {
-      const int p = (wm * FM + f) * 16 + frow;
-      const int oh = oh0 + p / TW, ow = ow0 + p % TW;
+    for (int f = 0; f < FMX; ++f) {
+      int py, px;
+      c64_pix<FMX>(wm, f, frow, py, px);
+      const int oh = oh0 + py, ow = ow0 + px;
       if (oh >= a.H || ow >= a.W) continue;
       const size_t m = ((size_t)b * a.H + oh) * a.W + ow;
       float4v v = acc[i][f] + bvr[i];
@@ -264,13 +310,21 @@ __global__ void __launch_bounds__(512, 1) conv3x3_c64_kernel(const C64Args a) {
     __builtin_amdgcn_global_load_lds((glb_void_q*)src, (lds_void_q*)(smem + i * 1024), 16, 0, 0);
   }
 
-  // per-lane B fragment bases: output pixel -> patch row of tap (0, 0)
+  // per-lane B fragment bases: output pixel -> patch row of tap (0, 0), for the
+  // plain and the paired fragment map
   const int frow = lane & 15;
-  int pbase[FM];
+  int pbase[FM], pbase3[FM - 1];
 #pragma unroll
   for (int f = 0; f < FM; ++f) {
-    const int p = (wm * FM + f) * 16 + frow;
-    pbase[f] = (p / TW) * PW + (p % TW);
+    int py, px;
+    c64_pix<FM>(wm, f, frow, py, px);
+    pbase[f] = py * PW + px;
+  }
+#pragma unroll
+  for (int f = 0; f < FM - 1; ++f) {
+    int py, px;
+    c64_pix<FM - 1>(wm, f, frow, py, px);
+    pbase3[f] = py * PW + px;
   }
 
   char* p0 = smem + W_BYTES;
@@ -279,11 +333,18 @@ __global__ void __launch_bounds__(512, 1) conv3x3_c64_kernel(const C64Args a) {
   c64_issue_patch(a, t_begin, p0, wave, lrow, lslot);
   if constexpr (HAS_RES) c64_load_res(a, t_begin, rA, wn, wm, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // weights + first patch (+ residual) landed
-  // two tiles per trip so the buffers and residual registers swap statically
+  // one tile in its mode (wave-uniform branch); two tiles per trip so the
+  // buffers and residual registers swap statically
+  auto tile = [&](int t, bool more, const char* cur, char* nxt, half4v(&rv)[FN][FM], half4v(&rvn)[FN][FM]) {
+    c64_tile_head<HAS_RES>(a, t, more, nxt, rvn, wave, wn, wm, lane);
+    if (c64_paired(a, t))
+      c64_tile<HAS_RES, FM - 1>(a, t, smem, cur, bvr, pbase3, rv, wn, wm, lane);
+    else
+      c64_tile<HAS_RES, FM>(a, t, smem, cur, bvr, pbase, rv, wn, wm, lane);
+  };
   for (int t = t_begin; t < t_end; t += 2) {
-    c64_tile<HAS_RES>(a, t, t + 1 < t_end, smem, p0, p1, bvr, pbase, rA, rB, wave, wn, wm, lane);
-    if (t + 1 < t_end)
-      c64_tile<HAS_RES>(a, t + 1, t + 2 < t_end, smem, p1, p0, bvr, pbase, rB, rA, wave, wn, wm, lane);
+    tile(t, t + 1 < t_end, p0, p1, rA, rB);
+    if (t + 1 < t_end) tile(t + 1, t + 2 < t_end, p1, p0, rB, rA);
   }
 }
 
@@ -306,6 +367,8 @@ void conv3x3_c64_launch(const half_t* x, const half_t* w, const float* bias, con
   a.tiles_x = (W + TW - 1) / TW;
   a.tiles_y = (H + TH - 1) / TH;
   a.ntiles = B * a.tiles_x * a.tiles_y;
+  const int last_w = W - (a.tiles_x - 1) * TW;   // valid width of the last x-tile
+  a.pair_tx = (last_w > 16 && last_w <= 24) ? a.tiles_x - 1 : -1;
   // LDS opt-in and CU count per (kernel, device), thread-safe (launch_util.h)
   ensure_lds_attr(reinterpret_cast<const void*>(&conv3x3_c64_kernel<true>), LDS);
   ensure_lds_attr(reinterpret_cast<const void*>(&conv3x3_c64_kernel<false>), LDS);
