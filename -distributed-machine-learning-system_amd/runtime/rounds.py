@@ -675,13 +675,17 @@ class RoundPlane:
         # the whole round at once: one copy of the class and probability planes
         # (every chunk's arrays are row views of them, so the host ring slot can be
         # reused), one header read and one out-of-range test for all members
-        cls_all = np.ascontiguousarray(arr[:, :mc, 0])
-        prob_all = np.ascontiguousarray(arr[:, :mc, 1]).view(np.float32)
+        # only the rows the round's longest chunk filled (a 400-image query over 8
+        # members fills 50 of max_chunk's rows): one block copy, planes as views
+        lens = [0 if row is None else row[3] - row[2] + 1 for row in r.table]
+        used = max(max(lens), 1)
+        blk = arr[:, :used].copy()
+        cls_all = blk[:, :, 0]
+        prob_all = blk[:, :, 1].view(np.float32)
         hdr = arr[:, mc:mc + HDR_ROWS, :].reshape(len(arr), 2 * HDR_ROWS).tolist()  # (us, model id, n, tag)
         bad = None
         if cls_all.min() < 0:             # rare: some row holds a range-guard mark (or stale tail)
-            lens = np.array([0 if row is None else row[3] - row[2] + 1 for row in r.table])
-            bad = ((cls_all < 0) & (np.arange(mc) < lens[:, None])).any(axis=1).tolist()
+            bad = ((cls_all < 0) & (np.arange(used) < np.array(lens)[:, None])).any(axis=1).tolist()
         # one scheduler observation per model per round: the members' summed compute
         # time over their summed images (a per-image time), scaled to the model's batch
         obs = {}
