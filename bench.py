@@ -1239,6 +1239,9 @@ def _drive_system(a, node, W: int, B: int) -> dict:
     out = {"value_system": round(ips, 2), "ms_per_step_system": round(1000 * elapsed / a.steps, 4),
            "p50_system_s": round(p50, 6),
            "p50_system_loaded_s": round(loaded[len(loaded) // 2], 6) if loaded else None,
+           # the loaded p50 is over `steps` queries submitted at once: a query's
+           # latency includes the queue ahead of it
+           "system_loaded_queue_depth": a.steps,
            "system_path": ("client -> coordinator Node (membership, hot standby) -> fair-time split -> "
                            + (("RCCL rounds" if W > 1 else "pipelined rounds (one-member group)")
                               if node.rounds is not None else "local JOB queue")
