@@ -22,16 +22,19 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--splits", default="1,2,4")
+    ap.add_argument("--dtype", default="fp16", help="fp16, or fp32 (split fp16, the headline)")
+    ap.add_argument("--queries", action="store_true",
+                    help="S whole queries (S graphs of --batch images) on S streams per step, not S sub-batches")
     a = ap.parse_args()
     from idunno import ops
     from idunno.models import HipRunner, build_program
 
     dev = torch.device("cuda")
-    runner = HipRunner(build_program(a.model), dev)
-    shard = ops.synth_images(1234, 0, 2 * a.batch, dev)
+    runner = HipRunner(build_program(a.model, dtype=a.dtype), dev)
+    shard = ops.synth_images(1234, 0, 5 * a.batch, dev)
     cfgs = {}
     for S in [int(s) for s in a.splits.split(",")]:
-        n = a.batch // S
+        n = a.batch if a.queries else a.batch // S
         streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
         # graph k reads images [k*n, (k+1)*n) of the shard (distinct views -> distinct graphs)
         graphs = []
@@ -64,8 +67,10 @@ def main():
             res[S].append(t0.elapsed_time(t1) / a.iters)
     for S, v in res.items():
         ms = min(v)
-        print(f"{a.model} batch {a.batch} as {S} x {a.batch // S} on {S} streams: {ms:.3f} ms/step "
-              f"({a.batch / ms * 1e3:,.0f} img/s)  all rounds {[round(x, 3) for x in v]}", flush=True)
+        imgs = a.batch * S if a.queries else a.batch
+        what = f"{S} queries of {a.batch}" if a.queries else f"{S} x {a.batch // S}"
+        print(f"{a.model} batch {a.batch} as {what} on {S} streams: {ms:.3f} ms/step "
+              f"({imgs / ms * 1e3:,.0f} img/s)  all rounds {[round(x, 3) for x in v]}", flush=True)
 
 
 if __name__ == "__main__":
