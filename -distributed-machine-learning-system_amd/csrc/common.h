@@ -160,4 +160,31 @@ __device__ __forceinline__ void split_guard(int* ovf, const float4v v) {
 __device__ __forceinline__ void reg_tie(half4v& r) { asm volatile("" : "+v"(r)); }
 __device__ __forceinline__ void reg_tie(float4v& r) { asm volatile("" : "+v"(r)); }
 
+// ---- 16-byte split epilogue accesses (cdna_hip_programming T21) ------------------
+// In the 16x16 C/D layout lane group q = lane >> 4 holds output channels
+// nb + 4q .. nb + 4q + 3 of one pixel, as hi and lo half4s: two 8-byte accesses
+// per lane.  One v_permlane16_swap per dword (rows 1/3 of the hi register trade
+// with rows 0/2 of the lo register) leaves q even with the hi halfs of channels
+// nb + 8(q/2) .. +7 and q odd with their lo halfs: ONE 16-byte access per lane at
+// split_off_q(nb, q).  The inverse (split_swap_in) is the same swap.
+typedef unsigned int u32x2_sw __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_sw __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int split_off_q(int nb, int q) { return split_off(nb + 8 * (q >> 1)) + 32 * (q & 1); }
+
+__device__ __forceinline__ u32x4_sw split_swap_out(half4v h, half4v l) {
+  const u32x2_sw hv = __builtin_bit_cast(u32x2_sw, h), lv = __builtin_bit_cast(u32x2_sw, l);
+  const auto s0 = __builtin_amdgcn_permlane16_swap(hv[0], lv[0], false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(hv[1], lv[1], false, false);
+  return u32x4_sw{s0[0], s1[0], s0[1], s1[1]};
+}
+
+__device__ __forceinline__ void split_swap_in(float4v r, half4v& h, half4v& l) {
+  const u32x4_sw v = __builtin_bit_cast(u32x4_sw, r);
+  const auto s0 = __builtin_amdgcn_permlane16_swap(v[0], v[2], false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(v[1], v[3], false, false);
+  h = __builtin_bit_cast(half4v, u32x2_sw{s0[0], s1[0]});
+  l = __builtin_bit_cast(half4v, u32x2_sw{s0[1], s1[1]});
+}
+
 }  // namespace idunno

@@ -196,28 +196,29 @@ __device__ __forceinline__ void band_vmcnt() {
 }
 
 // Epilogue of one tile: x 2^-e, + bias (+ split residual), ReLU, split (or fp32)
-// buffer stores -- exactly FN*FM*(OUT_F32 ? 1 : 2) store instructions per wave
+// buffer stores -- exactly FN*FM store instructions per wave (16 B per lane when split)
 // (rows past M get an offset past the descriptor and are dropped); clears acc.
 template <int FM, bool HAS_RES, bool OUT_F32, bool F16, typename Rsrc>
 __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile& cur, float4v (&acc)[bnd::FN][FM],
                                               int wn, int wm, int frow, int q, Rsrc y_rsrc, bool& bad) {
   using namespace bnd;
     const int mw = cur.m0 + wm * 16 * FM + frow;
-    half4v rh[HAS_RES ? FN : 1][HAS_RES ? FM : 1], rl[HAS_RES ? FN : 1][HAS_RES ? FM : 1];
+    // split residual: one 16-byte load per lane and fragment (split_swap_in)
+    half4v rh[HAS_RES ? FN : 1][HAS_RES ? FM : 1];
+    float4v rw[HAS_RES && !F16 ? FN : 1][HAS_RES && !F16 ? FM : 1];
     if constexpr (HAS_RES) {
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
         const int m = min(mw + 16 * j, a.M - 1);
 #pragma unroll
         for (int i = 0; i < FN; ++i) {
-          const int n = cur.n0 + wn * 32 + 16 * i + 4 * q;
-          const half_t* p = a.res + (size_t)m * a.ldr + (F16 ? n : split_off(n));
-          if (a.flags & 4) {
-            rh[i][j] = half4v{0, 0, 0, 0};
-            rl[i][j] = half4v{0, 0, 0, 0};
+          const int nb = cur.n0 + wn * 32 + 16 * i;
+          if constexpr (F16) {
+            const half_t* p = a.res + (size_t)m * a.ldr + nb + 4 * q;
+            rh[i][j] = (a.flags & 4) ? half4v{0, 0, 0, 0} : gload_b64_untracked(p);
           } else {
-            rh[i][j] = gload_b64_untracked(p);
-            if constexpr (!F16) rl[i][j] = gload_b64_untracked(p + 32);
+            const half_t* p = a.res + (size_t)m * a.ldr + split_off_q(nb, q);
+            rw[i][j] = (a.flags & 4) ? float4v{0.f, 0.f, 0.f, 0.f} : gload_f4_untracked(p);
           }
         }
       }
@@ -231,8 +232,8 @@ __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile&
       for (int i = 0; i < FN; ++i)
 #pragma unroll
         for (int j = 0; j < FM; ++j) {
-          reg_tie(rh[i][j]);
-          if constexpr (!F16) reg_tie(rl[i][j]);
+          if constexpr (F16) reg_tie(rh[i][j]);
+          else reg_tie(rw[i][j]);
         }
     }
 #pragma unroll
@@ -243,9 +244,14 @@ __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile&
       for (int i = 0; i < FN; ++i) {
         const int n = cur.n0 + wn * 32 + 16 * i + 4 * q;
         float4v v = acc[i][j] * a.acc_scale + bv[i];
-        if constexpr (HAS_RES) {
+        if constexpr (HAS_RES && F16) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += F16 ? (float)rh[i][j][e] : (float)rh[i][j][e] + (float)rl[i][j][e];
+          for (int e = 0; e < 4; ++e) v[e] += (float)rh[i][j][e];
+        } else if constexpr (HAS_RES) {
+          half4v h, l;
+          split_swap_in(rw[i][j], h, l);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)h[e] + (float)l[e];
         }
         if (a.relu) {
 #pragma unroll
@@ -267,9 +273,11 @@ __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile&
           bad |= mok && !(fabsf(v[0]) < kMax && fabsf(v[1]) < kMax && fabsf(v[2]) < kMax && fabsf(v[3]) < kMax);
           half4v h, l;
           split_f16x4(v, h, l);
-          const uint32_t off = mok ? ((uint32_t)m * (uint32_t)a.ldy + (uint32_t)split_off(n)) * 2u : OOR;
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_bd, h), y_rsrc, (int)off, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_bd, l), y_rsrc, (int)(off + 64u), 0, 0);
+          // one 16-byte store per lane (split_swap_out: q even hi, q odd lo of 8 channels)
+          const uint32_t off =
+              mok ? ((uint32_t)m * (uint32_t)a.ldy + (uint32_t)split_off_q(n - 4 * q, q)) * 2u : OOR;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_bd, split_swap_out(h, l)), y_rsrc,
+                                                 (int)off, 0, 0);
         }
         acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
       }
@@ -284,7 +292,7 @@ __global__ void __launch_bounds__(256 * WM, WM) conv3x3_band_kernel(const BandAr
   using namespace bnd;
   constexpr int NW = G::NW, GW = G::GW;
   constexpr int NPI = G::NPI;
-  constexpr int NEPI = (OUT_F32 || F16) ? FN * FM : 2 * FN * FM;   // epilogue stores per wave and tile
+  constexpr int NEPI = FN * FM;                                      // epilogue stores per wave and tile
   static_assert(NEPI < 64 && NPI <= 8, "vmcnt immediates; patch chunks go out at taps 0 .. NPI-1");
   static_assert(!(F16 && OUT_F32), "fp16 band conv stores fp16");
   extern __shared__ __attribute__((aligned(16))) char smem[];

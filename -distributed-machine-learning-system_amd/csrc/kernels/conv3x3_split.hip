@@ -41,7 +41,7 @@ constexpr int RING = 5;            // rows y-2 .. y+1 in use (a row pair's tail 
 constexpr int BIAS = RING * RB;    // the 64 biases (fp32), read by the epilogue: no VGPRs held for them
 constexpr int LDS = BIAS + 256;    // 77,056 B: 2 workgroups per CU
 constexpr int WMAX = 56;           // 3 full fragments + an 8-column tail per row
-constexpr int NST = 6;             // epilogue stores per wave and row, at least (3 fragments x hi, lo)
+constexpr int NST = 3;             // epilogue stores per wave and row, at least (3 fragments, 16 B a lane)
 }  // namespace c64s
 
 struct C64sArgs {
@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
       auto body = [&](auto nft) {
         constexpr int NF = decltype(nft)::value;       // 3: fragments 0-2; 4: + the tail
         constexpr int NG = 18 * NF;                    // groups (tap, block, fragment)
-        half4v rh[HAS_RES ? NF : 1], rl[HAS_RES ? NF : 1];
+        float4v rw[HAS_RES ? NF : 1];                   // 16-byte split residual (split_swap_in)
         // residual of the row's fragments -> registers when the row starts
         // (untracked loads, retired by the epilogue's vmcnt(0)): a load issued in
         // the epilogue exposed a full memory latency per row (+25 % on the residual
@@ -222,9 +222,8 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
           if constexpr (HAS_RES) {
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
-              const uint32_t off = (f < 3 ? rowpix + 16 * f + frow : tpix) * PIX + split_off(n0);
-              rh[f] = gload_b64_untracked(a.res + off);
-              rl[f] = gload_b64_untracked(a.res + off + 32);
+              const uint32_t off = (f < 3 ? rowpix + 16 * f + frow : tpix) * PIX + split_off_q(n0 - 4 * q, q);
+              rw[f] = gload_f4_untracked(a.res + off);
             }
           }
         };
@@ -274,31 +273,31 @@ __global__ void __launch_bounds__(256, 2) conv3x3_split_c64_kernel(const C64sArg
         if constexpr (HAS_RES) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-          for (int f = 0; f < NF; ++f) {
-            reg_tie(rh[f]);
-            reg_tie(rl[f]);
-          }
+          for (int f = 0; f < NF; ++f) reg_tie(rw[f]);
         }
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
-          // fragments 0-2: columns 0..47 < W, every lane stores; the tail: lane 0
-          // (column 48 < W) always does, so every store instruction issues
-          if (f == 3 && !tok) continue;
-          const uint32_t off = (f < 3 ? rowpix + 16 * f + frow : tpix) * PIX + split_off(n0);
+          // one 16-byte store per lane (split_swap_out: q even hi, q odd lo of 8
+          // channels); the lane swap runs on every lane, the tail's store only
+          // where its column is < W (lane 0 always: every store instruction issues)
+          const uint32_t off = (f < 3 ? rowpix + 16 * f + frow : tpix) * PIX + split_off_q(n0 - 4 * q, q);
           float4v v = acc[f] * a.acc_scale + *reinterpret_cast<const float4v*>(smem + BIAS + 4 * n0);
           if constexpr (HAS_RES) {
+            half4v h, l;
+            split_swap_in(rw[f], h, l);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += (float)rh[f][e] + (float)rl[f][e];
+            for (int e = 0; e < 4; ++e) v[e] += (float)h[e] + (float)l[e];
           }
           if (a.relu) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
           }
-          split_guard(a.ovf, v);
           half4v h, l;
           split_f16x4(v, h, l);
-          *reinterpret_cast<half4v*>(a.y + off) = h;
-          *reinterpret_cast<half4v*>(a.y + off + 32) = l;
+          const u32x4_sw o = split_swap_out(h, l);
+          if (f == 3 && !tok) continue;
+          split_guard(a.ovf, v);
+          *reinterpret_cast<u32x4_sw*>(a.y + off) = o;
         }
       };
       if (pair || single) body(c64s_nf<4>{});

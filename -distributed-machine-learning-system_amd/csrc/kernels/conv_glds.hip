@@ -290,7 +290,8 @@ conv_glds_kernel(const ConvArgs a) {
   // spill of an asm load's destination before the load lands corrupts it.
   constexpr bool LATE_RES = SPLIT || BMD != BM;
   half4v rv[HAS_RES ? FN : 1][HAS_RES ? FM : 1];
-  half4v rl[HAS_RES && SPLIT ? FN : 1][HAS_RES && SPLIT ? FM : 1];   // SPLIT: residual lo parts
+  // SPLIT: the residual as one 16-byte load per lane and fragment (split_swap_in)
+  float4v rw[HAS_RES && SPLIT ? FN : 1][HAS_RES && SPLIT ? FM : 1];
   if constexpr (HAS_RES && !LATE_RES) {
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
@@ -408,9 +409,9 @@ conv_glds_kernel(const ConvArgs a) {
       const int m = m0 + wm * TM + j * 16 + (lane & 15);
       const bool ok = m < a.M && n < a.Cout;
       if constexpr (SPLIT) {
-        const size_t off = ok ? (size_t)m * (a.ldr ? a.ldr : 2 * a.Cout) + split_off(n) : 0;
-        rv[i][j] = *reinterpret_cast<const half4v*>(a.res + off);
-        rl[i][j] = *reinterpret_cast<const half4v*>(a.res + off + 32);
+        const int q = lane >> 4;
+        const size_t off = ok ? (size_t)m * (a.ldr ? a.ldr : 2 * a.Cout) + split_off_q(n - 4 * q, q) : 0;
+        rw[i][j] = *reinterpret_cast<const float4v*>(a.res + off);
       } else {
         const size_t off = ok ? (size_t)m * (a.ldr ? a.ldr : a.Cout) + n : 0;
         rv[i][j] = *reinterpret_cast<const half4v*>(a.res + off);
@@ -445,11 +446,12 @@ conv_glds_kernel(const ConvArgs a) {
       if constexpr (HAS_RES) {
         const half4v r = rv[i][j];
         if constexpr (SPLIT) {
-          const half4v q = rl[i][j];
-          v[0] += (float)r[0] + (float)q[0];
-          v[1] += (float)r[1] + (float)q[1];
-          v[2] += (float)r[2] + (float)q[2];
-          v[3] += (float)r[3] + (float)q[3];
+          half4v h, l;
+          split_swap_in(rw[i][j], h, l);
+          v[0] += (float)h[0] + (float)l[0];
+          v[1] += (float)h[1] + (float)l[1];
+          v[2] += (float)h[2] + (float)l[2];
+          v[3] += (float)h[3] + (float)l[3];
         } else {
           v[0] += (float)r[0];
           v[1] += (float)r[1];
@@ -469,9 +471,11 @@ conv_glds_kernel(const ConvArgs a) {
         split_guard(a.ovf, v);
         half4v h, l;
         split_f16x4(v, h, l);
-        half_t* yp = static_cast<half_t*>(a.y) + (size_t)m * a.ldy + split_off(n);
-        *reinterpret_cast<half4v*>(yp) = h;
-        *reinterpret_cast<half4v*>(yp + 32) = l;
+        // one 16-byte store per lane: q even the hi, q odd the lo halfs of 8 channels
+        // (the lanes of one pixel share m, so a pixel's lanes swap together)
+        const int q = lane >> 4;
+        half_t* yp = static_cast<half_t*>(a.y) + (size_t)m * a.ldy + split_off_q(n - 4 * q, q);
+        *reinterpret_cast<u32x4_sw*>(yp) = split_swap_out(h, l);
       } else {
         half4v o;
         o[0] = (half_t)v[0];
