@@ -179,6 +179,11 @@ __device__ __forceinline__ u32x4_sw split_swap_out(half4v h, half4v l) {
   return u32x4_sw{s0[0], s1[0], s0[1], s1[1]};
 }
 
+// fp16 outputs of two 16-channel fragments (lane group q: channels nb + 4q .. +3
+// and nb + 16 + 4q .. +3): the same swap leaves lane q with 8 consecutive
+// channels at f16_pair_off(nb, q) -> one 16-byte store per lane and pair.
+__device__ __forceinline__ int f16_pair_off(int nb, int q) { return nb + 16 * (q & 1) + 8 * (q >> 1); }
+
 __device__ __forceinline__ void split_swap_in(float4v r, half4v& h, half4v& l) {
   const u32x4_sw v = __builtin_bit_cast(u32x4_sw, r);
   const auto s0 = __builtin_amdgcn_permlane16_swap(v[0], v[2], false, false);

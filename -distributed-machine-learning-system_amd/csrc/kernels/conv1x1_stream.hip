@@ -143,7 +143,10 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
                 "LIO shapes: whole 1 KiB instructions, contiguous wave row segments");
   static_assert(!LIO || N2 == 0 || ((BM * NY * 2) % (1024 * NW) == 0 && (BM * ROW2) % 1024 == 0 && ROW2 <= ROWW &&
                                     (CPR2 & (CPR2 - 1)) == 0 && YROW == 512), "LIO + fused next shapes");
-  constexpr int GS = LIO ? GLY + GLZ : FN * FM * SP + (N2 ? FN2 * FM : 0);   // stores per wave and item (y, z)
+  // register-path stores are 16 bytes a lane (common.h split_swap_out): one per
+  // fragment when split, one per fragment pair in fp16 (FN even)
+  constexpr bool PAIR16 = !SPLIT && FN % 2 == 0;
+  constexpr int GS = LIO ? GLY + GLZ : (PAIR16 ? FN / 2 : FN) * FM + (N2 ? FN2 * FM : 0);   // stores per wave and item
   constexpr int GR = HAS_RES ? (LIO ? GLI : FN * FM * SP) : 0;
   static_assert(GS + GX + GR < 64, "vmcnt immediate");
 
@@ -247,6 +250,11 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
   // (SPLIT: channel n sits at split_off(n) of a 2N-half pixel; nw0 % 32 == 0 or FN == 1,
   // so fragment i's offset from the lane part is the constant c1_frag_off(i))
   const uint32_t lane_off = (uint32_t)((frow * a.N * OPX + (SPLIT ? split_off(nw0) : nw0) + 4 * fch) * 2);
+  // 16-byte stores after the lane swap: lane group fch holds channels 8 (fch >> 1)
+  // .. +7 of the fragment's 16 (split: hi for fch even, lo for fch odd) or, fp16,
+  // 16 (fch & 1) + 8 (fch >> 1) .. +7 of the fragment pair's 32
+  const uint32_t lane_st = (uint32_t)((frow * a.N * OPX + (SPLIT ? split_off(nw0) + 8 * (fch >> 1) + 32 * (fch & 1)
+                                                                   : nw0 + 16 * (fch & 1) + 8 * (fch >> 1))) * 2);
   int4s res_rsrc = {0, 0, 0, 0};
   if constexpr (HAS_RES) {
     const unsigned long long rp = reinterpret_cast<unsigned long long>(a.res);
@@ -512,6 +520,7 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
       const uint32_t soff = (uint32_t)(t * BM + j * 16) * (uint32_t)a.N * (uint32_t)(2 * OPX);
+      half4v op[PAIR16 ? FN : 1];
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
         float4v v = SPLIT ? acc[i][j] * a.acc_scale + bv[i] : acc[i][j] + bv[i];
@@ -531,13 +540,20 @@ __global__ void __launch_bounds__(64 * NW, 2) conv1x1_stream_kernel   // 2nd: mi
           split_guard(a.ovf, v);
           half4v h, l;
           split_f16x4(v, h, l);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_c1, h), out_rsrc, voff, (int)soff, 0);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_c1, l), out_rsrc, voff + 64, (int)soff, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c1, split_swap_out(h, l)), out_rsrc,
+                                                 (int)lane_st + c1_frag_off<SPLIT>(i), (int)soff, 0);
         } else {
           half4v o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = (half_t)v[e];
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_c1, o), out_rsrc, voff, (int)soff, 0);
+          if constexpr (PAIR16) {
+            op[i] = o;
+            if (i & 1)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c1, split_swap_out(op[i - 1], o)),
+                                                     out_rsrc, (int)lane_st + 32 * (i - 1), (int)soff, 0);
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_c1, o), out_rsrc, voff, (int)soff, 0);
+          }
           if constexpr (N2 > 0) {
             // output tile -> LDS [pixel][NY] fp16, 16-byte chunk c of pixel row p at c ^ (p & 15)
             const int p = j * 16 + frow, c = (wave * CW + i * 16 + 4 * fch) >> 3;

@@ -240,6 +240,7 @@ __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile&
     for (int j = 0; j < FM; ++j) {
       const int m = mw + 16 * j;
       const bool mok = m < a.M;
+      half4v o16[F16 ? FN : 1];                  // F16: the fragment pair, stored as one 16-byte lane
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
         const int n = cur.n0 + wn * 32 + 16 * i + 4 * q;
@@ -260,11 +261,8 @@ __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile&
         if (a.flags & 2) {
           if (v[0] == 12345.f) bad = true;           // keep the math alive
         } else if constexpr (F16) {
-          half4v h;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) h[e] = (half_t)v[e];
-          const uint32_t off = mok ? ((uint32_t)m * (uint32_t)a.ldy + (uint32_t)n) * 2u : OOR;
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_bd, h), y_rsrc, (int)off, 0, 0);
+          for (int e = 0; e < 4; ++e) o16[i][e] = (half_t)v[e];
         } else if constexpr (OUT_F32) {
           const uint32_t off = mok ? ((uint32_t)m * (uint32_t)a.ldy + (uint32_t)n) * 4u : OOR;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_bd, v), y_rsrc, (int)off, 0, 0);
@@ -281,6 +279,15 @@ __device__ __forceinline__ void band_epilogue(const BandArgs& a, const BandTile&
         }
         acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
       }
+      if constexpr (F16) {
+        static_assert(FN == 2, "fragment pair");
+        if (!(a.flags & 2)) {
+          const uint32_t off =
+              mok ? ((uint32_t)m * (uint32_t)a.ldy + (uint32_t)f16_pair_off(cur.n0 + wn * 32, q)) * 2u : OOR;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_bd, split_swap_out(o16[0], o16[1])), y_rsrc,
+                                                 (int)off, 0, 0);
+        }
+      }
     }
   }
 
@@ -292,7 +299,7 @@ __global__ void __launch_bounds__(256 * WM, WM) conv3x3_band_kernel(const BandAr
   using namespace bnd;
   constexpr int NW = G::NW, GW = G::GW;
   constexpr int NPI = G::NPI;
-  constexpr int NEPI = FN * FM;                                      // epilogue stores per wave and tile
+  constexpr int NEPI = F16 ? FM : FN * FM;                           // epilogue stores per wave and tile
   static_assert(NEPI < 64 && NPI <= 8, "vmcnt immediates; patch chunks go out at taps 0 .. NPI-1");
   static_assert(!(F16 && OUT_F32), "fp16 band conv stores fp16");
   extern __shared__ __attribute__((aligned(16))) char smem[];

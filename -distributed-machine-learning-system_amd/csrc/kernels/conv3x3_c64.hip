@@ -241,20 +241,20 @@ __device__ __forceinline__ void c64_tile(const C64Args& a, int t, const char* __
   // residual and the previous tile's stores: all had a tile of MFMAs to land
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // ---- epilogue: bias (+residual) (+ReLU), NHWC 8-byte stores -------------------
+  // ---- epilogue: bias (+residual) (+ReLU); the two 16-cout fragments of a
+  // pixel fragment swap halves (f16_pair_off) -> one 16-byte NHWC store a lane
   const int per = a.tiles_x * a.tiles_y;
   const int b = t / per, r = t - b * per;
   const int oh0 = (r / a.tiles_x) * TH, ow0 = (r % a.tiles_x) * TW;
+  static_assert(FN == 2, "fragment pair");
 #pragma unroll
-  for (int i = 0; i < FN; ++i) {
-    const int n = wn * (FN * 16) + i * 16 + fch * 4;
+  for (int f = 0; f < FMX; ++f) {
+    int py, px;
+    c64_pix<FMX>(wm, f, frow, py, px);
+    const int oh = oh0 + py, ow = ow0 + px;
+    half4v o[FN];
 #pragma unroll
-    for (int f = 0; f < FMX; ++f) {
-      int py, px;
-      c64_pix<FMX>(wm, f, frow, py, px);
-      const int oh = oh0 + py, ow = ow0 + px;
-      if (oh >= a.H || ow >= a.W) continue;
-      const size_t m = ((size_t)b * a.H + oh) * a.W + ow;
+    for (int i = 0; i < FN; ++i) {
       float4v v = acc[i][f] + bvr[i];
       if constexpr (HAS_RES) {
         const half4v rr = rv[i][f];
@@ -269,13 +269,15 @@ __device__ __forceinline__ void c64_tile(const C64Args& a, int t, const char* __
         v[2] = fmaxf(v[2], 0.f);
         v[3] = fmaxf(v[3], 0.f);
       }
-      half4v o;
-      o[0] = (half_t)v[0];
-      o[1] = (half_t)v[1];
-      o[2] = (half_t)v[2];
-      o[3] = (half_t)v[3];
-      *reinterpret_cast<half4v*>(a.y + m * CO + n) = o;
+      o[i][0] = (half_t)v[0];
+      o[i][1] = (half_t)v[1];
+      o[i][2] = (half_t)v[2];
+      o[i][3] = (half_t)v[3];
     }
+    const u32x4_sw w = split_swap_out(o[0], o[1]);     // every lane swaps
+    if (oh >= a.H || ow >= a.W) continue;
+    const size_t m = ((size_t)b * a.H + oh) * a.W + ow;
+    *reinterpret_cast<u32x4_sw*>(a.y + m * CO + f16_pair_off(wn * (FN * 16), fch)) = w;
   }
 }
 

@@ -430,6 +430,45 @@ conv_glds_kernel(const ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < FM; ++j) reg_tie(rv[i][j]);
   }
+  // fp16 output: the two 16-cout fragments of a pair swap halves (f16_pair_off),
+  // one 16-byte store per lane and pair instead of two 8-byte ones
+  constexpr bool PAIR_ST = !SPLIT && !OUT_F32 && FN % 2 == 0 && !(HAS_RES && RES_PER_I);
+  if constexpr (PAIR_ST) {
+    if (a.Cout % 32 == 0 && a.ldy % 8 == 0) {   // pairs never straddle Cout; 16-byte rows (uniform)
+      const int q = lane >> 4;
+#pragma unroll
+      for (int i = 0; i < FN; i += 2) {
+        const int nb = n0 + wn * TN + i * 16;
+        if (nb >= a.Cout) continue;
+        const float4v bv0 = *reinterpret_cast<const float4v*>(a.bias + nb + 4 * q);
+        const float4v bv1 = *reinterpret_cast<const float4v*>(a.bias + nb + 16 + 4 * q);
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          const int m = m0 + wm * TM + j * 16 + (lane & 15);
+          half4v o[2];
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            float4v v = acc[i + k][j] + (k ? bv1 : bv0);
+            if constexpr (HAS_RES) {
+              const half4v r = rv[i + k][j];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+            }
+            if (relu) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[k][e] = (half_t)v[e];
+          }
+          const u32x4_sw w = split_swap_out(o[0], o[1]);   // every lane swaps
+          if (m < a.M)
+            *reinterpret_cast<u32x4_sw*>(static_cast<half_t*>(a.y) + (size_t)m * a.ldy + f16_pair_off(nb, q)) = w;
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
     const int n = n0 + wn * TN + i * 16 + (lane >> 4) * 4;
