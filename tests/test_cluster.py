@@ -181,13 +181,9 @@ def test_shell_commands(cluster, tmp_path, monkeypatch):
 
 
 def test_tcp_cluster_small():
-    import socket
+    from test_multiprocess import _base_port
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    base = s.getsockname()[1] + 1
-    s.close()
-    c = LocalCluster(num_nodes=3, transport="tcp", base_port=base, **FAST).start()
+    c = LocalCluster(num_nodes=3, transport="tcp", base_port=_base_port(3), **FAST).start()
     try:
         cl = c.client()
         cl.inference(0, 299, "alexnet")

@@ -22,12 +22,23 @@ from idunno.runtime.transport import TcpTransport, wait_for
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _ephemeral_low() -> int:
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            return int(f.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        return 32768
+
+
 def _base_port(n):
+    """n consecutive free ports BELOW the ephemeral range: a range taken from
+    the ephemeral ports races the outgoing connections other tests (and other
+    processes) open meanwhile ("Address already in use")."""
+    import random
+
+    hi = max(_ephemeral_low() - n - 1, 11000)
     for _ in range(50):
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        p = s.getsockname()[1]
-        s.close()
+        p = random.randint(10000, hi)
         ok = True
         for i in range(n):
             t = socket.socket()
