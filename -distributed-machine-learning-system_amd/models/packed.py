@@ -1115,6 +1115,12 @@ class HipRunner:
 
     __call__ = forward
 
+    def has_window(self, shard: torch.Tensor, batch: int, packed: torch.Tensor | None = None) -> bool:
+        """A window graph over ``shard`` (own start scalar) is already captured."""
+        key = ("win", shard.data_ptr(), tuple(shard.shape), batch, None, 0,
+               None if packed is None else packed.data_ptr(), self._variant())
+        return key in self._graphs
+
     def capture_window(self, shard: torch.Tensor, batch: int, start: torch.Tensor | None = None,
                        start_offset: int = 0, packed: torch.Tensor | None = None):
         """hipGraph of forward over a device-side window of ``shard``.

@@ -247,10 +247,21 @@ class HipExecutor(Executor):
         with torch.cuda.device(self.device), self.run_lock:
             s = self._enter(images)
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            base = images._base
+            # a view of a resident dataset (ResidentSource): the window graph reads
+            # the images in place from a device-side start index -- no input copy
+            window = (base is not None and base.dim() == images.dim() and images.is_contiguous()
+                      and base.is_contiguous() and base.dtype == images.dtype
+                      and tuple(base.shape[1:]) == tuple(images.shape[1:]))
             with torch.cuda.stream(s):
                 ev0.record(s)
-                if not self.closed and ((self.use_graphs and len(r._graphs) < self.max_graphs)
-                                        or r.has_graph(n, packed=packed)):
+                can_graph = not self.closed and self.use_graphs and len(r._graphs) < self.max_graphs
+                if window and (can_graph or r.has_window(base, n, packed=packed)):
+                    per = images[0].numel() * images.element_size()
+                    start, replay = r.capture_window(base, n, packed=packed)
+                    start.fill_((images.data_ptr() - base.data_ptr()) // per)
+                    replay()
+                elif can_graph or (not self.closed and r.has_graph(n, packed=packed)):
                     sin, replay = r.capture(n, packed=packed)
                     sin.copy_(images)
                     replay()

@@ -1071,7 +1071,7 @@ def run_node(a) -> int:
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from idunno.config import ClusterConfig
-    from idunno.runtime.data import SyntheticSource
+    from idunno.runtime.data import ResidentSource
     from idunno.runtime.executor import FakeExecutor, HipExecutor
     from idunno.runtime.node import Node
     from idunno.runtime.transport import TcpTransport
@@ -1120,7 +1120,16 @@ def run_node(a) -> int:
     name = cfg.node_name(rank)
     ex = FakeExecutor() if a.dry_run else HipExecutor(dev, seed=a.seed, dtype=a.dtype, fp32_impl=a.fp32_impl)
     node = Node(cfg, name, TcpTransport(name, cfg.address, cfg.address(name)), ex)
-    node.source = None if a.dry_run else SyntheticSource(cfg.data_seed, dev)
+    node.source = None
+    if not a.dry_run:
+        # the dataset resident in HBM as in the raw loop: the system phase's query
+        # ranges generated once before any clock starts (rounds read them in place)
+        src = ResidentSource(cfg.data_seed, dev)
+        if a.phase == "system":
+            share = -(-n // max(1, torch.cuda.device_count())) if (a.rehearse_gloo or a.rehearse_rccl) else 1
+            want = W * B * (a.warmup + a.steps + max(5, min(a.steps, 20)) + 2)
+            src.make_resident(min(want, (32 << 30) // (224 * 224 * 3) // max(1, share)))
+        node.source = src
     if not a.dry_run:
         ex.warmup(a.model, B)                           # capture before any clock starts
     if rank != 0:

@@ -220,3 +220,32 @@ def test_hip_executor_submit_two_in_flight():
     for (cls, prob), (wc, wp) in zip((ra, rb, rc), want):
         assert np.array_equal(cls, wc) and np.array_equal(prob, wp)
     ex.close()
+
+
+def test_run_packed_resident_window_matches_copy():
+    """run_packed on views of a ResidentSource reads the images in place (window
+    graph, device-side start) and gives the same (class, prob) as a copy of the
+    same images; a view at a new offset reuses the graph (no new capture)."""
+    from idunno.runtime.data import ResidentSource, synth_images_cpu
+    from idunno.runtime.executor import HipExecutor
+
+    ex = HipExecutor("cuda", seed=0)
+    src = ResidentSource(7, "cuda")
+    src.make_resident(200)
+    assert torch.equal(src.get(30, 35).cpu(), torch.from_numpy(synth_images_cpu(7, 30, 6)))
+    packed = torch.zeros(64, 2, dtype=torch.int32, device="cuda")
+    r = ex.runner("resnet18")
+    for start in (0, 40, 136):
+        view = src.get(start, start + 47)
+        assert view._base is not None
+        ex.run_packed("resnet18", view, packed[:48])
+        torch.cuda.synchronize()
+        got = packed[:48].clone()
+        ngraphs = len(r._graphs)
+        want_cls, want_prob = _eager(ex, "resnet18", view.clone())
+        assert np.array_equal(got[:, 0].cpu().numpy(), want_cls)
+        assert np.array_equal(got[:, 1].cpu().numpy().view(np.float32), want_prob)
+        assert r.has_window(src.data, 48, packed=packed[:48])
+    assert len(r._graphs) == ngraphs
+    assert src.get(195, 205).shape[0] == 11         # past the resident range: generated per request
+    ex.close()
