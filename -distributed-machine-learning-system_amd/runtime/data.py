@@ -66,6 +66,16 @@ class SyntheticSource:
         return torch.from_numpy(synth_images_cpu(self.seed, start, n))
 
 
+_RESIDENT: dict = {}     # data_ptr -> weakref of the ResidentSource tensors (HipExecutor.run_packed)
+
+
+def is_resident(t: torch.Tensor) -> bool:
+    """``t`` is a ResidentSource dataset tensor: its views are read in place by
+    window graphs (one graph per dataset, not per SDFS shard or request)."""
+    r = _RESIDENT.get(t.data_ptr())
+    return r is not None and r() is t
+
+
 class ResidentSource:
     """The synthetic dataset resident in HBM, as the raw bench loop holds it
     ("dataset replicated in every GPU's HBM"): images [0, n) generated once
@@ -89,6 +99,9 @@ class ResidentSource:
         with torch.cuda.device(self.device):
             self.data = ops.synth_images(self.seed, 0, n, self.device)
             torch.cuda.current_stream(self.device).synchronize()
+        import weakref
+
+        _RESIDENT[self.data.data_ptr()] = weakref.ref(self.data)
 
     def get(self, start: int, end: int) -> torch.Tensor:
         d = self.data

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from ..models import reference as ref
+from .data import is_resident
 
 
 class Done:
@@ -250,13 +251,20 @@ class HipExecutor(Executor):
             base = images._base
             # a view of a resident dataset (ResidentSource): the window graph reads
             # the images in place from a device-side start index -- no input copy
-            window = (base is not None and base.dim() == images.dim() and images.is_contiguous()
+            # (SDFS shards and other views keep the static-input graph: a window
+            # graph per shard would be captured inside the serving path)
+            window = (base is not None and is_resident(base) and base.dim() == images.dim() and images.is_contiguous()
                       and base.is_contiguous() and base.dtype == images.dtype
                       and tuple(base.shape[1:]) == tuple(images.shape[1:]))
             with torch.cuda.stream(s):
                 ev0.record(s)
                 can_graph = not self.closed and self.use_graphs and len(r._graphs) < self.max_graphs
                 if window and (can_graph or r.has_window(base, n, packed=packed)):
+                    if can_graph and not r.has_graph(n, packed=packed):
+                        # the static-input form for this slot as well, now (warm-up
+                        # rounds): a later non-resident view (an SDFS shard) must not
+                        # capture it inside a timed or serving round
+                        r.capture(n, packed=packed)
                     per = images[0].numel() * images.element_size()
                     start, replay = r.capture_window(base, n, packed=packed)
                     start.fill_((images.data_ptr() - base.data_ptr()) // per)

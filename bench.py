@@ -1125,7 +1125,7 @@ def run_node(a) -> int:
         # the dataset resident in HBM as in the raw loop: the system phase's query
         # ranges generated once before any clock starts (rounds read them in place)
         src = ResidentSource(cfg.data_seed, dev)
-        if a.phase == "system":
+        if a.phase == "system" and not os.environ.get("IDUNNO_BENCH_NO_RESIDENT"):
             share = -(-n // max(1, torch.cuda.device_count())) if (a.rehearse_gloo or a.rehearse_rccl) else 1
             want = W * B * (a.warmup + a.steps + max(5, min(a.steps, 20)) + 2)
             src.make_resident(min(want, (32 << 30) // (224 * 224 * 3) // max(1, share)))

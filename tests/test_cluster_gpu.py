@@ -248,4 +248,10 @@ def test_run_packed_resident_window_matches_copy():
         assert r.has_window(src.data, 48, packed=packed[:48])
     assert len(r._graphs) == ngraphs
     assert src.get(195, 205).shape[0] == 11         # past the resident range: generated per request
+    # a view of any other tensor (an SDFS shard) keeps the static-input graph
+    other = src.data.clone()
+    n0 = len(r._graphs)
+    ex.run_packed("resnet18", other[8:56], packed[:48])
+    torch.cuda.synchronize()
+    assert not r.has_window(other, 48, packed=packed[:48]) and len(r._graphs) <= n0 + 1
     ex.close()
