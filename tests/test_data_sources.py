@@ -179,3 +179,17 @@ def test_sdfs_source_prefetch_range_stages_in_background():
     assert src.cached(0, 39) and sorted(store.reads) == [shard_name(k) for k in range(4)]
     assert torch.equal(src.get(5, 34), torch.from_numpy(synth_images_cpu(8, 5, 30)))
     assert len(store.reads) == 4                         # nothing read twice
+
+
+def test_resident_source_cpu_falls_back_to_synthetic():
+    """On a CPU device ResidentSource keeps nothing resident and serves every
+    request as SyntheticSource would (same bytes); is_resident() is false for
+    ordinary tensors (so the executor never takes the window path for them)."""
+    from idunno.runtime.data import ResidentSource, SyntheticSource, is_resident
+
+    src = ResidentSource(5, "cpu")
+    src.make_resident(100)
+    assert src.data is None
+    a = src.get(10, 19)
+    assert torch.equal(a, SyntheticSource(5, "cpu").get(10, 19))
+    assert not is_resident(a) and not is_resident(torch.zeros(3))
