@@ -208,14 +208,19 @@ class ElasticGroup:
         return not self._aborters
 
     def form(self, me: str, members: list[str], epoch: int, host: str, port: int,
-             standby: str | None = None) -> bool:
+             standby: str | None = None, check=None) -> bool:
         """Join epoch ``epoch`` (blocking rendezvous of all ``members``; rank 0
         = members[0] hosts the TCPStore).  With ``standby`` (a member other
         than rank 0) every round is gathered to it as well (the
         reference sends every RESULT to the standby too,
         mp4_machinelearning.py:603-613), so a promoted standby already holds
         the rounds that completed before the coordinator died.  Every member
-        must be given the same ``standby``.  Returns False on failure."""
+        must be given the same ``standby``.  ``check()`` (the failure detector:
+        False once a member of the epoch is dead) is polled while the RCCL
+        communicator is set up: a member killed inside that set-up would
+        otherwise block every other member's form() in the backend's bootstrap
+        (bench --rehearse-rccl coordinator failover at N >= 4, round 5).
+        Returns False on failure."""
         with self.lock:
             self.teardown()
             if me not in members:
@@ -241,8 +246,9 @@ class ElasticGroup:
                     pg = dist.ProcessGroupNCCL(pstore, rank, world, op_to)
                     # communicator set-up now, while every member is in form()
                     eager = getattr(pg, "eager_connect_single_device", None)
-                    if eager is not None:
-                        eager(self.device)
+                    if eager is not None and not self._connect(pg, eager, check):
+                        log.warning("%s: epoch %d: a member failed during communicator set-up", me, epoch)
+                        return False
                 else:
                     pg = dist.ProcessGroupGloo(pstore, rank, world, op_to)
             except Exception:  # noqa: BLE001
@@ -257,6 +263,36 @@ class ElasticGroup:
                 self.abort_async()
                 return False
             return True
+
+    def _connect(self, pg, eager, check) -> bool:
+        """Run the blocking communicator set-up on a helper thread and poll
+        ``check`` meanwhile; a failed check (or the store timeout) aborts the
+        communicator from here, which ends the set-up on every live member."""
+        done, err = threading.Event(), []
+
+        def run():
+            try:
+                eager(self.device)
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+            done.set()
+
+        th = threading.Thread(target=run, name="rccl-connect", daemon=True)
+        th.start()
+        end = time.monotonic() + self.timeout_s
+        while not done.wait(0.01):
+            if (check is not None and not check()) or time.monotonic() > end:
+                def abort():
+                    try:
+                        _shutdown_backend(pg, abort=True)
+                    except Exception:  # noqa: BLE001
+                        log.exception("abort of a communicator in set-up failed")
+
+                ab = threading.Thread(target=abort, name="rccl-abort", daemon=True)
+                ab.start()
+                self._aborters = [t for t in self._aborters if t.is_alive()] + [ab]
+                return False
+        return not err
 
     def _warm_up(self) -> bool:
         """One gather (pair) of every member while all of them are still in

@@ -781,7 +781,9 @@ class RoundPlane:
         for m in members[1:]:
             n.transport.send(m, {"t": Type.GROUP_FORM, "epoch": epoch, "members": members, "port": port,
                                  "standby": standby})
-        ok = self.group.form(n.name, members, epoch, self.cfg.host, port, standby=standby)
+        others = members[1:]
+        ok = self.group.form(n.name, members, epoch, self.cfg.host, port, standby=standby,
+                             check=lambda: n.alive_flag and all(n.membership.is_alive(m) for m in others))
         self._next_seq = 0
         with self.cv:
             self.healthy = ok and self._reform_at is None and epoch == self.epoch
@@ -817,7 +819,14 @@ class RoundPlane:
                 return
             self.epoch, self.members = epoch, members
             self._round_msgs = {k: v for k, v in self._round_msgs.items() if k[0] >= epoch}
-        if not self.group.form(n.name, members, epoch, self.cfg.host, port, standby=msg.get("standby")):
+        coord = members[0]
+
+        def alive() -> bool:       # the epoch's coordinator still alive, no newer epoch announced
+            return n.alive_flag and self._pending_form is None and \
+                (coord == n.name or n.membership.is_alive(coord))
+
+        if not self.group.form(n.name, members, epoch, self.cfg.host, port, standby=msg.get("standby"),
+                               check=alive):
             return
         self._follow(epoch, members)
         if self._pending_form is not None:
