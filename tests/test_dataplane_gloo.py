@@ -370,3 +370,40 @@ def test_scatter_bucket_split_round_robin():
     seen = [(o.peer, o.t.shape[0]) for o in ops]
     assert seen == [(1, 3), (2, 2), (3, 3), (1, 3), (3, 3), (1, 1), (3, 3)]
     assert [o.t.shape[0] for o in rops] == [3, 3, 1]
+
+
+def test_connect_aborts_on_failed_check():
+    """ElasticGroup._connect (the RCCL communicator set-up of form()): a set-up
+    blocked on a dead member ends when check() fails -- the communicator is
+    aborted from a helper thread, which releases the blocked connect -- and a
+    set-up that finishes returns True."""
+    import threading
+    import time
+
+    import torch
+
+    from idunno.parallel.elastic import ElasticGroup
+
+    class FakePg:
+        def __init__(self):
+            self.released = threading.Event()
+            self.aborted = False
+
+        def connect(self, device):          # blocks like a bootstrap waiting on a dead rank
+            self.released.wait(30)
+
+        def abort(self):
+            self.aborted = True
+            self.released.set()
+
+    g = ElasticGroup(torch.device("cpu"), timeout_s=20)
+    pg = FakePg()
+    t0 = time.monotonic()
+    alive = {"ok": True}
+    threading.Timer(0.2, lambda: alive.update(ok=False)).start()
+    assert g._connect(pg, pg.connect, lambda: alive["ok"]) is False
+    assert time.monotonic() - t0 < 5
+    assert g.join_aborters(5) and pg.aborted
+    ok_pg = FakePg()
+    ok_pg.released.set()
+    assert g._connect(ok_pg, ok_pg.connect, lambda: True) is True and not ok_pg.aborted
