@@ -1412,7 +1412,8 @@ def _sdfs_pass(a, node, per_q: int) -> dict:
     put_s = time.perf_counter() - t
     keep = node.source
     src = SdfsSource(node.sdfs, node.device if node.device is not None else "cpu", shard_images=500,
-                     peer_copy=False, readahead=4)
+                     peer_copy=False, readahead=4,
+                     stage_streams=int(os.environ.get("IDUNNO_BENCH_STAGE_STREAMS", "1")))
     gpu = src.device.type == "cuda"
     node.source = src
     out = {}
