@@ -547,12 +547,15 @@ bool conv3x3_band_default(int B, int W, int Cout) {
   return conv3x3_band_tiles(B, W, Cout) >= device_cu_count();
 }
 
-// fp16 (round-5 per-layer A/B, profiles/r5_band_f16_layers.log): 2 MFMAs per
-// 128-byte K block leave the band kernel ahead of the im2col tiles only at W 28
-// without a residual (ResNet50 layer2 -2.4 %, ResNet18 layer2 c0 -7 %); with the
-// all-W rule the whole graph lost 1.1 % (ResNet50 b1024) / 2.6 % (ResNet18 b400)
+// fp16: with 8-byte epilogue stores the band kernel led the im2col tiles only
+// at W 28 without a residual (profiles/r5_band_f16_layers.log).  With the
+// 16-byte epilogue (f16_pair_off) it leads or ties per layer at every W
+// (profiles/r5_band_f16_layers_b128.log), but in the whole graph only W 28 pays:
+// W 28 with or without residual +1.0 % ResNet18 fp16 (ResNet50 -0.04 %), every W
+// -2.0 % / -0.6 % (profiles/r5_ab_band_f16_rule_b128.log).
 bool conv3x3_band_f16_default(int B, int W, int Cout, bool res) {
-  return W == 28 && !res && conv3x3_band_tiles(B, W, Cout) >= device_cu_count();
+  (void)res;
+  return W == 28 && conv3x3_band_tiles(B, W, Cout) >= device_cu_count();
 }
 
 int conv3x3_band_tiles(int B, int W, int Cout) {
