@@ -98,36 +98,63 @@ std::vector<double> stage_file_native(const std::string& path, torch::Tensor out
   TORCH_CHECK(fd >= 0, "open ", path, ": ", std::strerror(errno));
   std::vector<hipEvent_t> done(nb, nullptr);
   std::string fail;
+  bool issued = false;                       // some copy out of a pinned buffer was queued
+  // every exit path (a read or HIP error included) closes the file, waits until no
+  // copy out of the pinned buffers is in flight -- the caller reuses them at once --
+  // and destroys the events; the first error is reported only after that
+  struct Tail {
+    int fd;
+    std::vector<hipEvent_t>& done;
+    const std::string& fail;
+    const bool& issued;
+    hipStream_t st;
+    ~Tail() {
+      ::close(fd);
+      if (!fail.empty() && issued) (void)hipStreamSynchronize(st);   // an event may be missing
+      for (auto e : done) {
+        if (e != nullptr) {
+          (void)hipEventSynchronize(e);
+          (void)hipEventDestroy(e);
+        }
+      }
+    }
+  };
+  auto hip_ok = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && fail.empty()) fail = std::string(what) + ": " + hipGetErrorString(e);
+    return e == hipSuccess;
+  };
   using clk = std::chrono::steady_clock;
   double t_read = 0, t_wait = 0, t_tail = 0;
   auto secs = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); };
-  for (size_t off = 0, i = 0; off < nbytes; off += step, ++i) {
-    const int b = (int)(i % nb);
-    const size_t n = std::min(step, nbytes - off);
-    auto t0 = clk::now();
-    if (done[b] != nullptr) check_hip(hipEventSynchronize(done[b]), "hipEventSynchronize");
-    auto t1 = clk::now();
-    int err = 0;
-    const bool ok = pread_parallel(fd, pb[b], n, off, (int)nthreads, &err);
-    auto t2 = clk::now();
-    t_wait += secs(t0, t1);
-    t_read += secs(t1, t2);
-    if (!ok) {
-      fail = std::string("read ") + path + ": " + std::strerror(err);
-      break;
+  clk::time_point t3;
+  {
+    Tail tail{fd, done, fail, issued, st};
+    for (size_t off = 0, i = 0; off < nbytes; off += step, ++i) {
+      const int b = (int)(i % nb);
+      const size_t n = std::min(step, nbytes - off);
+      auto t0 = clk::now();
+      if (done[b] != nullptr && !hip_ok(hipEventSynchronize(done[b]), "hipEventSynchronize")) break;
+      auto t1 = clk::now();
+      int err = 0;
+      const bool ok = pread_parallel(fd, pb[b], n, off, (int)nthreads, &err);
+      auto t2 = clk::now();
+      t_wait += secs(t0, t1);
+      t_read += secs(t1, t2);
+      if (!ok) {
+        fail = std::string("read ") + path + ": " + std::strerror(err);
+        break;
+      }
+      if (!hip_ok(hipMemcpyAsync(dst + off, pb[b], n, hipMemcpyHostToDevice, st), "hipMemcpyAsync")) break;
+      issued = true;
+      if (done[b] == nullptr &&
+          !hip_ok(hipEventCreateWithFlags(&done[b], hipEventDisableTiming), "hipEventCreate")) {
+        done[b] = nullptr;
+        break;
+      }
+      if (!hip_ok(hipEventRecord(done[b], st), "hipEventRecord")) break;
     }
-    check_hip(hipMemcpyAsync(dst + off, pb[b], n, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
-    if (done[b] == nullptr) check_hip(hipEventCreateWithFlags(&done[b], hipEventDisableTiming), "hipEventCreate");
-    check_hip(hipEventRecord(done[b], st), "hipEventRecord");
-  }
-  ::close(fd);
-  auto t3 = clk::now();
-  for (auto e : done) {
-    if (e != nullptr) {
-      (void)hipEventSynchronize(e);       // the pinned buffers are free for the next call
-      (void)hipEventDestroy(e);
-    }
-  }
+    t3 = clk::now();
+  }                                          // ~Tail: the last copies out of the pinned buffers
   t_tail = secs(t3, clk::now());
   TORCH_CHECK(fail.empty(), fail);
   return {t_read, t_wait, t_tail};

@@ -258,7 +258,7 @@ class ElasticGroup:
             self.pg = pg
             self.epoch, self.members, self.rank = epoch, list(members), rank
             self._alloc(world)
-            if self.backend == "nccl" and not self._warm_up():
+            if self.backend == "nccl" and not self._warm_up(check):
                 log.error("%s: epoch %d: warm-up gather did not complete", me, epoch)
                 self.abort_async()
                 return False
@@ -282,30 +282,40 @@ class ElasticGroup:
         end = time.monotonic() + self.timeout_s
         while not done.wait(0.01):
             if (check is not None and not check()) or time.monotonic() > end:
-                def abort():
-                    try:
-                        _shutdown_backend(pg, abort=True)
-                    except Exception:  # noqa: BLE001
-                        log.exception("abort of a communicator in set-up failed")
-
-                ab = threading.Thread(target=abort, name="rccl-abort", daemon=True)
-                ab.start()
-                self._aborters = [t for t in self._aborters if t.is_alive()] + [ab]
+                self._abort_in_background(pg)
                 return False
-        return not err
+        if err:
+            # a set-up that raised leaves a half-built communicator: end it too
+            self._abort_in_background(pg)
+            return False
+        return True
 
-    def _warm_up(self) -> bool:
+    def _abort_in_background(self, pg) -> None:
+        def abort():
+            try:
+                _shutdown_backend(pg, abort=True)
+            except Exception:  # noqa: BLE001
+                log.exception("abort of a communicator in set-up failed")
+
+        ab = threading.Thread(target=abort, name="rccl-abort", daemon=True)
+        ab.start()
+        self._aborters = [t for t in self._aborters if t.is_alive()] + [ab]
+
+    def _warm_up(self, check=None) -> bool:
         """One gather (pair) of every member while all of them are still in
         ``form()``: RCCL sets up a pair's point-to-point connection at the pair's
         first operation, and that handshake blocks the POSTING thread until the
         peer posts too.  Without it the coordinator's first post of an epoch
         waited on a member paused in its chunk, and when that member was killed,
         for the backend's whole timeout (120 s) instead of the failure detector's
-        2 s (bench --rehearse-rccl worker failover, round 5)."""
+        2 s (bench --rehearse-rccl worker failover, round 5).  ``check`` (the
+        failure detector, as in ``form``) is polled too: a member that dies
+        between the set-up and the warm-up ends the wait at once, not after
+        ``timeout_s`` (the caller aborts the epoch)."""
         work = self.post_gather(0)
         end = time.monotonic() + self.timeout_s
         while not work.is_completed():
-            if time.monotonic() > end:
+            if time.monotonic() > end or (check is not None and not check()):
                 return False
             time.sleep(0.001)
         work.wait()

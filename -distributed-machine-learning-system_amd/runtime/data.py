@@ -436,9 +436,14 @@ class SdfsSource:
             if ev is not None:
                 cs.wait_event(ev)
             key = (k, cs.cuda_stream)
-            if key not in self._rec:
+            with self.lock:
+                fresh = key not in self._rec and self.cache.get(k) is t
+                if fresh:
+                    self._rec.add(key)
+            if fresh:
                 t.record_stream(cs)
-                self._rec.add(key)
+            elif self.cache.get(k) is not t:
+                t.record_stream(cs)           # not the cached tensor (evicted meanwhile): always
         return t
 
     def _fetch(self, k: int) -> torch.Tensor:
@@ -479,7 +484,15 @@ class SdfsSource:
                 t, ev = self.stagers[k % self.nstage]._stage(data, (n, HW, HW, 3))
         dropped = []
         with self.lock:
+            held = self.cache.get(k)
+            if held is not None:
+                # another fetch of k (round thread vs background readahead) filled the
+                # cache first: keep that tensor -- consumers may already hold it and
+                # record_stream'ed it -- and drop this duplicate (its copy is ordered
+                # on the stager's stream, which is the stream its block returns to)
+                return held
             self.fetches += 1
+            self._rec = {x for x in self._rec if x[0] != k}
             self.cache[k] = t
             self.ver[k] = ver
             self._ready[k] = ev

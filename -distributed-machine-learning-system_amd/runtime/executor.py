@@ -27,6 +27,8 @@ from .data import is_resident
 class Done:
     """An already finished ``Executor.submit`` (synchronous executors)."""
 
+    synchronous = True           # the chunk ran inside submit() (the node times that call)
+
     def __init__(self, res):
         self._res = res
 

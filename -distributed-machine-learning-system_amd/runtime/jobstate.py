@@ -504,6 +504,12 @@ class JobState:
         with self.lock:
             return list(self.working_vm_set.get(worker, []))
 
+    def busy_workers(self) -> dict:
+        """worker -> the models it has chunks running of (the fair-time
+        hand-over waits for a worker's chunks of its old job)."""
+        with self.lock:
+            return {w: {c[0] for c in cs} for w, cs in self.working_vm_set.items() if cs}
+
     def reassign(self, failed: str, new_worker: str, chunk: tuple, now: float | None = None) -> None:
         """Move one in-flight chunk of a failed worker to ``new_worker``
         (reference transfer_failed_inference_work, mp4_machinelearning.py:706-760)."""

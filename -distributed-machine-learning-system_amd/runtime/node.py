@@ -66,6 +66,8 @@ class Node:
         self._standby_ack: tuple | None = None     # (epoch, seq) the standby has applied; None = re-sync
         self.meta_bytes = 0                        # bytes of the last METADATA push (delta size check)
         self.chunks_done = 0
+        self.warm_shapes: set = set()              # (model, chunk size) this node has computed once
+        self._submit_lock = threading.Lock()
         self.logger = self._make_logger()
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
@@ -314,10 +316,16 @@ class Node:
         if qnum is None:
             qnum = self.state.new_query_number(model)
         self.sched.active_jobs = self.state.active_models() | {model}
-        # a query boundary with nothing in flight: the fair-time split may follow the EMA
-        plan = self.sched.assign(model, start, end, alive, drained=self.state.pending_count() == 0)
-        now = self.clock()
-        self.state.assign(model, qnum, plan, now)
+        # this job's query boundary: the fair-time split follows the current averages.
+        # On the TCP path a worker still running the other job's chunks changes hands
+        # only once they are done (busy); the round path re-splits queued queries
+        # before they are posted, so it hands workers over at once
+        rounds_ok = self.rounds is not None and self.rounds.healthy
+        with self._submit_lock:       # plan + record as one step: the next plan sees these chunks busy
+            plan = self.sched.assign(model, start, end, alive, boundary=True,
+                                     busy=None if rounds_ok else self.state.busy_workers())
+            now = self.clock()
+            self.state.assign(model, qnum, plan, now)
         self.tracer.instant("query.submit", model=model, q=qnum, start=start, end=end, workers=len(plan))
         prefetch = getattr(self.source, "prefetch", None)
         if prefetch is not None:
@@ -411,11 +419,12 @@ class Node:
         self.tracer.instant("result.ingest", model=msg["model"], q=msg["qnum"], start=msg["start"],
                             worker=msg["worker"], new=new)
         cs = msg.get("compute_s")
-        if new and cs is not None and self.is_coordinator:
+        if new and cs is not None and self.is_coordinator and not msg.get("cold"):
             # (round results carry no compute_s: the members report their own GPU
-            # time in the gather header instead, see rounds.RoundPlane._finalize)
+            # time in the gather header instead, see rounds.RoundPlane._finalize);
+            # a worker's first chunk of a model and size (graph capture) never counts
             n = msg["end"] - msg["start"] + 1
-            self.sched.observe(msg["model"], cs / n * self.cfg.batch_for(msg["model"]))
+            self.sched.observe_chunk(msg["model"], n, cs, self.cfg.batch_for(msg["model"]))
         if new:
             with self._progress:
                 self._progress.notify_all()
@@ -796,11 +805,15 @@ class Node:
         self._prefetch_next()                 # next JOB's images stage while this one computes
         t_launch = time.time()
         handle = self.executor.submit(model, imgs, s, e)
-        return (msg, t0, tags, t_launch, handle)
+        # a synchronous executor ran the chunk inside submit(): its own time is that
+        # call plus the staging (the pipelined worker finishes chunk k only after
+        # chunk k+1 ran, so completion-to-completion would not measure it)
+        sync_dt = time.perf_counter() - t0 if getattr(handle, "synchronous", False) else None
+        return (msg, t0, tags, t_launch, handle, sync_dt)
 
     def finish_chunk(self, ctx) -> None:
         """Wait for a launched chunk, send / ingest its RESULT."""
-        msg, t0, tags, t_launch, handle = ctx
+        msg, t0, tags, t_launch, handle, sync_dt = ctx
         cls, prob = handle.result()
         t_done = time.time()
         self.tracer.complete("chunk.compute", t_launch, t_done, **tags)
@@ -808,14 +821,20 @@ class Node:
         # it had to queue behind that one on the GPU (fair-time averages)
         prev = self._last_chunk_done
         self._last_chunk_done = t_done
-        dt = (time.perf_counter() - t0) if prev is None or prev <= t_launch else (t_done - prev)
+        dt = sync_dt if sync_dt is not None else \
+            (time.perf_counter() - t0) if prev is None or prev <= t_launch else (t_done - prev)
         if not self.alive_flag:
             return
         model, s, e = msg["model"], int(msg["start"]), int(msg["end"])
+        shape = (model, e - s + 1)
+        cold = shape not in self.warm_shapes
+        self.warm_shapes.add(shape)
         res = {"t": Type.RESULT, "model": model, "qnum": msg["qnum"], "start": s, "end": e,
                "worker": self.name, "cls": np.ascontiguousarray(cls, np.int32).tobytes(),
                "prob": np.ascontiguousarray(prob, np.float32).tobytes(), "compute_s": dt,
                "epoch": msg.get("epoch", 0)}
+        if cold:
+            res["cold"] = True
         self.chunks_done += 1
         targets = {self.membership.master, self.standby}
         for dst in targets:

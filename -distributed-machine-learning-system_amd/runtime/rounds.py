@@ -108,7 +108,7 @@ class RoundPlane:
         self._release_done = threading.Event()
         self._wake = threading.Event()
         self._thread: threading.Thread | None = None
-        self._timings: deque = deque(maxlen=64)   # (model_id, n, (ev0, ev1) | seconds)
+        self._timings: deque = deque(maxlen=64)   # (model_id, n, (ev0, ev1) | seconds, cold)
         self._hdr = None
         self._tag = 0
         self._next_seq = 0                    # coordinator: seq of the next round of this epoch
@@ -299,20 +299,24 @@ class RoundPlane:
         with n.tracer.span("round.stage", **tags):
             imgs = n.source.get(s, e) if n.source is not None else None
         run_packed = getattr(n.executor, "run_packed", None)
+        # a member's first chunk of a model and size (graph capture, kernel load) is
+        # reported as cold: it never seeds the coordinator's fair-time average
+        cold = (model, cnt) not in n.warm_shapes
+        n.warm_shapes.add((model, cnt))
         c0 = time.thread_time()
         with n.tracer.span("round.launch", **tags):
             if run_packed is not None and imgs is not None and imgs.device.type == "cuda" and \
                     send.device == imgs.device:
                 evs = run_packed(model, imgs, send[:cnt])
                 if evs is not None:
-                    self._timings.append((mid, cnt, evs))
+                    self._timings.append((mid, cnt, evs, cold))
                     tl = n.gpu_timeline
                     if tl is not None:
                         tl.append(("fwd", evs[0], evs[1], cnt))
             else:
                 t0 = time.perf_counter()
                 cls, prob = n.executor.run(model, imgs, s, e)
-                self._timings.append((mid, cnt, time.perf_counter() - t0))
+                self._timings.append((mid, cnt, time.perf_counter() - t0, cold))
                 pack_into(send, cls, prob)
         self.launch_cpu_s += time.thread_time() - c0     # this thread's CPU time in the launch (vs its wall span)
         n.chunks_done += 1
@@ -322,7 +326,7 @@ class RoundPlane:
         header rows: (us, model_id), (n_images, tag); zeros if none finished."""
         us = mid = cnt = 0
         if self._timings:
-            m, c, t = self._timings[0]
+            m, c, t, cold = self._timings[0]
             if isinstance(t, tuple):
                 ev0, ev1 = t
                 if ev1.query():
@@ -331,6 +335,8 @@ class RoundPlane:
             else:
                 us, mid, cnt = int(t * 1e6), m, c
                 self._timings.popleft()
+            if cold:
+                us = mid = cnt = 0             # measured, but not reported (see _run_chunk)
         self._tag += 1
         vals = (us, mid, cnt, self._tag)
         hdr = self.group.header(seq)
@@ -517,8 +523,10 @@ class RoundPlane:
                     tb, cb = time.perf_counter(), time.thread_time()
                     rounds = self._build_rounds(members)
                     if rounds:
-                        self._announce(rounds, members)
+                        # owed before the multicast: a failed announce (a member lost,
+                        # worker failover) falls back on these rounds' queries too
                         announced.extend(rounds)
+                        self._announce(rounds, members)
                     self.host_s += time.perf_counter() - tb
                     self.host_cpu_s += time.thread_time() - cb
                 if not announced:
@@ -686,17 +694,13 @@ class RoundPlane:
         bad = None
         if cls_all.min() < 0:             # rare: some row holds a range-guard mark (or stale tail)
             bad = ((cls_all < 0) & (np.arange(used) < np.array(lens)[:, None])).any(axis=1).tolist()
-        # one scheduler observation per model per round: the members' summed compute
-        # time over their summed images (a per-image time), scaled to the model's batch
-        obs = {}
+        # every member's reported (warm) chunk is one (size, seconds) point of its
+        # model's chunk-time line; the scheduler's average is that line's full-query
+        # time, which does not move with how the split cut the queries
         for us, hmid, cnt, _ in hdr:
-            if cnt > 0 and hmid in MODEL_NAMES:
-                o = obs.setdefault(hmid, [0, 0])
-                o[0] += us
-                o[1] += cnt
-        for hmid, (us, cnt) in obs.items():
-            model = MODEL_NAMES[hmid]
-            n.sched.observe(model, us * 1e-6 / cnt * self.cfg.batch_for(model))
+            if cnt > 0 and us > 0 and hmid in MODEL_NAMES:
+                model = MODEL_NAMES[hmid]
+                n.sched.observe_chunk(model, cnt, us * 1e-6, self.cfg.batch_for(model))
         for i, row in enumerate(r.table):
             if row is None:
                 continue
@@ -917,7 +921,6 @@ class RoundPlane:
         seq, work, rows, done = x
         if done or rows is None:
             return
-        x[3] = True
         arr = self.group.collect(seq, work, check)
         recs = []
         for i, row in enumerate(rows):
@@ -930,4 +933,5 @@ class RoundPlane:
                 continue
             recs.append((MODEL_NAMES[mid], qnum, members[i], s, e, cls, arr[i, :k, 1].copy().view(np.float32)))
         self.node._ingest_round(recs, time.time(), seq=seq)
+        x[3] = True                  # only once held: a collect that raised is retried by the sweep
         self.standby_rounds += 1

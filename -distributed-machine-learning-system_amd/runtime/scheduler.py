@@ -18,6 +18,7 @@ constant 100 s that is never written.
 from __future__ import annotations
 
 import random
+import threading
 from dataclasses import dataclass, field
 
 
@@ -105,6 +106,49 @@ def partition(avg_time: dict[str, float], models, workers: list, budget: int) ->
     return out
 
 
+class ChunkTimeFit:
+    """A model's chunk compute time as ``t(n) = a + b*n`` (fixed per-chunk cost
+    + per-image cost), fitted by exponentially-forgotten least squares over the
+    observed (chunk size, seconds) pairs.
+
+    Why: the fair-time rule needs each model's *query*
+    time, but a chunk's per-image time falls as the chunk grows (the fixed
+    launch / tail cost is spread over more images) and the chunk size is set by
+    the split itself -- a model given more workers gets smaller chunks, looks
+    slower per image and would be given still more workers.  ``full(B)`` = a +
+    b*B, the time ONE worker needs for a whole B-image query, does not depend on
+    how the current split cut it.  Until two clearly different chunk sizes have
+    been seen the fit falls back to the per-image time scaled to B, and it does
+    so too when the line claims more than half of a chunk's time is fixed cost:
+    a per-image time that CHANGED (the model got slower) together with the chunk
+    size fits such a line, and it would fade only as the old points are
+    forgotten."""
+
+    MAX_FIXED = 0.5                 # intercept / mean chunk time above which the line is not trusted
+
+    def __init__(self, forget: float = 0.2):
+        self.forget = forget
+        self.w = self.sn = self.st = self.snn = self.snt = 0.0
+        self.nmin = self.nmax = None
+
+    def add(self, n: int, t: float) -> None:
+        k = 1.0 - self.forget
+        self.w, self.sn, self.st = k * self.w + 1.0, k * self.sn + n, k * self.st + t
+        self.snn, self.snt = k * self.snn + n * n, k * self.snt + n * t
+
+    def full(self, B: int) -> float | None:
+        if self.w <= 0:
+            return None
+        mn, mt = self.sn / self.w, self.st / self.w
+        var = self.snn / self.w - mn * mn
+        if var > (0.1 * mn) ** 2:                 # chunk sizes spread by >10 %: fit the line
+            b = (self.snt / self.w - mn * mt) / var
+            a = mt - b * mn
+            if b > 0 and 0 <= a <= self.MAX_FIXED * mt:
+                return a + b * B
+        return mt / max(mn, 1e-9) * B
+
+
 @dataclass
 class FairTimeScheduler:
     """Chooses workers and chunks for each query.
@@ -119,13 +163,17 @@ class FairTimeScheduler:
     seed: int | None = None
     avg_time: dict = field(default_factory=lambda: {"alexnet": 1.0, "resnet18": 1.0})
     active_jobs: set = field(default_factory=set)
-    hysteresis: float = 0.1          # workers past the rounding point before a drained re-split
+    hysteresis: float = 0.1          # workers past the rounding point before a re-split
 
     def __post_init__(self):
         self._rng = random.Random(self.seed)
         self._seen: set = set()
         self._part: dict = {}
-        self.repartitions = 0        # drained-boundary re-splits of the current (active, workers) key
+        self._fits: dict = {}
+        self._leaving: dict = {}     # worker -> (donor, receiver): handed over once the donor's chunks end
+        self._lock = threading.Lock()
+        self.repartitions = 0        # query-boundary re-splits of the current (active, workers) key
+        self.moves_deferred = 0      # hand-overs that waited for the donor's chunks on the worker
 
     def effective_avg(self, models) -> dict[str, float]:
         """Per-model average query time for the split: a model with no
@@ -136,38 +184,93 @@ class FairTimeScheduler:
         fill = sum(seen) / len(seen) if seen else 1.0
         return {m: (self.avg_time[m] if m in self._seen else fill) for m in models}
 
-    def subsets(self, active, workers: list, drained: bool = False) -> dict[str, list]:
+    def target_sizes(self, active, workers: list) -> dict[str, int]:
+        """Subset sizes the current averages prescribe (``partition``'s rule)."""
+        return {m: len(v) for m, v in partition(self.effective_avg(active), active, list(workers),
+                                                self.budget).items()}
+
+    def subsets(self, active, workers: list, boundary: bool = False, busy: dict | None = None,
+                drained: bool = False) -> dict[str, list]:
         """``partition`` of ``workers`` over the ``active`` models.
 
-        The split is computed when the active set (a job starts or ends), the
-        worker set (a failure / join) or the set of measured models changes,
-        and kept while queries are in flight, so EMA jitter never moves a job's
-        GPUs under its running queries (a moved subset would collide with the
-        other job's in-flight chunks).  At a DRAINED query boundary (no query of
-        any job in flight, ``drained``) it follows the measured averages again,
-        like the reference, which re-plans every query from the current averages
-        (mp4_machinelearning.py:501-521; report Fig 2: 5/5 -> 4/6): the split
-        moves when some model's exact share (t_i / sum(t) x workers) is more than
-        ``hysteresis`` workers past the half-way point of its current count."""
+        A fresh split is computed when the active set (a job starts or ends) or
+        the worker set (a failure / join) changes.  Otherwise the split is
+        re-planned at every query BOUNDARY
+        (``boundary``: a job's next query is being planned), like the
+        reference, which re-plans every query from the current averages
+        (mp4_machinelearning.py:501-521; report Fig 2: 5/5 -> 4/6): when some
+        model's exact share (t_i / sum(t) x workers) is more than
+        ``hysteresis`` workers past the half-way point of its current count,
+        workers move from the models above their target to the ones below it.
+        Each model keeps the workers it is not giving up, so its queries keep
+        landing on the same GPUs.
+
+        Subsets never overlap in-flight chunks: ``busy`` (worker -> models with
+        chunks running there) marks a donor's worker that still runs the
+        donor's chunks; it leaves the donor's subset at once (the donor's next
+        queries no longer use it) and joins the receiver at the first boundary
+        after those chunks finished.  ``busy=None`` (the collective round path:
+        queued queries are re-split onto the new subsets before they are
+        posted, and a round gives each member one row) hands workers over at
+        once.  ``drained`` is the old name of ``boundary``."""
+        boundary = boundary or drained
         active = frozenset(active)
-        key = (active, tuple(workers), frozenset(self._seen & active))
-        cur = self._part.get(key)
-        if cur is None:
-            cur = partition(self.effective_avg(active), active, list(workers), self.budget)
-            self._part = {key: cur}
-            self.repartitions = 0
-        elif drained and len(active) > 1:
-            avg = self.effective_avg(active)
-            eff = max(1, min(self.budget, len(workers)))
-            sh = time_shares(avg, active)
-            moved = any(abs(sh[m] * eff - len(cur[m])) > 0.5 + self.hysteresis for m in active)
-            if moved:
-                new = partition(avg, active, list(workers), self.budget)
-                if {m: len(v) for m, v in new.items()} != {m: len(v) for m, v in cur.items()}:
+        key = (active, tuple(workers))
+        with self._lock:
+            cur = self._part.get(key)
+            if cur is None:
+                cur = partition(self.effective_avg(active), active, list(workers), self.budget)
+                self._part = {key: cur}
+                self._leaving = {}
+                self.repartitions = 0
+            elif boundary and 1 < len(active) <= max(1, min(self.budget, len(workers))):
+                new = {m: list(v) for m, v in cur.items()}
+                changed = self._settle(new, busy)
+                size = {m: len(new[m]) + sum(1 for _d, r in self._leaving.values() if r == m) for m in active}
+                eff = max(1, min(self.budget, len(workers)))
+                sh = time_shares(self.effective_avg(active), active)
+                if any(abs(sh[m] * eff - size[m]) > 0.5 + self.hysteresis for m in active):
+                    changed |= self._shift(new, size, self.target_sizes(active, workers), busy)
+                if changed:
                     cur = new
                     self._part = {key: cur}
                     self.repartitions += 1
-        return cur
+            return cur
+
+    def _settle(self, cur: dict, busy: dict | None) -> bool:
+        """Workers handed over while still busy with their donor's chunks join
+        their receiver once those chunks are done."""
+        moved = False
+        for w, (donor, recv) in list(self._leaving.items()):
+            if recv in cur and (busy is None or donor not in busy.get(w, ())):
+                cur[recv].append(w)
+                del self._leaving[w]
+                moved = True
+        return moved
+
+    def _shift(self, cur: dict, size: dict, want: dict, busy: dict | None) -> bool:
+        """Move workers from models above their target size to models below
+        it: a donor's idle workers first (its last ones first, so slices stay
+        contiguous when nothing is busy); a busy one goes through
+        ``_leaving``."""
+        need = [m for m in sorted(cur) for _ in range(max(0, want.get(m, 0) - size[m]))]
+        moved = False
+        for donor in sorted(cur, key=lambda m: (size[m] - want.get(m, 0), m), reverse=True):
+            while need and cur[donor] and size[donor] > max(1, want.get(donor, 0)):
+                cands = list(reversed(cur[donor]))
+                free = [w for w in cands if busy is None or donor not in busy.get(w, ())]
+                w = free[0] if free else cands[0]
+                cur[donor].remove(w)
+                size[donor] -= 1
+                recv = need.pop(0)
+                size[recv] += 1
+                if free:
+                    cur[recv].append(w)
+                else:
+                    self._leaving[w] = (donor, recv)
+                    self.moves_deferred += 1
+                moved = True
+        return moved
 
     def observe(self, model: str, normalized_query_time: float) -> None:
         """Feed a measured full-query-equivalent time for ``model`` (EMA)."""
@@ -177,6 +280,21 @@ class FairTimeScheduler:
         else:
             old = self.avg_time[model]
             self.avg_time[model] = (1 - self.ema) * old + self.ema * float(normalized_query_time)
+
+    def observe_chunk(self, model: str, n: int, seconds: float, batch: int) -> None:
+        """One warm chunk of ``n`` images took ``seconds`` of compute: refit the
+        model's chunk-time line and take its full-query time ``a + b*batch``
+        (``ChunkTimeFit``) as the model's average.  Callers leave out cold
+        chunks (a worker's first chunk of a model and chunk size: graph capture,
+        kernel load), so they never seed the average."""
+        if n <= 0 or seconds <= 0:
+            return
+        fit = self._fits.setdefault(model, ChunkTimeFit())
+        fit.add(int(n), float(seconds))
+        t = fit.full(int(batch))
+        if t is not None:
+            self.avg_time[model] = t
+            self._seen.add(model)
 
     def adopt(self, avg_time: dict) -> None:
         """Take over measured averages (standby mirror, checkpoint restore):
@@ -193,20 +311,22 @@ class FairTimeScheduler:
         return max(1, fair_share(self.effective_avg(act), model, self.budget, len(alive), act))
 
     def assign(self, model: str, start: int, end: int, alive: list,
-               n: int | None = None, shuffle: bool = True, drained: bool = False) -> list[tuple]:
+               n: int | None = None, shuffle: bool = True, drained: bool = False,
+               boundary: bool = False, busy: dict | None = None) -> list[tuple]:
         """Returns [(worker, s, e), ...] for the inclusive query range.
 
         A single active job gets the whole budget (a random sample of the
         alive workers when the budget is smaller, as the reference samples,
         :520-521).  With several active jobs each gets its own disjoint,
         fair-time-sized subset (``partition``), so concurrent jobs share the
-        node in space instead of queueing on the same GPUs; ``drained`` (no
-        query in flight) lets that split follow the measured averages."""
+        node in space instead of queueing on the same GPUs; ``boundary`` (this
+        is a job's next query) lets that split follow the measured averages
+        (``subsets``)."""
         if not alive:
             return []
         active = set(self.active_jobs) | {model}
         if n is None and len(active) > 1:
-            workers = self.subsets(active, list(alive), drained=drained)[model]
+            workers = self.subsets(active, list(alive), boundary=boundary or drained, busy=busy)[model]
         else:
             n = self.n_workers(model, alive) if n is None else max(1, min(n, len(alive)))
             workers = self._rng.sample(list(alive), n) if shuffle else list(alive)[:n]

@@ -112,6 +112,10 @@ def parse(argv=None):
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N > 1: keep the descriptor broadcast and result gather between the forwards "
                          "(default: double-buffered, overlapped with the next round's forward)")
+    ap.add_argument("--host-wait", default="auto", choices=["auto", "spin", "poll"],
+                    help="how rank host threads wait for the GPU: spin (HIP synchronize), or poll (event "
+                         "query + sleep, at most 2 rounds queued ahead); auto = poll for N > 1 (N rank "
+                         "processes plus their RCCL proxy threads must not spin every CPU of the box)")
     ap.add_argument("--no-extras", action="store_true", help="skip the strong-scaling / fp16 / numerics extras")
     ap.add_argument("--no-system", action="store_true", help="skip phases 2-3 (system + failover)")
     ap.add_argument("--node-phases", default="system,failover,worker",
@@ -473,6 +477,13 @@ def main(argv=None) -> int:
         # before any RCCL communicator: a host id of this process's own (see --rehearse-rccl)
         os.environ["NCCL_HOSTID"] = f"idunno-rehearse-{os.getpid()}"
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    if (a.rehearse_rccl or a.rehearse_gloo) and role in ("rank", "node") and a.gpus > 4:
+        # before the HIP runtime starts: N rank processes on ONE GPU with HIP's 4 hardware
+        # queues each oversubscribe the card's queue slots, and the scheduler then
+        # time-slices queues while RCCL kernels spin waiting for peers (VERDICT r5 item 1:
+        # 8 ranks, gather 14.5 ms per round with 4 queues, 0.4 ms with 1,
+        # profiles/r6_rehearse_n8.md).  One GPU per rank never shares its queues.
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("IDUNNO_REHEARSE_HW_QUEUES", "1")
     if role == "rank":
         return run_rank(a)
     if role == "node":
@@ -546,8 +557,26 @@ def run_rank(a) -> int:
     # factor = world): any chunk of a query can be served by any rank
     D = max(a.dataset_images, (W + 1) * B)
 
+    poll = a.host_wait == "poll" or (a.host_wait == "auto" and W > 1)
+
+    def wait_ev(ev):
+        """The host waits for a recorded event: HIP's synchronize spins a CPU; the
+        poll mode sleeps between queries (N rank processes on a box whose CPU
+        share the RCCL proxy threads need too)."""
+        if ev is None:
+            return
+        if not poll:
+            ev.synchronize()
+            return
+        while not ev.query():
+            time.sleep(50e-6)
+
     def sync():
         if gpu:
+            if poll:
+                ev = torch.cuda.Event()
+                ev.record()
+                wait_ev(ev)
             torch.cuda.synchronize()
 
     def barrier():
@@ -646,7 +675,7 @@ def run_rank(a) -> int:
             print(f"bench: rank {env.rank} failing on purpose (--fail-rank)", file=sys.stderr, flush=True)
             os._exit(3)
 
-    def run_phases(step, drain, lat, steps, warmup, timing=None):
+    def run_phases(step, drain, lat, steps, warmup, timing=None, cpu_stats=None):
         """Warmup rounds, then EXACTLY ``steps`` timed rounds (each rank's own
         region between a drain + barrier on both sides; the slowest rank's
         counts), then >= 5 unloaded rounds one at a time for the p50 latency.
@@ -657,20 +686,27 @@ def run_rank(a) -> int:
         lat.clear()
         if timing is not None:
             timing[0] = True
+        cg0 = _cgroup_cpu() if coord else None
+        c_start = _proc_cpu_s()
         t_start = time.perf_counter()
         for q in range(warmup, warmup + steps):
             step(q, q + 1 < warmup + steps)
         drain()
         elapsed = time.perf_counter() - t_start
+        cpu = _proc_cpu_s() - c_start
+        cg1 = _cgroup_cpu() if coord else None
         if timing is not None:
             timing[0] = False
-        per_rank = [elapsed]
+        per_rank, cpu_rank = [elapsed], [cpu]
         if env.distributed:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
+            t = torch.tensor([elapsed, cpu], dtype=torch.float64, device=env.device)
             outs = [torch.zeros_like(t) for _ in range(W)]
             dist.all_gather(outs, t)
-            per_rank = [float(x.item()) for x in outs]
+            per_rank = [float(x[0].item()) for x in outs]
+            cpu_rank = [float(x[1].item()) for x in outs]
             elapsed = max(per_rank)
+        if cpu_stats is not None:
+            cpu_stats[:] = [cpu_rank, _cgroup_delta(cg0, cg1, elapsed)]
         p50_loaded = statistics.median(lat) if lat else None
         lat.clear()
         for q in range(warmup + steps, warmup + steps + max(5, min(steps, 20))):
@@ -696,15 +732,29 @@ def run_rank(a) -> int:
         lat, pending = [], []
         step, drain, gtimes, timing = (pipelined_round if pipelined else serial_round)(
             run, per_round, warmup, state, host, lat, pending)
-        elapsed, per_rank, p50_loaded, p50 = run_phases(step, drain, lat, steps, warmup, timing)
+        cpu_stats = []
+        elapsed, per_rank, p50_loaded, p50 = run_phases(step, drain, lat, steps, warmup, timing, cpu_stats)
         g_us = ([1000.0 * g0.elapsed_time(g1) for g0, g1 in gtimes] if gpu else [1e6 * x for x in gtimes]) \
             if gtimes else []
         recorded = state.images_done(a.model) if coord else None
         return {"elapsed": elapsed, "ips": per_round * steps / elapsed, "p50": p50, "p50_loaded": p50_loaded,
                 "recorded": recorded, "label": label,
                 "rank_ms": [1000.0 * x / steps for x in per_rank],
+                "cpu": cpu_stats,
                 "gather_us": statistics.median(g_us) if g_us else None,
                 "verified": verify(state, runner)}
+
+    ahead = {}      # poll mode: round -> event after its forward (the host queues <= 2 rounds ahead)
+
+    def throttle_before(q: int) -> None:
+        if poll and gpu:
+            wait_ev(ahead.pop(q - 2, None))
+
+    def mark_after(q: int) -> None:
+        if poll and gpu:
+            ev = torch.cuda.Event()
+            ev.record()
+            ahead[q] = ev
 
     def serial_round(run, per_round, warmup, state, host, lat, pending):
         """Round q: descriptor broadcast, forward, gather, one after another on
@@ -715,13 +765,13 @@ def run_rank(a) -> int:
 
         def ingest():
             ev, table, slot, t0 = pending.pop(0)
-            if ev is not None:
-                ev.synchronize()
+            wait_ev(ev)
             record_round(state, host[slot].numpy(), table, time.perf_counter())
             lat.append(time.perf_counter() - t0)
 
         def step(q: int, nxt: bool):
             t0 = time.perf_counter()
+            throttle_before(q)
             table = None
             if coord:
                 chunks, table = table_of(q, per_round)
@@ -741,6 +791,7 @@ def run_rank(a) -> int:
                 gtimes.append(time.perf_counter() - g0)
             else:
                 plane.gather(None, None)
+            mark_after(q)
             if coord:
                 slot = q % 2
                 host[slot].copy_(plane.gathered_all, non_blocking=gpu)
@@ -756,6 +807,7 @@ def run_rank(a) -> int:
             if coord:
                 while pending:
                     ingest()
+            ahead.clear()
             barrier()
         return step, drain, gtimes, timing
 
@@ -772,8 +824,7 @@ def run_rank(a) -> int:
 
         def ingest():
             ev, q = pending.pop(0)
-            if ev is not None:
-                ev.synchronize()
+            wait_ev(ev)
             record_round(state, host[q % 2].numpy(), tables.pop(q)[1], time.perf_counter())
             lat.append(time.perf_counter() - t0s.pop(q))
 
@@ -795,6 +846,7 @@ def run_rank(a) -> int:
 
         def step(q: int, nxt: bool):
             t0s[q] = time.perf_counter()
+            throttle_before(q)
             if q not in posted:
                 post(q)
             if coord:
@@ -808,6 +860,7 @@ def run_rank(a) -> int:
             if gathers:
                 finish_gather()      # round q-1's gather ran under round q's forward
             gathers.append((q, plane.post_gather(q % 2)))
+            mark_after(q)
 
         def drain():
             while gathers:
@@ -815,6 +868,7 @@ def run_rank(a) -> int:
             if coord:
                 while pending:
                     ingest()
+            ahead.clear()
             barrier()
         return step, drain, [], None
 
@@ -970,6 +1024,58 @@ def run_rank(a) -> int:
 
 
 
+def _proc_cpu_s() -> float:
+    """CPU seconds of this process, every thread (RCCL proxy, watchdog) included."""
+    import resource
+
+    r = resource.getrusage(resource.RUSAGE_SELF)
+    return r.ru_utime + r.ru_stime
+
+
+def _cgroup_cpu() -> dict | None:
+    """cgroup v2 CPU accounting of the container (every rank of this box):
+    usage and CFS-quota throttling counters, plus the quota itself."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            st = {k: int(v) for k, v in (ln.split() for ln in f if ln.strip())}
+    except (OSError, ValueError):
+        return None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        st["quota_cpus"] = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        st["quota_cpus"] = None
+    return st
+
+
+def _cgroup_delta(c0, c1, wall: float) -> dict:
+    if not c0 or not c1:
+        return {}
+    d = {"cgroup_cpus_used": round((c1.get("usage_usec", 0) - c0.get("usage_usec", 0)) / 1e6 / wall, 2),
+         "cgroup_quota_cpus": c1.get("quota_cpus")}
+    if "nr_throttled" in c1:
+        d["cgroup_throttled_periods"] = c1["nr_throttled"] - c0.get("nr_throttled", 0)
+        d["cgroup_throttled_ms"] = round((c1.get("throttled_usec", 0) - c0.get("throttled_usec", 0)) / 1e3, 1)
+    return d
+
+
+def _cpu_keys(head: dict, a) -> dict:
+    """Host CPU use of the timed headline region: every rank process's CPU
+    seconds per wall second (summed), and the container cgroup's usage and
+    quota throttling.  At N ranks on ONE box (rehearsals) the ranks and their
+    RCCL proxy threads share the box's CPU share."""
+    st = head.get("cpu") or []
+    if not st:
+        return {}
+    cpu_rank, cg = st
+    wall = head["elapsed"]
+    mode = a.host_wait if a.host_wait != "auto" else ("poll" if a.gpus > 1 else "spin")
+    hwq = os.environ.get("GPU_MAX_HW_QUEUES")
+    return {"host_wait": mode, **({"gpu_max_hw_queues": int(hwq)} if hwq and hwq.isdigit() else {}), "host_cpus_used_by_ranks": round(sum(cpu_rank) / wall, 2),
+            "host_cpu_per_rank_max": round(max(cpu_rank) / wall, 2), **cg}
+
+
 def headline_line(a, W, B, head, extras, runner, env, dist, serial) -> dict:
     """The bench line (rank 0) from the headline measurement and the extras so far."""
     import torch
@@ -1011,6 +1117,7 @@ def headline_line(a, W, B, head, extras, runner, env, dist, serial) -> dict:
         "ms_per_step_rank_max": round(max(head["rank_ms"]), 4),
         "gather_us_per_round": (round(serial["gather_us"], 1) if serial and serial["gather_us"] is not None else
                                 round(head["gather_us"], 1) if head["gather_us"] is not None else None),
+        **_cpu_keys(head, a),
         **extras,
     }
     if runner is not None:

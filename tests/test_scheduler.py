@@ -59,9 +59,9 @@ def test_partition_budget_below_model_count():
 
 
 def test_subsets_fixed_under_ema_jitter():
-    """While the same two jobs run on the same workers the split never moves,
-    whatever the EMA does; it is recomputed when a job starts / ends, a worker
-    dies, or a model gets its first measurement."""
+    """Between query boundaries the split never moves, whatever the EMA does;
+    it is recomputed when a job starts / ends or a worker dies, and re-planned
+    at a query boundary."""
     import random
 
     s = FairTimeScheduler(budget=8, seed=0)
@@ -69,9 +69,10 @@ def test_subsets_fixed_under_ema_jitter():
     both = {"alexnet", "resnet18"}
     first = s.subsets(both, ws)                       # no measurements: equal split
     assert [len(first["alexnet"]), len(first["resnet18"])] == [4, 4]
-    s.observe("alexnet", 3.0)                         # first measurements: recompute once
+    s.observe("alexnet", 3.0)                         # first measurements: the next boundary re-plans
     s.observe("resnet18", 5.0)
-    p0 = s.subsets(both, ws)
+    assert s.subsets(both, ws) == first
+    p0 = s.subsets(both, ws, boundary=True)
     assert (len(p0["alexnet"]), len(p0["resnet18"])) == (3, 5)      # slower model gets more
     assert set(p0["alexnet"]).isdisjoint(p0["resnet18"])
     rng = random.Random(7)
@@ -98,10 +99,11 @@ def test_adopted_averages_count_as_measurements():
     assert (len(p["alexnet"]), len(p["resnet18"])) == (2, 6)
 
 
-def test_split_follows_ema_only_at_drained_boundaries():
-    """with fake EMA drift, the fair-time split moves (5/5 ->
-    4/6 like report Fig 2) only at a query boundary where nothing is in flight,
-    and the two jobs' subsets never overlap -- before, at, or after the move."""
+def test_split_follows_ema_only_at_query_boundaries():
+    """with fake EMA drift, the fair-time split
+    moves (5/5 -> 4/6 like report Fig 2) only at a query boundary (a job's next
+    query being planned; ``drained`` is the old keyword), and the two jobs'
+    subsets never overlap -- before, at, or after the move."""
     s = FairTimeScheduler(budget=10, seed=0)
     ws = [f"rank{i}" for i in range(10)]
     both = {"alexnet", "resnet18"}
@@ -138,3 +140,54 @@ def test_split_follows_ema_only_at_drained_boundaries():
     p2 = s.assign("alexnet", 0, 399, ws, drained=True)
     assert len(p2) == 5 and s.repartitions == 2
 
+
+
+def test_chunk_time_fit_is_independent_of_the_split():
+    """chunks of one model cut 3 or 5 ways have different
+    per-image times (fixed cost per chunk); the fitted full-query time must be
+    the same whichever way the queries were cut."""
+    from idunno.runtime.scheduler import ChunkTimeFit
+
+    a, b, B = 0.002, 0.0001, 400           # 2 ms per chunk + 0.1 ms per image
+    f = ChunkTimeFit()
+    for n in (133, 134, 133):
+        f.add(n, a + b * n)
+    per_image_only = f.full(B)             # one chunk size: per-image fallback, includes a's share
+    assert abs(per_image_only / ((a / 133 + b) * B) - 1) < 1e-3
+    for n in (80, 80, 80, 133, 80):
+        f.add(n, a + b * n)
+    assert abs(f.full(B) - (a + b * B)) < 1e-6
+    # a per-image time that changed together with the chunk size is not a fixed cost
+    g = ChunkTimeFit()
+    for _ in range(5):
+        g.add(167, 167 * 100e-6)
+    for _ in range(2):
+        g.add(100, 100 * 160e-6)
+    assert g.full(500) > 500 * 100e-6      # never below the old regime's per-image time
+
+
+def test_boundary_hand_over_waits_for_the_donors_chunks():
+    """A worker moving between jobs joins the receiver only once the donor's
+    chunks on it are done; meanwhile it is in neither subset."""
+    s = FairTimeScheduler(budget=8, seed=0)
+    ws = [f"r{i}" for i in range(8)]
+    both = {"alexnet", "resnet18"}
+    s.adopt({"alexnet": 1.0, "resnet18": 1.0})
+    p0 = s.subsets(both, ws)
+    assert (len(p0["alexnet"]), len(p0["resnet18"])) == (4, 4)
+    s.adopt({"alexnet": 1.0, "resnet18": 3.0})         # exact share 2 / 6
+    busy = {w: {"alexnet"} for w in p0["alexnet"]}
+    p1 = s.subsets(both, ws, boundary=True, busy=busy)
+    assert len(p1["alexnet"]) == 2 and len(p1["resnet18"]) == 4     # two workers in hand-over
+    assert s.moves_deferred == 2
+    left = set(ws) - set(p1["alexnet"]) - set(p1["resnet18"])
+    assert left <= set(p0["alexnet"]) and len(left) == 2
+    # still busy with alexnet: nothing moves; once free they join resnet18
+    assert s.subsets(both, ws, boundary=True, busy=busy) == p1
+    p2 = s.subsets(both, ws, boundary=True, busy={w: {"alexnet"} for w in p1["alexnet"]})
+    assert len(p2["alexnet"]) == 2 and len(p2["resnet18"]) == 6 and left <= set(p2["resnet18"])
+    assert set(p2["alexnet"]).isdisjoint(p2["resnet18"])
+    # busy=None (round path): hand over at once
+    s.adopt({"alexnet": 3.0, "resnet18": 1.0})
+    p3 = s.subsets(both, ws, boundary=True)
+    assert (len(p3["alexnet"]), len(p3["resnet18"])) == (6, 2)
