@@ -482,7 +482,7 @@ _CAPTURE_LOCK = threading.Lock()
 
 
 @contextlib.contextmanager
-def _capture_nosync(g, device):
+def _capture_nosync(g, device, pool=None):
     """``torch.cuda.graph(g, capture_error_mode="thread_local")`` without the
     device-wide synchronize (and gc / empty_cache) that context manager does
     first: a runtime that captures a graph for a new send slot while an RCCL
@@ -494,7 +494,7 @@ def _capture_nosync(g, device):
     s = torch.cuda.Stream(device=device)
     s.wait_stream(torch.cuda.current_stream(device))
     with torch.cuda.stream(s):
-        g.capture_begin(capture_error_mode="thread_local")
+        g.capture_begin(pool=pool, capture_error_mode="thread_local")
         try:
             yield
         finally:
@@ -582,6 +582,13 @@ class HipRunner:
         self.device = torch.device(device or "cuda")
         self.p = program.to(self.device)
         self._graphs: dict[int, tuple] = {}
+        # memory pool shared by this runner's captures (None: one private pool per
+        # graph).  Sharing is safe only where every replay is stream-ordered on ONE
+        # stream and a graph's outputs are consumed before another graph of the
+        # pool replays (its intermediates may reuse their memory): HipExecutor
+        # sets it (one private stream, outputs copied out or written to the
+        # caller's buffer in the same stream order)
+        self.graph_pool = None
         # split range guard: the split kernels set this flag
         # when an activation leaves fp16's range (|v| >= 65504 has no finite hi
         # half); softmax_top1 then marks the batch (class -2) and the eager
@@ -1155,7 +1162,7 @@ class HipRunner:
             g = torch.cuda.CUDAGraph()
             self._capturing = True
             try:
-                with _capture_nosync(g, self.device):
+                with _capture_nosync(g, self.device, self.graph_pool):
                     sout = self.forward(shard, start, batch, start_offset, packed)
             finally:
                 self._capturing = False
@@ -1219,7 +1226,7 @@ class HipRunner:
             g = torch.cuda.CUDAGraph()
             self._capturing = True
             try:
-                with _capture_nosync(g, self.device):
+                with _capture_nosync(g, self.device, self.graph_pool):
                     sout = self.forward(sin, packed=packed)
             finally:
                 self._capturing = False

@@ -141,6 +141,7 @@ class HipExecutor(Executor):
         self.max_graphs = max_graphs
         self._HipRunner, self._build = HipRunner, build_program
         self.runners: dict[str, object] = {}
+        self._pool = None
         self.lock = threading.Lock()
         self.run_lock = threading.Lock()      # one forward (copy-in, replay, read-back) at a time
         self.stream = None      # private HIP stream: nodes sharing a GPU overlap
@@ -160,6 +161,15 @@ class HipExecutor(Executor):
                 with torch.cuda.device(self.device):
                     r = self._HipRunner(self._build(name, seed=self.seed, dtype=self.dtype), self.device)
                     r.split = self.fp32_impl == "split"
+                    # every graph of this executor replays on its one private stream and
+                    # its outputs are read (D2H / the caller's packed buffer) before the
+                    # next replay: one memory pool for all of them, so graph memory is
+                    # the largest graph's, not the sum over chunk sizes (8 node
+                    # processes sharing one GPU ran out of its 288 GB with a pool per
+                    # graph once the fair-time split re-planned chunk sizes, round 6)
+                    if self._pool is None:
+                        self._pool = torch.cuda.graph_pool_handle()
+                    r.graph_pool = self._pool
                 self.runners[name] = r
         return r
 

@@ -291,20 +291,30 @@ class JobState:
 
     def _assign_locked(self, model, qnum, chunks, now, emit: bool) -> None:
         key = (model, qnum)
-        chunks = [(w, int(s), int(e)) for w, s, e in chunks]
         self.query_submit_time.setdefault(key, now)
         ents = self.worker_set[key]
+        done, vms = self._done_keys, self.working_vm_set
+        log, n_open = [], 0
+        lo = hi = None
         for w, s, e in chunks:
-            if (model, qnum, s, e) in self._done_keys:      # mirror: result already held
+            s, e = int(s), int(e)
+            log.append([w, s, e])
+            lo = s if lo is None or s < lo else lo
+            hi = e if hi is None or e > hi else hi
+            if (model, qnum, s, e) in done:                # mirror: result already held
                 ents.append((w, s, e, "f", now, now))
                 continue
             ents.append((w, s, e, "w", now, now))
-            self.working_vm_set[w].append((model, qnum, s, e))
-            self._open_add(key, 1)
+            vms[w].append((model, qnum, s, e))
+            n_open += 1
+        if n_open:
+            self._open_add(key, n_open)
         if ents:
-            self._spans.add((model, min(x[1] for x in ents), max(x[2] for x in ents)))
+            if len(ents) > len(log):                       # earlier entries of this query too
+                lo, hi = min(x[1] for x in ents), max(x[2] for x in ents)
+            self._spans.add((model, lo, hi))
         if emit:
-            self._bump("assign", model, qnum, [list(c) for c in chunks], now)
+            self._bump("assign", model, qnum, log, now)
 
     def record_result(self, model: str, qnum, worker: str, start: int, end: int, cls, prob,
                       now: float | None = None) -> bool:
@@ -393,32 +403,34 @@ class JobState:
         pos = {(x[0], x[1], x[2]): i for i, x in enumerate(ents) if x[3] == "w"}
         bsz = self.batchsize.get(model)             # None: per-chunk time, as record_result
         tot = 0
-        res = self.results[f"{model} {qnum}"]
+        res_append = self.results[f"{model} {qnum}"].append
         chunks = []
         vms = self.working_vm_set
-        done = self._done_keys
-        pw = self._ptime_win[model]
+        done_add = self._done_keys.add
+        pw_append = self._ptime_win[model].append
+        i32, f32, nd = np.int32, np.float32, np.ndarray
         for _, _, w, s, e, c, p in recs:
-            s, e = int(s), int(e)
             i = pos[(w, s, e)]
             t_start = ents[i][4]
             ents[i] = (w, s, e, "f", t_start, now)
+            ck = (model, qnum, s, e)
             vm = vms.get(w)
             if vm is not None:
-                try:
-                    vm.remove((model, qnum, s, e))
-                except ValueError:
-                    pass
+                if vm and vm[0] == ck:                  # the usual case: the worker's oldest chunk
+                    del vm[0]
+                else:
+                    try:
+                        vm.remove(ck)
+                    except ValueError:
+                        pass
                 if not vm:
                     del vms[w]
-            done.add((model, qnum, s, e))
+            done_add(ck)
             n = e - s + 1
             tot += n
-            pw.append((now, (now - t_start) / n * (n if bsz is None else bsz)))
-            res.append(ChunkResult(s, e, c if type(c) is np.ndarray and c.dtype == np.int32 else
-                                   np.asarray(c, dtype=np.int32),
-                                   p if type(p) is np.ndarray and p.dtype == np.float32 else
-                                   np.asarray(p, dtype=np.float32), w))
+            pw_append((now, (now - t_start) * (1.0 if bsz is None else bsz / n)))
+            res_append(ChunkResult(s, e, c if type(c) is nd and c.dtype == i32 else np.asarray(c, dtype=i32),
+                                   p if type(p) is nd and p.dtype == f32 else np.asarray(p, dtype=f32), w))
             chunks.append([s, e])
         self._open_add(key, -len(recs))
         # the round's chunks are usually one contiguous range: merge them first, then

@@ -46,6 +46,7 @@ collective posted, so no RCCL kernel spins on an idle GPU.
 """
 from __future__ import annotations
 
+import gc
 import logging
 import os
 import threading
@@ -80,6 +81,7 @@ class RoundPlane:
     HDR_RING = 4        # pinned header buffers (> depth: a slot is rewritten only after its gather)
     CHECK_PERIOD_S = 0.002   # liveness re-check period inside a coordinator's poll loops
     ANNOUNCE_ROUNDS = 4      # rounds whose descriptors share one multicast frame (backlog only)
+    GC_FREEZE_ROUNDS = 256   # coordinator: gc.freeze() every this many ingested rounds
 
     def __init__(self, node, device):
         self.node = node
@@ -697,10 +699,14 @@ class RoundPlane:
         # every member's reported (warm) chunk is one (size, seconds) point of its
         # model's chunk-time line; the scheduler's average is that line's full-query
         # time, which does not move with how the split cut the queries
+        obs = {}
         for us, hmid, cnt, _ in hdr:
-            if cnt > 0 and us > 0 and hmid in MODEL_NAMES:
-                model = MODEL_NAMES[hmid]
-                n.sched.observe_chunk(model, cnt, us * 1e-6, self.cfg.batch_for(model))
+            if cnt > 0 and us > 0:
+                obs.setdefault(hmid, []).append((cnt, us * 1e-6))
+        for hmid, pts in obs.items():
+            model = MODEL_NAMES.get(hmid)
+            if model is not None:
+                n.sched.observe_chunks(model, pts, self.cfg.batch_for(model))
         for i, row in enumerate(r.table):
             if row is None:
                 continue
@@ -717,6 +723,12 @@ class RoundPlane:
             recs.append((MODEL_NAMES[mid], qnum, members[i], s, e, cls, prob))
         n._ingest_round(recs, now, seq=r.seq)
         self.rounds_done += 1
+        if self.rounds_done % self.GC_FREEZE_ROUNDS == 0:
+            # the job-state tables grow by a few objects per chunk and hold no cycles:
+            # move everything allocated so far out of the cyclic collector's reach, so
+            # its periodic full passes stop re-walking the whole history (-30 % host
+            # time per 8-member round, tools/hostcost_probe.py)
+            gc.freeze()
         sb = g.standby_rank
         if sb > 0:
             g.release(r.work, check)        # the standby's gather of this slot too, before reuse

@@ -131,10 +131,13 @@ class ChunkTimeFit:
         self.w = self.sn = self.st = self.snn = self.snt = 0.0
         self.nmin = self.nmax = None
 
-    def add(self, n: int, t: float) -> None:
-        k = 1.0 - self.forget
-        self.w, self.sn, self.st = k * self.w + 1.0, k * self.sn + n, k * self.st + t
-        self.snn, self.snt = k * self.snn + n * n, k * self.snt + n * t
+    def add(self, n: int, t: float, w: float = 1.0) -> None:
+        """One point (n images, t seconds) of weight ``w``: w equal points at once
+        (one round's members with the same chunk size) forget the past as w
+        separate adds would."""
+        k = (1.0 - self.forget) ** w
+        self.w, self.sn, self.st = k * self.w + w, k * self.sn + w * n, k * self.st + w * t
+        self.snn, self.snt = k * self.snn + w * n * n, k * self.snt + w * n * t
 
     def full(self, B: int) -> float | None:
         if self.w <= 0:
@@ -280,6 +283,22 @@ class FairTimeScheduler:
         else:
             old = self.avg_time[model]
             self.avg_time[model] = (1 - self.ema) * old + self.ema * float(normalized_query_time)
+
+    def observe_chunks(self, model: str, points, batch: int) -> None:
+        """``observe_chunk`` for several (n, seconds) points of one model (one
+        collective round's members), with one refit."""
+        fit = self._fits.setdefault(model, ChunkTimeFit())
+        by_n = {}
+        for n, sec in points:
+            if n > 0 and sec > 0:
+                a = by_n.get(n)
+                by_n[n] = (sec, 1) if a is None else (a[0] + sec, a[1] + 1)
+        for n, (tot, c) in by_n.items():          # equal chunk sizes: their mean, weighted
+            fit.add(int(n), tot / c, c)
+        t = fit.full(int(batch))
+        if t is not None:
+            self.avg_time[model] = t
+            self._seen.add(model)
 
     def observe_chunk(self, model: str, n: int, seconds: float, batch: int) -> None:
         """One warm chunk of ``n`` images took ``seconds`` of compute: refit the

@@ -997,6 +997,14 @@ def run_rank(a) -> int:
                 extras.update(numerics_check(runner, a, env.device))
             progress("numerics checked")
             emit()
+        if not a.dry_run and W == 1 and a.model == "resnet18" and a.dtype == "fp32" and budget_left("b50"):
+            extras.update(b50_extra(a, env, runner, dataset))
+            progress("b50 forward measured")
+            emit()
+        if not a.dry_run and W == 1 and a.model == "resnet18" and budget_left("alexnet"):
+            extras.update(alexnet_extra(a, env))
+            progress("alexnet measured")
+            emit()
         if not a.dry_run and W == 1 and a.model == "resnet18" and budget_left("resnet50"):
             extras.update(resnet50_extra(a, env, make_run))
             progress("resnet50 measured")
@@ -1127,10 +1135,10 @@ def headline_line(a, W, B, head, extras, runner, env, dist, serial) -> dict:
     return out
 
 
-def resnet50_extra(a, env, make_run) -> dict:
-    """BASELINE config 5 (ResNet50 bs=1024 fp16) as extra keys of the default line:
-    the same round loop (descriptor, hipGraph replay of the forward, top-1 to
-    the host, job-state ingest) at 1024 images per step on this GPU."""
+def _round_extra(a, env, model: str, batch: int, dtype: str, split: bool, model_id: int, seed_off: int):
+    """One model's round loop on this GPU (descriptor, hipGraph replay of the
+    forward, top-1 to the host, job-state ingest) at ``batch`` images per step:
+    (images/s, ms per step, results recorded)."""
     import torch
 
     from idunno import ops
@@ -1138,22 +1146,22 @@ def resnet50_extra(a, env, make_run) -> dict:
     from idunno.parallel.dataplane import QueryPlane
     from idunno.runtime.jobstate import JobState
 
-    B5 = 1024
-    ds = ops.synth_images(a.seed + 99, 0, 2 * B5, env.device)
-    r5 = HipRunner(build_program("resnet50", seed=a.seed, dtype="fp16"), env.device)
-    plane = QueryPlane(env, coordinator=0, max_chunk=B5, nbuf=1)
-    _, run = r5.capture_window(ds, B5, start=plane.row_start(), start_offset=0, packed=plane.send_buffer)
+    ds = ops.synth_images(a.seed + seed_off, 0, 2 * batch, env.device)
+    r = HipRunner(build_program(model, seed=a.seed, dtype=dtype), env.device)
+    r.split = split
+    plane = QueryPlane(env, coordinator=0, max_chunk=batch, nbuf=1)
+    _, run = r.capture_window(ds, batch, start=plane.row_start(), start_offset=0, packed=plane.send_buffer)
     state = JobState()
-    host = torch.empty(1, B5, 2, dtype=torch.int32, pin_memory=True)
+    host = torch.empty(1, batch, 2, dtype=torch.int32, pin_memory=True)
 
     def step(q):
-        off = (q % 2) * B5
-        state.assign("resnet50", q, [("rank0", off, off + B5 - 1)], time.perf_counter())
-        plane.dispatch_device([(2, q, off, off + B5 - 1)], slot=q)
+        off = (q % 2) * batch
+        state.assign(model, q, [("rank0", off, off + batch - 1)], time.perf_counter())
+        plane.dispatch_device([(model_id, q, off, off + batch - 1)], slot=q)
         run()
         plane.gather(None, None)
         host.copy_(plane.gathered_all)
-        state.record_result("resnet50", q, "rank0", off, off + B5 - 1, host[0, :, 0].numpy().copy(),
+        state.record_result(model, q, "rank0", off, off + batch - 1, host[0, :, 0].numpy().copy(),
                             host[0, :, 1].view(torch.float32).numpy().copy(), time.perf_counter())
 
     steps = max(5, min(a.steps, 20))
@@ -1165,8 +1173,51 @@ def resnet50_extra(a, env, make_run) -> dict:
         step(q)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    return {"value_resnet50_fp16": round(B5 * steps / el, 2), "ms_per_step_resnet50_fp16": round(1000 * el / steps, 4),
-            "resnet50_batch": B5, "resnet50_results_recorded": state.images_done("resnet50")}
+    recorded = state.images_done(model)
+    r.close()
+    return batch * steps / el, 1000 * el / steps, recorded
+
+
+def resnet50_extra(a, env, make_run) -> dict:
+    """BASELINE config 5 (ResNet50 bs=1024 fp16) as extra keys of the default line."""
+    ips, ms, rec = _round_extra(a, env, "resnet50", 1024, "fp16", False, 2, 99)
+    return {"value_resnet50_fp16": round(ips, 2), "ms_per_step_resnet50_fp16": round(ms, 4),
+            "resnet50_batch": 1024, "resnet50_results_recorded": rec}
+
+
+def alexnet_extra(a, env) -> dict:
+    """BASELINE config 3's other job (AlexNet, 500-image queries, report p.1) at the
+    headline's precision: fp32 via split fp16 (reference alexnet_resnet.py:17-18)."""
+    ips, ms, rec = _round_extra(a, env, "alexnet", QUERY_ALEXNET, "fp32", True, 0, 77)
+    return {"value_alexnet_b500": round(ips, 2), "ms_per_step_alexnet_b500": round(ms, 4),
+            "alexnet_precision": "fp32 (split fp16)", "alexnet_results_recorded": rec}
+
+
+def b50_extra(a, env, runner, dataset) -> dict:
+    """The per-GPU compute of the north-star strong-scaling query: one 400-image
+    ResNet18 query over 8 GPUs is a 50-image forward per GPU (reference
+    mp4_machinelearning.py:523-536 chunks a query over its workers).  The
+    headline runner's split-fp32 hipGraph at B=50, replayed back to back
+    between two events (the graph reads its window start on the device)."""
+    import torch
+
+    Bs = 50
+    st = torch.zeros(1, dtype=torch.int64, device=env.device)
+    buf = torch.zeros(Bs, 2, dtype=torch.int32, device=env.device)
+    _, run = runner.capture_window(dataset, Bs, start=st, start_offset=0, packed=buf)
+    for _ in range(5):
+        run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    iters = 200
+    e0.record()
+    for _ in range(iters):
+        run()
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    return {"ms_per_forward_b50": round(ms, 4), "images_per_s_b50": round(Bs / ms * 1e3, 1),
+            "b50_precision": "fp32 (split fp16)" if runner.split else "fp32 (f32 MFMA)"}
 
 # ---------------------------------------------------------------------------
 # phases 2-3: one node process of the fault-tolerant runtime
@@ -1317,11 +1368,11 @@ def _drive_system(a, node, W: int, B: int) -> dict:
     per_q = W * B
     nxt = [0]
 
-    def submit(k):
+    def submit(k, size=per_q):
         for _ in range(k):
             s0 = nxt[0]
-            nxt[0] += per_q
-            cl.submit(a.model, s0, s0 + per_q - 1)
+            nxt[0] += size
+            cl.submit(a.model, s0, s0 + size - 1)
 
     def wait_done(target, timeout=300):
         # block on the coordinator's progress condition (notified per ingested round)
@@ -1384,6 +1435,24 @@ def _drive_system(a, node, W: int, B: int) -> dict:
             if d:
                 out[f"system_{nm.replace('.', '_')}_ms"] = round(1000 * statistics.mean(d), 4)
         out["system_host_send_ms_per_round"] = round(1000 * (rb["host_send_s"] - ra["host_send_s"]) / nr, 4)
+
+    # strong scaling (the north star's p50): ONE 400-image query split over the W
+    # members, one at a time (p50), then `steps` of them queued at once (images/s);
+    # two untimed queries first capture the graphs of the chunk size
+    submit(2, QUERY)
+    assert wait_done(nxt[0])
+    ls0 = len(st.query_latency[a.model])
+    for _ in range(max(5, min(a.steps, 20))):
+        submit(1, QUERY)
+        assert wait_done(nxt[0])
+    strong = sorted(st.query_latency[a.model][ls0:])
+    t0 = time.perf_counter()
+    submit(a.steps, QUERY)
+    assert wait_done(nxt[0]), st.summary()
+    el_strong = time.perf_counter() - t0
+    out.update({"p50_system_strong_s": round(strong[len(strong) // 2], 6),
+                "images_per_s_system_strong": round(QUERY * a.steps / el_strong, 2),
+                "system_strong_chunk_per_gpu": -(-QUERY // W)})
 
     if W == 1 and a.sdfs_images > 0:
         out.update(_sdfs_pass(a, node, per_q))

@@ -78,19 +78,26 @@ def test_split_follows_averages_while_both_jobs_run():
             time.sleep(0.01)
         before = (_sizes(coord.state, "alexnet"), _sizes(coord.state, "resnet18"))
         per_image.update(alexnet=160e-6, resnet18=100e-6)
+        # the split planned while BOTH jobs still run (at the very end one job is
+        # alone and takes every GPU, as it should)
+        while coord.state.images_done("alexnet") < 500 * Q * 85 // 100 and time.monotonic() < deadline:
+            time.sleep(0.01)
+        both_running = coord.state.active_models() == {"alexnet", "resnet18"}
+        after = (_sizes(coord.state, "alexnet"), _sizes(coord.state, "resnet18"))
         s = cl.wait_idle(90, {"alexnet": 500 * Q, "resnet18": 400 * Q})
         stop.set()
         th.join(2)
         assert s["done"]["alexnet"] == 500 * Q and s["done"]["resnet18"] == 400 * Q, s
-        a_all, r_all = _sizes(coord.state, "alexnet"), _sizes(coord.state, "resnet18")
         a0, r0 = before
-        print("alexnet split per query:", a_all)
-        print("resnet18 split per query:", r_all)
+        a_all, r_all = after
+        print("alexnet split per query:", _sizes(coord.state, "alexnet"))
+        print("resnet18 split per query:", _sizes(coord.state, "resnet18"))
         print("averages:", coord.sched.avg_time, "re-splits:", coord.sched.repartitions,
               "deferred hand-overs:", coord.sched.moves_deferred)
         # converged to the reference rule's 3 / 5 before the flip ...
         assert a0[-3:] == [3, 3, 3] and r0[-3:] == [5, 5, 5], (a0, r0)
         # ... and to 5 / 3 after it, within a few queries
+        assert both_running
         assert a_all[-3:] == [5, 5, 5] and r_all[-3:] == [3, 3, 3], (a_all, r_all)
         assert coord.sched.repartitions >= 2
         assert not overlaps, overlaps[:5]
