@@ -14,6 +14,7 @@ All return ``(cls int32 [n], prob float32 [n])`` numpy arrays.
 """
 from __future__ import annotations
 
+import logging
 import threading
 import time
 
@@ -22,6 +23,8 @@ import torch
 
 from ..models import reference as ref
 from .data import is_resident
+
+log = logging.getLogger("idunno.executor")
 
 
 class Done:
@@ -142,6 +145,7 @@ class HipExecutor(Executor):
         self._HipRunner, self._build = HipRunner, build_program
         self.runners: dict[str, object] = {}
         self._pool = None
+        self.graphs_broken = False      # a capture failed: eager forwards only (see _capture)
         self.lock = threading.Lock()
         self.run_lock = threading.Lock()      # one forward (copy-in, replay, read-back) at a time
         self.stream = None      # private HIP stream: nodes sharing a GPU overlap
@@ -178,16 +182,44 @@ class HipExecutor(Executor):
             with torch.cuda.device(self.device), self.run_lock:
                 self.runner(model).capture(batch)
 
+    def _can_capture(self, r) -> bool:
+        return not self.closed and self.use_graphs and not self.graphs_broken and len(r._graphs) < self.max_graphs
+
+    def _capture(self, r, fn):
+        """Run a graph lookup / capture ``fn``.  A NEW capture is followed by
+        ``empty_cache``: its eager warm-up forwards left activation blocks of
+        that chunk size cached outside the graph pool, and with chunk sizes that
+        move with the fair-time split those blocks pile up (8 node processes on
+        one GPU: 20 GB reserved-but-unused each).  A capture that fails (e.g.
+        out of memory) leaves the pool it recorded into unusable: the runners
+        get a fresh pool, no further graphs are captured and the caller runs
+        the chunk eagerly (returns None)."""
+        before = len(r._graphs)
+        try:
+            out = fn()
+        except (RuntimeError, torch.cuda.OutOfMemoryError) as e:   # includes AcceleratorError
+            log.warning("graph capture failed (%s); eager forwards from now on", e)
+            self.graphs_broken = True
+            with self.lock:
+                self._pool = torch.cuda.graph_pool_handle()
+                for rr in self.runners.values():
+                    rr.graph_pool = self._pool
+            return None
+        if len(r._graphs) > before:
+            torch.cuda.empty_cache()
+        return out
+
     def _forward(self, r, images, packed, slot: int = 0):
         """cls, prob of ``images`` on the private stream (caller holds run_lock);
         with ``packed`` the (class, prob bits) pairs are also written there.
         Launch slot ``slot`` replays its own graph (own static buffers)."""
         n = images.shape[0]
-        if not self.closed and packed is None and \
-                ((self.use_graphs and len(r._graphs) < self.max_graphs) or r.has_graph(n, slot=slot)):
-            sin, replay = r.capture(n, slot=slot)
-            sin.copy_(images)
-            return replay()
+        if not self.closed and packed is None and (self._can_capture(r) or r.has_graph(n, slot=slot)):
+            got = self._capture(r, lambda: r.capture(n, slot=slot))
+            if got is not None:
+                sin, replay = got
+                sin.copy_(images)
+                return replay()
         return r.forward(images.contiguous(), packed=packed)
 
     def _enter(self, images):
@@ -270,22 +302,29 @@ class HipExecutor(Executor):
                       and tuple(base.shape[1:]) == tuple(images.shape[1:]))
             with torch.cuda.stream(s):
                 ev0.record(s)
-                can_graph = not self.closed and self.use_graphs and len(r._graphs) < self.max_graphs
+                can_graph = self._can_capture(r)
+                done = False
                 if window and (can_graph or r.has_window(base, n, packed=packed)):
                     if can_graph and not r.has_graph(n, packed=packed):
                         # the static-input form for this slot as well, now (warm-up
                         # rounds): a later non-resident view (an SDFS shard) must not
                         # capture it inside a timed or serving round
-                        r.capture(n, packed=packed)
+                        self._capture(r, lambda: r.capture(n, packed=packed))
                     per = images[0].numel() * images.element_size()
-                    start, replay = r.capture_window(base, n, packed=packed)
-                    start.fill_((images.data_ptr() - base.data_ptr()) // per)
-                    replay()
+                    got = self._capture(r, lambda: r.capture_window(base, n, packed=packed))
+                    if got is not None:
+                        start, replay = got
+                        start.fill_((images.data_ptr() - base.data_ptr()) // per)
+                        replay()
+                        done = True
                 elif can_graph or (not self.closed and r.has_graph(n, packed=packed)):
-                    sin, replay = r.capture(n, packed=packed)
-                    sin.copy_(images)
-                    replay()
-                else:
+                    got = self._capture(r, lambda: r.capture(n, packed=packed))
+                    if got is not None:
+                        sin, replay = got
+                        sin.copy_(images)
+                        replay()
+                        done = True
+                if not done:
                     r.forward(images.contiguous(), packed=packed)
                 ev1.record(s)
             torch.cuda.current_stream(self.device).wait_stream(s)
