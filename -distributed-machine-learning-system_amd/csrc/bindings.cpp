@@ -48,6 +48,9 @@ static torch::Tensor zero_buffer(const torch::Device& dev) {
 constexpr int kRouteNoBand = 1;      // no band-staged 3x3 kernel (tile 70)
 constexpr int kRouteNoC64 = 2;       // no row-streaming 3x3 64->64 kernels (tile 50)
 constexpr int kRouteNoStream1x1 = 4; // no streaming 1x1 kernels (tile 80)
+constexpr int kRouteC64TwoPerCU = 16;  // row-streaming 64->64 kernel: always two workgroups per CU (A/B arm)
+constexpr int kRouteLegacySmallM = 8; // split convs: round-5 small-M rules (streaming 1x1 at every M, split-K
+                                      // up to two blocks per CU) -- the A/B arm of the round-6 rules
 
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
@@ -540,7 +543,7 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
   if (tile == 50 || (tile < 0 && c64_ok && !(route & kRouteNoC64))) {
     TORCH_CHECK(c64_ok, "tile 50 (row-streaming split 3x3 64->64 conv) does not support this shape");
     TORCH_CHECK(conv3x3_split_c64_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, B, H, W,
-                                         a.relu, a.acc_scale, a.ovf, cur_stream()),
+                                         a.relu, a.acc_scale, a.ovf, cur_stream(), (route & kRouteC64TwoPerCU) ? 2 : 0),
                 "row-streaming split conv: tensor too large for 32-bit offsets");
     check_launch("conv3x3_split_c64");
     return y;
@@ -559,17 +562,24 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
   }
   const bool c1s_ok = KH == 1 && KW == 1 && (stride == 1 || stride == 2) && pad == 0 && !out_f32 && !strided &&
                       nsplit == 0 && conv1x1_stream_split_supported(C2 / 2, Cout, M);
-  if (tile == 80 || (tile < 0 && c1s_ok && !(route & kRouteNoStream1x1) && conv1x1_stream_split_default(C2 / 2, stride))) {
+  const bool legacy_small = (route & kRouteLegacySmallM) != 0;
+  if (tile == 80 || (tile < 0 && c1s_ok && !(route & kRouteNoStream1x1) && conv1x1_stream_split_default(C2 / 2, stride) &&
+                     (legacy_small || !conv1x1_small_m(M)))) {
     TORCH_CHECK(c1s_ok, "tile 80 (streaming split 1x1 conv) does not support this shape");
     conv1x1_stream_split_launch(a.x, a.w, a.bias, a.res, reinterpret_cast<half_t*>(a.y), a.zero, a.M, C2 / 2, Cout,
                                 a.relu, a.acc_scale, a.ovf, H, W, Wo, Ho * Wo, stride, cur_stream());
     check_launch("conv1x1_stream_split");
     return y;
   }
-  const int t = tile >= 0 ? (int)tile : conv_glds_split_pick(a.M, Cout);
+  // a small-M 1x1 (the downsample at a few dozen images per GPU) on the 128 x 64 tile
+  // (a forced ksplit > 1 keeps the split-K tile: tests drive that path at small M)
+  const bool small_1x1 = KH == 1 && KW == 1 && !legacy_small && conv1x1_small_m(M) && Cout % 128 == 0 && ksplit <= 1;
+  const int t = tile >= 0 ? (int)tile : (small_1x1 ? 38 : conv_glds_split_pick(a.M, Cout));
   const int nk_total = (int)(KH * KW) * (C2 / 64);
   // split-K: auto only for the auto-picked tile (a forced tile runs its own epilogue)
-  const int ks = nsplit == 0 ? conv_split_ksplit(a.M, Cout, t, nk_total, tile >= 0 && ksplit < 0 ? 1 : (int)ksplit) : 1;
+  const int ks = nsplit == 0 ? conv_split_ksplit(a.M, Cout, t, nk_total, tile >= 0 && ksplit < 0 ? 1 : (int)ksplit,
+                                                 legacy_small)
+                             : 1;
   TORCH_CHECK(ksplit <= 1 || ks == ksplit, "split-K: ", ksplit, " slices do not divide the K loop of tile ", t);
   if (ks > 1) {
     // small M: K slices into fp32 partials in one launch, then one combine

@@ -135,7 +135,8 @@ bool conv_glds_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 bool conv_glds_split_launch(ConvArgs a, bool out_f32, int tile, hipStream_t st);
 int conv_glds_split_pick(int M, int Cout);
 // K slices for a conv (1: none): force < 0 auto (the default tile), 0 / 1 off, k > 1 k slices (split-K tiles 27 / 36 / 42)
-int conv_split_ksplit(int M, int Cout, int tile, int nk_total, int force);
+int conv_split_ksplit(int M, int Cout, int tile, int nk_total, int force, bool legacy = false);
+bool conv1x1_small_m(long M);
 // fmt: 0 split residual/output, 1 split residual + fp32 output, 2 fp16 residual/output, 3 fp16 residual + fp32 output
 void splitk_reduce_res_launch(const float* part, int S, long MN, int N, const float* bias, const half_t* res,
                               int ldr, int relu, void* y, int ldy, int fmt, int* ovf, hipStream_t st);
@@ -168,7 +169,7 @@ bool conv1x1_stream_split_default(int C, int stride);
 bool conv3x3_split_c64_supported(int H, int W, int C, int Cout);
 bool conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
                               const void* zero, int B, int H, int W, int relu, float acc_scale, int* ovf,
-                              hipStream_t st);
+                              hipStream_t st, int per_cu = 0);
 // band-staged 3x3/s1/p1 conv (conv3x3_band.hip): ResNet layers 2-4 (W 28 / 14 / 7,
 // C % 64 == 0, Cout % 128 == 0); x / res read in place at pixel strides ldx / ldr (halfs).
 // Split operands by default; f16: plain fp16 operands, weights [Cout][9*C], fp16 output.

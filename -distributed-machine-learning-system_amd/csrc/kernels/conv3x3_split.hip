@@ -330,7 +330,7 @@ bool conv3x3_split_c64_supported(int H, int W, int C, int Cout) {
 
 bool conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bias, const half_t* res, half_t* y,
                               const void* zero, int B, int H, int W, int relu, float acc_scale, int* ovf,
-                              hipStream_t st) {
+                              hipStream_t st, int per_cu) {
   using namespace c64s;
   C64sArgs a;
   a.ovf = ovf;
@@ -346,7 +346,11 @@ bool conv3x3_split_c64_launch(const half_t* x, const half_t* w, const float* bia
   a.relu = relu;
   a.acc_scale = acc_scale;
   if ((long)B * H * W * c64s::PIX * 2 >= (1L << 31)) return false;   // 32-bit byte offsets
-  const int per = 2 * device_cu_count();
+  // per_cu 0 = auto: two workgroups per CU, or one when two would leave each fewer than
+  // 8 rows (B = 50 per GPU: 5.5 rows each, +1.0 % whole forward with one per CU,
+  // profiles/r6b_route.md)
+  if (per_cu <= 0) per_cu = B * H < 16 * device_cu_count() ? 1 : 2;
+  const int per = per_cu * device_cu_count();
   // equal row shares over the resident workgroups, at least 4 rows each (a band
   // loads 2 halo rows and waits for its first 3 rows before computing)
   a.nrows = B * H;

@@ -673,27 +673,37 @@ static void ks_tile_dims(int tile, int& bn, int& bm) {
     default: bn = 128; bm = 128; return;        // 36
   }
 }
-static int ksplit_rule(int force, int M, int Cout, int tile, int nk_total) {
+// target_blocks: the grid the doubling may reach; min_stages: K stages each slice keeps.
+static int ksplit_rule(int force, int M, int Cout, int tile, int nk_total, long target_blocks, int min_stages) {
   if (tile != 27 && tile != 36 && tile != 42) return 1;   // split-K instantiations (glds_dispatch_ks)
   if (force == 0 || force == 1) return 1;
   if (force > 1) return nk_total % force == 0 ? force : 1;
-  if (nk_total < 8) return 1;
+  if (nk_total < 2 * min_stages) return 1;
   int bn, bm;
   ks_tile_dims(tile, bn, bm);
   const long blocks = (long)((M + bm - 1) / bm) * ((Cout + bn - 1) / bn);
-  const long target = 2L * device_cu_count();  // two blocks per CU
   int s = 1;
-  // double the slices while the grid stays within one wave of two blocks per CU,
-  // each slice keeps >= 4 stages and the slices divide the K loop evenly (at most 8:
+  // double the slices while the grid stays within target_blocks, each slice keeps
+  // >= min_stages stages and the slices divide the K loop evenly (at most 8:
   // capping at 4 lost 11 % at B = 8, profiles/r4_ab_ksplit_cap4_b8.log)
-  while (s < 8 && blocks * s * 2 <= target && nk_total % (s * 2) == 0 && nk_total / (s * 2) >= 4) s *= 2;
+  while (s < 8 && blocks * s * 2 <= target_blocks && nk_total % (s * 2) == 0 && nk_total / (s * 2) >= min_stages)
+    s *= 2;
   return s;
 }
-int conv_split_ksplit(int M, int Cout, int tile, int nk_total, int force) {
-  return ksplit_rule(force, M, Cout, tile, nk_total);
+// Split convs (round 6, per-layer sweep at B = 50, profiles/r6a_b50_sweep.log): double
+// only while the grid stays within ONE block per CU and every slice keeps >= 8 stages.
+// The round-4 rule (two blocks per CU, >= 4 stages; legacy = true) split ResNet18
+// layer2 at B = 50 in two (t42k2 49.0 vs t42k1 43.2 us on the residual conv) and the
+// layer4 1x1 downsample (16.6 vs 11.5 us): the fp32 partials' round trip through
+// splitk_reduce_res cost more than the half-empty wave it filled.
+int conv_split_ksplit(int M, int Cout, int tile, int nk_total, int force, bool legacy) {
+  if (legacy) return ksplit_rule(force, M, Cout, tile, nk_total, 2L * device_cu_count(), 4);
+  return ksplit_rule(force, M, Cout, tile, nk_total, (long)device_cu_count(), 8);
 }
 int conv_f16_ksplit(int M, int Cout, int tile, int nk_total, int force) {
-  return ksplit_rule(force, M, Cout, tile, nk_total);     // same rule: fp16's BK-64 tiles 27 / 42
+  // fp16's BK-64 tiles 27 / 42 keep the round-4 rule (fp16 small batches are bound by
+  // the per-layer launch chain more than by occupancy, docs/KERNELS.md)
+  return ksplit_rule(force, M, Cout, tile, nk_total, 2L * device_cu_count(), 4);
 }
 
 // Default split tile (a stage is 32 channels instead of 64, so a tile does 3x the
@@ -704,6 +714,12 @@ int conv_glds_split_pick(int M, int Cout) {
   if (Cout % 128 == 0) return M >= 50000 ? 36 : 42;
   return 27;
 }
+
+// Small-M 1x1 convs (the ResNet downsample at B = 50 per GPU: M 9800 / 2450) run on the
+// 128 x 64 8-wave tile without split-K instead of the persistent streaming 1x1 kernel,
+// whose register-resident weights and 2-tile ring do not amortise over a few tiles per
+// CU (layer3 ds 13.2 -> 8.6 us, layer4 ds 12.4 -> 7.4 us, profiles/r6a_b50_sweep.log).
+bool conv1x1_small_m(long M) { return M < 16384; }
 
 bool conv_glds_split_p3_launch(ConvArgs a, int tile, hipStream_t st) {
   if (a.res != nullptr || a.cpk <= 0) return false;

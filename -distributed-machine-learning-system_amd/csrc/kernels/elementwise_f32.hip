@@ -239,36 +239,37 @@ void maxpool_f32_launch(const float* x, float* y, int B, int H, int W, int C, in
 // NHWC global average pool -> [B][C] fp32.  One 256-thread workgroup per
 // image; thread (g, c4) sums pixels g, g+G, ... of 4-channel chunk c4, the G
 // partial sums meet in LDS (same decomposition as the fp16 avgpool_kernel).
+// Global average pool, fp32 NHWC [B][HW][C] -> [B][C].  A workgroup takes one
+// image and 32 channel quads (128 channels); its 8 pixel groups each sum every
+// 8th pixel (independent 16-byte loads, unrolled), then one LDS pass adds the
+// groups.  Grid B x C/128: at B = 50 (strong scaling) and C = 512 that is 200
+// workgroups of ~6 loads per lane instead of 50 of ~25 (round 5: 8.3 us).
 __global__ void __launch_bounds__(256) avgpool_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int B,
                                                           int HW, int C) {
   __shared__ float4v part[256];
   const int b = blockIdx.x;
   const int cv = C / 4;
+  const int q = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int c4 = blockIdx.y * 32 + q;
   const float* p = x + (size_t)b * HW * C;
-  const float inv = 1.f / (float)HW;
-  if (cv >= 256) {
-    for (int c4 = threadIdx.x; c4 < cv; c4 += 256) {
-      float4v acc = float4v{0.f, 0.f, 0.f, 0.f};
-      for (int i = 0; i < HW; ++i) acc += *reinterpret_cast<const float4v*>(p + (size_t)i * C + c4 * 4);
-      *reinterpret_cast<float4v*>(y + (size_t)b * C + c4 * 4) = acc * inv;
-    }
-    return;
-  }
-  const int G = 256 / cv;
-  const int c4 = threadIdx.x % cv, g = threadIdx.x / cv;
   float4v acc = float4v{0.f, 0.f, 0.f, 0.f};
-  if (g < G)
-    for (int i = g; i < HW; i += G) acc += *reinterpret_cast<const float4v*>(p + (size_t)i * C + c4 * 4);
+  if (c4 < cv) {
+    int i = g;
+#pragma unroll 4
+    for (; i < HW; i += 8) acc += *reinterpret_cast<const float4v*>(p + (size_t)i * C + c4 * 4);
+  }
   part[threadIdx.x] = acc;
   __syncthreads();
-  if (g == 0) {
-    for (int k = 1; k < G; ++k) acc += part[k * cv + c4];
-    *reinterpret_cast<float4v*>(y + (size_t)b * C + c4 * 4) = acc * inv;
+  if (g == 0 && c4 < cv) {
+#pragma unroll
+    for (int k = 1; k < 8; ++k) acc += part[k * 32 + q];
+    *reinterpret_cast<float4v*>(y + (size_t)b * C + c4 * 4) = acc * (1.f / (float)HW);
   }
 }
 
 void avgpool_f32_launch(const float* x, float* y, int B, int HW, int C, hipStream_t st) {
-  hipLaunchKernelGGL(avgpool_f32_kernel, dim3((unsigned)B), dim3(256), 0, st, x, y, B, HW, C);
+  hipLaunchKernelGGL(avgpool_f32_kernel, dim3((unsigned)B, (unsigned)((C / 4 + 31) / 32)), dim3(256), 0, st, x, y, B,
+                     HW, C);
 }
 
 }  // namespace idunno

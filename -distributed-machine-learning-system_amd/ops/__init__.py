@@ -25,7 +25,8 @@ def conv2d_split(x, w, bias, acc_scale: float, kh: int, kw: int, stride: int, pa
     ``out_f32``).  ``tile`` forces a kernel (-1: the shape's default), ``ksplit``
     forces split-K slices (-1: auto for the default tile), ``route`` opts out of
     the specialised kernels (bit 0 band 3x3, bit 1 row-streaming 64->64, bit 2
-    streaming 1x1) -- kernel choice depends on these arguments only."""
+    streaming 1x1; bit 3 restores the round-5 small-M rules for A/Bs) -- kernel
+    choice depends on these arguments only."""
     return load().conv2d_split(x, w, bias, residual, kh, kw, stride, pad, relu, acc_scale, out_f32, tile, out,
                                ksplit, route)
 

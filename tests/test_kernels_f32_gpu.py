@@ -140,7 +140,7 @@ def test_pools_f32(ops):
     assert torch.equal(y, F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1))
     x2 = torch.randn(2, 13, 13, 256, device=DEV)
     assert torch.equal(ops.maxpool2d(x2, 3, 2, 0), F.max_pool2d(x2.permute(0, 3, 1, 2), 3, 2, 0).permute(0, 2, 3, 1))
-    for shape in [(4, 7, 7, 512), (2, 7, 7, 2048), (3, 5, 5, 12)]:
+    for shape in [(4, 7, 7, 512), (2, 7, 7, 2048), (3, 5, 5, 12), (50, 7, 7, 512), (2, 3, 3, 1000), (1, 1, 1, 4)]:
         x3 = torch.randn(*shape, device=DEV)
         _check(ops.global_avgpool(x3), x3.double().mean(dim=(1, 2)), rel=1e-6)
 

@@ -340,6 +340,24 @@ def test_softmax_top1(ops):
     assert torch.allclose(prob, v, rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("N", [10, 64, 1000, 1024, 1500])
+def test_softmax_top1_widths(ops, N):
+    """Register-resident rows (N <= 1024) and the streaming fallback (N > 1024);
+    ties inside one lane (j, j + 64) and across lanes resolve to the lowest index."""
+    torch.manual_seed(N)
+    logits = torch.randn(9, N, device=DEV)
+    if N > 80:
+        logits[1, 74] = logits[1, 10] = 50.0      # same lane (10 = 74 - 64)
+        logits[2, N - 1] = logits[2, 3] = 50.0    # different lanes
+    cls, prob = ops.softmax_top1(logits)
+    p = torch.softmax(logits.double(), dim=1)
+    v, i = p.max(dim=1)
+    assert torch.equal(cls.long(), i)
+    if N > 80:
+        assert cls[1].item() == 10 and cls[2].item() == 3
+    assert torch.allclose(prob.double(), v, rtol=1e-5, atol=1e-7)
+
+
 @pytest.mark.parametrize("name", ["resnet18", "alexnet", "resnet50"])
 def test_model_end_to_end_vs_fp32_oracle(ops, name):
     from idunno.models import HipRunner, compile_model

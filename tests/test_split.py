@@ -438,8 +438,12 @@ def test_model_split_vs_fp64_oracle(ops, name, B):
     img = ops.synth_images(0, 0, B, DEV)
     got = r.logits(img).double().cpu()
     if name.startswith("resnet") and B >= 8:
-        r.split_front = 2                      # stem + layer1 on batch parts: same numbers
-        assert torch.equal(r.logits(img).double().cpu(), got)
+        # stem + layer1 on batch parts: the same numbers, up to the summation order of
+        # a part's small-M 1x1 convs (M < 16384 runs them on the 128 x 64 tile, not
+        # the streaming 1x1 kernel: conv1x1_small_m)
+        r.split_front = 2
+        got_f = r.logits(img).double().cpu()
+        assert (got_f - got).abs().max().item() <= 2e-6 * got.abs().max().item()
         r.split_front = None
     if name.startswith("resnet") and B >= 64:
         # two half-batch streams: the same numbers, up to the summation order of
