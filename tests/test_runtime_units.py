@@ -198,7 +198,8 @@ def test_round_finalize_reruns_range_guard_rows_only():
     """RoundPlane._finalize: a row whose split forward left fp16's range (class
     -2 inside its chunk) goes back to its member as a TCP JOB (f32 rerun); rows
     with stale negatives only past their chunk's end are ingested as usual; the
-    scheduler gets one observation per model per round."""
+    scheduler gets the round's (chunk size, seconds) points of each model in one
+    call (observe_chunks), every member's header included."""
     import numpy as np
 
     from idunno.config import ClusterConfig
@@ -225,7 +226,8 @@ def test_round_finalize_reruns_range_guard_rows_only():
 
     sent, ingested, observed = [], [], []
     node = types.SimpleNamespace(
-        name="node00", standby="node00", sched=types.SimpleNamespace(observe=lambda m, t: observed.append((m, t))),
+        name="node00", standby="node00",
+        sched=types.SimpleNamespace(observe_chunks=lambda m, pts, b: observed.append((m, list(pts), b))),
         _send_job=lambda *a: sent.append(a), _ingest_round=lambda recs, now, seq: ingested.extend(recs),
         membership=types.SimpleNamespace(is_alive=lambda n: True))
     rp = RoundPlane.__new__(RoundPlane)
@@ -238,7 +240,10 @@ def test_round_finalize_reruns_range_guard_rows_only():
     assert [(r[2], r[3], r[4]) for r in ingested] == [("node00", 0, 3), ("node02", 8, 13)]
     assert list(ingested[1][5]) == list(range(200, 206)) and np.all(ingested[1][6] == 0.5)
     assert len(observed) == 1 and observed[0][0] == "resnet18"
-    assert abs(observed[0][1] - 1800e-6 / 14 * rp.cfg.batch_for("resnet18")) < 1e-12
+    pts = observed[0][1]
+    assert [n for n, _ in pts] == [4, 4, 6]
+    assert all(abs(t - u * 1e-6) < 1e-12 for (_, t), u in zip(pts, (400, 800, 600)))
+    assert observed[0][2] == rp.cfg.batch_for("resnet18")
 
 
 def test_send_frame_falls_back_when_the_socket_buffer_is_full():
