@@ -139,6 +139,7 @@ class ElasticGroup:
         self.poll_s = 0.0005
         self.standby_rank = -1                # second gather root (the hot standby), -1: none
         self._send = self._gathered = self._host = None
+        self._gopt: dict = {}                      # root rank -> GatherOptions
         self._d2h = None
 
     @property
@@ -326,6 +327,7 @@ class ElasticGroup:
     def _alloc(self, world: int) -> None:
         dev, rows, D = self.device, self.max_chunk + HDR_ROWS, self.depth
         self._send = [torch.zeros(rows, 2, dtype=torch.int32, device=dev) for _ in range(D)]
+        self._send_list = [[t] for t in self._send]          # gather input lists, built once
         root = self.rank == 0 or self.rank == self.standby_rank
         if isinstance(self.pg, _Solo):
             self._gathered = [s.unsqueeze(0) for s in self._send]       # the send buffer IS the round
@@ -359,17 +361,22 @@ class ElasticGroup:
                 ev = torch.cuda.Event()
                 ev.record(torch.cuda.current_stream(self.device))
             return _EventWork(ev)
-        opts = dist.GatherOptions()
-        opts.rootRank = 0
         slot = seq % self.depth
         outs = self._gather_outs[slot] if self.rank == 0 else []
-        work = pg.gather(outs, [self._send[slot]], opts)
+        work = pg.gather(outs, self._send_list[slot], self._gopts(0))
         sb = self.standby_rank
         if sb <= 0:
             return work
-        o2 = dist.GatherOptions()
-        o2.rootRank = sb
-        return _PairWork(work, pg.gather(self._gather_outs[slot] if self.rank == sb else [], [self._send[slot]], o2))
+        return _PairWork(work, pg.gather(self._gather_outs[slot] if self.rank == sb else [], self._send_list[slot],
+                                         self._gopts(sb)))
+
+    def _gopts(self, root: int):
+        """GatherOptions per root, built once (two per round otherwise)."""
+        o = self._gopt.get(root)
+        if o is None:
+            o = self._gopt[root] = dist.GatherOptions()
+            o.rootRank = root
+        return o
 
     def wait(self, work, check=None, spin_s: float = 0.001) -> None:
         """Poll ``work`` until it completes; ``check()`` raises RoundAbandoned

@@ -370,9 +370,84 @@ class JobState:
         (duplicates, re-split ranges, several queries) takes the per-chunk path."""
         now = self.clock() if now is None else now
         with self.lock:
+            if recs and self._whole_ok(recs):
+                return self._record_whole(recs, now)
             if recs and self._bulk_ok(recs):
                 return self._record_bulk(recs, now)
             return sum(1 for m, q, w, s, e, c, p in recs if self.record_result(m, q, w, s, e, c, p, now))
+
+    def _whole_ok(self, recs) -> bool:
+        """The commonest round: it answers EVERY chunk of one query, in the order
+        the query was assigned, and nothing of that query is held yet (a query
+        split over the round's members).  Then every entry is
+        'w' (the open count equals the entry count) and no chunk is a duplicate."""
+        model, qnum = recs[0][0], recs[0][1]
+        key = (model, qnum)
+        ents = self.worker_set.get(key)
+        if not ents or len(ents) != len(recs) or self._open.get(key) != len(recs) or self._done_imgs.get(key):
+            return False
+        for ent, r in zip(ents, recs):
+            if ent[0] != r[2] or ent[1] != r[3] or ent[2] != r[4] or r[0] != model or r[1] != qnum:
+                return False
+        return True
+
+    def _record_whole(self, recs, now: float) -> int:
+        """``_record_bulk`` for a round that closes its whole query (``_whole_ok``):
+        one pass, no position index, the query's done intervals set at once."""
+        model, qnum = recs[0][0], recs[0][1]
+        key = (model, qnum)
+        ents = self.worker_set[key]
+        bsz = self.batchsize.get(model)
+        vms = self.working_vm_set
+        done_add = self._done_keys.add
+        pw_append = self._ptime_win[model].append
+        res = self.results[f"{model} {qnum}"]
+        i32, f32, nd = np.int32, np.float32, np.ndarray
+        new_ents, chunks, tot = [], [], 0
+        for (w, s, e, _, t_start, _), r in zip(ents, recs):
+            ck = (model, qnum, s, e)
+            vm = vms.get(w)
+            if vm is not None:
+                if vm and vm[0] == ck:
+                    del vm[0]
+                else:
+                    try:
+                        vm.remove(ck)
+                    except ValueError:
+                        pass
+                if not vm:
+                    del vms[w]
+            done_add(ck)
+            n = e - s + 1
+            tot += n
+            pw_append((now, (now - t_start) * (1.0 if bsz is None else bsz / n)))
+            new_ents.append((w, s, e, "f", t_start, now))
+            c, p = r[5], r[6]
+            res.append(ChunkResult(s, e, c if type(c) is nd and c.dtype == i32 else np.asarray(c, dtype=i32),
+                                   p if type(p) is nd and p.dtype == f32 else np.asarray(p, dtype=f32), w))
+            chunks.append([s, e])
+        self.worker_set[key] = new_ents
+        self._open.pop(key, None)
+        chunks.sort()
+        ivs = self._done_imgs[key]
+        cs, ce = chunks[0]
+        for s, e in chunks[1:]:
+            if s == ce + 1:
+                ce = e
+            else:
+                _add_interval(ivs, cs, ce)
+                cs, ce = s, e
+        _add_interval(ivs, cs, ce)
+        self.finished_queries[model] += 1
+        t0 = self.query_submit_time.get(key)
+        if t0 is not None:
+            self.query_latency[model].append(now - t0)
+        self.finished_images[model] += tot
+        self._rate_win[model].append((now, tot))
+        self._expire(model, now)
+        self._c2_dirty.add(model)
+        self._bump("results", model, qnum, chunks, now)
+        return len(recs)
 
     def _bulk_ok(self, recs) -> bool:
         model, qnum = recs[0][0], recs[0][1]

@@ -127,6 +127,8 @@ class RoundPlane:
         self.launch_cpu_s = 0.0               # thread CPU time of this node's chunk launches
         self.host_post_s = 0.0                # of host_s: posting (descriptors, own chunk, gather)
         self.host_send_s = 0.0                # of host_post_s: ROUND descriptor sends
+        self.host_release_s = 0.0             # of host_s: waiting for the standby's gather of a reused slot
+        self._rel: dict = {}                  # coordinator: slot -> gather pair to release before reuse
 
     # -- lifecycle -------------------------------------------------------------------
     def start(self) -> None:
@@ -239,7 +241,7 @@ class RoundPlane:
                 "max_queries_per_round": self.max_queries_per_round,
                 "parked": self.parked, "pending_collectives": self.pending_collectives(),
                 "host_s": self.host_s, "host_cpu_s": self.host_cpu_s, "host_wait_s": self.host_wait_s, "host_post_s": self.host_post_s,
-                "host_send_s": self.host_send_s, "announce_frames": self.announce_frames, "standby_rounds": self.standby_rounds, "launch_cpu_s": self.launch_cpu_s,
+                "host_send_s": self.host_send_s, "host_release_s": self.host_release_s, "announce_frames": self.announce_frames, "standby_rounds": self.standby_rounds, "launch_cpu_s": self.launch_cpu_s,
                 "queued": len(self._queue)}
 
     def pending_collectives(self) -> int:
@@ -394,6 +396,7 @@ class RoundPlane:
         with self.cv:
             self.healthy = False
         self._inflight.clear()
+        self._rel.clear()
         if abandoned:
             self.group.abort_async()          # collectives may still be pending on dead peers
         else:
@@ -547,14 +550,15 @@ class RoundPlane:
                         return        # hand back to the driver loop now and then (cheap)
                     continue
                 idle_since = time.monotonic()
-                self._post_next(announced, members)
+                self._post_next(announced, members, check)
             # rounds already announced are owed to the members (they wait for each seq)
             while announced:
                 while len(inflight) >= g.depth:
                     self._finalize_oldest(members, check)
-                self._post_next(announced, members)
+                self._post_next(announced, members, check)
             while inflight:
                 self._finalize_oldest(members, check)
+            self._release_all(check)
             self._stop_epoch()
             if self._released:
                 self._release_done.set()
@@ -614,10 +618,11 @@ class RoundPlane:
         self.host_send_s += time.perf_counter() - ts
         self.announce_frames += 1
 
-    def _post_next(self, announced: deque, members: tuple) -> None:
+    def _post_next(self, announced: deque, members: tuple, check=None) -> None:
         tp, cp = time.perf_counter(), time.thread_time()
         r = announced.popleft()
         self._inflight.append(r)
+        self._release_slot(r.seq, check)
         self._post(r, members)
         dt = time.perf_counter() - tp
         self.host_s += dt
@@ -632,6 +637,22 @@ class RoundPlane:
                     return
                 self.cv.wait(0.0002 if time.perf_counter() - t0 < 0.01 else 0.002)
             check()
+
+    def _release_slot(self, seq: int, check) -> None:
+        """Before round ``seq`` rewrites its slot: the standby's gather of the
+        round that last used the slot (``depth`` rounds back) must be done.
+        Released here, not when that round was ingested: by now it has long
+        finished, so the wait is free (on the CPU path it had been a poll on the
+        critical path of every round's ingest)."""
+        w = self._rel.pop(seq % self.group.depth, None)
+        if w is not None:
+            t = time.perf_counter()
+            self.group.release(w, check)
+            self.host_release_s += time.perf_counter() - t
+
+    def _release_all(self, check) -> None:
+        for slot in list(self._rel):
+            self._release_slot(slot, check)
 
     @staticmethod
     def _table(members: tuple, qs: list) -> list:
@@ -731,7 +752,7 @@ class RoundPlane:
             gc.freeze()
         sb = g.standby_rank
         if sb > 0:
-            g.release(r.work, check)        # the standby's gather of this slot too, before reuse
+            self._rel[r.seq % g.depth] = r.work   # the standby's gather of this slot: released before reuse
         gathered_by_standby = sb > 0 and members[sb] == n.standby
         if recs and not gathered_by_standby and n.standby != n.name and n.membership.is_alive(n.standby):
             self._mirror(recs, now)

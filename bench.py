@@ -1435,6 +1435,7 @@ def _drive_system(a, node, W: int, B: int) -> dict:
             if d:
                 out[f"system_{nm.replace('.', '_')}_ms"] = round(1000 * statistics.mean(d), 4)
         out["system_host_send_ms_per_round"] = round(1000 * (rb["host_send_s"] - ra["host_send_s"]) / nr, 4)
+        out["system_host_release_ms_per_round"] = round(1000 * (rb["host_release_s"] - ra["host_release_s"]) / nr, 4)
 
     # strong scaling (the north star's p50): ONE 400-image query split over the W
     # members, one at a time (p50), then `steps` of them queued at once (images/s);

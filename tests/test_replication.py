@@ -163,3 +163,41 @@ def test_bulk_and_per_chunk_same_c2_without_configured_batchsize():
     for k in sa:
         if k != "seq":
             assert sa[k] == sb[k], k
+
+
+def test_whole_query_fast_path_and_bulk_fallback_agree():
+    """A round answering every chunk of its query in assignment order takes the
+    whole-query path (_whole_ok); reordered or partial rounds take the bulk path.
+    Both leave the tables per-chunk record_result leaves."""
+    import numpy as np
+
+    from idunno.runtime.jobstate import JobState
+
+    W, B = 4, 25
+    cls, prob = np.arange(B, dtype=np.int32), np.full(B, 0.5, np.float32)
+    a, b = JobState(), JobState()
+    for q in range(1, 4):
+        plan = [(f"n{r}", q * 1000 + r * B, q * 1000 + (r + 1) * B - 1) for r in range(W)]
+        for st in (a, b):
+            st.assign("alexnet", q, plan, now=1.0)
+        recs = [("alexnet", q, w, s, e, cls, prob) for w, s, e in plan]
+        if q == 1:
+            assert a._whole_ok(recs)
+            assert a.record_results(recs, now=2.0) == W
+        elif q == 2:
+            rev = recs[::-1]
+            assert not a._whole_ok(rev) and a._bulk_ok(rev)
+            assert a.record_results(rev, now=2.0) == W
+        else:
+            assert not a._whole_ok(recs[:2])
+            assert a.record_results(recs[:2], now=2.0) == 2
+            assert not a._whole_ok(recs[2:])      # half the query is already held
+            assert a.record_results(recs[2:], now=2.0) == 2
+        for r in (recs[::-1] if q == 2 else recs):     # same arrival order as a
+            b.record_result(*r, now=2.0)
+    sa, sb = a.snapshot(), b.snapshot()
+    for k in sa:
+        if k != "seq":
+            assert sa[k] == sb[k], k
+    assert a.inference_result_list() == b.inference_result_list()
+    assert a.pending_count() == 0 and a.finished_queries["alexnet"] == 3
