@@ -127,8 +127,7 @@ class RoundPlane:
         self.launch_cpu_s = 0.0               # thread CPU time of this node's chunk launches
         self.host_post_s = 0.0                # of host_s: posting (descriptors, own chunk, gather)
         self.host_send_s = 0.0                # of host_post_s: ROUND descriptor sends
-        self.host_release_s = 0.0             # of host_s: waiting for the standby's gather of a reused slot
-        self._rel: dict = {}                  # coordinator: slot -> gather pair to release before reuse
+        self.host_release_s = 0.0             # of host_s: waiting for the standby's gather of an ingested round
 
     # -- lifecycle -------------------------------------------------------------------
     def start(self) -> None:
@@ -396,7 +395,6 @@ class RoundPlane:
         with self.cv:
             self.healthy = False
         self._inflight.clear()
-        self._rel.clear()
         if abandoned:
             self.group.abort_async()          # collectives may still be pending on dead peers
         else:
@@ -550,15 +548,14 @@ class RoundPlane:
                         return        # hand back to the driver loop now and then (cheap)
                     continue
                 idle_since = time.monotonic()
-                self._post_next(announced, members, check)
+                self._post_next(announced, members)
             # rounds already announced are owed to the members (they wait for each seq)
             while announced:
                 while len(inflight) >= g.depth:
                     self._finalize_oldest(members, check)
-                self._post_next(announced, members, check)
+                self._post_next(announced, members)
             while inflight:
                 self._finalize_oldest(members, check)
-            self._release_all(check)
             self._stop_epoch()
             if self._released:
                 self._release_done.set()
@@ -618,11 +615,10 @@ class RoundPlane:
         self.host_send_s += time.perf_counter() - ts
         self.announce_frames += 1
 
-    def _post_next(self, announced: deque, members: tuple, check=None) -> None:
+    def _post_next(self, announced: deque, members: tuple) -> None:
         tp, cp = time.perf_counter(), time.thread_time()
         r = announced.popleft()
         self._inflight.append(r)
-        self._release_slot(r.seq, check)
         self._post(r, members)
         dt = time.perf_counter() - tp
         self.host_s += dt
@@ -637,22 +633,6 @@ class RoundPlane:
                     return
                 self.cv.wait(0.0002 if time.perf_counter() - t0 < 0.01 else 0.002)
             check()
-
-    def _release_slot(self, seq: int, check) -> None:
-        """Before round ``seq`` rewrites its slot: the standby's gather of the
-        round that last used the slot (``depth`` rounds back) must be done.
-        Released here, not when that round was ingested: by now it has long
-        finished, so the wait is free (on the CPU path it had been a poll on the
-        critical path of every round's ingest)."""
-        w = self._rel.pop(seq % self.group.depth, None)
-        if w is not None:
-            t = time.perf_counter()
-            self.group.release(w, check)
-            self.host_release_s += time.perf_counter() - t
-
-    def _release_all(self, check) -> None:
-        for slot in list(self._rel):
-            self._release_slot(slot, check)
 
     @staticmethod
     def _table(members: tuple, qs: list) -> list:
@@ -752,7 +732,11 @@ class RoundPlane:
             gc.freeze()
         sb = g.standby_rank
         if sb > 0:
-            self._rel[r.seq % g.depth] = r.work   # the standby's gather of this slot: released before reuse
+            # the standby's gather of this slot too, before reuse (deferring it to the
+            # slot's next post measured the same: with depth 2 that post follows at once)
+            tr = time.perf_counter()
+            g.release(r.work, check)
+            self.host_release_s += time.perf_counter() - tr
         gathered_by_standby = sb > 0 and members[sb] == n.standby
         if recs and not gathered_by_standby and n.standby != n.name and n.membership.is_alive(n.standby):
             self._mirror(recs, now)
