@@ -49,7 +49,9 @@ constexpr int kRouteNoBand = 1;      // no band-staged 3x3 kernel (tile 70)
 constexpr int kRouteNoC64 = 2;       // no row-streaming 3x3 64->64 kernels (tile 50)
 constexpr int kRouteNoStream1x1 = 4; // no streaming 1x1 kernels (tile 80)
 constexpr int kRouteC64TwoPerCU = 16;  // row-streaming 64->64 kernel: always two workgroups per CU (A/B arm)
-constexpr int kRouteLegacySmallM = 8; // split convs: round-5 small-M rules (streaming 1x1 at every M, split-K
+constexpr int kRouteLegacySmallM = 8;
+constexpr int kRouteBandW7 = 32;      // A/B: the band-staged 3x3 at W 7 too (the round-5 rule)
+constexpr int kRouteNoBandW28 = 64;   // A/B: no band-staged 3x3 at W 28 (ResNet layer2) // split convs: round-5 small-M rules (streaming 1x1 at every M, split-K
                                       // up to two blocks per CU) -- the A/B arm of the round-6 rules
 
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
@@ -552,7 +554,10 @@ static torch::Tensor conv2d_split_impl(torch::Tensor x, torch::Tensor w, torch::
   // that give every CU a tile (conv3x3_band_default; otherwise the im2col tiles + split-K)
   const bool band_ok = KH == 3 && KW == 3 && stride == 1 && pad == 1 && nsplit == 0 &&
                        conv3x3_band_supported(H, W, C2 / 2, Cout);
-  if (tile == 70 || (tile < 0 && band_ok && !(route & kRouteNoBand) && conv3x3_band_default(B, W, Cout))) {
+  const bool band_off = (route & kRouteNoBand) || (W == 28 && (route & kRouteNoBandW28));
+  const bool band_on = conv3x3_band_default(B, W, Cout) ||
+                       (W == 7 && (route & kRouteBandW7) && conv3x3_band_tiles(B, W, Cout) >= device_cu_count());
+  if (tile == 70 || (tile < 0 && band_ok && !band_off && band_on)) {
     TORCH_CHECK(band_ok, "tile 70 (band-staged split 3x3 conv) does not support this shape");
     TORCH_CHECK(conv3x3_band_launch(a.x, (int)xP, a.w, a.bias, rp, (int)rP, a.y, (int)ych, out_f32, B, H, W, C2 / 2,
                                     Cout, a.relu, a.acc_scale, a.ovf, 0, 0, cur_stream()),

@@ -538,12 +538,14 @@ bool conv3x3_band_supported(int H, int W, int C, int Cout) {
 
 int conv3x3_band_tiles(int B, int W, int Cout);
 
-// Auto selection (round-5 per-layer A/B at B = 400, profiles/r5_band_ab.md): layer2
-// (W 28, 1225 tiles) and layer4 (W 7, 492 tiles; 4-5 % under the 128 x 160 im2col
-// tile) take the band kernel; layer3 (W 14) ties the 128 x 128 im2col tile and keeps it.
+// Auto selection: layer2 (W 28, 1225 tiles at B = 400) takes the band kernel; layer3
+// (W 14) ties the 128 x 128 im2col tile and keeps it.  Layer4 (W 7) took it in round 5
+// (4-5 % under the 128 x 160 im2col tile then), but after the round-5 16-byte epilogues
+// the 128 x 160 tile wins the whole graph: ResNet18 b400 split +1.2 % same process
+// without the band kernel at W 7, -1.1 % without it at W 28 (profiles/r6f_ab_route_*.log).
 // Below one tile per CU (small per-GPU batches) the im2col tiles + split-K win.
 bool conv3x3_band_default(int B, int W, int Cout) {
-  if (W != 28 && W != 7) return false;
+  if (W != 28) return false;
   return conv3x3_band_tiles(B, W, Cout) >= device_cu_count();
 }
 
