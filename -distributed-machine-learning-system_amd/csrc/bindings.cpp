@@ -45,14 +45,14 @@ static torch::Tensor zero_buffer(const torch::Device& dev) {
 // switches, VERDICT r4 weakness 4): `tile` forces a kernel, `ksplit` forces split-K
 // slices (-1 auto for the auto-picked tile), `route` (a per-runner policy, bits
 // below) opts a call out of the specialised kernels for whole-graph A/Bs.
-constexpr int kRouteNoBand = 1;      // no band-staged 3x3 kernel (tile 70)
-constexpr int kRouteNoC64 = 2;       // no row-streaming 3x3 64->64 kernels (tile 50)
-constexpr int kRouteNoStream1x1 = 4; // no streaming 1x1 kernels (tile 80)
+constexpr int kRouteNoBand = 1;        // no band-staged 3x3 kernel (tile 70)
+constexpr int kRouteNoC64 = 2;         // no row-streaming 3x3 64->64 kernels (tile 50)
+constexpr int kRouteNoStream1x1 = 4;   // no streaming 1x1 kernels (tile 80)
+constexpr int kRouteLegacySmallM = 8;  // split convs: the round-5 small-M rules (streaming 1x1 at every M,
+                                       // split-K up to two blocks per CU) -- A/B arm of the round-6 rules
 constexpr int kRouteC64TwoPerCU = 16;  // row-streaming 64->64 kernel: always two workgroups per CU (A/B arm)
-constexpr int kRouteLegacySmallM = 8;
-constexpr int kRouteBandW7 = 32;      // A/B: the band-staged 3x3 at W 7 too (the round-5 rule)
-constexpr int kRouteNoBandW28 = 64;   // A/B: no band-staged 3x3 at W 28 (ResNet layer2) // split convs: round-5 small-M rules (streaming 1x1 at every M, split-K
-                                      // up to two blocks per CU) -- the A/B arm of the round-6 rules
+constexpr int kRouteBandW7 = 32;       // the band-staged 3x3 at W 7 too (the round-5 rule, A/B arm)
+constexpr int kRouteNoBandW28 = 64;    // no band-staged 3x3 at W 28 (ResNet layer2, A/B arm)
 
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
