@@ -101,6 +101,9 @@ class RoundPlane:
         self.rounds_failed = 0
         self.mixed_rounds = 0                 # rounds that carried more than one model
         self.mixed_splits: dict = {}          # "alexnet:3,resnet18:5" -> rounds with that worker split
+        # the last mixed rounds: (seq, split key, the scheduler's averages and exact shares
+        # at posting time) -- whether the split the round ran follows its own averages
+        self.mixed_log: deque = deque(maxlen=128)
         self.max_queries_per_round = 0
         self.parked = True                    # member: waiting on the control plane, nothing posted
         self._inflight: deque = deque()       # this node's posted, unfinished gathers
@@ -237,6 +240,7 @@ class RoundPlane:
         return {"ok": True, "epoch": g.epoch, "formed": g.formed, "members": list(g.members),
                 "rounds_done": self.rounds_done, "rounds_failed": self.rounds_failed,
                 "mixed_rounds": self.mixed_rounds, "mixed_splits": dict(self.mixed_splits),
+                "mixed_log": list(self.mixed_log),
                 "max_queries_per_round": self.max_queries_per_round,
                 "parked": self.parked, "pending_collectives": self.pending_collectives(),
                 "host_s": self.host_s, "host_cpu_s": self.host_cpu_s, "host_wait_s": self.host_wait_s, "host_post_s": self.host_post_s,
@@ -661,6 +665,12 @@ class RoundPlane:
             self.mixed_rounds += 1
             key = ",".join(f"{m}:{c}" for m, c in sorted(per.items()))
             self.mixed_splits[key] = self.mixed_splits.get(key, 0) + 1
+            sched = self.node.sched
+            avg = sched.effective_avg(per)
+            tot = sum(avg.values()) or 1.0
+            used = sum(per.values())
+            self.mixed_log.append([r.seq, key, {m: round(v, 6) for m, v in avg.items()},
+                                   {m: round(avg[m] / tot * used, 2) for m in avg}])
         self.max_queries_per_round = max(self.max_queries_per_round, len(r.queries))
 
     def _finalize_oldest(self, members: tuple, check) -> None:

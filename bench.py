@@ -1501,7 +1501,12 @@ def _drive_system(a, node, W: int, B: int) -> dict:
                 "two_job_mixed_splits": {k: v - r0.get("mixed_splits", {}).get(k, 0)
                                          for k, v in r1.get("mixed_splits", {}).items()
                                          if v > r0.get("mixed_splits", {}).get(k, 0)} if r1 else None,
-                "sched_avg_time_s": {m: round(v, 6) for m, v in node.sched.avg_time.items()}})
+                "sched_avg_time_s": {m: round(v, 6) for m, v in node.sched.avg_time.items()},
+                # every mixed round of the timed jobs: [seq, split, the averages the scheduler held
+                # when the round was posted, the exact fair-time shares they give]
+                "two_job_split_log": r1.get("mixed_log", [])[
+                    -max(0, min(24, r1.get("mixed_rounds", 0) - r0.get("mixed_rounds", 0))):] if r1 and
+                    r1.get("mixed_rounds", 0) > r0.get("mixed_rounds", 0) else [] if r1 else None})
 
     # time to start a second job (report Fig 3: 40-42 s AlexNet first, 45-49 s ResNet18 first): job A
     # runs; job B is submitted; until B's first query has finished
