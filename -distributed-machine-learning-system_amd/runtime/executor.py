@@ -146,6 +146,7 @@ class HipExecutor(Executor):
         self.runners: dict[str, object] = {}
         self._pool = None
         self.graphs_broken = False      # a capture failed: eager forwards only (see _capture)
+        self.trim_ok = None             # callable: True when empty_cache cannot wait on a collective
         self.lock = threading.Lock()
         self.run_lock = threading.Lock()      # one forward (copy-in, replay, read-back) at a time
         self.stream = None      # private HIP stream: nodes sharing a GPU overlap
@@ -193,7 +194,14 @@ class HipExecutor(Executor):
         one GPU: 20 GB reserved-but-unused each).  A capture that fails (e.g.
         out of memory) leaves the pool it recorded into unusable: the runners
         get a fresh pool, no further graphs are captured and the caller runs
-        the chunk eagerly (returns None)."""
+        the chunk eagerly (returns None).
+
+        ``empty_cache`` frees with ``hipFree``, which waits for ALL work on the
+        device while holding the interpreter lock: behind an RCCL gather pending
+        on a dead member it stalled the whole node process, heartbeats included,
+        until the communicator timed out (8-rank RCCL rehearsal, worker failover
+        with 4 / 8 chunks in flight).  ``trim_ok`` (set by the node) says when no
+        collective can be pending; otherwise the cache is left for later."""
         before = len(r._graphs)
         try:
             out = fn()
@@ -205,7 +213,7 @@ class HipExecutor(Executor):
                 for rr in self.runners.values():
                     rr.graph_pool = self._pool
             return None
-        if len(r._graphs) > before:
+        if len(r._graphs) > before and (self.trim_ok is None or self.trim_ok()):
             torch.cuda.empty_cache()
         return out
 

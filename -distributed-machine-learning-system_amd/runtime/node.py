@@ -129,6 +129,8 @@ class Node:
             self.rounds = RoundPlane(self, torch.device(self.device) if self.device is not None else
                                      torch.device("cpu"))
             self.rounds.start()
+            if hasattr(self.executor, "trim_ok"):
+                self.executor.trim_ok = self.rounds.collectives_quiet
         self.transport.start(self.handle)
         self.membership.start()
         for fn, nm in ((self._worker_loop, "worker"), (self._metadata_loop, "meta"),

@@ -247,6 +247,16 @@ class RoundPlane:
                 "host_send_s": self.host_send_s, "host_release_s": self.host_release_s, "announce_frames": self.announce_frames, "standby_rounds": self.standby_rounds, "launch_cpu_s": self.launch_cpu_s,
                 "queued": len(self._queue)}
 
+    def collectives_quiet(self) -> bool:
+        """No collective of this node can be pending on the device: no epoch of
+        more than one member is formed and no aborted communicator is still
+        being torn down (HipExecutor's empty_cache waits for every kernel on the
+        device, a gather stuck on a dead peer included)."""
+        g = self.group
+        if any(t.is_alive() for t in list(g._aborters)):
+            return False
+        return not g.formed or len(g.members) <= 1
+
     def pending_collectives(self) -> int:
         """Posted gathers of this node that have not completed."""
         works = [x.work if isinstance(x, _Round) else x[1] for x in list(self._inflight)]

@@ -322,3 +322,47 @@ def test_round_batch_announce_and_member_unpack():
     assert staged == [(102, 102), (202, 202)]          # its announced chunks start staging at once
     assert sorted(mem._round_msgs) == [(5, 0), (5, 1)]
     assert mem._round_msgs[(5, 1)]["rows"][3] == [rid, 2, 203, 203]
+
+
+def test_executor_trims_cache_only_when_no_collective_can_pend(monkeypatch):
+    """HipExecutor._capture frees the allocator cache after a new capture only
+    while ``trim_ok`` says no collective can be pending: hipFree waits for every
+    kernel on the device with the interpreter lock held, and behind a gather
+    stuck on a dead peer it stalled the whole node (8-rank RCCL rehearsal)."""
+    import torch
+
+    from idunno.runtime.executor import HipExecutor
+    from idunno.runtime.rounds import RoundPlane
+
+    calls = []
+    monkeypatch.setattr(torch.cuda, "empty_cache", lambda: calls.append(1))
+    ex = HipExecutor.__new__(HipExecutor)
+    ex.graphs_broken = False
+    r = types.SimpleNamespace(_graphs={})
+
+    def cap():
+        r._graphs[len(r._graphs)] = object()
+        return "replay"
+
+    ex.trim_ok = lambda: False
+    assert ex._capture(r, cap) == "replay" and calls == []
+    ex.trim_ok = None
+    assert ex._capture(r, cap) == "replay" and calls == [1]
+    assert ex._capture(r, lambda: "hit") == "hit" and calls == [1]      # no new graph: no trim
+
+    class Alive:
+        def __init__(self, alive):
+            self.alive = alive
+
+        def is_alive(self):
+            return self.alive
+
+    rp = RoundPlane.__new__(RoundPlane)
+    rp.group = types.SimpleNamespace(_aborters=[], formed=False, members=[])
+    assert rp.collectives_quiet()
+    rp.group = types.SimpleNamespace(_aborters=[], formed=True, members=["a"])
+    assert rp.collectives_quiet()                        # a one-member (solo) epoch
+    rp.group = types.SimpleNamespace(_aborters=[], formed=True, members=["a", "b"])
+    assert not rp.collectives_quiet()
+    rp.group = types.SimpleNamespace(_aborters=[Alive(True)], formed=False, members=[])
+    assert not rp.collectives_quiet()                    # an aborted communicator still tearing down
