@@ -146,7 +146,8 @@ class HipExecutor(Executor):
         self.runners: dict[str, object] = {}
         self._pool = None
         self.graphs_broken = False      # a capture failed: eager forwards only (see _capture)
-        self.trim_ok = None             # callable: True when empty_cache cannot wait on a collective
+        self.trim_ok = None             # callable(need) -> bool: may empty_cache run now (see _capture)
+        self.trim_slack_bytes = 16 << 30      # reserved-but-unused cache that counts as a need to trim
         self.lock = threading.Lock()
         self.run_lock = threading.Lock()      # one forward (copy-in, replay, read-back) at a time
         self.stream = None      # private HIP stream: nodes sharing a GPU overlap
@@ -200,8 +201,11 @@ class HipExecutor(Executor):
         device while holding the interpreter lock: behind an RCCL gather pending
         on a dead member it stalled the whole node process, heartbeats included,
         until the communicator timed out (8-rank RCCL rehearsal, worker failover
-        with 4 / 8 chunks in flight).  ``trim_ok`` (set by the node) says when no
-        collective can be pending; otherwise the cache is left for later."""
+        with 4 / 8 chunks in flight).  ``trim_ok(need)`` (set by the node) says
+        whether to trim now: always when no collective can be pending; while an
+        RCCL epoch runs only when the cache's unused part exceeds
+        ``trim_slack_bytes`` (``need``: node processes sharing one GPU) and every
+        member is alive, so the wait is for gathers that are progressing."""
         before = len(r._graphs)
         try:
             out = fn()
@@ -213,8 +217,11 @@ class HipExecutor(Executor):
                 for rr in self.runners.values():
                     rr.graph_pool = self._pool
             return None
-        if len(r._graphs) > before and (self.trim_ok is None or self.trim_ok()):
-            torch.cuda.empty_cache()
+        if len(r._graphs) > before:
+            need = torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device) \
+                > self.trim_slack_bytes
+            if self.trim_ok is None or self.trim_ok(need):
+                torch.cuda.empty_cache()
         return out
 
     def _forward(self, r, images, packed, slot: int = 0):

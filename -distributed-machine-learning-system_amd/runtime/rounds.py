@@ -247,15 +247,21 @@ class RoundPlane:
                 "host_send_s": self.host_send_s, "host_release_s": self.host_release_s, "announce_frames": self.announce_frames, "standby_rounds": self.standby_rounds, "launch_cpu_s": self.launch_cpu_s,
                 "queued": len(self._queue)}
 
-    def collectives_quiet(self) -> bool:
-        """No collective of this node can be pending on the device: no epoch of
-        more than one member is formed and no aborted communicator is still
-        being torn down (HipExecutor's empty_cache waits for every kernel on the
-        device, a gather stuck on a dead peer included)."""
+    def collectives_quiet(self, need: bool = False) -> bool:
+        """May HipExecutor's empty_cache run now?  It waits for every kernel on
+        the device with the interpreter lock held, a gather stuck on a dead peer
+        included.  True when no collective of this node can be pending (no epoch
+        of more than one member formed, no aborted communicator still tearing
+        down); with ``need`` (the cache holds more than its slack: node processes
+        sharing one GPU) also while every member of the epoch is alive -- its
+        gathers are progressing and the wait is short."""
         g = self.group
         if any(t.is_alive() for t in list(g._aborters)):
             return False
-        return not g.formed or len(g.members) <= 1
+        if not g.formed or len(g.members) <= 1:
+            return True
+        ms = self.node.membership
+        return need and all(ms.is_alive(m) for m in list(g.members))
 
     def pending_collectives(self) -> int:
         """Posted gathers of this node that have not completed."""

@@ -1277,6 +1277,10 @@ def run_node(a) -> int:
                                         os.path.basename((a.work_dir or a.phase).rstrip("/"))))
     name = cfg.node_name(rank)
     ex = FakeExecutor() if a.dry_run else HipExecutor(dev, seed=a.seed, dtype=a.dtype, fp32_impl=a.fp32_impl)
+    if not a.dry_run and (a.rehearse_gloo or a.rehearse_rccl) and n > max(1, torch.cuda.device_count()):
+        # node processes sharing one GPU: free cached activation blocks of retired chunk
+        # sizes early (executor._capture), or eight caches fill the card's 288 GB
+        ex.trim_slack_bytes = 2 << 30
     node = Node(cfg, name, TcpTransport(name, cfg.address, cfg.address(name)), ex)
     node.source = None
     if not a.dry_run:

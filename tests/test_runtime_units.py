@@ -344,8 +344,15 @@ def test_executor_trims_cache_only_when_no_collective_can_pend(monkeypatch):
         r._graphs[len(r._graphs)] = object()
         return "replay"
 
-    ex.trim_ok = lambda: False
-    assert ex._capture(r, cap) == "replay" and calls == []
+    monkeypatch.setattr(torch.cuda, "memory_reserved", lambda d=None: 10 << 30)
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda d=None: 1 << 30)
+    ex.device = "cuda:0"
+    ex.trim_slack_bytes = 16 << 30
+    seen = []
+    ex.trim_ok = lambda need: seen.append(need) or False
+    assert ex._capture(r, cap) == "replay" and calls == [] and seen == [False]
+    ex.trim_slack_bytes = 2 << 30                        # 9 GiB unused > 2 GiB slack: a need
+    assert ex._capture(r, cap) == "replay" and calls == [] and seen == [False, True]
     ex.trim_ok = None
     assert ex._capture(r, cap) == "replay" and calls == [1]
     assert ex._capture(r, lambda: "hit") == "hit" and calls == [1]      # no new graph: no trim
@@ -357,12 +364,16 @@ def test_executor_trims_cache_only_when_no_collective_can_pend(monkeypatch):
         def is_alive(self):
             return self.alive
 
+    alive = {"a": True, "b": True}
     rp = RoundPlane.__new__(RoundPlane)
+    rp.node = types.SimpleNamespace(membership=types.SimpleNamespace(is_alive=lambda m: alive[m]))
     rp.group = types.SimpleNamespace(_aborters=[], formed=False, members=[])
     assert rp.collectives_quiet()
     rp.group = types.SimpleNamespace(_aborters=[], formed=True, members=["a"])
     assert rp.collectives_quiet()                        # a one-member (solo) epoch
     rp.group = types.SimpleNamespace(_aborters=[], formed=True, members=["a", "b"])
-    assert not rp.collectives_quiet()
+    assert not rp.collectives_quiet() and rp.collectives_quiet(need=True)
+    alive["b"] = False                                   # a dead member: its gather may never end
+    assert not rp.collectives_quiet(need=True)
     rp.group = types.SimpleNamespace(_aborters=[Alive(True)], formed=False, members=[])
-    assert not rp.collectives_quiet()                    # an aborted communicator still tearing down
+    assert not rp.collectives_quiet(need=True)           # an aborted communicator still tearing down
