@@ -147,6 +147,7 @@ class HipExecutor(Executor):
         self._pool = None
         self.graphs_broken = False      # a capture failed: eager forwards only (see _capture)
         self.trim_ok = None             # callable(need) -> bool: may empty_cache run now (see _capture)
+        self._trim_wanted = False       # a new capture's trim is still owed (maybe_trim)
         self.trim_slack_bytes = 16 << 30      # reserved-but-unused cache that counts as a need to trim
         self.lock = threading.Lock()
         self.run_lock = threading.Lock()      # one forward (copy-in, replay, read-back) at a time
@@ -201,11 +202,12 @@ class HipExecutor(Executor):
         device while holding the interpreter lock: behind an RCCL gather pending
         on a dead member it stalled the whole node process, heartbeats included,
         until the communicator timed out (8-rank RCCL rehearsal, worker failover
-        with 4 / 8 chunks in flight).  ``trim_ok(need)`` (set by the node) says
-        whether to trim now: always when no collective can be pending; while an
-        RCCL epoch runs only when the cache's unused part exceeds
-        ``trim_slack_bytes`` (``need``: node processes sharing one GPU) and every
-        member is alive, so the wait is for gathers that are progressing."""
+        with 4 / 8 chunks in flight).  ``trim_ok(need)`` (set by the node,
+        ``RoundPlane.collectives_quiet``) says whether to trim now: always when no
+        collective can be pending; while an RCCL epoch runs only when the
+        cache's unused part exceeds ``trim_slack_bytes`` (``need``: node
+        processes sharing one GPU) and none of the node's gathers is in flight.
+        A trim that may not run now stays wanted (``maybe_trim``)."""
         before = len(r._graphs)
         try:
             out = fn()
@@ -218,11 +220,20 @@ class HipExecutor(Executor):
                     rr.graph_pool = self._pool
             return None
         if len(r._graphs) > before:
-            need = torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device) \
-                > self.trim_slack_bytes
-            if self.trim_ok is None or self.trim_ok(need):
-                torch.cuda.empty_cache()
+            self._trim_wanted = True
+            self.maybe_trim()
         return out
+
+    def maybe_trim(self) -> None:
+        """``empty_cache`` after new captures, when ``trim_ok(need)`` allows it
+        (see ``_capture``); otherwise it stays wanted for a later call."""
+        if not self._trim_wanted:
+            return
+        need = torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device) \
+            > self.trim_slack_bytes
+        if self.trim_ok is None or self.trim_ok(need):
+            self._trim_wanted = False
+            torch.cuda.empty_cache()
 
     def _forward(self, r, images, packed, slot: int = 0):
         """cls, prob of ``images`` on the private stream (caller holds run_lock);

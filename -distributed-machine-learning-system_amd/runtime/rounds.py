@@ -248,20 +248,30 @@ class RoundPlane:
                 "queued": len(self._queue)}
 
     def collectives_quiet(self, need: bool = False) -> bool:
-        """May HipExecutor's empty_cache run now?  It waits for every kernel on
-        the device with the interpreter lock held, a gather stuck on a dead peer
-        included.  True when no collective of this node can be pending (no epoch
-        of more than one member formed, no aborted communicator still tearing
-        down); with ``need`` (the cache holds more than its slack: node processes
-        sharing one GPU) also while every member of the epoch is alive -- its
-        gathers are progressing and the wait is short."""
+        """May HipExecutor's empty_cache run now?  It frees with hipFree, which
+        waits for every kernel of this process on the device with the
+        interpreter lock held -- a gather stuck on a peer that just died
+        included, and then nothing in the process runs (heartbeats, the failure
+        detector, the abort that would end the gather) until the RCCL watchdog
+        fires (8-rank rehearsal, worker failover: 120 s).  True when no collective
+        of this node can be pending: no epoch of more than one member formed and
+        no aborted communicator still tearing down; with ``need`` (the cache
+        holds more than its slack: node processes sharing one GPU) also on the
+        round driver thread -- the only thread that posts collectives -- once
+        every gather it posted has completed."""
         g = self.group
         if any(t.is_alive() for t in list(g._aborters)):
             return False
         if not g.formed or len(g.members) <= 1:
             return True
-        ms = self.node.membership
-        return need and all(ms.is_alive(m) for m in list(g.members))
+        return need and threading.current_thread() is self._thread and self.pending_collectives() == 0
+
+    def _maybe_trim(self) -> None:
+        """A trim the executor had to defer (``collectives_quiet``), retried at
+        the round driver's quiet points."""
+        fn = getattr(self.node.executor, "maybe_trim", None)
+        if fn is not None:
+            fn()
 
     def pending_collectives(self) -> int:
         """Posted gathers of this node that have not completed."""
@@ -311,6 +321,7 @@ class RoundPlane:
         buffer.  A GPU executor returns at once (timing events are kept for a
         later header); a host executor is timed here."""
         n = self.node
+        self._maybe_trim()
         mid, qnum, s, e = (int(v) for v in row)
         model = MODEL_NAMES[mid]
         delay = self.cfg.worker_start_delay_s + n.extra_delay_s
@@ -561,6 +572,7 @@ class RoundPlane:
                         continue
                     if self._released:
                         break
+                    self._maybe_trim()
                     with self.cv:
                         if not self._queue and not self._released and self._reform_at is None:
                             self.cv.wait(0.05)
@@ -886,6 +898,8 @@ class RoundPlane:
         reports rounds still pending the wait is short."""
         while True:
             busy = idle() if idle is not None else False
+            if not busy and not self._round_msgs:
+                self._maybe_trim()
             with self.cv:
                 msg = self._round_msgs.pop((epoch, seq), None)
                 if msg is None:

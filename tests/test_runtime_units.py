@@ -347,14 +347,19 @@ def test_executor_trims_cache_only_when_no_collective_can_pend(monkeypatch):
     monkeypatch.setattr(torch.cuda, "memory_reserved", lambda d=None: 10 << 30)
     monkeypatch.setattr(torch.cuda, "memory_allocated", lambda d=None: 1 << 30)
     ex.device = "cuda:0"
+    ex._trim_wanted = False
     ex.trim_slack_bytes = 16 << 30
     seen = []
     ex.trim_ok = lambda need: seen.append(need) or False
     assert ex._capture(r, cap) == "replay" and calls == [] and seen == [False]
     ex.trim_slack_bytes = 2 << 30                        # 9 GiB unused > 2 GiB slack: a need
     assert ex._capture(r, cap) == "replay" and calls == [] and seen == [False, True]
-    ex.trim_ok = None
-    assert ex._capture(r, cap) == "replay" and calls == [1]
+    assert ex._trim_wanted                               # owed: retried at a quiet point
+    ex.trim_ok = lambda need: True
+    ex.maybe_trim()
+    assert calls == [1] and not ex._trim_wanted
+    ex.maybe_trim()
+    assert calls == [1]                                  # nothing owed
     assert ex._capture(r, lambda: "hit") == "hit" and calls == [1]      # no new graph: no trim
 
     class Alive:
@@ -364,16 +369,30 @@ def test_executor_trims_cache_only_when_no_collective_can_pend(monkeypatch):
         def is_alive(self):
             return self.alive
 
-    alive = {"a": True, "b": True}
+    import threading
+    from collections import deque
+
+    class Work:
+        def __init__(self, done):
+            self.done = done
+
+        def is_completed(self):
+            return self.done
+
     rp = RoundPlane.__new__(RoundPlane)
-    rp.node = types.SimpleNamespace(membership=types.SimpleNamespace(is_alive=lambda m: alive[m]))
+    rp._thread = threading.current_thread()              # as if on the round driver
+    rp._inflight = deque()
     rp.group = types.SimpleNamespace(_aborters=[], formed=False, members=[])
     assert rp.collectives_quiet()
     rp.group = types.SimpleNamespace(_aborters=[], formed=True, members=["a"])
     assert rp.collectives_quiet()                        # a one-member (solo) epoch
     rp.group = types.SimpleNamespace(_aborters=[], formed=True, members=["a", "b"])
     assert not rp.collectives_quiet() and rp.collectives_quiet(need=True)
-    alive["b"] = False                                   # a dead member: its gather may never end
+    rp._inflight.append([3, Work(False), None, False])    # a gather still in flight: it may never end
+    assert not rp.collectives_quiet(need=True)
+    rp._inflight[0][1].done = True
+    assert rp.collectives_quiet(need=True)
+    rp._thread = None                                    # not the driver thread: it may post meanwhile
     assert not rp.collectives_quiet(need=True)
     rp.group = types.SimpleNamespace(_aborters=[Alive(True)], formed=False, members=[])
     assert not rp.collectives_quiet(need=True)           # an aborted communicator still tearing down
