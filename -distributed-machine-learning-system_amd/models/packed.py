@@ -807,7 +807,14 @@ class HipRunner:
             var = self.wino_variant if self.wino_variant is not None else 3
             return self.ops.conv2d_wino(x, c.wino, c.b, c.relu, residual, var)
         return self.ops.conv2d(x, c.w, c.b, c.kh, c.kw, c.stride, c.pad, c.relu, residual=residual, out=out,
-                               route=self.route)
+                               route=self.route | self._f16_route(x.shape[0]))
+
+    def _f16_route(self, nb: int) -> int:
+        """Measured per-model default on top of ``route``: ResNet50 fp16 at
+        B >= 768 skips the band-staged 3x3 at W 28 (+1.2 % at B = 1024, -0.4 % at
+        B = 400; ResNet18 fp16 keeps it: -0.7 % / -2.2 % without it at B = 400 /
+        1024; profiles/r6q_ab_r50_route_0_1.log, profiles/r6r_*)."""
+        return 1 if self.p.name == "resnet50" and nb >= 768 else 0
 
     def _blocks(self, blocks, x):
         """fp16 residual stages; with ``fuse_next_1x1`` a bottleneck block whose
