@@ -403,7 +403,8 @@ class RoundPlane:
             self._drive()
         finally:
             pr.disable()
-            pr.dump_stats(path)
+            # one file per driver thread (a re-formed plane starts a new one)
+            pr.dump_stats(f"{path}.{os.getpid()}.{threading.get_ident()}")
 
     def _drive(self) -> None:
         n = self.node

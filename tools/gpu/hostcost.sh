@@ -10,5 +10,5 @@ for n in 1 8; do
   timeout -k 10 300 python -u bench.py --dry-run --system --gpus $n --steps 400 --warmup 10 --sdfs-images 0 \
     --two-job-queries 2 > $OUT/hostcost_n$n.log 2>&1 || exit 15
 done
-IDUNNO_PROFILE_DRIVER=$OUT/drv8.prof IDUNNO_PROFILE_DRIVER_CPU=1 timeout -k 10 300 python -u bench.py --dry-run \
+IDUNNO_PROFILE_DRIVER=$OUT/drv8 IDUNNO_PROFILE_DRIVER_CPU=1 timeout -k 10 300 python -u bench.py --dry-run \
   --system --gpus 8 --steps 400 --warmup 10 --sdfs-images 0 --two-job-queries 2 > $OUT/hostcost_n8_prof.log 2>&1 || exit 16
