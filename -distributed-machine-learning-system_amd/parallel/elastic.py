@@ -199,6 +199,11 @@ class ElasticGroup:
             th.start()
             self._aborters = [t for t in self._aborters if t.is_alive()] + [th]
 
+    def aborting(self) -> bool:
+        """A communicator abort is still running on a background thread (its
+        collectives may still be on the device)."""
+        return any(t.is_alive() for t in list(self._aborters))
+
     def join_aborters(self, timeout: float | None = None) -> bool:
         """Wait (bounded by ``abort_join_s``) for background aborts to end;
         True if none is left running.  Used before a process exits."""

@@ -260,7 +260,7 @@ class RoundPlane:
         round driver thread -- the only thread that posts collectives -- once
         every gather it posted has completed."""
         g = self.group
-        if any(t.is_alive() for t in list(g._aborters)):
+        if g.aborting():
             return False
         if not g.formed or len(g.members) <= 1:
             return True

@@ -362,13 +362,6 @@ def test_executor_trims_cache_only_when_no_collective_can_pend(monkeypatch):
     assert calls == [1]                                  # nothing owed
     assert ex._capture(r, lambda: "hit") == "hit" and calls == [1]      # no new graph: no trim
 
-    class Alive:
-        def __init__(self, alive):
-            self.alive = alive
-
-        def is_alive(self):
-            return self.alive
-
     import threading
     from collections import deque
 
@@ -382,11 +375,14 @@ def test_executor_trims_cache_only_when_no_collective_can_pend(monkeypatch):
     rp = RoundPlane.__new__(RoundPlane)
     rp._thread = threading.current_thread()              # as if on the round driver
     rp._inflight = deque()
-    rp.group = types.SimpleNamespace(_aborters=[], formed=False, members=[])
+    def group(formed, members, aborting=False):
+        return types.SimpleNamespace(formed=formed, members=members, aborting=lambda: aborting)
+
+    rp.group = group(False, [])
     assert rp.collectives_quiet()
-    rp.group = types.SimpleNamespace(_aborters=[], formed=True, members=["a"])
+    rp.group = group(True, ["a"])
     assert rp.collectives_quiet()                        # a one-member (solo) epoch
-    rp.group = types.SimpleNamespace(_aborters=[], formed=True, members=["a", "b"])
+    rp.group = group(True, ["a", "b"])
     assert not rp.collectives_quiet() and rp.collectives_quiet(need=True)
     rp._inflight.append([3, Work(False), None, False])    # a gather still in flight: it may never end
     assert not rp.collectives_quiet(need=True)
@@ -394,5 +390,5 @@ def test_executor_trims_cache_only_when_no_collective_can_pend(monkeypatch):
     assert rp.collectives_quiet(need=True)
     rp._thread = None                                    # not the driver thread: it may post meanwhile
     assert not rp.collectives_quiet(need=True)
-    rp.group = types.SimpleNamespace(_aborters=[Alive(True)], formed=False, members=[])
+    rp.group = group(False, [], aborting=True)
     assert not rp.collectives_quiet(need=True)           # an aborted communicator still tearing down
