@@ -131,6 +131,41 @@ def test_pack_stem_split_exact_u8_cpu():
     assert err < 1e-6, err
 
 
+def test_pack_alex_stem_split_cpu():
+    """The fused AlexNet stem's operands (K layout of alex_stem_k_index, exact-u8
+    bias and border prefix sums) reproduce conv11x11/4(normalise(u)) in fp64."""
+    from idunno.models import reference as ref
+
+    torch.manual_seed(4)
+    w = torch.randn(64, 3, 11, 11) * 0.03
+    b = torch.randn(64) * 0.1
+    fs, scale, bias, psum = P.pack_alex_stem_split(w, b)
+    assert fs.shape == (2, 64, 17 * 32) and psum.shape == (12, 12, 64)
+    v = ((fs[0].double() + fs[1].double()) * scale).reshape(64, 17, 32)
+    ws = torch.zeros(64, 3, 11, 11, dtype=torch.float64)
+    used = torch.zeros(17, 32, dtype=torch.bool)
+    for i in range(11):
+        for j in range(11):
+            st, k0 = P.alex_stem_k_index(i, j)
+            assert not used[st, k0:k0 + 4].any()
+            used[st, k0:k0 + 4] = True
+            ws[:, :, i, j] = v[:, st, k0:k0 + 3]
+            assert (v[:, st, k0 + 3] == 0).all()              # the patch's 4th channel slot
+    assert (v[:, ~used] == 0).all()                            # slots no tap owns hold zeros
+    u = torch.randint(0, 256, (2, 47, 39, 3), dtype=torch.uint8)
+    H, W = 47, 39
+    want = F.conv2d(ref.preprocess_u8(u).double(), w.double(), b.double(), 4, 2)
+    got = F.conv2d(u.permute(0, 3, 1, 2).double(), ws, bias.double(), 4, 2)
+    ps = psum.double()
+    for oy in range(got.shape[2]):
+        hlo, hhi = max(0, 2 - 4 * oy), min(11, H + 2 - 4 * oy)
+        for ox in range(got.shape[3]):
+            wlo, whi = max(0, 2 - 4 * ox), min(11, W + 2 - 4 * ox)
+            got[:, :, oy, ox] += ps[hhi, whi] - ps[hlo, whi] - ps[hhi, wlo] + ps[hlo, wlo] - ps[11, 11]
+    err = ((got - want).abs().max() / want.abs().max()).item()
+    assert err < 1e-6, err
+
+
 def _emu_split_conv(x, sw, scale, cout, cin, k, stride, pad):
     """The kernel's arithmetic in fp64 on CPU: hi*hi + hi*lo + lo*hi."""
     xs = P.to_split(x).double().reshape(*x.shape[:-1], cin // 32, 2, 32)
@@ -387,6 +422,32 @@ def test_stem_split_fused(ops, B, hw):
     want = F.max_pool2d(want, 3, 2, 1).permute(0, 2, 3, 1)
     assert y.shape == (*want.shape[:3], 128)
     _check(P.from_split(y), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,W", [(3, 224, 224), (2, 100, 131), (1, 31, 23)])
+def test_alex_stem_split_fused(ops, B, H, W):
+    """uint8 -> normalise -> conv11x11/4 pad 2 -> +bias -> ReLU -> maxpool3x3/2, split
+    out, in one kernel (alex_stem.hip); ragged tiles and image borders included."""
+    from idunno.models import reference as ref
+
+    torch.manual_seed(B + H)
+    img = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=DEV)
+    w = torch.randn(64, 3, 11, 11) / (3 * 121) ** 0.5
+    b = torch.randn(64) * 0.1
+    fs, scale, bias, psum = P.pack_alex_stem_split(w, b)
+    y = ops.alex_stem_split(img, fs.to(DEV), bias.to(DEV), psum.to(DEV), scale)
+    x = ref.preprocess_u8(img).permute(0, 2, 3, 1)
+    want = _ref64(x, w, b, 4, 2, True).permute(0, 3, 1, 2)
+    want = F.max_pool2d(want, 3, 2, 0).permute(0, 2, 3, 1)
+    assert y.shape == (*want.shape[:3], 128)
+    _check(P.from_split(y), want)
+    # device-side window of an HBM-resident shard: rows start - offset .. + batch
+    big = torch.cat([img, img.flip(0)])
+    start = torch.tensor([B + 5], dtype=torch.long, device=DEV)
+    y2 = ops.alex_stem_split(big, fs.to(DEV), bias.to(DEV), psum.to(DEV), scale, start, B, 5)
+    assert torch.equal(y2, ops.alex_stem_split(img.flip(0).contiguous(), fs.to(DEV), bias.to(DEV),
+                                               psum.to(DEV), scale))
 
 
 @pytest.mark.gpu
