@@ -189,6 +189,11 @@ int conv_glds_pick(int M, int Cout);
 // split-fp16 (fp32-accurate) fused stem, exact-u8 form: w = [2][64][7*32] hi/lo of
 // w * s_c (pre-scaled by 1/acc_scale), bias = folded bias + full sum of w * c_c,
 // psum = [8][8][64] 2D prefix sums of w * c_c over (kh, kw); y = split [B][Hp][Wp][128]
+// fused split AlexNet stem: uint8 -> conv 11x11/4 (exact-u8, split weights) -> ReLU -> max pool 3x3/2
+// -> split [B][Hp][Wp][128]; w = [2][64][17*32] (models/packed.py pack_alex_stem_split)
+bool alex_stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum,
+                            float acc_scale, half_t* y, int B, int H, int W, const long long* start_idx,
+                            long long start_off, long long max_start, long long sub, int* ovf, hipStream_t st);
 void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
                        half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,
                        long long max_start, long long sub, int* ovf, hipStream_t st);

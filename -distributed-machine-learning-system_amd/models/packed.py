@@ -326,6 +326,51 @@ def pack_stem_split(w: torch.Tensor, b: torch.Tensor | None = None):
     return torch.stack([hi, lo]).contiguous(), 2.0 ** -e, bias.float().contiguous(), ps.float().contiguous()
 
 
+def alex_stem_k_index(kh: int, kw: int) -> tuple[int, int]:
+    """(K step, slot of 8-k group base) of tap (kh, kw) in the fused AlexNet stem's
+    K layout (alex_stem.hip): step kh holds taps 0..7 of row kh as 8 x 4 channels;
+    tail step 11 + t holds taps 8, 9 (k 0..7) and 10 (k 8..11) of row 2t, and the
+    same of row 2t + 1 at k 16..27.  Returns (step, k of channel 0)."""
+    if kw < 8:
+        return kh, 4 * kw
+    t, second = divmod(kh, 2)
+    base = 16 * second
+    return 11 + t, base + (4 * (kw - 8) if kw < 10 else 8)
+
+
+def pack_alex_stem_split(w: torch.Tensor, b: torch.Tensor | None = None):
+    """AlexNet conv1 [64, 3, 11, 11] (+ bias) -> operands of the fused split
+    AlexNet stem (alex_stem.hip alex_stem_split_kernel, exact-u8 form):
+
+      fs     [2, 64, 17*32] half: hi and lo of w' = w * s_c, s_c = 1/(255 std_c),
+             in the kernel's K layout (alex_stem_k_index), scaled by 2^e;
+      scale  2^-e;
+      bias   [64] f32: b + sum over all taps of w * c_c, c_c = -mean_c / std_c;
+      psum   [12, 12, 64] f32: 2D prefix sums over (kh, kw) of sum_c w * c_c (border
+             outputs get their in-image taps' sum from it)."""
+    cout, cin, kh, kw = w.shape
+    if (cout, cin, kh, kw) != (64, 3, 11, 11):
+        raise ValueError("the fused split AlexNet stem takes a [64, 3, 11, 11] conv")
+    w = w.double()
+    mean = torch.tensor(ref.IMAGENET_MEAN, dtype=torch.float64)
+    std = torch.tensor(ref.IMAGENET_STD, dtype=torch.float64)
+    ws = w * (1.0 / (255.0 * std)).view(1, 3, 1, 1)
+    p = torch.zeros(cout, 17, 32, dtype=torch.float64)
+    for i in range(kh):
+        for j in range(kw):
+            st, k0 = alex_stem_k_index(i, j)
+            p[:, st, k0:k0 + 3] = ws[:, :, i, j]
+    e = _split_scale(ws)
+    p = p.reshape(cout, 17 * 32) * (2.0 ** e)
+    hi = p.half()
+    lo = (p - hi.double()).half()
+    corr = (w * (-mean / std).view(1, 3, 1, 1)).sum(dim=1)            # [64, 11, 11]
+    ps = torch.zeros(12, 12, cout, dtype=torch.float64)
+    ps[1:, 1:] = corr.permute(1, 2, 0).cumsum(0).cumsum(1)
+    bias = (torch.zeros(cout, dtype=torch.float64) if b is None else b.double()) + ps[11, 11]
+    return torch.stack([hi, lo]).contiguous(), 2.0 ** -e, bias.float().contiguous(), ps.float().contiguous()
+
+
 def unpack_split_weight(c: "Conv") -> torch.Tensor:
     """Inverse of pack_split_weight -> fp32 [Cout, Cin, KH, KW] (hi + lo, unscaled)."""
     v = c.sw.double().reshape(c.cout, c.kh, c.kw, c.cin // SPLIT_BLOCK, 2, SPLIT_BLOCK)
@@ -370,6 +415,10 @@ def make_conv(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, relu: bool, dtype: str
     if tuple(conv.weight.shape) == (64, 3, 7, 7) and conv.stride[0] == 2 and conv.padding[0] == 3:
         # the exact-u8 stem: split (fp32 programs) or its hi parts alone (fp16, ops.stem_u8_f16)
         c.fs, c.fs_scale, c.fs_bias, c.fs_psum = pack_stem_split(*fold_bn_f64(conv.weight, conv.bias, bn))
+    elif dtype == "fp32" and tuple(conv.weight.shape) == (64, 3, 11, 11) and conv.stride[0] == 4 \
+            and conv.padding[0] == 2:
+        # the fused split AlexNet stem (ops.alex_stem_split)
+        c.fs, c.fs_scale, c.fs_bias, c.fs_psum = pack_alex_stem_split(*fold_bn_f64(conv.weight, conv.bias, bn))
     return c
 
 
@@ -938,11 +987,20 @@ class HipRunner:
         return all(c.sw is not None for b in p.blocks for c in [*b.convs, *([b.down] if b.down else [])])
 
     def _alexnet_split(self, first, img_u8, start, batch, start_offset):
-        """fp32-accurate AlexNet: split packed-row conv1 (fp32 out) -> pools into
-        the split layout -> split convs 2-5 -> split FCs (split-K), fp32 logits."""
+        """fp32-accurate AlexNet: the fused split stem (uint8 -> conv1 + ReLU + max
+        pool in one kernel, alex_stem.hip; without it: split packed-row conv1 with
+        fp32 out, then the pool into the split layout) -> split convs 2-5 -> split
+        FCs (split-K), fp32 logits."""
         o, p = self.ops, self.p
-        x = self._stem_f32(first, img_u8, start, batch, start_offset)
-        for k, v in p.features[1:]:
+        feats = p.features[1:]
+        if self.fuse_stem and first.fs is not None and first.kh == 11 and first.relu and feats \
+                and feats[0][0] == "pool" and tuple(feats[0][1]) == (3, 2, 0):
+            x = o.alex_stem_split(img_u8, first.fs, first.fs_bias, first.fs_psum, first.fs_scale, start, batch,
+                                  start_offset)
+            feats = feats[1:]
+        else:
+            x = self._stem_f32(first, img_u8, start, batch, start_offset)
+        for k, v in feats:
             x = self._conv_split(v, x) if k == "conv" else o.maxpool2d_split(x, *v)
         x = x.reshape(x.shape[0], -1)         # split [B, 6*6*2*256]: the split layout of the NHWC flatten
         for i, fc in enumerate(p.fcs):

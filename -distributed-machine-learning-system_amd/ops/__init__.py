@@ -65,6 +65,14 @@ def stem_split(img_u8, w, bias, psum, acc_scale: float, start=None, batch: int =
     return load().stem_split(img_u8, w, bias, psum, acc_scale, start, batch, start_offset, window, sub)
 
 
+def alex_stem_split(img_u8, w, bias, psum, acc_scale: float, start=None, batch: int = -1, start_offset: int = 0,
+                    window: int = -1, sub: int = 0):
+    """fp32-accurate fused AlexNet stem on split fp16: uint8 [B,224,224,3] ->
+    split [B,27,27,128] (normalise, conv 11x11/4 pad 2 + bias, ReLU, max pool
+    3x3/2); ``w, acc_scale, bias, psum`` = models.packed.pack_alex_stem_split(w, b)."""
+    return load().alex_stem_split(img_u8, w, bias, psum, acc_scale, start, batch, start_offset, window, sub)
+
+
 def stem_u8_f16(img_u8, w, bias, psum, acc_scale: float, start=None, batch: int = -1, start_offset: int = 0,
                 window: int = -1, sub: int = 0):
     """fp16 fused ResNet stem in the exact-u8 form: uint8 [B,224,224,3] -> fp16
