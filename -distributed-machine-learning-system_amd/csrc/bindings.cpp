@@ -1612,6 +1612,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("f32_from_split", &f32_from_split, "split-fp16 layout -> fp32 NHWC");
   m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),
         py::arg("k"), py::arg("s"), py::arg("pad"), py::arg("out") = py::none());
+  m.def("set_astem_ahead", &set_astem_ahead);
+  m.def("set_astem_variant", &set_astem_variant);
+  m.def("set_astem_phased", &set_astem_phased);
   m.def("alex_stem_split", &alex_stem_split, "fused split AlexNet stem (conv 11x11/4 + ReLU + max pool 3x3/2)",
         py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("psum"), py::arg("acc_scale"),
         py::arg("start") = py::none(), py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1,

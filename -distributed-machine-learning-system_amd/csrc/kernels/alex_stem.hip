@@ -25,13 +25,26 @@
 // within a step: 17 steps instead of 22 for 11 x 11 taps.
 //
 // Work item: a 4-row x 7-column tile of pooled outputs of one image = 9 conv rows
-// x 15 conv columns.  Wave w owns couts 16w .. 16w+15 (A fragments of all 17
-// steps, hi and lo, in 136 VGPRs for the whole launch) and computes all 9 conv
-// rows as 9 independent accumulator chains (lane & 15 = conv column, lane 15 an
-// unused column), so the pool is done in registers: horizontal 3-max by DPP row
-// shifts, vertical 3-max across the accumulators.  The tile's uint8 patch
-// (43 rows x 76 pixels) is prefetched into registers one tile ahead and staged in
-// LDS as [row][pixel][4] fp16.
+// x 15 conv columns.  Wave w owns couts 16w .. 16w+15 and computes all 9 conv rows
+// as 9 independent accumulator chains (lane & 15 = conv column, lane 15 an unused
+// column), so the pool is done in registers: horizontal 3-max by DPP row shifts,
+// vertical 3-max across the accumulators.  The tile's uint8 patch (43 rows x 76
+// pixels) is staged in LDS as [row][pixel][4] fp16; the border prefix sums live in
+// LDS too.
+//
+// Two forms (set_astem_variant; B = 500, tools/astem_ablate.py):
+//   alex_stem_split_kernel   one 256-thread workgroup per CU, A hi + lo in 136 VGPRs,
+//                            accumulators in AGPRs, patch loads one tile ahead:
+//                            MFMA loop, staging and epilogue run back to back
+//                            (~305 us);
+//   alex_stem_split_kernel2  (default) one 512-thread workgroup = two halves whose
+//                            MFMA loops and epilogue/staging phases alternate, so
+//                            each SIMD interleaves one wave's MFMAs with the other's
+//                            VALU work (~230 us; AlexNet b500 forward -3.8 %).
+//                            A lo moves to LDS to fit 256 registers a wave.
+// The waitcnt lesson of both: nothing issued before the tile loop may stay in
+// flight into it (vmcnt(0) ahead of the loop), or the loop's first-use waits on it
+// turn into waits on the next patch's loads from the second tile on.
 #include "../kernels.h"
 #include "../launch_util.h"
 
@@ -51,6 +64,9 @@ constexpr int NQUAD = IPR * QPR;             // 817
 constexpr int QPT = (NQUAD + 255) / 256;     // quads per thread (4)
 constexpr int NKS = KH + (KH + 1) / 2;       // 17 K steps
 constexpr int PATCH_BYTES = IPR * IPC * 8;   // 26144
+constexpr int PSUM_FLOATS = (KH + 1) * (KH + 1) * 64;   // border prefix sums [12][12][64] f32
+constexpr int LDS_BYTES = PATCH_BYTES + PSUM_FLOATS * 4; // 62,1xx B: one workgroup per CU anyway
+static_assert(PATCH_BYTES % 16 == 0, "float4 prefix-sum reads");
 static_assert(CRX <= 15, "one conv row per 16-lane fragment");
 static_assert(4 * 15 + XOFF + 12 <= IPC, "every B read of lane 15 stays inside the patch row");
 }  // namespace astem
@@ -118,27 +134,38 @@ __device__ __forceinline__ void astem_load(const uint8_t* __restrict__ img, cons
   }
 }
 
+// two uint8 of a pixel quad -> two exact fp16 values: v_perm_b32 builds the halves
+// 0x64XX = 1024 + XX (byte selectors 4..7 pick the 0x64 bytes of the constant, 0x0C a
+// zero byte), one packed subtract of 1024 leaves XX exactly.  17 VALU per quad instead
+// of a convert-to-f32, convert-to-f16 and pack per byte (~30)
+typedef uint32_t uint4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t astem_h2(uint32_t v) {
+  half2v h = __builtin_bit_cast(half2v, v) - half2v{(_Float16)1024.f, (_Float16)1024.f};
+  return __builtin_bit_cast(uint32_t, h);
+}
+
 // registers -> the patch in LDS as [row][pixel][r, g, b, 0] fp16 (bytes exact);
-// pixels outside the image (and whole quads never loaded) are 0
+// pixels outside the image (and whole quads never loaded) hold 0 bytes -> 0
 __device__ __forceinline__ void astem_store(char* patch, int tid, const AQuads& q) {
   using namespace astem;
+  constexpr uint32_t C = 0x64646464u;
 #pragma unroll
   for (int k = 0; k < QPT; ++k) {
     const int i = tid + 256 * k;
     if (i >= NQUAD) continue;
-    half8v o[2];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-#pragma unroll
-      for (int ch = 0; ch < 3; ++ch) {
-        const int byte = 3 * j + ch;
-        o[j >> 1][4 * (j & 1) + ch] = (half_t)(float)((q.d[k][byte >> 2] >> (8 * (byte & 3))) & 0xFFu);
-      }
-      o[j >> 1][4 * (j & 1) + 3] = (half_t)0.f;
-    }
-    half8v* d = reinterpret_cast<half8v*>(patch + (size_t)i * 32);   // quad i = row r, pixels 4qc .. 4qc+3
-    d[0] = o[0];
-    d[1] = o[1];
+    const uint32_t d0 = q.d[k][0], d1 = q.d[k][1], d2 = q.d[k][2];
+    uint4v o0, o1;
+    o0[0] = astem_h2(__builtin_amdgcn_perm(C, d0, 0x04010400u));                  // r0 g0
+    o0[1] = astem_h2(__builtin_amdgcn_perm(C, d0, 0x040C0402u));                  // b0 0
+    o0[2] = astem_h2(__builtin_amdgcn_perm(d1, d0, 0x0C040C03u) | 0x64006400u);   // r1 g1 (two dwords)
+    o0[3] = astem_h2(__builtin_amdgcn_perm(C, d1, 0x040C0401u));                  // b1 0
+    o1[0] = astem_h2(__builtin_amdgcn_perm(C, d1, 0x04030402u));                  // r2 g2
+    o1[1] = astem_h2(__builtin_amdgcn_perm(C, d2, 0x040C0400u));                  // b2 0
+    o1[2] = astem_h2(__builtin_amdgcn_perm(C, d2, 0x04020401u));                  // r3 g3
+    o1[3] = astem_h2(__builtin_amdgcn_perm(C, d2, 0x040C0403u));                  // b3 0
+    uint4v* d = reinterpret_cast<uint4v*>(patch + (size_t)i * 32);   // quad i = row r, pixels 4qc .. 4qc+3
+    d[0] = o0;
+    d[1] = o1;
   }
 }
 
@@ -165,6 +192,84 @@ __device__ __forceinline__ float astem_shl(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x100 | N, 0xF, 0xF, true));
 }
 
+// epilogue of one tile, registers only: border corrections, the 3x3/2 max pool (DPP
+// row shifts across columns, the accumulators across rows), bias, ReLU, split store
+__device__ __forceinline__ void astem_epilogue(float4v (&acc)[astem::CRY], const AStemGeom& g, int b, int py0,
+                                               int px0, int cx, int c0, const float* ps, float inv_scale,
+                                               float acc_scale, float4v bv, half_t* __restrict__ y) {
+  using namespace astem;
+  // ---- epilogue of tile t, registers only ----
+  // border conv outputs: their out-of-image taps saw u = 0, not the zero of x: add
+  // the sum over the in-image taps of w * c minus the full sum in the bias, from the
+  // 2D prefix sums S(kh, kw) (S(0, .) = S(., 0) = 0).  Rows with all 11 kernel rows
+  // in the image (all but the first and last conv row) need only the column part,
+  // S(11, whi) - S(11, wlo) - S(11, 11), computed once per tile
+  const int cc = px0 * PS + cx;              // this lane's conv column
+  const bool colv = cc < g.Wc;
+  const int wlo = max(0, CP - CS * cc), whi = max(0, min(KH, g.W + CP - CS * cc));
+  const bool colb = colv && (wlo > 0 || whi < KH);
+  float4v colcorr = float4v{0.f, 0.f, 0.f, 0.f};
+  if (colb) {
+    const float4v s_h = *reinterpret_cast<const float4v*>(ps + (KH * 12 + whi) * 64 + c0);
+    const float4v s_l = *reinterpret_cast<const float4v*>(ps + (KH * 12 + wlo) * 64 + c0);
+    const float4v s_f = *reinterpret_cast<const float4v*>(ps + (KH * 12 + KH) * 64 + c0);
+    colcorr = (s_h - s_l - s_f) * inv_scale;
+  }
+#pragma unroll
+  for (int r = 0; r < CRY; ++r) {
+    const int cr = py0 * PS + r;             // wave-uniform
+    if (cr < g.Hc) {
+      const int hlo = max(0, CP - CS * cr), hhi = min(KH, g.H + CP - CS * cr);
+      if (hlo > 0 || hhi < KH) {
+        if (colv) {
+          const float4v s_hh = *reinterpret_cast<const float4v*>(ps + (hhi * 12 + whi) * 64 + c0);
+          const float4v s_lh = *reinterpret_cast<const float4v*>(ps + (hlo * 12 + whi) * 64 + c0);
+          const float4v s_hl = *reinterpret_cast<const float4v*>(ps + (hhi * 12 + wlo) * 64 + c0);
+          const float4v s_ll = *reinterpret_cast<const float4v*>(ps + (hlo * 12 + wlo) * 64 + c0);
+          const float4v s_ff = *reinterpret_cast<const float4v*>(ps + (KH * 12 + KH) * 64 + c0);
+          acc[r] += (s_hh - s_lh - s_hl + s_ll - s_ff) * inv_scale;
+        }
+      } else {
+        acc[r] += colcorr;
+      }
+    }
+    // horizontal 3-max: lane cx holds max over conv columns cx .. cx+2
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float v = acc[r][e];
+      acc[r][e] = fmaxf(v, fmaxf(astem_shl<1>(v), astem_shl<2>(v)));
+    }
+  }
+  const int px = cx >> 1;
+  const int ox = px0 + px;
+  const bool col_ok = !(cx & 1) && px < PTX && ox < g.Wp;
+  bool bad = false;
+#pragma unroll
+  for (int py = 0; py < PTY; ++py) {
+    const int oy = py0 + py;
+    if (oy >= g.Hp) break;                   // uniform
+    float4v m;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      m[e] = fmaxf(fmaxf(acc[2 * py][e], acc[2 * py + 1][e]), acc[2 * py + 2][e]);
+      m[e] = fmaxf(m[e] * acc_scale + bv[e], 0.f);     // bias and ReLU commute with the max
+    }
+    if (col_ok) {
+      constexpr float kMax = 65504.f;
+      bad |= !(fabsf(m[0]) < kMax && fabsf(m[1]) < kMax && fabsf(m[2]) < kMax && fabsf(m[3]) < kMax);
+      half4v h, l;
+      split_f16x4(m, h, l);
+      half_t* dst = y + (((size_t)b * g.Hp + oy) * g.Wp + ox) * 128 + split_off(c0);
+      *reinterpret_cast<half4v*>(dst) = h;
+      *reinterpret_cast<half4v*>(dst + 32) = l;
+    }
+  }
+  if (bad && g.ovf != nullptr) *g.ovf = 1;
+}
+
+// ABL: ablation bits for tools/astem_ablate.py (0 in production): 1 no MFMA loop,
+// 2 no epilogue (accumulators kept alive by a never-taken store), 4 no patch staging
+template <bool AHEAD, int ABL = 0>
 __global__ void __launch_bounds__(256, 1)
 alex_stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w, const float* __restrict__ bias,
                        const float* __restrict__ psum, float acc_scale, half_t* __restrict__ y, const AStemGeom g,
@@ -199,7 +304,14 @@ alex_stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict
   const float4v bv = *reinterpret_cast<const float4v*>(bias + c0);
   const float inv_scale = 1.f / acc_scale;
 
+  // the border prefix sums go to LDS once: the corrections of edge tiles then cost
+  // LDS reads, not dependent L2 round trips inside the epilogue
+  float* ps = reinterpret_cast<float*>(smem + PATCH_BYTES);
+  for (int i = tid; i < PSUM_FLOATS / 4; i += 256)
+    reinterpret_cast<float4v*>(ps)[i] = reinterpret_cast<const float4v*>(psum)[i];
   astem_store(smem, tid, q);
+  int tn = t + gridDim.x;
+  if (AHEAD && tn < g.ntiles) astem_load(img, g, tn, tid, q);   // one tile ahead (held in AGPRs)
   __syncthreads();
 
   // per-lane patch byte offsets (conv row 0): main steps read pixels
@@ -209,6 +321,10 @@ alex_stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict
   const uint32_t mainb = (uint32_t)(4 * cx + XOFF + 2 * fch) * 8u;
   const uint32_t tailb = (uint32_t)(4 * cx + XOFF + 8 + 2 * (fch & 1)) * 8u;
   const int trow = fch >> 1;
+  // the A loads above must not stay in flight into the tile loop: the waitcnt pass
+  // would put their vmcnt waits inside the loop, where from the second tile on they
+  // wait for the next patch's global loads instead (a stall on every K step)
+  __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
 
   for (;;) {
     int b, py0, px0;
@@ -223,6 +339,7 @@ alex_stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict
     astem_read_b(smem, 0, mainb, tailb, trow, bf[0]);
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
+      if (ABL & 1) break;
       if (s + 1 < NKS) astem_read_b(smem, s + 1, mainb, tailb, trow, bf[(s + 1) & 1]);
 #pragma unroll
       for (int r = 0; r < CRY; ++r)
@@ -237,65 +354,160 @@ alex_stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict
     // the next tile's patch loads go out now (not a tile ahead: the 136 A registers, 36
     // accumulators and 9 B fragments leave no room to hold them across the MFMA loop)
     // and land while this tile's epilogue runs
-    const int tnext = t + gridDim.x;
-    if (tnext < g.ntiles) astem_load(img, g, tnext, tid, q);
+    const int tnext = tn;
+    if constexpr (AHEAD) {
+      if (!(ABL & 4) && tnext < g.ntiles) astem_store(smem, tid, q);
+      tn = tnext + gridDim.x;
+    } else {
+      tn = tnext + gridDim.x;
+      if (tnext < g.ntiles) astem_load(img, g, tnext, tid, q);
+    }
 
-    // ---- epilogue of tile t, registers only ----
-    const int cc = px0 * PS + cx;              // this lane's conv column
-    int wlo = max(0, CP - CS * cc), whi = min(KH, g.W + CP - CS * cc);
+    if constexpr ((ABL & 2) != 0) {
+      if (g.B < 0) {                           // never: keeps the MFMA loop alive
 #pragma unroll
-    for (int r = 0; r < CRY; ++r) {
-      const int cr = py0 * PS + r;
-      const int hlo = max(0, CP - CS * cr), hhi = min(KH, g.H + CP - CS * cr);
-      if ((hlo > 0 || hhi < KH || wlo > 0 || whi < KH) && cr < g.Hc && cc < g.Wc) {
-        // border conv output: its out-of-image taps saw u = 0, not the zero of x:
-        // add sum over the in-image taps of w * c minus the full sum in the bias
-        const float4v s_hh = *reinterpret_cast<const float4v*>(psum + (hhi * 12 + whi) * 64 + c0);
-        const float4v s_lh = *reinterpret_cast<const float4v*>(psum + (hlo * 12 + whi) * 64 + c0);
-        const float4v s_hl = *reinterpret_cast<const float4v*>(psum + (hhi * 12 + wlo) * 64 + c0);
-        const float4v s_ll = *reinterpret_cast<const float4v*>(psum + (hlo * 12 + wlo) * 64 + c0);
-        const float4v s_ff = *reinterpret_cast<const float4v*>(psum + (KH * 12 + KH) * 64 + c0);
-        acc[r] += (s_hh - s_lh - s_hl + s_ll - s_ff) * inv_scale;
+        for (int r = 0; r < CRY; ++r) *reinterpret_cast<float4v*>(y + 8 * r) = acc[r];
       }
-      // horizontal 3-max: lane cx holds max over conv columns cx .. cx+2
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = acc[r][e];
-        acc[r][e] = fmaxf(v, fmaxf(astem_shl<1>(v), astem_shl<2>(v)));
-      }
-      __builtin_amdgcn_sched_barrier(0);       // one row's correction loads live at a time
+      if (AHEAD && !(ABL & 4) && tn < g.ntiles) astem_load(img, g, tn, tid, q);
+      __syncthreads();
+      if (tnext >= g.ntiles) break;
+      t = tnext;
+      continue;
     }
-    const int px = cx >> 1;
-    const int ox = px0 + px;
-    const bool col_ok = !(cx & 1) && px < PTX && ox < g.Wp;
-    bool bad = false;
-#pragma unroll
-    for (int py = 0; py < PTY; ++py) {
-      const int oy = py0 + py;
-      if (oy >= g.Hp) break;                   // uniform
-      float4v m;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        m[e] = fmaxf(fmaxf(acc[2 * py][e], acc[2 * py + 1][e]), acc[2 * py + 2][e]);
-        m[e] = fmaxf(m[e] * acc_scale + bv[e], 0.f);     // bias and ReLU commute with the max
-      }
-      if (col_ok) {
-        constexpr float kMax = 65504.f;
-        bad |= !(fabsf(m[0]) < kMax && fabsf(m[1]) < kMax && fabsf(m[2]) < kMax && fabsf(m[3]) < kMax);
-        half4v h, l;
-        split_f16x4(m, h, l);
-        half_t* dst = y + (((size_t)b * g.Hp + oy) * g.Wp + ox) * 128 + split_off(c0);
-        *reinterpret_cast<half4v*>(dst) = h;
-        *reinterpret_cast<half4v*>(dst + 32) = l;
-      }
-    }
-    if (bad && g.ovf != nullptr) *g.ovf = 1;
-    if (tnext < g.ntiles) astem_store(smem, tid, q);
+    astem_epilogue(acc, g, b, py0, px0, cx, c0, ps, inv_scale, acc_scale, bv, y);
+    if (!AHEAD && tnext < g.ntiles) astem_store(smem, tid, q);
+    // the loads of the tile after next go out behind this tile's border-correction
+    // loads and output stores (vmcnt retires in order: those waits do not cover them)
+    // and land during tile tnext's MFMA loop
+    if (AHEAD && !(ABL & 4) && tn < g.ntiles) astem_load(img, g, tn, tid, q);
     __syncthreads();                           // tile tnext's patch is in LDS
     if (tnext >= g.ntiles) break;
     t = tnext;
   }
 }
+
+// Phased form: ONE workgroup of 512 threads per CU = two halves of 4 waves, each half
+// on its own tiles (tile 2*blockIdx + h, then + 2*gridDim).  Phases alternate: while
+// half 0 runs a tile's MFMA loop, half 1 runs its previous tile's epilogue and stages
+// its next patch, then the roles swap (one workgroup barrier per phase).  SIMD k holds
+// wave k of each half, so one wave's VALU/LDS/global work issues between the other's
+// MFMAs instead of after them (the one-half form runs them back to back: MFMA loop
+// 157 us + staging ~60 + epilogue ~90 at B = 500, tools/astem_ablate.py).  Two waves
+// per SIMD leave 256 registers a wave: the A lo fragments move to LDS (one 16-byte read
+// per K step, reused by 9 MFMAs) next to the two patches and the prefix sums.
+namespace astem {
+constexpr int PS_OFF = 2 * PATCH_BYTES;                  // border prefix sums
+constexpr int AL_OFF = PS_OFF + PSUM_FLOATS * 4;         // A lo [64][17*32] fp16
+constexpr int LDS2_BYTES = AL_OFF + 64 * NKS * 32 * 2;   // 158,784 B
+static_assert(LDS2_BYTES <= 160 * 1024, "one workgroup per CU");
+}  // namespace astem
+
+template <int ABL = 0>   // ablations (tools/astem_ablate.py): 1 no MFMA loop, 2 no E phase
+__global__ void __launch_bounds__(512, 1)
+alex_stem_split_kernel2(const uint8_t* __restrict__ img, const half_t* __restrict__ w, const float* __restrict__ bias,
+                        const float* __restrict__ psum, float acc_scale, half_t* __restrict__ y, const AStemGeom g,
+                        const long long* __restrict__ start_idx, long long start_off, long long max_start,
+                        long long sub) {
+  using namespace astem;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (start_idx != nullptr) {
+    long long s = *start_idx - start_off;
+    s = (s < 0 ? 0 : (s > max_start ? max_start : s)) + sub;
+    img += (size_t)s * g.H * g.W * 3;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = wave >> 2, w4 = wave & 3, htid = tid & 255;
+  const int cx = lane & 15, fch = lane >> 4;
+  const int stride = 2 * gridDim.x;
+  // tiles of half h: t0 + k * stride, k < nh; C(k) runs in phase 2k + h, E(k) in 2k + h + 1
+  const int f0 = 2 * blockIdx.x, f1 = f0 + 1;
+  const int n0 = f0 < g.ntiles ? (g.ntiles - 1 - f0) / stride + 1 : 0;
+  const int n1 = f1 < g.ntiles ? (g.ntiles - 1 - f1) / stride + 1 : 0;
+  if (n0 == 0) return;                          // uniform (n0 >= n1)
+  const int t0 = h ? f1 : f0, nh = h ? n1 : n0;
+  const int nphase = max(2 * n0 + 1, 2 * n1 + 2);
+  char* patch = smem + h * PATCH_BYTES;
+  float* ps = reinterpret_cast<float*>(smem + PS_OFF);
+  const char* al = smem + AL_OFF;
+
+  AQuads q;
+  if (nh > 0) astem_load(img, g, t0, htid, q);
+  half8v aH[NKS];
+  const uint32_t aoff = (uint32_t)((16 * w4 + cx) * (NKS * 32) + 8 * fch) * 2u;   // bytes, hi and lo alike
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) aH[s] = *reinterpret_cast<const half8v*>(reinterpret_cast<const char*>(w) + aoff + s * 64);
+  for (int i = tid; i < PSUM_FLOATS / 4; i += 512)
+    reinterpret_cast<float4v*>(ps)[i] = reinterpret_cast<const float4v*>(psum)[i];
+  for (int i = tid; i < 64 * NKS * 32 / 8; i += 512)
+    reinterpret_cast<half8v*>(smem + AL_OFF)[i] = reinterpret_cast<const half8v*>(w + 64 * NKS * 32)[i];
+  const int c0 = 16 * w4 + 4 * fch;
+  const float4v bv = *reinterpret_cast<const float4v*>(bias + c0);
+  const float inv_scale = 1.f / acc_scale;
+  if (nh > 0) astem_store(patch, htid, q);
+  __builtin_amdgcn_s_waitcnt(0x0F70);           // vmcnt(0): nothing of the prologue stays in flight
+  if (nh > 1) astem_load(img, g, t0 + stride, htid, q);
+  const uint32_t mainb = (uint32_t)(4 * cx + XOFF + 2 * fch) * 8u;
+  const uint32_t tailb = (uint32_t)(4 * cx + XOFF + 8 + 2 * (fch & 1)) * 8u;
+  const int trow = fch >> 1;
+  __syncthreads();
+
+  float4v acc[CRY];
+#pragma unroll
+  for (int r = 0; r < CRY; ++r) acc[r] = float4v{0.f, 0.f, 0.f, 0.f};
+  for (int p = 0; p < nphase; ++p) {
+    const int d = p - h;                        // wave-uniform
+    if (d >= 0 && !(d & 1) && (d >> 1) < nh) {
+      // ---- C(k): the MFMA loop of tile t0 + k * stride on this half's patch ----
+#pragma unroll
+      for (int r = 0; r < CRY; ++r) acc[r] = float4v{0.f, 0.f, 0.f, 0.f};
+      if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+        for (int r = 0; r < CRY; ++r) acc[r] = *reinterpret_cast<const float4v*>(patch + 64 * r + 16 * fch);
+      } else {
+      half8v bf[2][CRY];
+      half8v al_s[2];
+      astem_read_b(patch, 0, mainb, tailb, trow, bf[0]);
+      al_s[0] = *reinterpret_cast<const half8v*>(al + aoff);
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        if (s + 1 < NKS) {
+          astem_read_b(patch, s + 1, mainb, tailb, trow, bf[(s + 1) & 1]);
+          al_s[(s + 1) & 1] = *reinterpret_cast<const half8v*>(al + aoff + (s + 1) * 64);
+        }
+#pragma unroll
+        for (int r = 0; r < CRY; ++r)
+          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aH[s], bf[s & 1][r], acc[r], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < CRY; ++r)
+          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al_s[s & 1], bf[s & 1][r], acc[r], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      }
+    } else if (d >= 1 && (d & 1) && ((d - 1) >> 1) < nh) {
+      // ---- E(k): stage tile k+1's patch, send tile k+2's loads, epilogue of tile k ----
+      const int kk = (d - 1) >> 1;
+      if constexpr ((ABL & 2) != 0) {
+        if (g.B < 0) {                           // never: keeps the MFMA loop alive
+#pragma unroll
+          for (int r = 0; r < CRY; ++r) *reinterpret_cast<float4v*>(y + 8 * r) = acc[r];
+        }
+        __syncthreads();
+        continue;
+      }
+      if (kk + 1 < nh) astem_store(patch, htid, q);
+      if (kk + 2 < nh) astem_load(img, g, t0 + (kk + 2) * stride, htid, q);
+      int b, py0, px0;
+      astem_tile(g, t0 + kk * stride, b, py0, px0);
+      astem_epilogue(acc, g, b, py0, px0, cx, c0, ps, inv_scale, acc_scale, bv, y);
+    }
+    __syncthreads();
+  }
+}
+
+static int g_astem_variant = 64;
+void set_astem_ahead(bool on) { g_astem_variant = on ? 0 : 16; }
+void set_astem_phased(bool on) { g_astem_variant = on ? 64 : 0; }
+void set_astem_variant(int v) { g_astem_variant = v; }
 
 bool alex_stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum,
                             float acc_scale, half_t* y, int B, int H, int W, const long long* start_idx,
@@ -318,8 +530,27 @@ bool alex_stem_split_launch(const uint8_t* img, const half_t* w, const float* bi
   if (g.ntiles <= 0) return true;
   const int per = device_cu_count();          // one workgroup per CU (all 512 registers)
   const int grid = g.ntiles < per ? g.ntiles : per;
-  hipLaunchKernelGGL(alex_stem_split_kernel, dim3(grid), dim3(256), PATCH_BYTES, st, img, w, bias, psum,
-                     acc_scale, y, g, start_idx, start_off, max_start, sub);
+  auto k = alex_stem_split_kernel<true>;
+  switch (g_astem_variant) {
+    case 16: k = alex_stem_split_kernel<false>; break;
+    case 1: k = alex_stem_split_kernel<true, 1>; break;
+    case 2: k = alex_stem_split_kernel<true, 2>; break;
+    case 4: k = alex_stem_split_kernel<true, 4>; break;
+    case 6: k = alex_stem_split_kernel<true, 6>; break;
+    default: break;
+  }
+  if (g_astem_variant >= 64) {
+    const int grid2 = (g.ntiles + 1) / 2 < per ? (g.ntiles + 1) / 2 : per;
+    auto k2 = alex_stem_split_kernel2<0>;
+    if (g_astem_variant == 65) k2 = alex_stem_split_kernel2<1>;
+    if (g_astem_variant == 66) k2 = alex_stem_split_kernel2<2>;
+    ensure_lds_attr(reinterpret_cast<const void*>(k2), LDS2_BYTES);
+    hipLaunchKernelGGL(k2, dim3(grid2), dim3(512), LDS2_BYTES, st, img, w, bias, psum, acc_scale,
+                       y, g, start_idx, start_off, max_start, sub);
+    return true;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), LDS_BYTES, st, img, w, bias, psum, acc_scale, y, g, start_idx,
+                     start_off, max_start, sub);
   return true;
 }
 

@@ -425,10 +425,22 @@ def test_stem_split_fused(ops, B, hw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,H,W", [(3, 224, 224), (2, 100, 131), (1, 31, 23)])
-def test_alex_stem_split_fused(ops, B, H, W):
+@pytest.mark.parametrize("variant", [0, 64])
+@pytest.mark.parametrize("B,H,W", [(3, 224, 224), (2, 100, 131), (1, 31, 23), (5, 64, 72)])
+def test_alex_stem_split_fused(ops, B, H, W, variant):
     """uint8 -> normalise -> conv11x11/4 pad 2 -> +bias -> ReLU -> maxpool3x3/2, split
-    out, in one kernel (alex_stem.hip); ragged tiles and image borders included."""
+    out, in one kernel (alex_stem.hip); ragged tiles and image borders included.
+    variant: the kernel form (set_astem_variant; 0 one half per CU, 64 phased halves)."""
+    from idunno.models import reference as ref
+
+    ops.load().set_astem_variant(variant)
+    try:
+        _alex_stem_check(ops, B, H, W)
+    finally:
+        ops.load().set_astem_variant(64)
+
+
+def _alex_stem_check(ops, B, H, W):
     from idunno.models import reference as ref
 
     torch.manual_seed(B + H)
