@@ -1615,6 +1615,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_astem_ahead", &set_astem_ahead);
   m.def("set_astem_variant", &set_astem_variant);
   m.def("set_astem_phased", &set_astem_phased);
+  m.def("set_stem_prewait", &set_stem_prewait);
   m.def("alex_stem_split", &alex_stem_split, "fused split AlexNet stem (conv 11x11/4 + ReLU + max pool 3x3/2)",
         py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("psum"), py::arg("acc_scale"),
         py::arg("start") = py::none(), py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1,

@@ -197,6 +197,7 @@ void set_astem_variant(int v);   // tools/astem_ablate.py: 0 production, 16 load
 bool alex_stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum,
                             float acc_scale, half_t* y, int B, int H, int W, const long long* start_idx,
                             long long start_off, long long max_start, long long sub, int* ovf, hipStream_t st);
+void set_stem_prewait(bool on);  // A/B switch: vmcnt(0) ahead of the split stem's tile loop
 void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
                        half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,
                        long long max_start, long long sub, int* ovf, hipStream_t st);

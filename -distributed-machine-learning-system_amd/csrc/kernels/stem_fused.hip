@@ -229,6 +229,11 @@ stem_fused_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
   const int c8 = tid & 7, vpx = (tid >> 3) % PTX, vpy2 = tid / (8 * PTX);
   const int cx = frow;   // conv column of this lane in every fragment
 
+  // nothing issued above may stay in flight into the tile loop: the waitcnt pass puts
+  // the first-use waits of the A fragments / pool bias inside the loop, where from the
+  // second tile on they wait for the next patch's loads and the last tile's output
+  // stores instead (alex_stem.hip has the measurement)
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
   while (true) {
     int b, py0, px0;
     tile_coords(g, t, b, py0, px0);
@@ -412,7 +417,7 @@ __device__ __forceinline__ void tap_range(int o, int n, int& lo, int& hi) {
 // F16: the fp16 programs' stem in the same exact-u8 form -- only the hi
 // MFMA (w' rounded to fp16 once; the input u is exact, unlike the normalised
 // fp16 input of stem_fused_kernel) and a plain fp16 [B][Hp][Wp][64] output
-template <int NIWS, int RP = 1, bool F16 = false>
+template <int NIWS, int RP = 1, bool F16 = false, bool PREWAIT = true>
 __global__ void __launch_bounds__(256, NIWS == 1 ? 3 : 2)
 stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w, const float* __restrict__ bias,
                   const float* __restrict__ psum, float acc_scale, half_t* __restrict__ y, const StemGeom g,
@@ -466,6 +471,11 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
   }
   const int cx = frow;
 
+  // nothing issued above may stay in flight into the tile loop: the waitcnt pass puts
+  // the first-use waits of the A fragments / pool bias inside the loop, where from the
+  // second tile on they wait for the next patch's loads and the last tile's output
+  // stores instead (alex_stem.hip has the measurement)
+  if (PREWAIT) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
   while (true) {
     int b, py0, px0;
     tile_coords(g, t, b, py0, px0);
@@ -641,6 +651,9 @@ stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w,
   }
 }
 
+static int g_stem_prewait = 1;
+void set_stem_prewait(bool on) { g_stem_prewait = on; }
+
 void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum, float acc_scale,
                        half_t* y, int B, int H, int W, const long long* start_idx, long long start_off,
                        long long max_start, long long sub, int* ovf, hipStream_t st) {
@@ -659,7 +672,8 @@ void stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, c
   g.ntiles = B * g.tiles_x * g.tiles_y;
   const int per = 3 * device_cu_count();
   const int grid = g.ntiles < per ? g.ntiles : per;
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(stem_split_kernel<1, 2>), dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias,
+  auto k = g_stem_prewait ? stem_split_kernel<1, 2> : stem_split_kernel<1, 2, false, false>;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), stem_s::LDS, st, img, w, bias,
                      psum, acc_scale, y, g, start_idx, start_off, max_start, sub);
 }
 
