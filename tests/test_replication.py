@@ -166,9 +166,10 @@ def test_bulk_and_per_chunk_same_c2_without_configured_batchsize():
 
 
 def test_whole_query_fast_path_and_bulk_fallback_agree():
-    """A round answering every chunk of its query in assignment order takes the
-    whole-query path (_whole_ok); reordered or partial rounds take the bulk path.
-    Both leave the tables per-chunk record_result leaves."""
+    """A round answering every chunk of its query (in any order: the round lists
+    members in group order, the plan has the scheduler's sampled order) takes the
+    whole-query path (_whole_ok); partial rounds take the bulk path.  Both leave
+    the tables per-chunk record_result leaves."""
     import numpy as np
 
     from idunno.runtime.jobstate import JobState
@@ -186,7 +187,7 @@ def test_whole_query_fast_path_and_bulk_fallback_agree():
             assert a.record_results(recs, now=2.0) == W
         elif q == 2:
             rev = recs[::-1]
-            assert not a._whole_ok(rev) and a._bulk_ok(rev)
+            assert a._whole_ok(rev) and a._bulk_ok(rev)
             assert a.record_results(rev, now=2.0) == W
         else:
             assert not a._whole_ok(recs[:2])
