@@ -1268,6 +1268,50 @@ torch::Tensor alex_stem_split(torch::Tensor img, torch::Tensor w, torch::Tensor 
   return y;
 }
 
+torch::Tensor alex_stem_u8_f16(torch::Tensor img, torch::Tensor w, torch::Tensor bias, torch::Tensor psum,
+                              double acc_scale, c10::optional<torch::Tensor> start, int64_t batch,
+                              int64_t start_offset, int64_t window, int64_t sub) {
+  CHECK_DEV(img);
+  CHECK_DEV(w);
+  CHECK_DEV(bias);
+  CHECK_DEV(psum);
+  CHECK_CONTIG(img);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(bias);
+  CHECK_CONTIG(psum);
+  CHECK_DT(img, torch::kUInt8);
+  CHECK_DT(w, torch::kHalf);
+  CHECK_DT(bias, torch::kFloat);
+  CHECK_DT(psum, torch::kFloat);
+  TORCH_CHECK(w.device() == img.device() && bias.device() == img.device() && psum.device() == img.device(),
+              "operands on different devices");
+  TORCH_CHECK(img.dim() == 4 && img.size(3) == 3, "img must be [B, H, W, 3] uint8");
+  TORCH_CHECK(w.dim() == 3 && w.size(0) == 2 && w.size(1) == 64 && w.size(2) == 17 * 32,
+              "split AlexNet stem weight must be [2, 64, 17*32]");
+  TORCH_CHECK(bias.numel() == 64, "bias must have 64 entries");
+  TORCH_CHECK(psum.numel() == 12 * 12 * 64, "psum must be [12, 12, 64]");
+  const int H = img.size(1), W = img.size(2);
+  int B;
+  long long max_start;
+  const long long* sp = window_args(img, start, batch, window, sub, B, max_start);
+  TORCH_CHECK(H >= 11 && W >= 11, "image too small");
+  TORCH_CHECK((long)B * H * W * 3 < (1L << 31), "batch too large");
+  const int Hc = (H + 4 - 11) / 4 + 1, Wc = (W + 4 - 11) / 4 + 1;
+  const int Hp = (Hc - 3) / 2 + 1, Wp = (Wc - 3) / 2 + 1;
+  TORCH_CHECK(Hc >= 3 && Wc >= 3, "image too small for the pool");
+  TORCH_CHECK((long)B * Hp * Wp * 128 < (1L << 31), "batch too large");
+  auto y = torch::empty({B, Hp, Wp, 64}, img.options().dtype(torch::kHalf));
+  if (B) {
+    TORCH_CHECK(alex_stem_u8_f16_launch(img.data_ptr<uint8_t>(), reinterpret_cast<const half_t*>(w.data_ptr()),
+                                        bias.data_ptr<float>(), psum.data_ptr<float>(), (float)acc_scale,
+                                        reinterpret_cast<half_t*>(y.data_ptr()), B, H, W, sp, start_offset, max_start,
+                                        sp ? sub : 0, cur_stream()),
+                "alex stem: bad geometry");
+    check_launch("alex_stem_u8_f16");
+  }
+  return y;
+}
+
 torch::Tensor stem_split(torch::Tensor img, torch::Tensor w, torch::Tensor bias, torch::Tensor psum, double acc_scale,
                          c10::optional<torch::Tensor> start, int64_t batch, int64_t start_offset, int64_t window,
                          int64_t sub) {
@@ -1613,6 +1657,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),
         py::arg("k"), py::arg("s"), py::arg("pad"), py::arg("out") = py::none());
   m.def("set_astem_ahead", &set_astem_ahead);
+  m.def("alex_stem_u8_f16", &alex_stem_u8_f16, "fp16 fused AlexNet stem (exact-u8 form, hi MFMA only)",
+        py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("psum"), py::arg("acc_scale"),
+        py::arg("start") = py::none(), py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1,
+        py::arg("sub") = 0);
   m.def("set_astem_variant", &set_astem_variant);
   m.def("set_astem_phased", &set_astem_phased);
   m.def("set_stem_prewait", &set_stem_prewait);

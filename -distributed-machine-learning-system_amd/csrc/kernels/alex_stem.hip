@@ -194,6 +194,8 @@ __device__ __forceinline__ float astem_shl(float v) {
 
 // epilogue of one tile, registers only: border corrections, the 3x3/2 max pool (DPP
 // row shifts across columns, the accumulators across rows), bias, ReLU, split store
+// (F16: plain fp16 [B][Hp][Wp][64], the fp16 programs' stem)
+template <bool F16 = false>
 __device__ __forceinline__ void astem_epilogue(float4v (&acc)[astem::CRY], const AStemGeom& g, int b, int py0,
                                                int px0, int cx, int c0, const float* ps, float inv_scale,
                                                float acc_scale, float4v bv, half_t* __restrict__ y) {
@@ -254,7 +256,12 @@ __device__ __forceinline__ void astem_epilogue(float4v (&acc)[astem::CRY], const
       m[e] = fmaxf(fmaxf(acc[2 * py][e], acc[2 * py + 1][e]), acc[2 * py + 2][e]);
       m[e] = fmaxf(m[e] * acc_scale + bv[e], 0.f);     // bias and ReLU commute with the max
     }
-    if (col_ok) {
+    if (col_ok && F16) {
+      half4v o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (half_t)m[e];
+      *reinterpret_cast<half4v*>(y + (((size_t)b * g.Hp + oy) * g.Wp + ox) * 64 + c0) = o;
+    } else if (col_ok) {
       constexpr float kMax = 65504.f;
       bad |= !(fabsf(m[0]) < kMax && fabsf(m[1]) < kMax && fabsf(m[2]) < kMax && fabsf(m[3]) < kMax);
       half4v h, l;
@@ -402,7 +409,10 @@ constexpr int LDS2_BYTES = AL_OFF + 64 * NKS * 32 * 2;   // 158,784 B
 static_assert(LDS2_BYTES <= 160 * 1024, "one workgroup per CU");
 }  // namespace astem
 
-template <int ABL = 0>   // ablations (tools/astem_ablate.py): 1 no MFMA loop, 2 no E phase
+// ABL: ablations (tools/astem_ablate.py): 1 no MFMA loop, 2 no E phase.  F16: the fp16
+// programs' stem in the same exact-u8 form -- hi MFMA only (w' rounded to fp16 once,
+// u exact), fp16 output
+template <int ABL = 0, bool F16 = false>
 __global__ void __launch_bounds__(512, 1)
 alex_stem_split_kernel2(const uint8_t* __restrict__ img, const half_t* __restrict__ w, const float* __restrict__ bias,
                         const float* __restrict__ psum, float acc_scale, half_t* __restrict__ y, const AStemGeom g,
@@ -438,8 +448,9 @@ alex_stem_split_kernel2(const uint8_t* __restrict__ img, const half_t* __restric
   for (int s = 0; s < NKS; ++s) aH[s] = *reinterpret_cast<const half8v*>(reinterpret_cast<const char*>(w) + aoff + s * 64);
   for (int i = tid; i < PSUM_FLOATS / 4; i += 512)
     reinterpret_cast<float4v*>(ps)[i] = reinterpret_cast<const float4v*>(psum)[i];
-  for (int i = tid; i < 64 * NKS * 32 / 8; i += 512)
-    reinterpret_cast<half8v*>(smem + AL_OFF)[i] = reinterpret_cast<const half8v*>(w + 64 * NKS * 32)[i];
+  if constexpr (!F16)
+    for (int i = tid; i < 64 * NKS * 32 / 8; i += 512)
+      reinterpret_cast<half8v*>(smem + AL_OFF)[i] = reinterpret_cast<const half8v*>(w + 64 * NKS * 32)[i];
   const int c0 = 16 * w4 + 4 * fch;
   const float4v bv = *reinterpret_cast<const float4v*>(bias + c0);
   const float inv_scale = 1.f / acc_scale;
@@ -467,19 +478,21 @@ alex_stem_split_kernel2(const uint8_t* __restrict__ img, const half_t* __restric
       half8v bf[2][CRY];
       half8v al_s[2];
       astem_read_b(patch, 0, mainb, tailb, trow, bf[0]);
-      al_s[0] = *reinterpret_cast<const half8v*>(al + aoff);
+      if constexpr (!F16) al_s[0] = *reinterpret_cast<const half8v*>(al + aoff);
 #pragma unroll
       for (int s = 0; s < NKS; ++s) {
         if (s + 1 < NKS) {
           astem_read_b(patch, s + 1, mainb, tailb, trow, bf[(s + 1) & 1]);
-          al_s[(s + 1) & 1] = *reinterpret_cast<const half8v*>(al + aoff + (s + 1) * 64);
+          if constexpr (!F16) al_s[(s + 1) & 1] = *reinterpret_cast<const half8v*>(al + aoff + (s + 1) * 64);
         }
 #pragma unroll
         for (int r = 0; r < CRY; ++r)
           acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aH[s], bf[s & 1][r], acc[r], 0, 0, 0);
+        if constexpr (!F16) {
 #pragma unroll
-        for (int r = 0; r < CRY; ++r)
-          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al_s[s & 1], bf[s & 1][r], acc[r], 0, 0, 0);
+          for (int r = 0; r < CRY; ++r)
+            acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al_s[s & 1], bf[s & 1][r], acc[r], 0, 0, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
       }
@@ -498,22 +511,14 @@ alex_stem_split_kernel2(const uint8_t* __restrict__ img, const half_t* __restric
       if (kk + 2 < nh) astem_load(img, g, t0 + (kk + 2) * stride, htid, q);
       int b, py0, px0;
       astem_tile(g, t0 + kk * stride, b, py0, px0);
-      astem_epilogue(acc, g, b, py0, px0, cx, c0, ps, inv_scale, acc_scale, bv, y);
+      astem_epilogue<F16>(acc, g, b, py0, px0, cx, c0, ps, inv_scale, acc_scale, bv, y);
     }
     __syncthreads();
   }
 }
 
-static int g_astem_variant = 64;
-void set_astem_ahead(bool on) { g_astem_variant = on ? 0 : 16; }
-void set_astem_phased(bool on) { g_astem_variant = on ? 64 : 0; }
-void set_astem_variant(int v) { g_astem_variant = v; }
-
-bool alex_stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum,
-                            float acc_scale, half_t* y, int B, int H, int W, const long long* start_idx,
-                            long long start_off, long long max_start, long long sub, int* ovf, hipStream_t st) {
+static bool astem_geom(AStemGeom& g, int B, int H, int W, const uint8_t* img, int* ovf) {
   using namespace astem;
-  AStemGeom g;
   g.ovf = ovf;
   g.B = B;
   g.H = H;
@@ -527,6 +532,37 @@ bool alex_stem_split_launch(const uint8_t* img, const half_t* w, const float* bi
   g.tiles_x = (g.Wp + PTX - 1) / PTX;
   g.tiles_y = (g.Hp + PTY - 1) / PTY;
   g.ntiles = B * g.tiles_x * g.tiles_y;
+  return true;
+}
+
+// fp16 programs: the phased exact-u8 stem, hi MFMA only, fp16 [B][Hp][Wp][64] out
+bool alex_stem_u8_f16_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum,
+                             float acc_scale, half_t* y, int B, int H, int W, const long long* start_idx,
+                             long long start_off, long long max_start, long long sub, hipStream_t st) {
+  using namespace astem;
+  AStemGeom g;
+  if (!astem_geom(g, B, H, W, img, nullptr)) return false;
+  if (g.ntiles <= 0) return true;
+  const int per = device_cu_count();
+  const int grid2 = (g.ntiles + 1) / 2 < per ? (g.ntiles + 1) / 2 : per;
+  auto k2 = alex_stem_split_kernel2<0, true>;
+  ensure_lds_attr(reinterpret_cast<const void*>(k2), LDS2_BYTES);
+  hipLaunchKernelGGL(k2, dim3(grid2), dim3(512), LDS2_BYTES, st, img, w, bias, psum, acc_scale, y, g, start_idx,
+                     start_off, max_start, sub);
+  return true;
+}
+
+static int g_astem_variant = 64;
+void set_astem_ahead(bool on) { g_astem_variant = on ? 0 : 16; }
+void set_astem_phased(bool on) { g_astem_variant = on ? 64 : 0; }
+void set_astem_variant(int v) { g_astem_variant = v; }
+
+bool alex_stem_split_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum,
+                            float acc_scale, half_t* y, int B, int H, int W, const long long* start_idx,
+                            long long start_off, long long max_start, long long sub, int* ovf, hipStream_t st) {
+  using namespace astem;
+  AStemGeom g;
+  if (!astem_geom(g, B, H, W, img, ovf)) return false;
   if (g.ntiles <= 0) return true;
   const int per = device_cu_count();          // one workgroup per CU (all 512 registers)
   const int grid = g.ntiles < per ? g.ntiles : per;

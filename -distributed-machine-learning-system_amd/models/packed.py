@@ -415,9 +415,9 @@ def make_conv(conv: nn.Conv2d, bn: nn.BatchNorm2d | None, relu: bool, dtype: str
     if tuple(conv.weight.shape) == (64, 3, 7, 7) and conv.stride[0] == 2 and conv.padding[0] == 3:
         # the exact-u8 stem: split (fp32 programs) or its hi parts alone (fp16, ops.stem_u8_f16)
         c.fs, c.fs_scale, c.fs_bias, c.fs_psum = pack_stem_split(*fold_bn_f64(conv.weight, conv.bias, bn))
-    elif dtype == "fp32" and tuple(conv.weight.shape) == (64, 3, 11, 11) and conv.stride[0] == 4 \
-            and conv.padding[0] == 2:
-        # the fused split AlexNet stem (ops.alex_stem_split)
+    elif tuple(conv.weight.shape) == (64, 3, 11, 11) and conv.stride[0] == 4 and conv.padding[0] == 2:
+        # the fused AlexNet stem: split (ops.alex_stem_split) or its hi parts alone
+        # (fp16 programs, ops.alex_stem_u8_f16)
         c.fs, c.fs_scale, c.fs_bias, c.fs_psum = pack_alex_stem_split(*fold_bn_f64(conv.weight, conv.bias, bn))
     return c
 
@@ -708,8 +708,15 @@ class HipRunner:
         fused = (self.fuse_stem and native and p.kind == "resnet" and s.small and s.kh == 7 and s.kw == 7
                  and s.stride == 2 and s.pad == 3 and s.cout == 64)
         first = p.features[0][1] if p.kind != "resnet" else None
-        p3 = (first is not None and native and self.pack3_f16 and first.p3 is not None)
-        if p3:
+        # AlexNet: uint8 -> conv1 + ReLU + max pool in one phased MFMA kernel (alex_stem.hip)
+        astem = (first is not None and native and self.fuse_stem and first.fs is not None and first.kh == 11
+                 and first.relu and len(p.features) > 1 and p.features[1][0] == "pool"
+                 and tuple(p.features[1][1]) == (3, 2, 0))
+        p3 = (first is not None and native and self.pack3_f16 and first.p3 is not None and not astem)
+        if astem:
+            x = o.alex_stem_u8_f16(img_u8, first.fs, first.fs_bias, first.fs_psum, first.fs_scale, start, batch,
+                                   start_offset)
+        elif p3:
             # AlexNet conv1 (11x11/4) on packed fp16 rows through conv_glds (K 448
             # vs 704 for NHWC4 on the register-staged conv_igemm): conv 290 -> 220
             # us at B=500, but the packed-row preprocess costs 133 vs 46 us, so it
@@ -719,6 +726,7 @@ class HipRunner:
                                first.relu)
         elif not fused:
             x = o.preprocess(img_u8, start, batch, start_offset) if native else o.resize_crop(img_u8, 256, 224)
+        feats = p.features[2:] if astem else (p.features[1:] if p3 else p.features)
         if p.kind == "resnet":
             nb = batch if start is not None else img_u8.shape[0]
             split = self.front_split if self.front_split is not None else \
@@ -734,7 +742,7 @@ class HipRunner:
             x = self._blocks(p.blocks[nfront:], x)
             x = o.global_avgpool(x)
         else:
-            for k, v in p.features[1:] if p3 else p.features:
+            for k, v in feats:
                 if k == "conv":
                     x = o.conv2d(x, v.w, v.b, v.kh, v.kw, v.stride, v.pad, v.relu)
                 else:

@@ -13,7 +13,7 @@ __all__ = [
     "available", "load", "so_path", "conv2d", "linear", "preprocess", "resize_crop",
     "maxpool2d", "global_avgpool", "softmax_top1", "pick_tile", "pick_tile_f32", "synth_images", "stem_fused",
     "conv2d_wino", "wino_supported", "preprocess_pack3", "conv2d_pack3",
-    "conv1x1_dual", "conv1x1_dual_split", "conv1x1_fused_next", "conv2d_split", "linear_split", "stem_split", "stem_u8_f16", "preprocess_pack3_split", "conv2d_pack3_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
+    "conv1x1_dual", "conv1x1_dual_split", "conv1x1_fused_next", "conv2d_split", "linear_split", "stem_split", "stem_u8_f16", "alex_stem_split", "alex_stem_u8_f16", "preprocess_pack3_split", "conv2d_pack3_split", "split_from_f32", "f32_from_split", "maxpool2d_split", "pick_tile_split",
 ]
 
 
@@ -71,6 +71,13 @@ def alex_stem_split(img_u8, w, bias, psum, acc_scale: float, start=None, batch: 
     split [B,27,27,128] (normalise, conv 11x11/4 pad 2 + bias, ReLU, max pool
     3x3/2); ``w, acc_scale, bias, psum`` = models.packed.pack_alex_stem_split(w, b)."""
     return load().alex_stem_split(img_u8, w, bias, psum, acc_scale, start, batch, start_offset, window, sub)
+
+
+def alex_stem_u8_f16(img_u8, w, bias, psum, acc_scale: float, start=None, batch: int = -1, start_offset: int = 0,
+                     window: int = -1, sub: int = 0):
+    """fp16 fused AlexNet stem in the exact-u8 form (hi MFMA only): uint8
+    [B,224,224,3] -> fp16 [B,27,27,64]; operands as ``alex_stem_split``."""
+    return load().alex_stem_u8_f16(img_u8, w, bias, psum, acc_scale, start, batch, start_offset, window, sub)
 
 
 def stem_u8_f16(img_u8, w, bias, psum, acc_scale: float, start=None, batch: int = -1, start_offset: int = 0,

@@ -539,6 +539,29 @@ def test_stem_u8_f16_vs_fp32(ops, B, H):
     _check(y, ref)
 
 
+@pytest.mark.parametrize("B,H,W", [(3, 224, 224), (2, 100, 131), (1, 31, 23)])
+def test_alex_stem_u8_f16_vs_fp32(ops, B, H, W):
+    """fp16 fused AlexNet stem (phased kernel, hi MFMA only) vs the fp32 conv 11x11/4
+    + ReLU + max pool 3x3/2 of the same image; device-side window included."""
+    from idunno.models.packed import pack_alex_stem_split
+    from idunno.models.reference import preprocess_u8
+
+    torch.manual_seed(H + B + 2)
+    img = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=DEV)
+    w = torch.randn(64, 3, 11, 11) / (3 * 121) ** 0.5
+    b = torch.randn(64) * 0.1
+    fs, scale, bias, psum = pack_alex_stem_split(w.double(), b.double())
+    fs, bias, psum = fs.to(DEV), bias.to(DEV), psum.to(DEV)
+    y = ops.alex_stem_u8_f16(img, fs, bias, psum, scale)
+    x = preprocess_u8(img)
+    ref = F.max_pool2d(F.relu(F.conv2d(x, w.to(DEV), b.to(DEV), 4, 2)), 3, 2, 0).permute(0, 2, 3, 1)
+    assert y.dtype == torch.float16 and y.shape == ref.shape
+    _check(y, ref)
+    big = torch.cat([img.flip(0), img])
+    st = torch.tensor([B + 3], dtype=torch.long, device=DEV)
+    assert torch.equal(ops.alex_stem_u8_f16(big, fs, bias, psum, scale, st, B, 3), y)
+
+
 def test_runner_fused_stem_matches_unfused(ops):
     from idunno.models import HipRunner, build_program
 
