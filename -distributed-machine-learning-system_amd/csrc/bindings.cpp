@@ -1657,6 +1657,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool2d_split", &maxpool2d_split, "NHWC max pool (fp32 or split in) -> split out", py::arg("x"),
         py::arg("k"), py::arg("s"), py::arg("pad"), py::arg("out") = py::none());
   m.def("set_astem_ahead", &set_astem_ahead);
+  m.def("set_astem_f16_two_wg", &set_astem_f16_two_wg);
   m.def("alex_stem_u8_f16", &alex_stem_u8_f16, "fp16 fused AlexNet stem (exact-u8 form, hi MFMA only)",
         py::arg("img"), py::arg("w"), py::arg("bias"), py::arg("psum"), py::arg("acc_scale"),
         py::arg("start") = py::none(), py::arg("batch") = -1, py::arg("start_offset") = 0, py::arg("window") = -1,

@@ -194,6 +194,7 @@ int conv_glds_pick(int M, int Cout);
 bool alex_stem_u8_f16_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum,
                              float acc_scale, half_t* y, int B, int H, int W, const long long* start_idx,
                              long long start_off, long long max_start, long long sub, hipStream_t st);
+void set_astem_f16_two_wg(bool on);
 void set_astem_ahead(bool on);   // A/B switch: patch loads one tile ahead (1) or after the MFMA loop
 void set_astem_phased(bool on);  // A/B switch: the phased two-half kernel (default) or the one-half form
 void set_astem_variant(int v);   // tools/astem_ablate.py: 0 production, 16 loads after the loop, 1/2/4/6 ablations

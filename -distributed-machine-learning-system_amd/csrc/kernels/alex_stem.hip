@@ -276,8 +276,12 @@ __device__ __forceinline__ void astem_epilogue(float4v (&acc)[astem::CRY], const
 
 // ABL: ablation bits for tools/astem_ablate.py (0 in production): 1 no MFMA loop,
 // 2 no epilogue (accumulators kept alive by a never-taken store), 4 no patch staging
-template <bool AHEAD, int ABL = 0>
-__global__ void __launch_bounds__(256, 1)
+// F16: the fp16 programs' stem (hi MFMA only, fp16 out) at two workgroups per CU:
+// without the A lo fragments a wave fits 256 registers, and with its MFMA loop half
+// as long the epilogue/staging work dominates, which two independent workgroups
+// overlap without phase barriers
+template <bool AHEAD, int ABL = 0, bool F16 = false>
+__global__ void __launch_bounds__(256, F16 ? 2 : 1)
 alex_stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict__ w, const float* __restrict__ bias,
                        const float* __restrict__ psum, float acc_scale, half_t* __restrict__ y, const AStemGeom g,
                        const long long* __restrict__ start_idx, long long start_off, long long max_start,
@@ -304,7 +308,7 @@ alex_stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
       aH[s] = *reinterpret_cast<const half8v*>(wr + s * 32);
-      aL[s] = *reinterpret_cast<const half8v*>(wr + (size_t)64 * NKS * 32 + s * 32);
+      if constexpr (!F16) aL[s] = *reinterpret_cast<const half8v*>(wr + (size_t)64 * NKS * 32 + s * 32);
     }
   }
   const int c0 = 16 * wave + 4 * fch;          // this lane's 4 output channels
@@ -351,9 +355,11 @@ alex_stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict
 #pragma unroll
       for (int r = 0; r < CRY; ++r)
         acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aH[s], bf[s & 1][r], acc[r], 0, 0, 0);
+      if constexpr (!F16) {
 #pragma unroll
-      for (int r = 0; r < CRY; ++r)
-        acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aL[s], bf[s & 1][r], acc[r], 0, 0, 0);
+        for (int r = 0; r < CRY; ++r)
+          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aL[s], bf[s & 1][r], acc[r], 0, 0, 0);
+      }
       // keeps the scheduler from hoisting later steps' reads (it spilled when it did)
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -381,7 +387,7 @@ alex_stem_split_kernel(const uint8_t* __restrict__ img, const half_t* __restrict
       t = tnext;
       continue;
     }
-    astem_epilogue(acc, g, b, py0, px0, cx, c0, ps, inv_scale, acc_scale, bv, y);
+    astem_epilogue<F16>(acc, g, b, py0, px0, cx, c0, ps, inv_scale, acc_scale, bv, y);
     if (!AHEAD && tnext < g.ntiles) astem_store(smem, tid, q);
     // the loads of the tile after next go out behind this tile's border-correction
     // loads and output stores (vmcnt retires in order: those waits do not cover them)
@@ -535,6 +541,11 @@ static bool astem_geom(AStemGeom& g, int B, int H, int W, const uint8_t* img, in
   return true;
 }
 
+// fp16 form: two one-half workgroups per CU (default, AlexNet fp16 b500 +1.8 % over the
+// phased halves: profiles/r6w_ab_alex_stem_f16_two_wg_b500.log) or the phased kernel
+static int g_astem_f16_two_wg = 1;
+void set_astem_f16_two_wg(bool on) { g_astem_f16_two_wg = on; }
+
 // fp16 programs: the phased exact-u8 stem, hi MFMA only, fp16 [B][Hp][Wp][64] out
 bool alex_stem_u8_f16_launch(const uint8_t* img, const half_t* w, const float* bias, const float* psum,
                              float acc_scale, half_t* y, int B, int H, int W, const long long* start_idx,
@@ -544,6 +555,12 @@ bool alex_stem_u8_f16_launch(const uint8_t* img, const half_t* w, const float* b
   if (!astem_geom(g, B, H, W, img, nullptr)) return false;
   if (g.ntiles <= 0) return true;
   const int per = device_cu_count();
+  if (g_astem_f16_two_wg) {
+    const int grid = g.ntiles < 2 * per ? g.ntiles : 2 * per;
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(alex_stem_split_kernel<true, 0, true>), dim3(grid), dim3(256), LDS_BYTES, st,
+                       img, w, bias, psum, acc_scale, y, g, start_idx, start_off, max_start, sub);
+    return true;
+  }
   const int grid2 = (g.ntiles + 1) / 2 < per ? (g.ntiles + 1) / 2 : per;
   auto k2 = alex_stem_split_kernel2<0, true>;
   ensure_lds_attr(reinterpret_cast<const void*>(k2), LDS2_BYTES);

@@ -539,12 +539,12 @@ def test_stem_u8_f16_vs_fp32(ops, B, H):
     _check(y, ref)
 
 
+@pytest.mark.parametrize("two_wg", [False, True])
 @pytest.mark.parametrize("B,H,W", [(3, 224, 224), (2, 100, 131), (1, 31, 23)])
-def test_alex_stem_u8_f16_vs_fp32(ops, B, H, W):
-    """fp16 fused AlexNet stem (phased kernel, hi MFMA only) vs the fp32 conv 11x11/4
+def test_alex_stem_u8_f16_vs_fp32(ops, B, H, W, two_wg):
+    """fp16 fused AlexNet stem (hi MFMA only; both kernel forms) vs the fp32 conv 11x11/4
     + ReLU + max pool 3x3/2 of the same image; device-side window included."""
     from idunno.models.packed import pack_alex_stem_split
-    from idunno.models.reference import preprocess_u8
 
     torch.manual_seed(H + B + 2)
     img = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=DEV)
@@ -552,6 +552,16 @@ def test_alex_stem_u8_f16_vs_fp32(ops, B, H, W):
     b = torch.randn(64) * 0.1
     fs, scale, bias, psum = pack_alex_stem_split(w.double(), b.double())
     fs, bias, psum = fs.to(DEV), bias.to(DEV), psum.to(DEV)
+    ops.load().set_astem_f16_two_wg(two_wg)      # the kernel form (phased halves / two one-half workgroups)
+    try:
+        _alex_f16_case(ops, img, w, b, fs, scale, bias, psum, B)
+    finally:
+        ops.load().set_astem_f16_two_wg(True)
+
+
+def _alex_f16_case(ops, img, w, b, fs, scale, bias, psum, B):
+    from idunno.models.reference import preprocess_u8
+
     y = ops.alex_stem_u8_f16(img, fs, bias, psum, scale)
     x = preprocess_u8(img)
     ref = F.max_pool2d(F.relu(F.conv2d(x, w.to(DEV), b.to(DEV), 4, 2)), 3, 2, 0).permute(0, 2, 3, 1)
